@@ -1,0 +1,133 @@
+#!/usr/bin/env python
+"""Headline benchmark: whole-node images/s of the ResNet-50 DAG train task.
+
+Metric/config from BASELINE.json: "images/sec (whole node) ResNet-50 DAG train task at
+1/2/4/8 MI355X", ImageNet-shape synthetic data (224x224x3, 1000 classes), random-init
+weights.  One process per GPU (torchrun), data-parallel over RCCL; per-GPU batch is fixed
+(weak scaling).  A timed step is a full training step: forward, loss, backward, gradient
+all-reduce, optimizer update.
+
+    python bench.py --gpus 1 --steps 20 --warmup 5
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        bench.py --gpus 8 --steps 20 --warmup 5
+
+``--impl native`` (default) runs the mlcomp_amd engine: NHWC bf16 activations, HIP
+kernels for conv/BN/ReLU/optimizer/loss and the framework's own RCCL gradient bucketer.
+``--impl torch`` runs stock PyTorch-ROCm (MIOpen convs, torch DDP) on the same model
+and data, which is the measured comparison baseline (BASELINE.md has no published
+number).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+# the reference publishes no number (BASELINE.json "published": {}); the comparison
+# baseline is the stock PyTorch-ROCm run measured on the same box (profiles/README.md)
+BASELINE_VALUE = None
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=5)
+    p.add_argument('--batch', type=int, default=256, help='per-GPU batch')
+    p.add_argument('--model', default='resnet50')
+    p.add_argument('--impl', default='native', choices=['native', 'torch'])
+    p.add_argument('--image-size', type=int, default=224)
+    p.add_argument('--graph', type=int, default=-1,
+                   help='capture the step in a HIP graph (default: on for native)')
+    p.add_argument('--json-out', default=None)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus and rank == 0:
+        print(f'warning: --gpus {args.gpus} but WORLD_SIZE={world}', file=sys.stderr)
+
+    if not torch.cuda.is_available():
+        print('bench.py needs a GPU', file=sys.stderr)
+        sys.exit(2)
+    torch.cuda.set_device(local_rank)
+    device = torch.device('cuda', local_rank)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=device)
+
+    from mlcomp_amd.train.imagenet import build_train_step
+    step = build_train_step(args.model, batch=args.batch, impl=args.impl,
+                            image_size=args.image_size, device=device,
+                            world_size=world,
+                            use_graph=(args.graph if args.graph >= 0 else None))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms = elapsed * 1000.0 / args.steps
+    images = args.batch * world * args.steps
+    value = images / elapsed
+    loss = step.last_loss()
+    if rank == 0:
+        out = {
+            'metric': 'images/sec (whole node) ResNet-50 DAG train task',
+            'value': round(value, 2),
+            'unit': 'images/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(ms, 3),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
+            'dtype': 'bf16',
+            'data': 'synthetic (ImageNet-shape 224x224x3, 1000 classes, random-init weights)',
+            'config': {
+                'model': args.model,
+                'global_batch': args.batch * world,
+                'per_gpu_batch': args.batch,
+                'image_size': args.image_size,
+                'seq_len': None,
+                'parallelism': f'dp{world}',
+                'impl': args.impl,
+                'optimizer': 'SGD momentum 0.9, wd 5e-5, fp32 master weights',
+                'final_loss': loss,
+            },
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, 'w') as f:
+                f.write(line + '\n')
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

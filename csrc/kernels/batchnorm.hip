@@ -1,0 +1,245 @@
+// Training BatchNorm for NHWC bf16 activations, fused with residual-add and ReLU.
+//
+// Forward statistics are NOT computed here: the producing conv accumulates per-channel
+// sum / sum-of-squares in its epilogue (igemm.hip EpiBF16), a C-thread finalize turns
+// them into (scale, shift), and BN forward is a single read-y / write-z pass:
+// z = act(y*scale + shift [+ residual]).
+// Backward is two passes: a per-channel reduction of dU and dU*(y-mean) (dU = dz masked
+// by z>0 when the ReLU is fused), then an elementwise pass producing dy (and the
+// residual-branch gradient dU).
+//
+// Channel-group ownership: launches use a thread count that is a multiple of C/8, so
+// each thread owns one fixed 8-channel group for its whole grid-stride loop and keeps
+// the per-channel constants in registers.  All accesses are 16 B per lane.
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+// per-channel finalize: reduce the conv epilogue's NSTAT partial copies, publish batch
+// mean / invstd, the fused affine (scale, shift) and update the running statistics
+__global__ void __launch_bounds__(NT)
+bn_finalize_kernel(const float* __restrict__ sum, const float* __restrict__ sumsq, int ncopy,
+                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                   float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                   float* __restrict__ scale, float* __restrict__ shift,
+                   float* __restrict__ run_mean, float* __restrict__ run_var,
+                   long rows, int C, float eps, float momentum) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int k = 0; k < ncopy; ++k) { s1 += sum[(long)k * C + c]; s2 += sumsq[(long)k * C + c]; }
+  const float inv_count = 1.f / (float)rows;
+  const float mean = s1 * inv_count;
+  const float var = fmaxf(s2 * inv_count - mean * mean, 0.f);
+  const float inv = rsqrtf(var + eps);
+  save_mean[c] = mean;
+  save_invstd[c] = inv;
+  const float g = gamma[c] * inv;
+  scale[c] = g;
+  shift[c] = beta[c] - mean * g;
+  if (run_mean) {
+    const float unbiased = rows > 1 ? var * (float)rows / (float)(rows - 1) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unbiased;
+  }
+}
+
+// z = act(y*scale + shift [+ res])
+__global__ void __launch_bounds__(NT)
+bn_fwd_apply_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf16* __restrict__ z,
+                    const float* __restrict__ scale_, const float* __restrict__ shift_,
+                    long rows, int C, int relu) {
+  const int G = C >> 3;
+  const long gtid = (long)blockIdx.x * NT + threadIdx.x;
+  const long stride = (long)gridDim.x * NT;
+  const int cg = (int)(gtid % G);
+  const int c0 = cg * 8;
+  float scale[8], shift[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { scale[j] = scale_[c0 + j]; shift[j] = shift_[c0 + j]; }
+  const long total = rows * G;
+  for (long i = gtid; i < total; i += stride) {
+    const long off = i * 8;  // row*C + c0 since i = row*G + cg
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(y + off), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = f[j] * scale[j] + shift[j];
+    if (res) {
+      float r[8];
+      unpack8(*reinterpret_cast<const uint4*>(res + off), r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += r[j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    }
+    *reinterpret_cast<uint4*>(z + off) = pack8(f);
+  }
+}
+
+// sums[0:C] += sum dU ; sums[C:2C] += sum dU*(y-mean)
+__global__ void __launch_bounds__(NT)
+bn_bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const bf16* __restrict__ y,
+                     const float* __restrict__ mean, float* __restrict__ sums, long rows, int C) {
+  __shared__ float red[2][NT][9];
+  const int G = C >> 3;
+  const long gtid = (long)blockIdx.x * NT + threadIdx.x;
+  const long stride = (long)gridDim.x * NT;
+  const int cg = (int)(gtid % G);
+  const int c0 = cg * 8;
+  float mu[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; s1[j] = 0.f; s2[j] = 0.f; }
+  const long total = rows * G;
+  for (long i = gtid; i < total; i += stride) {
+    const long off = i * 8;
+    float d[8], yy[8];
+    unpack8(*reinterpret_cast<const uint4*>(dz + off), d);
+    unpack8(*reinterpret_cast<const uint4*>(y + off), yy);
+    if (z) {
+      float zz[8];
+      unpack8(*reinterpret_cast<const uint4*>(z + off), zz);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = zz[j] > 0.f ? d[j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s1[j] += d[j]; s2[j] += d[j] * (yy[j] - mu[j]); }
+  }
+  // combine threads of this block owning the same channel group (tid ≡ tid' mod G)
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[0][t][j] = s1[j]; red[1][t][j] = s2[j]; }
+  __syncthreads();
+  const int lanes = NT < G ? NT : G;  // distinct groups present in this block
+  const int base_cg = (int)(((long)blockIdx.x * NT) % G);
+  if (t < lanes) {
+    float a[8], b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { a[j] = 0.f; b[j] = 0.f; }
+    for (int u = t; u < NT; u += G) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a[j] += red[0][u][j]; b[j] += red[1][u][j]; }
+    }
+    const int cgt = (base_cg + t) % G;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      atomicAdd(sums + cgt * 8 + j, a[j]);
+      atomicAdd(sums + C + cgt * 8 + j, b[j]);
+    }
+  }
+}
+
+// dy = gamma*invstd/M * (M*dU - S1 - (y-mean)*invstd^2 * S2);  dres = dU (optional)
+// also publishes dgamma = S2*invstd, dbeta = S1 (fp32, accumulated into dgamma/dbeta
+// if accumulate) from the threads with gtid < G.
+__global__ void __launch_bounds__(NT)
+bn_bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const bf16* __restrict__ y,
+                    const float* __restrict__ mean, const float* __restrict__ invstd,
+                    const float* __restrict__ gamma, const float* __restrict__ sums,
+                    bf16* __restrict__ dy, bf16* __restrict__ dres,
+                    float* __restrict__ dgamma, float* __restrict__ dbeta, long rows, int C) {
+  const int G = C >> 3;
+  const long gtid = (long)blockIdx.x * NT + threadIdx.x;
+  const long stride = (long)gridDim.x * NT;
+  const int cg = (int)(gtid % G);
+  const int c0 = cg * 8;
+  const float invM = 1.f / (float)rows;
+  float mu[8], k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float is = invstd[c0 + j];
+    const float S1 = sums[c0 + j], S2 = sums[C + c0 + j];
+    mu[j] = mean[c0 + j];
+    k1[j] = gamma[c0 + j] * is;                       // * dU
+    k2[j] = -k1[j] * S1 * invM;                       // const
+    k3[j] = -k1[j] * is * is * S2 * invM;             // * (y-mean)
+  }
+  if (gtid < G && dgamma) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      dgamma[c0 + j] = sums[C + c0 + j] * invstd[c0 + j];
+      dbeta[c0 + j] = sums[c0 + j];
+    }
+  }
+  const long total = rows * G;
+  for (long i = gtid; i < total; i += stride) {
+    const long off = i * 8;
+    float d[8], yy[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(dz + off), d);
+    unpack8(*reinterpret_cast<const uint4*>(y + off), yy);
+    if (z) {
+      float zz[8];
+      unpack8(*reinterpret_cast<const uint4*>(z + off), zz);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = zz[j] > 0.f ? d[j] : 0.f;
+    }
+    if (dres) *reinterpret_cast<uint4*>(dres + off) = pack8(d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = k1[j] * d[j] + k2[j] + k3[j] * (yy[j] - mu[j]);
+    *reinterpret_cast<uint4*>(dy + off) = pack8(o);
+  }
+}
+
+int grid_for(long rows, int C) {
+  const int G = C >> 3;
+  long total = rows * G;
+  // threads must be a multiple of G: blocks*256 % G == 0 always holds for G | 256;
+  // for G > 256 (C > 2048) make the block count a multiple of G/256.
+  long blocks = (total + NT * 4 - 1) / (NT * 4);   // ~4 chunks per thread
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  if (G > NT) {
+    const long m = G / NT;
+    blocks = ((blocks + m - 1) / m) * m;
+  }
+  return (int)blocks;
+}
+
+bool shape_ok(int C) {
+  const int G = C >> 3;
+  if (C % 8) return false;
+  if (G <= NT) return NT % G == 0;
+  return G % NT == 0;
+}
+
+}  // namespace
+
+MLC_EXPORT int mlc_bn_finalize(const float* sum, const float* sumsq, int ncopy, const float* gamma,
+                               const float* beta, float* save_mean, float* save_invstd, float* scale,
+                               float* shift, float* run_mean, float* run_var, long rows, int C,
+                               float eps, float momentum, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, st, sum, sumsq, ncopy,
+                     gamma, beta, save_mean, save_invstd, scale, shift, run_mean, run_var, rows, C, eps,
+                     momentum);
+  return hipGetLastError();
+}
+
+MLC_EXPORT int mlc_bn_fwd_apply(const bf16* y, const bf16* res, bf16* z, const float* scale,
+                                const float* shift, long rows, int C, int relu, hipStream_t st) {
+  if (!shape_ok(C)) return -1;
+  hipLaunchKernelGGL(bn_fwd_apply_kernel, dim3(grid_for(rows, C)), dim3(NT), 0, st, y, res, z, scale,
+                     shift, rows, C, relu);
+  return hipGetLastError();
+}
+
+// sums must hold 2*C floats and be zeroed by the caller (or accumulate)
+MLC_EXPORT int mlc_bn_bwd_reduce(const bf16* dz, const bf16* z, const bf16* y, const float* mean,
+                                 float* sums, long rows, int C, hipStream_t st) {
+  if (!shape_ok(C)) return -1;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_for(rows, C)), dim3(NT), 0, st, dz, z, y,
+                     mean, sums, rows, C);
+  return hipGetLastError();
+}
+
+MLC_EXPORT int mlc_bn_bwd_apply(const bf16* dz, const bf16* z, const bf16* y, const float* mean,
+                                const float* invstd, const float* gamma, const float* sums,
+                                bf16* dy, bf16* dres, float* dgamma, float* dbeta, long rows,
+                                int C, hipStream_t st) {
+  if (!shape_ok(C)) return -1;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(rows, C)), dim3(NT), 0, st, dz, z, y,
+                     mean, invstd, gamma, sums, dy, dres, dgamma, dbeta, rows, C);
+  return hipGetLastError();
+}

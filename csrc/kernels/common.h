@@ -1,0 +1,60 @@
+// Shared helpers for the mlcomp_amd CDNA4 (gfx950) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR(T) __attribute__((address_space(3))) T*
+
+#define MLC_EXPORT extern "C" __attribute__((visibility("default")))
+
+static __device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
+static __device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }
+
+// unpack 8 bf16 held in a uint4 into floats
+static __device__ __forceinline__ void unpack8(const uint4& u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+// round-to-nearest-even float -> bf16 bits
+static __device__ __forceinline__ uint32_t f2bf_bits(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (u >> 16) | ((u & 0xffff) ? 0x40u : 0u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+static __device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 r;
+  r.x = f2bf_bits(f[0]) | (f2bf_bits(f[1]) << 16);
+  r.y = f2bf_bits(f[2]) | (f2bf_bits(f[3]) << 16);
+  r.z = f2bf_bits(f[4]) | (f2bf_bits(f[5]) << 16);
+  r.w = f2bf_bits(f[6]) | (f2bf_bits(f[7]) << 16);
+  return r;
+}
+
+static __device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md T1):
+// blocks dealt round-robin to the 8 XCDs end up owning contiguous tile ranges.
+static __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7;
+  const int xcd = orig & 7, loc = orig >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}

@@ -1,0 +1,135 @@
+// Fused optimizers over flat parameter arenas (one launch for the whole model).
+//
+// The native engine keeps every parameter of a model in ONE contiguous fp32 master
+// buffer (decayed parameters first, then the no-decay ones: BN affine, biases), grads in
+// a parallel fp32 buffer that the RCCL bucketer all-reduces in place, and a bf16 mirror
+// of the decayed (matmul) weights that the MFMA kernels read.  An update is therefore a
+// single bandwidth-bound pass: read p, g, state; write p, state, bf16(p).
+// Learning rate and the grad scale live in device memory so the step can be captured in
+// a HIP graph and replayed with a new LR without re-capture.
+#include "common.h"
+
+namespace {
+constexpr int NT = 256;
+
+__device__ __forceinline__ void store_bf16x4(bf16* dst, const float* f) {
+  uint2 u;
+  u.x = f2bf_bits(f[0]) | (f2bf_bits(f[1]) << 16);
+  u.y = f2bf_bits(f[2]) | (f2bf_bits(f[3]) << 16);
+  *reinterpret_cast<uint2*>(dst) = u;
+}
+}  // namespace
+
+// hyper[0] = lr, hyper[1] = grad scale (e.g. 1/world_size / loss scale)
+__global__ void __launch_bounds__(NT)
+sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+           bf16* __restrict__ pbf, const float* __restrict__ hyper, long n4, long ndecay4,
+           long nbf4, float momentum, float dampening, float wd, int nesterov, int first) {
+  const float lr = hyper[0], gs = hyper[1];
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float pp[4] = {pv.x, pv.y, pv.z, pv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
+    const float w = i < ndecay4 ? wd : 0.f;
+    float mm[4];
+    if (momentum != 0.f) {
+      float4 mv = reinterpret_cast<float4*>(m)[i];
+      mm[0] = mv.x; mm[1] = mv.y; mm[2] = mv.z; mm[3] = mv.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float d = gg[j] * gs + w * pp[j];
+      if (momentum != 0.f) {
+        mm[j] = first ? d : momentum * mm[j] + (1.f - dampening) * d;
+        d = nesterov ? d + momentum * mm[j] : mm[j];
+      }
+      pp[j] -= lr * d;
+    }
+    reinterpret_cast<float4*>(p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+    if (momentum != 0.f) reinterpret_cast<float4*>(m)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
+    if (pbf && i < nbf4) store_bf16x4(pbf + i * 4, pp);
+  }
+}
+
+// Adam / AdamW.  hyper: [lr, grad_scale, bias_correction1, bias_correction2]
+__global__ void __launch_bounds__(NT)
+adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+            float* __restrict__ v, bf16* __restrict__ pbf, const float* __restrict__ hyper, long n4,
+            long ndecay4, long nbf4, float b1, float b2, float eps, float wd, int decoupled) {
+  const float lr = hyper[0], gs = hyper[1], bc1 = hyper[2], bc2 = hyper[3];
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 mv = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float pp[4] = {pv.x, pv.y, pv.z, pv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
+    float mm[4] = {mv.x, mv.y, mv.z, mv.w}, ww[4] = {vv.x, vv.y, vv.z, vv.w};
+    const float wdi = i < ndecay4 ? wd : 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float d = gg[j] * gs;
+      if (!decoupled) d += wdi * pp[j];
+      mm[j] = b1 * mm[j] + (1.f - b1) * d;
+      ww[j] = b2 * ww[j] + (1.f - b2) * d * d;
+      const float upd = (mm[j] / bc1) / (sqrtf(ww[j] / bc2) + eps);
+      if (decoupled) pp[j] -= lr * wdi * pp[j];
+      pp[j] -= lr * upd;
+    }
+    reinterpret_cast<float4*>(p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+    reinterpret_cast<float4*>(m)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
+    reinterpret_cast<float4*>(v)[i] = make_float4(ww[0], ww[1], ww[2], ww[3]);
+    if (pbf && i < nbf4) store_bf16x4(pbf + i * 4, pp);
+  }
+}
+
+// out[0] += sum(x^2) over a flat fp32 buffer (for grad-norm clipping)
+__global__ void __launch_bounds__(NT)
+sqnorm_kernel(const float* __restrict__ x, long n, float* __restrict__ out, float scale) {
+  float s = 0.f;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
+    const float v = x[i] * scale;
+    s += v * v;
+  }
+  s = wave_sum(s);
+  __shared__ float red[NT / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < NT / 64; ++k) t += red[k];
+    atomicAdd(out, t);
+  }
+}
+
+static int blocks_for(long work) {
+  long b = (work + NT - 1) / NT;
+  if (b > 8192) b = 8192;
+  return (int)(b < 1 ? 1 : b);
+}
+
+// n, ndecay, nbf must be multiples of 4 (the arena pads every segment to 4 floats)
+MLC_EXPORT int mlc_sgd(float* p, const float* g, float* m, bf16* pbf, const float* hyper, long n,
+                       long ndecay, long nbf, float momentum, float dampening, float wd, int nesterov,
+                       int first, hipStream_t st) {
+  if (n % 4 || ndecay % 4 || nbf % 4) return -1;
+  hipLaunchKernelGGL(sgd_kernel, dim3(blocks_for(n / 4)), dim3(NT), 0, st, p, g, m, pbf, hyper, n / 4,
+                     ndecay / 4, nbf / 4, momentum, dampening, wd, nesterov, first);
+  return hipGetLastError();
+}
+
+MLC_EXPORT int mlc_adam(float* p, const float* g, float* m, float* v, bf16* pbf, const float* hyper,
+                        long n, long ndecay, long nbf, float b1, float b2, float eps, float wd,
+                        int decoupled, hipStream_t st) {
+  if (n % 4 || ndecay % 4 || nbf % 4) return -1;
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n / 4)), dim3(NT), 0, st, p, g, m, v, pbf, hyper,
+                     n / 4, ndecay / 4, nbf / 4, b1, b2, eps, wd, decoupled);
+  return hipGetLastError();
+}
+
+MLC_EXPORT int mlc_sqnorm(const float* x, long n, float* out, float scale, hipStream_t st) {
+  long b = (n + NT * 8 - 1) / (NT * 8);
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  hipLaunchKernelGGL(sqnorm_kernel, dim3(b), dim3(NT), 0, st, x, n, out, scale);
+  return hipGetLastError();
+}

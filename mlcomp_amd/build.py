@@ -1,0 +1,110 @@
+"""Build the native parts of mlcomp_amd in-tree.
+
+* ``libmlcomp_kernels.so`` - every ``csrc/kernels/*.hip`` compiled for gfx950 with hipcc
+  (extern "C" launchers, loaded with ctypes by :mod:`mlcomp_amd.ops._lib`).
+* ``mlcomp-broker`` - the C++17 epoll task-queue daemon (``csrc/broker``), the native
+  replacement for the reference's vendored redis-server (`mlcomp/bin/redis-server`,
+  launched at `mlcomp/server/__main__.py:66-79`).
+* ``libmlcomp_runtime.so`` - host-side C++ runtime helpers (``csrc/runtime``): the
+  threaded batch loader / collate used by the data pipeline.
+
+Outputs live under ``mlcomp_amd/_native/`` so they travel with the repo snapshot.
+Compilation is incremental (mtime based) and parallel.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, 'mlcomp_amd', '_native')
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+ARCH = os.environ.get('MLC_OFFLOAD_ARCH', 'gfx950')
+
+KERNEL_LIB = os.path.join(OUT, 'libmlcomp_kernels.so')
+BROKER_BIN = os.path.join(OUT, 'mlcomp-broker')
+RUNTIME_LIB = os.path.join(OUT, 'libmlcomp_runtime.so')
+
+
+def _newer(target, sources):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError('command failed: ' + ' '.join(cmd) + '\n' + r.stdout + r.stderr)
+    return r
+
+
+def build_kernels(verbose=False, jobs=None):
+    os.makedirs(OUT, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(ROOT, 'csrc', 'kernels', '*.hip')))
+    headers = glob.glob(os.path.join(ROOT, 'csrc', 'kernels', '*.h'))
+    objdir = os.path.join(OUT, 'obj')
+    os.makedirs(objdir, exist_ok=True)
+    flags = ['-O3', '-std=c++17', '-fPIC', f'--offload-arch={ARCH}', '-Wno-unused-result',
+             '-munsafe-fp-atomics', '-I', os.path.join(ROOT, 'csrc', 'kernels')]
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(objdir, os.path.basename(s) + '.o')
+        objs.append(o)
+        if _newer(o, [s] + headers):
+            todo.append((s, o))
+    jobs = jobs or min(8, max(1, len(todo)))
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        futs = [ex.submit(_run, [HIPCC] + flags + ['-c', s, '-o', o]) for s, o in todo]
+        for f in futs:
+            f.result()
+    if todo or _newer(KERNEL_LIB, objs):
+        _run([HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', '-o', KERNEL_LIB] + objs)
+    if verbose:
+        print(f'[build] kernels: {len(todo)} rebuilt -> {KERNEL_LIB}')
+    return KERNEL_LIB
+
+
+def build_broker(verbose=False):
+    os.makedirs(OUT, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(ROOT, 'csrc', 'broker', '*.cpp')))
+    hdrs = glob.glob(os.path.join(ROOT, 'csrc', 'broker', '*.h'))
+    if not srcs:
+        return None
+    if _newer(BROKER_BIN, srcs + hdrs):
+        cxx = shutil.which('g++') or 'c++'
+        _run([cxx, '-O2', '-std=c++17', '-pthread', '-Wall', '-o', BROKER_BIN] + srcs)
+    if verbose:
+        print(f'[build] broker -> {BROKER_BIN}')
+    return BROKER_BIN
+
+
+def build_runtime(verbose=False):
+    os.makedirs(OUT, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(ROOT, 'csrc', 'runtime', '*.cpp')))
+    hdrs = glob.glob(os.path.join(ROOT, 'csrc', 'runtime', '*.h'))
+    if not srcs:
+        return None
+    if _newer(RUNTIME_LIB, srcs + hdrs):
+        cxx = shutil.which('g++') or 'c++'
+        _run([cxx, '-O3', '-std=c++17', '-pthread', '-fPIC', '-shared', '-Wall', '-o', RUNTIME_LIB]
+             + srcs)
+    if verbose:
+        print(f'[build] runtime -> {RUNTIME_LIB}')
+    return RUNTIME_LIB
+
+
+def build_all(verbose=True):
+    build_kernels(verbose)
+    build_broker(verbose)
+    build_runtime(verbose)
+
+
+if __name__ == '__main__':
+    build_all(verbose=True)
+    sys.exit(0)

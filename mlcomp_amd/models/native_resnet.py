@@ -1,0 +1,104 @@
+"""Native (HIP-kernel) execution of the ResNet family defined in
+:mod:`mlcomp_amd.models.resnet`.
+
+``NativeResNet(torch_model)`` lowers the module tree onto native layers
+(`mlcomp_amd.ops.layers`): every ConvBNAct becomes one fused conv+BN(+residual)(+ReLU)
+autograd node whose BN statistics come out of the conv epilogue, the stem takes the
+image as NHWC bf16 with channels padded 3 -> 8 (the MFMA loaders move 8 channels per
+16-byte chunk; the padded input channels are zero so their weights get zero gradient and
+stay zero), and the head fuses avg-pool, the FC layer and softmax cross-entropy.
+
+Weights are copied into the flat arenas once; ``export_to_torch()`` writes them back
+(for checkpoints in the standard PyTorch layout).
+"""
+from __future__ import annotations
+
+import torch
+
+from mlcomp_amd.ops.layers import ClassifierHead, ConvBN, MaxPool, NativeContext
+from .resnet import BasicBlock, Bottleneck, ResNet
+
+STEM_CIN = 8
+
+
+class NativeResNet:
+    def __init__(self, model: ResNet, device, smoothing: float = 0.0):
+        if model.groups != 1:
+            raise NotImplementedError('native ResNet path supports groups=1 (use impl=torch)')
+        self.torch_model = model
+        ctx = self.ctx = NativeContext()
+        stem = model.stem
+        self.stem = ConvBN(ctx, 'stem', stem.conv, stem.bn, act=True, cin_pad=STEM_CIN)
+        self.pool = MaxPool(3, 2, 1)
+        self.blocks = []
+        for li in range(1, 5):
+            for bi, blk in enumerate(getattr(model, f'layer{li}')):
+                pre = f'layer{li}.{bi}'
+                units = []
+                if isinstance(blk, Bottleneck):
+                    names = ('cb1', 'cb2', 'cb3')
+                elif isinstance(blk, BasicBlock):
+                    names = ('cb1', 'cb2')
+                else:
+                    raise TypeError(type(blk))
+                for nm in names:
+                    cb = getattr(blk, nm)
+                    units.append(ConvBN(ctx, f'{pre}.{nm}', cb.conv, cb.bn, act=cb.act))
+                down = None
+                if blk.downsample is not None:
+                    d = blk.downsample.cb
+                    down = ConvBN(ctx, f'{pre}.downsample.cb', d.conv, d.bn, act=False)
+                self.blocks.append((units, down))
+        self.head = ClassifierHead(ctx, 'fc', model.fc, smoothing)
+        ctx.finalize(device)
+        for u in self._units():
+            u.load_from_torch()
+        self.head.load_from_torch()
+        ctx.arena.decay.refresh_mirror()
+
+    def _units(self):
+        yield self.stem
+        for units, down in self.blocks:
+            yield from units
+            if down is not None:
+                yield down
+
+    # ------------------------------------------------------------------ execution
+    def features(self, x):
+        anchor = self.ctx.anchor
+        x = self.stem(x)
+        x = self.pool(x, anchor)
+        for units, down in self.blocks:
+            identity = down(x) if down is not None else x
+            y = x
+            for u in units[:-1]:
+                y = u(y)
+            x = units[-1](y, identity)
+        return x
+
+    def loss(self, x, labels):
+        """Summed cross-entropy (fp32 [1] view of the workspace)."""
+        return self.head(self.features(x), labels)
+
+    def logits(self, x):
+        return self.head.logits(self.features(x))
+
+    def train(self, mode=True):
+        self.ctx.training = mode
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    @property
+    def arena(self):
+        return self.ctx.arena
+
+    def export_to_torch(self):
+        for u in self._units():
+            u.export_to_torch()
+        self.head.export_to_torch()
+        return self.torch_model
+
+    def num_params(self):
+        return self.ctx.arena.num_params()

@@ -1,0 +1,91 @@
+"""ctypes binding of ``libmlcomp_kernels.so`` (csrc/kernels/*.hip, gfx950).
+
+Every launcher takes raw device pointers plus the current HIP stream of the calling
+PyTorch context, so the kernels interleave with (and are captured into HIP graphs
+together with) PyTorch's own work.  There is no fallback: on a GPU box a missing or
+stale library raises immediately (the driver checks that the native .so is what runs).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch
+
+_LIB = None
+_LOCK = threading.Lock()
+
+vp, i32, i64, f32 = C.c_void_p, C.c_int, C.c_long, C.c_float
+
+_SIGS = {
+    'mlc_conv_fwd': [vp, vp, vp, vp, vp] + [i32] * 12 + [vp],
+    'mlc_conv_dgrad': [vp, vp, vp] + [i32] * 12 + [vp],
+    'mlc_conv_wgrad': [vp, vp, vp] + [i32] * 14 + [vp],
+    'mlc_gemm_f32out': [vp, vp, vp, vp] + [i32] * 11 + [vp],
+    'mlc_gemm_bf16out': [vp, vp, vp] + [i32] * 8 + [vp],
+    'mlc_bn_stat_copies': [],
+    'mlc_bn_finalize': [vp, vp, i32] + [vp] * 8 + [i64, i32, f32, f32, vp],
+    'mlc_bn_fwd_apply': [vp] * 5 + [i64, i32, i32, vp],
+    'mlc_bn_bwd_reduce': [vp] * 5 + [i64, i32, vp],
+    'mlc_bn_bwd_apply': [vp] * 11 + [i64, i32, vp],
+    'mlc_maxpool_fwd': [vp, vp, vp] + [i32] * 9 + [vp],
+    'mlc_maxpool_bwd': [vp, vp, vp] + [i32] * 9 + [vp],
+    'mlc_avgpool_fwd': [vp, vp, i32, i32, i32, vp],
+    'mlc_avgpool_bwd': [vp, vp, i32, i32, i32, vp],
+    'mlc_softmax_ce': [vp] * 5 + [i32, i32, f32, f32, vp],
+    'mlc_colsum': [vp, vp, i32, i32, vp],
+    'mlc_nchw_to_nhwc': [vp, vp, i32, i32, i32, i32, vp],
+    'mlc_cast_f32_bf16': [vp, vp, i64, vp],
+    'mlc_sgd': [vp] * 5 + [i64, i64, i64, f32, f32, f32, i32, i32, vp],
+    'mlc_adam': [vp] * 6 + [i64, i64, i64, f32, f32, f32, f32, i32, vp],
+    'mlc_sqnorm': [vp, i64, vp, f32, vp],
+}
+
+
+def lib_path():
+    from mlcomp_amd.build import KERNEL_LIB
+    return KERNEL_LIB
+
+
+def load():
+    """Load (building first if absent) the kernel library."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        path = lib_path()
+        if not os.path.exists(path):
+            from mlcomp_amd.build import build_kernels
+            build_kernels()
+        lib = C.CDLL(path)
+        for name, args in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = C.c_int
+        _LIB = lib
+    return _LIB
+
+
+def available() -> bool:
+    return torch.cuda.is_available()
+
+
+def stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    if t is None:
+        return None
+    return C.c_void_p(t.data_ptr())
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f'{name} failed (rc={rc}); check shape constraints '
+                           f'(channels % 8 == 0) or HIP error')
+    return rc

@@ -1,0 +1,380 @@
+"""Functional NHWC ops of the native engine.
+
+Tensors on a GPU go to the hand-written HIP kernels (``csrc/kernels``); tensors on the
+CPU run the mathematically identical PyTorch reference below, which is what the CPU
+test-suite exercises (and what the GPU numerics tests compare the kernels against).
+There is no silent fallback for device tensors: a kernel that rejects a shape raises.
+
+Layout conventions
+  activations  NHWC bf16, contiguous ([N, H, W, C])
+  conv weight  [Co, KH, KW, Ci] (bf16 for compute; fp32 master/grad in the same order)
+  linear       weight [O, I] bf16, bias fp32
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+
+def _cuda(t):
+    return t is not None and t.is_cuda
+
+
+def conv_out_hw(H, W, KH, KW, stride, pad, dil):
+    Ho = (H + 2 * pad - dil * (KH - 1) - 1) // stride + 1
+    Wo = (W + 2 * pad - dil * (KW - 1) - 1) // stride + 1
+    return Ho, Wo
+
+
+# ---------------------------------------------------------------- conv
+def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, stride=1, pad=0, dil=1,
+               stats: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = conv(x, w) in NHWC; if ``stats`` given (see :func:`stat_buffers`: two
+    [NSTAT*Co] fp32 buffers), accumulates per-channel partial sums of y and y^2 into
+    them (the BN forward statistics, reduced over the NSTAT copies by bn_fwd_apply)."""
+    N, H, W, C = x.shape
+    Co, KH, KW, Ci = w.shape
+    assert Ci == C, (w.shape, x.shape)
+    Ho, Wo = conv_out_hw(H, W, KH, KW, stride, pad, dil)
+    if _cuda(x):
+        y = out if out is not None else torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.bfloat16)
+        s1, s2 = (stats if stats is not None else (None, None))
+        _lib.call('mlc_conv_fwd', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(s1), _lib.ptr(s2),
+                  N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo, _lib.stream())
+        return y
+    yf = F.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), None, stride, pad, dil)
+    if stats is not None:
+        stats[0][:Co].add_(yf.sum(dim=(0, 2, 3)))
+        stats[1][:Co].add_((yf * yf).sum(dim=(0, 2, 3)))
+    y = yf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=1, pad=0, dil=1) -> torch.Tensor:
+    N, H, W, C = x_shape
+    Co, KH, KW, Ci = w.shape
+    _, Ho, Wo, _ = dy.shape
+    if _cuda(dy):
+        dx = torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
+        _lib.call('mlc_conv_dgrad', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(dx), N, H, W, C, Co, KH, KW,
+                  stride, pad, dil, Ho, Wo, _lib.stream())
+        return dx
+    dxf = torch.nn.grad.conv2d_input((N, C, H, W), w.permute(0, 3, 1, 2).float(),
+                                     dy.permute(0, 3, 1, 2).float(), stride, pad, dil)
+    return dxf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+
+
+def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride=1, pad=0, dil=1,
+                 out: Optional[torch.Tensor] = None, accumulate=False) -> torch.Tensor:
+    """fp32 weight gradient in [Co, KH, KW, Ci] order (written into ``out`` if given)."""
+    Co, KH, KW, Ci = w_shape
+    N, H, W, C = x.shape
+    _, Ho, Wo, _ = dy.shape
+    if _cuda(dy):
+        dw = out if out is not None else torch.empty(Co, KH, KW, Ci, device=dy.device, dtype=torch.float32)
+        _lib.call('mlc_conv_wgrad', _lib.ptr(dy), _lib.ptr(x), _lib.ptr(dw), N, H, W, C, Co, KH, KW,
+                  stride, pad, dil, Ho, Wo, 0, int(accumulate), _lib.stream())
+        return dw
+    dwf = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).float(), (Co, Ci, KH, KW),
+                                      dy.permute(0, 3, 1, 2).float(), stride, pad, dil)
+    dwf = dwf.permute(0, 2, 3, 1)
+    if out is not None:
+        if accumulate:
+            out.add_(dwf.reshape(out.shape))
+        else:
+            out.copy_(dwf.reshape(out.shape))
+        return out
+    return dwf.contiguous()
+
+
+# ---------------------------------------------------------------- batch norm
+NSTAT = 32  # == mlc_bn_stat_copies(): partial-sum copies written by the conv epilogue
+
+
+def stat_buffers(C, device):
+    """Zeroed (sum, sumsq) buffers of NSTAT*C fp32 for conv2d_fwd(stats=...)."""
+    b = torch.zeros(2, NSTAT * C, device=device, dtype=torch.float32)
+    return b[0], b[1]
+
+
+def bn_fwd_apply(y, res, s1, s2, gamma, beta, save_mean, save_invstd, run_mean, run_var,
+                 eps=1e-5, momentum=0.1, relu=True, out=None, scale=None, shift=None):
+    """z = act(BN_train(y) [+ res]) given the conv epilogue's partial sums s1/s2
+    ([NSTAT*C] each).  Writes save_mean/save_invstd and updates running stats."""
+    rows = y.numel() // y.shape[-1]
+    C = y.shape[-1]
+    ncopy = s1.numel() // C
+    if _cuda(y):
+        z = out if out is not None else torch.empty_like(y)
+        if scale is None:
+            scale = torch.empty(2, C, device=y.device, dtype=torch.float32)
+            scale, shift = scale[0], scale[1]
+        _lib.call('mlc_bn_finalize', _lib.ptr(s1), _lib.ptr(s2), ncopy, _lib.ptr(gamma), _lib.ptr(beta),
+                  _lib.ptr(save_mean), _lib.ptr(save_invstd), _lib.ptr(scale), _lib.ptr(shift),
+                  _lib.ptr(run_mean), _lib.ptr(run_var), rows, C, float(eps), float(momentum),
+                  _lib.stream())
+        _lib.call('mlc_bn_fwd_apply', _lib.ptr(y), _lib.ptr(res), _lib.ptr(z), _lib.ptr(scale),
+                  _lib.ptr(shift), rows, C, int(relu), _lib.stream())
+        return z
+    s1t = s1.reshape(ncopy, C).sum(0)
+    s2t = s2.reshape(ncopy, C).sum(0)
+    mean = s1t / rows
+    var = (s2t / rows - mean * mean).clamp_min(0)
+    inv = torch.rsqrt(var + eps)
+    save_mean.copy_(mean)
+    save_invstd.copy_(inv)
+    if run_mean is not None:
+        unb = var * rows / max(rows - 1, 1)
+        run_mean.mul_(1 - momentum).add_(momentum * mean)
+        run_var.mul_(1 - momentum).add_(momentum * unb)
+    zf = (y.float() - mean) * (inv * gamma) + beta
+    if res is not None:
+        zf = zf + res.float()
+    if relu:
+        zf = zf.clamp_min(0)
+    z = zf.to(torch.bfloat16)
+    if out is not None:
+        out.copy_(z)
+        return out
+    return z
+
+
+def bn_bwd(dz, z, y, mean, invstd, gamma, want_dres=False, dgamma=None, dbeta=None, sums=None,
+           zero_sums=True):
+    """Backward of z = act(BN(y) [+res]).  ``z`` is the saved output (ReLU mask) or None
+    when there is no ReLU.  Returns (dy, dres or None); writes dgamma/dbeta (fp32).
+    ``sums`` (2*C fp32 scratch) must be zero on entry when ``zero_sums`` is False."""
+    rows = y.numel() // y.shape[-1]
+    C = y.shape[-1]
+    if _cuda(dz):
+        if sums is None:
+            sums = torch.zeros(2 * C, device=dz.device, dtype=torch.float32)
+        elif zero_sums:
+            sums.zero_()
+        _lib.call('mlc_bn_bwd_reduce', _lib.ptr(dz), _lib.ptr(z), _lib.ptr(y), _lib.ptr(mean),
+                  _lib.ptr(sums), rows, C, _lib.stream())
+        dy = torch.empty_like(y)
+        dres = torch.empty_like(y) if want_dres else None
+        _lib.call('mlc_bn_bwd_apply', _lib.ptr(dz), _lib.ptr(z), _lib.ptr(y), _lib.ptr(mean),
+                  _lib.ptr(invstd), _lib.ptr(gamma), _lib.ptr(sums), _lib.ptr(dy), _lib.ptr(dres),
+                  _lib.ptr(dgamma), _lib.ptr(dbeta), rows, C, _lib.stream())
+        return dy, dres
+    d = dz.float().reshape(rows, C)
+    if z is not None:
+        d = d * (z.reshape(rows, C).float() > 0)
+    yc = y.float().reshape(rows, C) - mean
+    S1 = d.sum(0)
+    S2 = (d * yc).sum(0)
+    if dgamma is not None:
+        dgamma.copy_(S2 * invstd)
+        dbeta.copy_(S1)
+    k1 = gamma * invstd
+    dyf = k1 * d - k1 * S1 / rows - k1 * invstd * invstd * S2 / rows * yc
+    dy = dyf.reshape(y.shape).to(torch.bfloat16)
+    dres = d.reshape(y.shape).to(torch.bfloat16) if want_dres else None
+    return dy, dres
+
+
+# ---------------------------------------------------------------- pooling
+def maxpool_fwd(x, k=3, s=2, p=1):
+    N, H, W, C = x.shape
+    Ho, Wo = conv_out_hw(H, W, k, k, s, p, 1)
+    if _cuda(x):
+        y = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.bfloat16)
+        idx = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.uint8)
+        _lib.call('mlc_maxpool_fwd', _lib.ptr(x), _lib.ptr(y), _lib.ptr(idx), N, H, W, C, Ho, Wo, k, s, p,
+                  _lib.stream())
+        return y, idx
+    xf = x.permute(0, 3, 1, 2).float()
+    yf, ind = F.max_pool2d(xf, k, s, p, return_indices=True)
+    return yf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous(), ind
+
+
+def maxpool_bwd(dy, idx, x_shape, k=3, s=2, p=1):
+    N, H, W, C = x_shape
+    _, Ho, Wo, _ = dy.shape
+    if _cuda(dy):
+        dx = torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
+        _lib.call('mlc_maxpool_bwd', _lib.ptr(dy), _lib.ptr(idx), _lib.ptr(dx), N, H, W, C, Ho, Wo, k, s,
+                  p, _lib.stream())
+        return dx
+    dyf = dy.permute(0, 3, 1, 2).float().reshape(N, C, -1)
+    dxf = torch.zeros(N, C, H * W).scatter_add_(2, idx.reshape(N, C, -1), dyf)
+    return dxf.reshape(N, C, H, W).permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+
+
+def avgpool_fwd(x):
+    N, H, W, C = x.shape
+    if _cuda(x):
+        y = torch.empty(N, C, device=x.device, dtype=torch.bfloat16)
+        _lib.call('mlc_avgpool_fwd', _lib.ptr(x), _lib.ptr(y), N, H * W, C, _lib.stream())
+        return y
+    return x.float().mean(dim=(1, 2)).to(torch.bfloat16)
+
+
+def avgpool_bwd(dy, x_shape):
+    N, H, W, C = x_shape
+    if _cuda(dy):
+        dx = torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
+        _lib.call('mlc_avgpool_bwd', _lib.ptr(dy), _lib.ptr(dx), N, H * W, C, _lib.stream())
+        return dx
+    return (dy.float()[:, None, None, :] / (H * W)).expand(N, H, W, C).to(torch.bfloat16).contiguous()
+
+
+# ---------------------------------------------------------------- linear
+def linear_fwd(x, w, bias=None):
+    """x [B, I] bf16, w [O, I] bf16 -> fp32 [B, O] (+bias)."""
+    B, I = x.shape
+    O = w.shape[0]
+    if _cuda(x):
+        out = torch.empty(B, O, device=x.device, dtype=torch.float32)
+        _lib.call('mlc_gemm_f32out', _lib.ptr(x), _lib.ptr(w), _lib.ptr(out), _lib.ptr(bias), B, O, I,
+                  I, I, O, 0, 1, 0, 0, 1, _lib.stream())
+        return out
+    out = x.float() @ w.float().t()
+    return out + bias if bias is not None else out
+
+
+def linear_dgrad(dout, w):
+    """dout [B, O] bf16, w [O, I] bf16 -> dx [B, I] bf16."""
+    B, O = dout.shape
+    I = w.shape[1]
+    if _cuda(dout):
+        dx = torch.empty(B, I, device=dout.device, dtype=torch.bfloat16)
+        _lib.call('mlc_gemm_bf16out', _lib.ptr(dout), _lib.ptr(w), _lib.ptr(dx), B, I, O, O, I, I, 0, 0,
+                  _lib.stream())
+        return dx
+    return (dout.float() @ w.float()).to(torch.bfloat16)
+
+
+def linear_wgrad(dout, x, out=None, accumulate=False):
+    """dW [O, I] fp32 = dout^T x."""
+    B, O = dout.shape
+    I = x.shape[1]
+    if _cuda(dout):
+        dw = out if out is not None else torch.empty(O, I, device=dout.device, dtype=torch.float32)
+        _lib.call('mlc_gemm_f32out', _lib.ptr(dout), _lib.ptr(x), _lib.ptr(dw), None, O, I, B, O, I, I,
+                  1, 0, 0, int(accumulate), 1, _lib.stream())
+        return dw
+    g = dout.float().t() @ x.float()
+    if out is not None:
+        if accumulate:
+            out.add_(g)
+        else:
+            out.copy_(g)
+        return out
+    return g
+
+
+def colsum(g, out):
+    R, Cc = g.shape
+    if _cuda(g):
+        _lib.call('mlc_colsum', _lib.ptr(g), _lib.ptr(out), R, Cc, _lib.stream())
+        return out
+    out.copy_(g.float().sum(0))
+    return out
+
+
+# ---------------------------------------------------------------- loss
+def softmax_ce(logits, labels, loss_sum, correct=None, scale=None, smoothing=0.0, want_grad=True):
+    """Fused softmax cross-entropy.  Accumulates the summed loss (and #correct) into
+    fp32 scalars; returns bf16 dlogits = (softmax - target) * scale (scale = 1/B)."""
+    B, V = logits.shape
+    scale = (1.0 / B) if scale is None else scale
+    if _cuda(logits):
+        dl = torch.empty(B, V, device=logits.device, dtype=torch.bfloat16) if want_grad else None
+        _lib.call('mlc_softmax_ce', _lib.ptr(logits), _lib.ptr(labels), _lib.ptr(dl), _lib.ptr(loss_sum),
+                  _lib.ptr(correct), B, V, float(scale), float(smoothing), _lib.stream())
+        return dl
+    lf = logits.float()
+    lse = torch.logsumexp(lf, 1)
+    nll = lse - lf.gather(1, labels[:, None])[:, 0]
+    sm = lse - lf.mean(1)
+    loss_sum.add_(((1 - smoothing) * nll + smoothing * sm).sum())
+    if correct is not None:
+        correct.add_((lf.argmax(1) == labels).float().sum())
+    if not want_grad:
+        return None
+    p = torch.softmax(lf, 1)
+    tgt = torch.full_like(p, smoothing / V)
+    tgt.scatter_add_(1, labels[:, None], torch.full((B, 1), 1 - smoothing, dtype=p.dtype))
+    return ((p - tgt) * scale).to(torch.bfloat16)
+
+
+# ---------------------------------------------------------------- layout helpers
+def nchw_to_nhwc(x, pad_to=None):
+    N, C, H, W = x.shape
+    Cp = pad_to or C
+    if _cuda(x) and x.dtype == torch.float32:
+        y = torch.empty(N, H, W, Cp, device=x.device, dtype=torch.bfloat16)
+        _lib.call('mlc_nchw_to_nhwc', _lib.ptr(x.contiguous()), _lib.ptr(y), N, C, H * W, Cp, _lib.stream())
+        return y
+    y = x.permute(0, 2, 3, 1).to(torch.bfloat16)
+    if Cp != C:
+        y = F.pad(y, (0, Cp - C))
+    return y.contiguous()
+
+
+# ---------------------------------------------------------------- optimizers
+def sgd_step(p, g, m, pbf, hyper, ndecay, nbf, momentum=0.9, dampening=0.0, wd=0.0,
+             nesterov=False, first=False):
+    n = p.numel()
+    if _cuda(p):
+        _lib.call('mlc_sgd', _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(pbf), _lib.ptr(hyper), n,
+                  ndecay, nbf, float(momentum), float(dampening), float(wd), int(nesterov), int(first),
+                  _lib.stream())
+        return
+    lr, gs = float(hyper[0]), float(hyper[1])
+    d = g * gs
+    wdv = torch.zeros_like(p)
+    wdv[:ndecay] = wd
+    d = d + wdv * p
+    if momentum:
+        if first:
+            m.copy_(d)
+        else:
+            m.mul_(momentum).add_(d, alpha=1 - dampening)
+        d = d + momentum * m if nesterov else m
+    p.sub_(lr * d)
+    if pbf is not None and nbf:
+        pbf[:nbf].copy_(p[:nbf].to(torch.bfloat16))
+
+
+def adam_step(p, g, m, v, pbf, hyper, ndecay, nbf, b1=0.9, b2=0.999, eps=1e-8, wd=0.0,
+              decoupled=True):
+    n = p.numel()
+    if _cuda(p):
+        _lib.call('mlc_adam', _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), _lib.ptr(pbf),
+                  _lib.ptr(hyper), n, ndecay, nbf, float(b1), float(b2), float(eps), float(wd),
+                  int(decoupled), _lib.stream())
+        return
+    lr, gs, bc1, bc2 = [float(h) for h in hyper[:4]]
+    d = g * gs
+    wdv = torch.zeros_like(p)
+    wdv[:ndecay] = wd
+    if not decoupled:
+        d = d + wdv * p
+    m.mul_(b1).add_((1 - b1) * d)
+    v.mul_(b2).add_((1 - b2) * d * d)
+    upd = (m / bc1) / ((v / bc2).sqrt() + eps)
+    if decoupled:
+        p.sub_(lr * wdv * p)
+    p.sub_(lr * upd)
+    if pbf is not None and nbf:
+        pbf[:nbf].copy_(p[:nbf].to(torch.bfloat16))
+
+
+def sqnorm(x, out, scale=1.0):
+    if _cuda(x):
+        _lib.call('mlc_sqnorm', _lib.ptr(x), x.numel(), _lib.ptr(out), float(scale), _lib.stream())
+        return out
+    out.add_(((x * scale) ** 2).sum())
+    return out

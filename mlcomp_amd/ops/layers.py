@@ -1,0 +1,251 @@
+"""Native layers: autograd Functions over the HIP kernels + arena-backed parameters.
+
+A native layer is a small Python object (not an ``nn.Module``) whose parameters are
+slots of a :class:`~mlcomp_amd.ops.arena.ParamArena`.  Its autograd Function writes
+parameter gradients *directly* into the arena's grad buffer (wgrad epilogues, BN
+dgamma/dbeta) and notifies the arena (``mark_ready``) so the gradient bucketer can
+launch the all-reduce of a completed bucket while backward continues.  Autograd only
+carries activation gradients; every Function takes the model's ``anchor`` tensor
+(requires_grad=True) so the graph is built even though the input image needs no grad.
+
+Per-step scratch that must start at zero (BN forward partial sums, BN backward sums,
+loss / accuracy accumulators) lives in one ``Workspace`` buffer cleared by a single
+memset at the start of the step.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import functional as Fn
+from .arena import ParamArena, Slot
+
+
+class Workspace:
+    """One zero-per-step fp32 buffer carved into named views."""
+
+    def __init__(self):
+        self._req: List[tuple] = []
+        self.buf = None
+        self.views = {}
+
+    def request(self, key, n):
+        self._req.append((key, int(n)))
+        return key
+
+    def finalize(self, device):
+        total = sum((n + 63) // 64 * 64 for _, n in self._req) or 64
+        self.buf = torch.zeros(total, device=device, dtype=torch.float32)
+        off = 0
+        for key, n in self._req:
+            self.views[key] = self.buf[off:off + n]
+            off += (n + 63) // 64 * 64
+
+    def __getitem__(self, key):
+        return self.views[key]
+
+    def zero(self):
+        self.buf.zero_()
+
+
+class NativeContext:
+    """Shared state of one native model: arena, workspace, anchor, train flag."""
+
+    def __init__(self):
+        self.arena = ParamArena()
+        self.ws = Workspace()
+        self.anchor = None
+        self.training = True
+        self.device = None
+
+    def finalize(self, device):
+        self.device = torch.device(device)
+        self.arena.finalize(device)
+        self.ws.finalize(device)
+        self.anchor = torch.zeros(1, device=device, requires_grad=True)
+
+
+# ---------------------------------------------------------------------------- conv+bn
+class ConvBN:
+    """conv (no bias) -> BatchNorm (train-mode batch stats) -> [+residual] -> [ReLU]."""
+
+    def __init__(self, ctx: NativeContext, name: str, conv: nn.Conv2d, bn: nn.BatchNorm2d,
+                 act: bool, cin_pad: Optional[int] = None):
+        assert conv.groups == 1, 'native ConvBN supports groups=1'
+        self.ctx = ctx
+        self.name = name
+        Co, Ci, KH, KW = conv.weight.shape
+        self.cin = Ci
+        self.cin_p = cin_pad or Ci
+        self.Co = Co
+        self.k = (KH, KW)
+        self.stride = conv.stride[0]
+        self.pad = conv.padding[0]
+        self.dil = conv.dilation[0]
+        self.act = act
+        self.eps = bn.eps
+        self.momentum = bn.momentum if bn.momentum is not None else 0.1
+        self.w = ctx.arena.weight(f'{name}.conv.weight', (Co, KH, KW, self.cin_p))
+        self.gamma = ctx.arena.vector(f'{name}.bn.weight', (Co,))
+        self.beta = ctx.arena.vector(f'{name}.bn.bias', (Co,))
+        self._src = (conv, bn)
+        self.k_s1 = ctx.ws.request(f'{name}.s1', Fn.NSTAT * Co)
+        self.k_s2 = ctx.ws.request(f'{name}.s2', Fn.NSTAT * Co)
+        self.k_bw = ctx.ws.request(f'{name}.bwd', 2 * Co)
+
+    def load_from_torch(self):
+        conv, bn = self._src
+        dev = self.ctx.device
+        w = conv.weight.detach().permute(0, 2, 3, 1).float()
+        if self.cin_p != self.cin:
+            w = torch.nn.functional.pad(w, (0, self.cin_p - self.cin))
+        self.w.master.copy_(w.to(dev))
+        self.gamma.master.copy_(bn.weight.detach().to(dev))
+        self.beta.master.copy_(bn.bias.detach().to(dev))
+        self.run_mean = bn.running_mean.detach().clone().float().to(dev)
+        self.run_var = bn.running_var.detach().clone().float().to(dev)
+        Co = self.Co
+        b = torch.zeros(4, Co, device=dev)
+        self.save_mean, self.save_invstd, self.scale, self.shift = b[0], b[1], b[2], b[3]
+
+    def export_to_torch(self):
+        conv, bn = self._src
+        w = self.w.master[..., :self.cin].permute(0, 3, 1, 2).contiguous()
+        conv.weight.data.copy_(w.to(conv.weight.device))
+        bn.weight.data.copy_(self.gamma.master.to(bn.weight.device))
+        bn.bias.data.copy_(self.beta.master.to(bn.bias.device))
+        bn.running_mean.copy_(self.run_mean.to(bn.running_mean.device))
+        bn.running_var.copy_(self.run_var.to(bn.running_var.device))
+
+    def __call__(self, x, res=None):
+        return _ConvBNFn.apply(x, res, self.ctx.anchor, self)
+
+
+class _ConvBNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, anchor, m: ConvBN):
+        ws = m.ctx.ws
+        s1, s2 = ws[m.k_s1], ws[m.k_s2]
+        y = Fn.conv2d_fwd(x, m.w.bf16, m.stride, m.pad, m.dil, stats=(s1, s2))
+        training = m.ctx.training
+        z = Fn.bn_fwd_apply(y, res, s1, s2, m.gamma.master, m.beta.master, m.save_mean,
+                            m.save_invstd, m.run_mean if training else None,
+                            m.run_var if training else None, m.eps, m.momentum, m.act,
+                            scale=m.scale, shift=m.shift)
+        ctx.m = m
+        ctx.has_res = res is not None
+        ctx.save_for_backward(x, y, z)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x, y, z = ctx.saved_tensors
+        m: ConvBN = ctx.m
+        arena = m.ctx.arena
+        dz = dz.contiguous()
+        dy, dres = Fn.bn_bwd(dz, z if m.act else None, y, m.save_mean, m.save_invstd,
+                             m.gamma.master, want_dres=ctx.has_res, dgamma=m.gamma.grad,
+                             dbeta=m.beta.grad, sums=m.ctx.ws[m.k_bw], zero_sums=False)
+        arena.mark_ready(m.gamma)
+        arena.mark_ready(m.beta)
+        Fn.conv2d_wgrad(dy, x, m.w.shape, m.stride, m.pad, m.dil, out=m.w.grad)
+        arena.mark_ready(m.w)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = Fn.conv2d_dgrad(dy, m.w.bf16, x.shape, m.stride, m.pad, m.dil)
+        return dx, dres, None, None
+
+
+# ---------------------------------------------------------------------------- pooling
+class MaxPool:
+    def __init__(self, k=3, s=2, p=1):
+        self.k, self.s, self.p = k, s, p
+
+    def __call__(self, x, anchor):
+        return _MaxPoolFn.apply(x, anchor, self)
+
+
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, m):
+        y, idx = Fn.maxpool_fwd(x, m.k, m.s, m.p)
+        ctx.m = m
+        ctx.xshape = tuple(x.shape)
+        ctx.save_for_backward(idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        m = ctx.m
+        return Fn.maxpool_bwd(dy.contiguous(), idx, ctx.xshape, m.k, m.s, m.p), None, None
+
+
+# ---------------------------------------------------------------------------- head
+class ClassifierHead:
+    """global avg-pool -> linear (+bias) -> fused softmax cross-entropy."""
+
+    def __init__(self, ctx: NativeContext, name: str, fc: nn.Linear, smoothing: float = 0.0):
+        self.ctx = ctx
+        self.name = name
+        self.fc = fc
+        self.O, self.I = fc.weight.shape
+        self.w = ctx.arena.weight(f'{name}.weight', (self.O, self.I))
+        self.b = ctx.arena.vector(f'{name}.bias', (self.O,))
+        self.smoothing = smoothing
+        self.k_loss = ctx.ws.request(f'{name}.loss', 1)
+        self.k_correct = ctx.ws.request(f'{name}.correct', 1)
+
+    def load_from_torch(self):
+        dev = self.ctx.device
+        self.w.master.copy_(self.fc.weight.detach().float().to(dev))
+        self.b.master.copy_(self.fc.bias.detach().float().to(dev))
+
+    def export_to_torch(self):
+        self.fc.weight.data.copy_(self.w.master.to(self.fc.weight.device))
+        self.fc.bias.data.copy_(self.b.master.to(self.fc.bias.device))
+
+    def loss_sum(self):
+        return self.ctx.ws[self.k_loss]
+
+    def correct(self):
+        return self.ctx.ws[self.k_correct]
+
+    def __call__(self, x, labels):
+        return _HeadFn.apply(x, labels, self.ctx.anchor, self)
+
+    def logits(self, x):
+        pooled = Fn.avgpool_fwd(x)
+        return Fn.linear_fwd(pooled, self.w.bf16, self.b.master)
+
+
+class _HeadFn(torch.autograd.Function):
+    """Returns the summed loss (fp32 [1]); backward assumes d(loss) = 1 and scales the
+    logits gradient by 1/B inside the CE kernel (mean reduction)."""
+
+    @staticmethod
+    def forward(ctx, x, labels, anchor, h: ClassifierHead):
+        pooled = Fn.avgpool_fwd(x)
+        logits = Fn.linear_fwd(pooled, h.w.bf16, h.b.master)
+        ws = h.ctx.ws
+        dl = Fn.softmax_ce(logits, labels, ws[h.k_loss], ws[h.k_correct],
+                           scale=1.0 / labels.shape[0], smoothing=h.smoothing)
+        ctx.h = h
+        ctx.xshape = tuple(x.shape)
+        ctx.save_for_backward(pooled, dl)
+        return ws[h.k_loss]
+
+    @staticmethod
+    def backward(ctx, dloss):
+        pooled, dl = ctx.saved_tensors
+        h: ClassifierHead = ctx.h
+        arena = h.ctx.arena
+        Fn.linear_wgrad(dl, pooled, out=h.w.grad)
+        arena.mark_ready(h.w)
+        Fn.colsum(dl, h.b.grad)
+        arena.mark_ready(h.b)
+        dpooled = Fn.linear_dgrad(dl, h.w.bf16)
+        dx = Fn.avgpool_bwd(dpooled, ctx.xshape)
+        return dx, None, None, None

@@ -1,0 +1,38 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs a real MI355X (HIP device)')
+    config.addinivalue_line('markers', 'slow: long-running test')
+
+
+def pytest_collection_modifyitems(config, items):
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if has_gpu:
+        return
+    skip = pytest.mark.skip(reason='no GPU')
+    for it in items:
+        if 'gpu' in it.keywords:
+            it.add_marker(skip)
+
+
+@pytest.fixture
+def mlc_root(tmp_path, monkeypatch):
+    """Fresh ROOT_FOLDER (data/models/tasks/db...) per test, like the reference's
+    per-xdist-worker ROOT_FOLDER (`mlcomp/__init__.py:10-13`)."""
+    monkeypatch.setenv('MLCOMP_ROOT', str(tmp_path / 'mlcomp'))
+    from mlcomp_amd import config as cfg
+    cfg.reset()
+    yield cfg.get()
+    cfg.reset()

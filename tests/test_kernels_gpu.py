@@ -1,0 +1,185 @@
+"""Numerics of the HIP kernels vs the fp32 PyTorch reference of the same op.
+
+Each test builds bf16 inputs once, runs the op on the GPU (HIP kernel from
+libmlcomp_kernels.so) and on the CPU (the reference path of mlcomp_amd.ops.functional,
+which is plain fp32 PyTorch math), and compares.
+"""
+import pytest
+import torch
+
+from mlcomp_amd.ops import functional as Fn
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+def rel_err(a, b):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _bf(*shape, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16)
+
+
+CONV_CASES = [
+    # N, H, W, C, Co, K, stride, pad
+    (2, 14, 14, 64, 64, 1, 1, 0),
+    (2, 14, 14, 64, 128, 3, 1, 1),
+    (2, 15, 13, 32, 64, 3, 2, 1),
+    (2, 16, 16, 64, 256, 1, 2, 0),
+    (2, 32, 32, 8, 64, 7, 2, 3),
+    (3, 9, 7, 136, 40, 3, 1, 1),
+    (1, 7, 7, 512, 2048, 1, 1, 0),
+    (2, 16, 16, 64, 128, 3, 2, 1),
+    (2, 15, 13, 128, 64, 3, 2, 1),
+    (3, 15, 15, 64, 128, 1, 2, 0),
+]
+
+
+@pytest.mark.parametrize('case', CONV_CASES)
+def test_conv_fwd_stats(case):
+    N, H, W, C, Co, K, s, p = case
+    x = _bf(N, H, W, C, seed=1)
+    w = _bf(Co, K, K, C, scale=(1.0 / (K * K * C)) ** 0.5, seed=2)
+    s1c, s2c = Fn.stat_buffers(Co, 'cpu')
+    ref = Fn.conv2d_fwd(x, w, s, p, stats=(s1c, s2c))
+    s1g, s2g = Fn.stat_buffers(Co, DEV)
+    out = Fn.conv2d_fwd(x.to(DEV), w.to(DEV), s, p, stats=(s1g, s2g))
+    torch.cuda.synchronize()
+    assert out.shape == ref.shape
+    assert rel_err(out, ref) < 1e-2
+    red = lambda t: t.reshape(Fn.NSTAT, Co).sum(0)
+    assert rel_err(red(s1g), red(s1c)) < 1e-2
+    assert rel_err(red(s2g), red(s2c)) < 1e-2
+
+
+def test_stat_copies_constant():
+    from mlcomp_amd.ops import _lib
+    assert _lib.load().mlc_bn_stat_copies() == Fn.NSTAT
+
+
+@pytest.mark.parametrize('case', [c for c in CONV_CASES if c[3] != 8])
+def test_conv_dgrad(case):
+    N, H, W, C, Co, K, s, p = case
+    x_shape = (N, H, W, C)
+    Ho, Wo = Fn.conv_out_hw(H, W, K, K, s, p, 1)
+    dy = _bf(N, Ho, Wo, Co, seed=3)
+    w = _bf(Co, K, K, C, scale=(1.0 / (K * K * C)) ** 0.5, seed=4)
+    ref = Fn.conv2d_dgrad(dy, w, x_shape, s, p)
+    out = Fn.conv2d_dgrad(dy.to(DEV), w.to(DEV), x_shape, s, p)
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize('case', CONV_CASES)
+def test_conv_wgrad(case):
+    N, H, W, C, Co, K, s, p = case
+    Ho, Wo = Fn.conv_out_hw(H, W, K, K, s, p, 1)
+    x = _bf(N, H, W, C, seed=5)
+    dy = _bf(N, Ho, Wo, Co, seed=6)
+    ref = Fn.conv2d_wgrad(dy, x, (Co, K, K, C), s, p)
+    out = Fn.conv2d_wgrad(dy.to(DEV), x.to(DEV), (Co, K, K, C), s, p)
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 5e-3
+
+
+@pytest.mark.parametrize('relu,res', [(True, True), (True, False), (False, False)])
+@pytest.mark.parametrize('C', [64, 256, 2048])
+def test_bn_fwd_bwd(relu, res, C):
+    rows_shape = (4, 5, 3, C)
+    y = _bf(*rows_shape, scale=2.0, seed=7) + 0.5
+    r = _bf(*rows_shape, seed=8) if res else None
+    gamma = torch.rand(C) + 0.5
+    beta = torch.randn(C) * 0.1
+    yf = y.float().reshape(-1, C)
+    s1, s2 = Fn.stat_buffers(C, 'cpu')
+    s1[:C], s2[:C] = yf.sum(0), (yf * yf).sum(0)
+
+    def run(dev):
+        t = lambda v: None if v is None else v.to(dev)
+        sm, si = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        z = Fn.bn_fwd_apply(t(y), t(r), t(s1), t(s2), t(gamma), t(beta), sm, si, rm, rv, relu=relu)
+        dz = _bf(*rows_shape, seed=9).to(dev)
+        dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        dy, dres = Fn.bn_bwd(dz, z if relu else None, t(y), sm, si, t(gamma), want_dres=res,
+                             dgamma=dg, dbeta=db)
+        return z, sm, si, rm, rv, dy, dres, dg, db
+
+    ref = run('cpu')
+    out = run(DEV)
+    torch.cuda.synchronize()
+    for a, b in zip(out, ref):
+        if b is None:
+            assert a is None
+            continue
+        assert rel_err(a, b) < 1e-2
+
+
+def test_maxpool():
+    x = _bf(2, 12, 12, 64, seed=10)
+    y_ref, idx_ref = Fn.maxpool_fwd(x)
+    y, idx = Fn.maxpool_fwd(x.to(DEV))
+    assert rel_err(y, y_ref) == 0.0
+    dy = _bf(*y.shape, seed=11)
+    dx_ref = Fn.maxpool_bwd(dy, idx_ref, x.shape)
+    dx = Fn.maxpool_bwd(dy.to(DEV), idx, x.shape)
+    torch.cuda.synchronize()
+    assert rel_err(dx, dx_ref) < 1e-2
+
+
+def test_avgpool():
+    x = _bf(3, 7, 7, 2048, seed=12)
+    assert rel_err(Fn.avgpool_fwd(x.to(DEV)), Fn.avgpool_fwd(x)) < 1e-2
+    dy = _bf(3, 2048, seed=13)
+    assert rel_err(Fn.avgpool_bwd(dy.to(DEV), x.shape), Fn.avgpool_bwd(dy, x.shape)) < 1e-2
+
+
+@pytest.mark.parametrize('B,I,O', [(16, 2048, 1000), (40, 64, 24)])
+def test_linear(B, I, O):
+    x = _bf(B, I, seed=14)
+    w = _bf(O, I, scale=I ** -0.5, seed=15)
+    b = torch.randn(O)
+    assert rel_err(Fn.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV)), Fn.linear_fwd(x, w, b)) < 1e-2
+    do = _bf(B, O, seed=16)
+    assert rel_err(Fn.linear_dgrad(do.to(DEV), w.to(DEV)), Fn.linear_dgrad(do, w)) < 1e-2
+    assert rel_err(Fn.linear_wgrad(do.to(DEV), x.to(DEV)), Fn.linear_wgrad(do, x)) < 1e-2
+
+
+def test_softmax_ce():
+    B, V = 32, 1000
+    logits = torch.randn(B, V) * 3
+    labels = torch.randint(0, V, (B,))
+    lc, cc = torch.zeros(1), torch.zeros(1)
+    dref = Fn.softmax_ce(logits, labels, lc, cc, smoothing=0.1)
+    lg, cg = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
+    d = Fn.softmax_ce(logits.to(DEV), labels.to(DEV), lg, cg, smoothing=0.1)
+    torch.cuda.synchronize()
+    assert abs(lg.item() - lc.item()) / lc.item() < 1e-4
+    assert cg.item() == cc.item()
+    assert rel_err(d, dref) < 1e-2
+
+
+def test_sgd_adam():
+    n, nd, nb = 4096, 3000, 3000
+    p = torch.randn(n)
+    g = torch.randn(n)
+    hyper = torch.tensor([0.1, 0.5, 0.9, 0.99])
+    for first in (True, False):
+        pc, mc = p.clone(), torch.randn(n)
+        pg, mg = pc.to(DEV), mc.to(DEV)
+        bfc, bfg = torch.zeros(n, dtype=torch.bfloat16), torch.zeros(n, dtype=torch.bfloat16, device=DEV)
+        Fn.sgd_step(pc, g, mc, bfc, hyper, nd, nb, 0.9, 0.0, 1e-4, True, first)
+        Fn.sgd_step(pg, g.to(DEV), mg, bfg, hyper.to(DEV), nd, nb, 0.9, 0.0, 1e-4, True, first)
+        torch.cuda.synchronize()
+        assert rel_err(pg, pc) < 1e-6 and rel_err(mg, mc) < 1e-6 and rel_err(bfg, bfc) < 1e-2
+    pc, mc, vc = p.clone(), torch.zeros(n), torch.zeros(n)
+    pg, mg, vg = pc.to(DEV), mc.to(DEV), vc.to(DEV)
+    Fn.adam_step(pc, g, mc, vc, None, hyper, nd, 0, wd=0.01)
+    Fn.adam_step(pg, g.to(DEV), mg, vg, None, hyper.to(DEV), nd, 0, wd=0.01)
+    torch.cuda.synchronize()
+    assert rel_err(pg, pc) < 1e-5

@@ -1,0 +1,44 @@
+"""The ctypes signatures in mlcomp_amd.ops._lib must match the C launchers exactly
+(parsed from csrc/kernels/*.hip), and every launcher must be exported by the built .so."""
+import glob
+import os
+import re
+
+from mlcomp_amd.ops import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_TYPES = {'int': 'i32', 'long': 'i64', 'float': 'f32'}
+
+
+def _parse():
+    decls = {}
+    for f in glob.glob(os.path.join(ROOT, 'csrc', 'kernels', '*.hip')):
+        src = open(f).read()
+        for m in re.finditer(r'MLC_EXPORT\s+int\s+(\w+)\s*\(([^)]*)\)', src):
+            args = [a.strip() for a in m.group(2).replace('\n', ' ').split(',') if a.strip()]
+            kinds = []
+            for a in args:
+                if '*' in a or a.startswith('hipStream_t'):
+                    kinds.append('vp')
+                else:
+                    kinds.append(_TYPES[a.split()[0]])
+            decls[m.group(1)] = kinds
+    return decls
+
+
+def test_signatures_match():
+    decls = _parse()
+    names = {_lib.vp: 'vp', _lib.i32: 'i32', _lib.i64: 'i64', _lib.f32: 'f32'}
+    assert set(decls) == set(_lib._SIGS), set(decls) ^ set(_lib._SIGS)
+    for name, kinds in decls.items():
+        got = [names[t] for t in _lib._SIGS[name]]
+        assert got == kinds, (name, got, kinds)
+
+
+def test_library_exports():
+    from mlcomp_amd.build import build_kernels
+    import ctypes
+    path = build_kernels()
+    lib = ctypes.CDLL(path)
+    for name in _lib._SIGS:
+        assert hasattr(lib, name), name

@@ -1,0 +1,54 @@
+"""CPU checks of the native op reference paths against autograd of plain PyTorch
+modules (the GPU kernels are in turn checked against these references)."""
+import torch
+import torch.nn.functional as F
+
+from mlcomp_amd.ops import functional as Fn
+
+
+def test_bn_reference_matches_autograd():
+    torch.manual_seed(0)
+    C = 16
+    y = (torch.randn(4, 5, 5, C) * 2).to(torch.bfloat16)
+    res = torch.randn(4, 5, 5, C).to(torch.bfloat16)
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C)
+    yf = y.float().reshape(-1, C)
+    s1, s2 = Fn.stat_buffers(C, 'cpu')
+    s1[:C], s2[:C] = yf.sum(0), (yf * yf).sum(0)
+    sm, si = torch.empty(C), torch.empty(C)
+    z = Fn.bn_fwd_apply(y, res, s1, s2, gamma, beta, sm, si, None, None, relu=True)
+    # autograd reference in NCHW
+    yt = y.float().permute(0, 3, 1, 2).requires_grad_()
+    g_t, b_t = gamma.clone().requires_grad_(), beta.clone().requires_grad_()
+    rt = res.float().permute(0, 3, 1, 2).requires_grad_()
+    zt = F.relu(F.batch_norm(yt, None, None, g_t, b_t, training=True) + rt)
+    assert (z.float() - zt.permute(0, 2, 3, 1)).abs().max() < 0.05
+    dz = torch.randn_like(z)
+    zt.backward(dz.float().permute(0, 3, 1, 2))
+    dg, db = torch.empty(C), torch.empty(C)
+    dy, dres = Fn.bn_bwd(dz, z, y, sm, si, gamma, want_dres=True, dgamma=dg, dbeta=db)
+    assert (dy.float() - yt.grad.permute(0, 2, 3, 1)).abs().max() < 0.05
+    assert (dres.float() - rt.grad.permute(0, 2, 3, 1)).abs().max() < 0.05
+    assert torch.allclose(dg, g_t.grad, atol=0.1, rtol=0.02)
+    assert torch.allclose(db, b_t.grad, atol=0.1, rtol=0.02)
+
+
+def test_conv_reference_shapes():
+    x = torch.randn(2, 9, 9, 8).to(torch.bfloat16)
+    w = torch.randn(16, 3, 3, 8).to(torch.bfloat16)
+    y = Fn.conv2d_fwd(x, w, 2, 1)
+    assert y.shape == (2, 5, 5, 16)
+    dx = Fn.conv2d_dgrad(torch.randn_like(y.float()).to(torch.bfloat16), w, x.shape, 2, 1)
+    assert dx.shape == x.shape
+    dw = Fn.conv2d_wgrad(y, x, w.shape, 2, 1)
+    assert dw.shape == w.shape and dw.dtype == torch.float32
+
+
+def test_maxpool_reference_matches_autograd():
+    x = torch.randn(2, 12, 12, 8).to(torch.bfloat16)
+    y, i = Fn.maxpool_fwd(x)
+    dy = torch.randn_like(y.float()).to(torch.bfloat16)
+    dx = Fn.maxpool_bwd(dy, i, x.shape)
+    xr = x.permute(0, 3, 1, 2).float().requires_grad_()
+    F.max_pool2d(xr, 3, 2, 1).backward(dy.permute(0, 3, 1, 2).float())
+    assert (dx.permute(0, 3, 1, 2).float() - xr.grad).abs().max() < 0.05
