@@ -80,7 +80,11 @@ bn_fwd_apply_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf
   }
 }
 
-// sums[0:C] += sum dU ; sums[C:2C] += sum dU*(y-mean)
+// Partial reductions for BN backward: copy k = block % NSTAT of sums[NSTAT][2][C]
+// receives  sum dU  and  sum dU*(y-mean)  of the block's rows (copies keep the
+// same-address atomic contention low: every address sees ~blocks/NSTAT adds).
+constexpr int NSTAT = 32;
+
 __global__ void __launch_bounds__(NT)
 bn_bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const bf16* __restrict__ y,
                      const float* __restrict__ mean, float* __restrict__ sums, long rows, int C) {
@@ -108,13 +112,14 @@ bn_bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, co
 #pragma unroll
     for (int j = 0; j < 8; ++j) { s1[j] += d[j]; s2[j] += d[j] * (yy[j] - mu[j]); }
   }
-  // combine threads of this block owning the same channel group (tid ≡ tid' mod G)
+  // combine threads of this block owning the same channel group (tid = tid' mod G)
   const int t = threadIdx.x;
 #pragma unroll
   for (int j = 0; j < 8; ++j) { red[0][t][j] = s1[j]; red[1][t][j] = s2[j]; }
   __syncthreads();
   const int lanes = NT < G ? NT : G;  // distinct groups present in this block
   const int base_cg = (int)(((long)blockIdx.x * NT) % G);
+  float* dst = sums + (size_t)(blockIdx.x % NSTAT) * 2 * C;
   if (t < lanes) {
     float a[8], b[8];
 #pragma unroll
@@ -126,43 +131,51 @@ bn_bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, co
     const int cgt = (base_cg + t) % G;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      atomicAdd(sums + cgt * 8 + j, a[j]);
-      atomicAdd(sums + C + cgt * 8 + j, b[j]);
+      atomicAdd(dst + cgt * 8 + j, a[j]);
+      atomicAdd(dst + C + cgt * 8 + j, b[j]);
     }
   }
 }
 
-// dy = gamma*invstd/M * (M*dU - S1 - (y-mean)*invstd^2 * S2);  dres = dU (optional)
-// also publishes dgamma = S2*invstd, dbeta = S1 (fp32, accumulated into dgamma/dbeta
-// if accumulate) from the threads with gtid < G.
+// per-channel: reduce the NSTAT copies, publish dgamma/dbeta and the three
+// coefficients of  dy = k1*dU + k2 + k3*(y-mean)  (coef[0:C]=k1, [C:2C]=k2, [2C:3C]=k3)
+__global__ void __launch_bounds__(NT)
+bn_bwd_finalize_kernel(const float* __restrict__ sums, const float* __restrict__ invstd,
+                       const float* __restrict__ gamma, float* __restrict__ coef,
+                       float* __restrict__ dgamma, float* __restrict__ dbeta, long rows, int C) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  float S1 = 0.f, S2 = 0.f;
+  for (int k = 0; k < NSTAT; ++k) {
+    S1 += sums[(size_t)k * 2 * C + c];
+    S2 += sums[(size_t)k * 2 * C + C + c];
+  }
+  const float invM = 1.f / (float)rows;
+  const float is = invstd[c];
+  const float k1 = gamma[c] * is;
+  coef[c] = k1;
+  coef[C + c] = -k1 * S1 * invM;
+  coef[2 * C + c] = -k1 * is * is * S2 * invM;
+  if (dgamma) { dgamma[c] = S2 * is; dbeta[c] = S1; }
+}
+
+// dy = k1*dU + k2 + k3*(y-mean);  dres = dU (optional)
 __global__ void __launch_bounds__(NT)
 bn_bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const bf16* __restrict__ y,
-                    const float* __restrict__ mean, const float* __restrict__ invstd,
-                    const float* __restrict__ gamma, const float* __restrict__ sums,
-                    bf16* __restrict__ dy, bf16* __restrict__ dres,
-                    float* __restrict__ dgamma, float* __restrict__ dbeta, long rows, int C) {
+                    const float* __restrict__ mean, const float* __restrict__ coef,
+                    bf16* __restrict__ dy, bf16* __restrict__ dres, long rows, int C) {
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
   const long stride = (long)gridDim.x * NT;
   const int cg = (int)(gtid % G);
   const int c0 = cg * 8;
-  const float invM = 1.f / (float)rows;
   float mu[8], k1[8], k2[8], k3[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float is = invstd[c0 + j];
-    const float S1 = sums[c0 + j], S2 = sums[C + c0 + j];
     mu[j] = mean[c0 + j];
-    k1[j] = gamma[c0 + j] * is;                       // * dU
-    k2[j] = -k1[j] * S1 * invM;                       // const
-    k3[j] = -k1[j] * is * is * S2 * invM;             // * (y-mean)
-  }
-  if (gtid < G && dgamma) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      dgamma[c0 + j] = sums[C + c0 + j] * invstd[c0 + j];
-      dbeta[c0 + j] = sums[c0 + j];
-    }
+    k1[j] = coef[c0 + j];
+    k2[j] = coef[C + c0 + j];
+    k3[j] = coef[2 * C + c0 + j];
   }
   const long total = rows * G;
   for (long i = gtid; i < total; i += stride) {
@@ -189,7 +202,7 @@ int grid_for(long rows, int C) {
   // threads must be a multiple of G: blocks*256 % G == 0 always holds for G | 256;
   // for G > 256 (C > 2048) make the block count a multiple of G/256.
   long blocks = (total + NT * 4 - 1) / (NT * 4);   // ~4 chunks per thread
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
   if (G > NT) {
     const long m = G / NT;
@@ -225,7 +238,7 @@ MLC_EXPORT int mlc_bn_fwd_apply(const bf16* y, const bf16* res, bf16* z, const f
   return hipGetLastError();
 }
 
-// sums must hold 2*C floats and be zeroed by the caller (or accumulate)
+// sums must hold NSTAT*2*C floats, zeroed by the caller
 MLC_EXPORT int mlc_bn_bwd_reduce(const bf16* dz, const bf16* z, const bf16* y, const float* mean,
                                  float* sums, long rows, int C, hipStream_t st) {
   if (!shape_ok(C)) return -1;
@@ -234,12 +247,20 @@ MLC_EXPORT int mlc_bn_bwd_reduce(const bf16* dz, const bf16* z, const bf16* y, c
   return hipGetLastError();
 }
 
+// coef must hold 3*C floats
+MLC_EXPORT int mlc_bn_bwd_finalize(const float* sums, const float* invstd, const float* gamma,
+                                   float* coef, float* dgamma, float* dbeta, long rows, int C,
+                                   hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, st, sums, invstd,
+                     gamma, coef, dgamma, dbeta, rows, C);
+  return hipGetLastError();
+}
+
 MLC_EXPORT int mlc_bn_bwd_apply(const bf16* dz, const bf16* z, const bf16* y, const float* mean,
-                                const float* invstd, const float* gamma, const float* sums,
-                                bf16* dy, bf16* dres, float* dgamma, float* dbeta, long rows,
-                                int C, hipStream_t st) {
+                                const float* coef, bf16* dy, bf16* dres, long rows, int C,
+                                hipStream_t st) {
   if (!shape_ok(C)) return -1;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(rows, C)), dim3(NT), 0, st, dz, z, y,
-                     mean, invstd, gamma, sums, dy, dres, dgamma, dbeta, rows, C);
+                     mean, coef, dy, dres, rows, C);
   return hipGetLastError();
 }

@@ -9,15 +9,18 @@
 // either K-contiguous ("KC": tile stored [mn][k], read with ds_read_b128) or
 // MN-contiguous ("MC": tile stored [k][mn], read transposed with ds_read_b64_tr_b16).
 //
-// Block: 256 threads = 4 waves (2x2), tile 128x128x64, each wave 64x64 = 2x2 MFMA
-// 32x32 tiles.  Register-staged double-buffered LDS (64 KiB), one barrier per K-tile,
-// XOR-swizzled LDS images (conflict-free b128 row reads and tr_b16 column reads),
-// bijective XCD remap + grouped tile order for L2 reuse.
+// Block: 256 threads = 4 waves, each wave owns a 64x64 output sub-tile (2x2 MFMA
+// 32x32 tiles); block tile BMxBN in {128x128, 256x64, 64x256} so narrow layers (64
+// channels) do not waste half the MFMA work.  K-step 64, register-staged
+// double-buffered LDS, one barrier per K-tile, XOR-swizzled LDS images
+// (conflict-free b128 row reads and tr_b16 column reads), bijective XCD remap +
+// grouped tile order for L2 reuse.  All index decompositions use precomputed
+// multiply-shift division (FastDiv) instead of runtime integer division.
 //
 // Strided dgrad: output rows are ordered by stride-parity class (all pixels with
-// hi%S==ph, wi%S==pw together) so a 128-row block belongs to ONE class, and every
-// K-tile (one filter tap when Co%64==0) whose tap cannot reach that class is skipped:
-// no MFMA work is spent on the structurally-zero taps of a stride-2 transpose conv.
+// hi%S==ph, wi%S==pw together) so a block belongs to ONE class, and every K-tile (one
+// filter tap when Co%64==0) whose tap cannot reach that class is skipped: no MFMA
+// work is spent on the structurally-zero taps of a stride-2 transpose conv.
 //
 // Epilogues: bf16 store through an LDS-staged 16 B/lane write (+ fused per-channel BN
 // sum / sum-of-squares, spread over NSTAT copies to avoid same-address atomic
@@ -26,32 +29,50 @@
 
 namespace igemm {
 
-constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
-constexpr int TILE_BYTES = BM * BK * 2;           // 16 KiB per operand per stage
-constexpr int LDS_BYTES = 4 * TILE_BYTES;         // A,B x 2 stages
+constexpr int BK = 64, NTHR = 256;
 constexpr int NSTAT = 32;                          // BN-stat partial copies
 
+// ------------------------------------------------------------------ fast division
+struct FastDiv {
+  unsigned d, mul, sh;
+  __host__ __device__ FastDiv() : d(1), mul(0), sh(0) {}
+  __host__ explicit FastDiv(unsigned dd) : d(dd) {
+    sh = 0;
+    while ((1u << sh) < d) ++sh;
+    mul = (unsigned)((((unsigned long long)1 << 32) * ((1ull << sh) - d)) / d + 1);
+  }
+  __device__ __forceinline__ unsigned div(unsigned n) const { return (__umulhi(n, mul) + n) >> sh; }
+  __device__ __forceinline__ void divmod(unsigned n, unsigned& q, unsigned& r) const {
+    q = div(n); r = n - q * d;
+  }
+};
+
 // ---------------------------------------------------------------- LDS images
-// KC image: [128 rows][64 k] bf16, 128 B rows, 16 B chunk c of row r stored at
+// KC image: [rows][64 k] bf16, 128 B rows, 16 B chunk c of row r stored at
 // chunk c ^ ((r>>1)&7): the 16-lane groups of ds_read_b128 hit 16 distinct slots.
 __device__ __forceinline__ int kc_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
-// MC image: [64 k][128 mn] bf16, 256 B rows, chunk c of row k stored at c ^ ((k&3)<<2):
-// each 32-lane half of a tr_b16 read covers 16 distinct slots.
-__device__ __forceinline__ int mc_off(int k, int c) { return k * 256 + ((c ^ ((k & 3) << 2)) << 4); }
+// MC image: [64 k][R mn] bf16 (R*2-byte rows); each 32-lane half of a tr_b16 read
+// (4 k-rows x 64 B) covers 16 distinct 16 B slots of the 256 B bank row.
+template <int R>
+__device__ __forceinline__ int mc_off(int k, int c) {
+  if (R == 64) return k * 128 + ((c ^ (((k >> 1) & 1) << 2)) << 4);
+  return k * (R * 2) + ((c ^ ((k & 3) << 2)) << 4);
+}
 
-template <bool KC>
-__device__ __forceinline__ void store_stage(char* lds, int tid, const uint4 (&v)[4]) {
+// tile of R rows (KC) / R cols (MC): NCH = R/32 chunks of 16 B per thread
+template <bool KC, int R>
+__device__ __forceinline__ void store_stage(char* lds, int tid, const uint4 (&v)[R / 32]) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < R / 32; ++i) {
     int off;
     if (KC) off = kc_off((tid >> 3) + 32 * i, tid & 7);
-    else off = mc_off((tid >> 4) + 16 * i, tid & 15);
+    else off = mc_off<R>(tid / (R / 8) + (NTHR / (R / 8)) * i, tid % (R / 8));
     *reinterpret_cast<uint4*>(lds + off) = v[i];
   }
 }
 
 // fragment of a 32-row (KC) / 32-col (MC) sub-tile for k-step s (16 deep)
-template <bool KC>
+template <bool KC, int R>
 __device__ __forceinline__ bf16x8 read_frag(const char* lds, int base, int s, int lane) {
   if (KC) {
     const int r = base + (lane & 31), c = 2 * s + (lane >> 5);
@@ -60,8 +81,8 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int base, int s, in
     const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
     const int m0 = base + 16 * (g & 1), k0 = 16 * s + 8 * (g >> 1);
     const int col = m0 + 4 * p;
-    const int a0 = mc_off(k0 + q, col >> 3) + (col & 7) * 2;
-    const int a1 = mc_off(k0 + 4 + q, col >> 3) + (col & 7) * 2;
+    const int a0 = mc_off<R>(k0 + q, col >> 3) + (col & 7) * 2;
+    const int a1 = mc_off<R>(k0 + 4 + q, col >> 3) + (col & 7) * 2;
     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(lds + a0));
     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(lds + a1));
     typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -75,218 +96,245 @@ __device__ __forceinline__ uint4 zero4() { return make_uint4(0, 0, 0, 0); }
 
 // Default K-tile iteration: every tile in [b, e).
 struct AllTiles {
-  __device__ int next(int kt, int) const { return kt; }
+  template <class S>
+  __device__ int next(const S&, int kt, int) const { return kt; }
 };
 
-// ---------------------------------------------------------------- loaders
-// A KC loader fills rows = m (or n) of the tile, 8 k per chunk: thread t owns rows
-// (t>>3)+32i, chunk t&7.  An MC loader fills k-rows (t>>4)+16i, chunk (8 mn) t&15.
-
-// plain row-major [rows][ld] matrix read K-contiguous
-struct MatKC : AllTiles {
-  static constexpr bool KC = true;
-  const bf16* p; int ld, rows, K;
-  int r_[4];
-  __device__ void init(int m0, int tid) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r_[i] = m0 + (tid >> 3) + 32 * i;
-  }
-  __device__ void load(int k0, int tid, uint4 (&v)[4]) const {
-    const int k = k0 + (tid & 7) * 8;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      v[i] = (r_[i] < rows && k < K) ? ld16(p + (size_t)r_[i] * ld + k) : zero4();
-  }
-};
-
-// plain row-major [K][ld] matrix whose rows are the reduction axis (MN-contiguous)
-struct MatMC : AllTiles {
-  static constexpr bool KC = false;
-  const bf16* p; int ld, K, cols;
-  int c_;
-  __device__ void init(int n0, int tid) { c_ = n0 + (tid & 15) * 8; }
-  __device__ void load(int k0, int tid, uint4 (&v)[4]) const {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = k0 + (tid >> 4) + 16 * i;
-      v[i] = (k < K && c_ < cols) ? ld16(p + (size_t)k * ld + c_) : zero4();
-    }
-  }
-};
-
+// ---------------------------------------------------------------- geometry
 struct ConvGeom {
   int N, H, W, C;      // input NHWC
   int Ho, Wo, Co;      // output
   int KH, KW, stride, pad, dil;
+  FastDiv fWo, fHo, fW, fH, fC, fCo, fKW;
 };
 
-// decompose a reduction index k = ((r*KW)+s)*CC + c ; if CC % BK == 0 a whole K-tile
-// shares one tap, so only the (wave-uniform) tile base needs the divisions.
-__device__ __forceinline__ void tap_of(int k, int k0, int CC, int KW, int& r, int& s, int& c) {
-  if (CC % BK == 0) {
-    const int rs = k0 / CC;
-    c = (k0 - rs * CC) + (k - k0);
-    s = rs % KW; r = rs / KW;
+// decompose k = ((r*KW)+s)*CC + c; if CC % BK == 0 a whole K-tile shares one tap, so
+// only the (wave-uniform) tile base is decomposed.
+__device__ __forceinline__ void tap_of(int k, int k0, const FastDiv& fCC, const FastDiv& fKW,
+                                       int& r, int& s, int& c) {
+  unsigned rs, cc, rr, ss;
+  if (fCC.d % BK == 0) {
+    fCC.divmod((unsigned)k0, rs, cc);
+    c = (int)cc + (k - k0);
   } else {
-    c = k % CC; const int rs = k / CC; s = rs % KW; r = rs / KW;
+    fCC.divmod((unsigned)k, rs, cc);
+    c = (int)cc;
   }
+  fKW.divmod(rs, rr, ss);
+  r = (int)rr; s = (int)ss;
 }
 
+// ---------------------------------------------------------------- loaders
+// KC loader of R rows: thread t owns rows (t>>3)+32i, chunk t&7 (8 k per chunk).
+// MC loader of R cols: thread t owns chunk t%(R/8) (8 mn), k-rows t/(R/8) + (256/(R/8))i.
+
+template <int R>
+struct MatKC : AllTiles {
+  static constexpr bool KC = true;
+  const bf16* p; int ld, rows, K;
+  struct St { int r[R / 32]; };
+  __device__ void init(St& st, int m0, int tid) const {
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) st.r[i] = m0 + (tid >> 3) + 32 * i;
+  }
+  __device__ void load(const St& st, int k0, int tid, uint4 (&v)[R / 32]) const {
+    const int k = k0 + (tid & 7) * 8;
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i)
+      v[i] = (st.r[i] < rows && k < K) ? ld16(p + (size_t)st.r[i] * ld + k) : zero4();
+  }
+};
+
+template <int R>
+struct MatMC : AllTiles {
+  static constexpr bool KC = false;
+  const bf16* p; int ld, K, cols;
+  struct St { int c; };
+  __device__ void init(St& st, int n0, int tid) const { st.c = n0 + (tid % (R / 8)) * 8; }
+  __device__ void load(const St& st, int k0, int tid, uint4 (&v)[R / 32]) const {
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) {
+      const int k = k0 + tid / (R / 8) + (NTHR / (R / 8)) * i;
+      v[i] = (k < K && st.c < cols) ? ld16(p + (size_t)k * ld + st.c) : zero4();
+    }
+  }
+};
+
 // conv fwd A operand: rows = output pixels, k = (r, s, ci) with ci fastest (C % 8 == 0)
+template <int R>
 struct ConvFwdA : AllTiles {
   static constexpr bool KC = true;
   const bf16* x; ConvGeom g; int M, K;
-  int hb_[4], wb_[4]; int nb_[4];   // per-row base input coords, nb_ = -1 if row >= M
-  __device__ void init(int m0, int tid) {
+  struct St { int hb[R / 32], wb[R / 32], nb[R / 32]; };  // per-row base input coords, nb=-1 if row >= M
+  __device__ void init(St& st, int m0, int tid) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < R / 32; ++i) {
+      // branch-free: a conditional store into st.* is sunk into a dynamic-index store
+      // by the compiler, which moves the whole array to scratch
       const int m = m0 + (tid >> 3) + 32 * i;
-      if (m < M) {
-        const int wo = m % g.Wo, t = m / g.Wo, ho = t % g.Ho, n = t / g.Ho;
-        hb_[i] = ho * g.stride - g.pad; wb_[i] = wo * g.stride - g.pad; nb_[i] = n;
-      } else { nb_[i] = -1; hb_[i] = 0; wb_[i] = 0; }
+      const bool ok = m < M;
+      unsigned t, wo, n, ho;
+      g.fWo.divmod((unsigned)(ok ? m : 0), t, wo);
+      g.fHo.divmod(t, n, ho);
+      st.hb[i] = (int)ho * g.stride - g.pad;
+      st.wb[i] = (int)wo * g.stride - g.pad;
+      st.nb[i] = ok ? (int)n : -1;
     }
   }
-  __device__ void load(int k0, int tid, uint4 (&v)[4]) const {
+  __device__ void load(const St& st, int k0, int tid, uint4 (&v)[R / 32]) const {
     const int k = k0 + (tid & 7) * 8;
     int r, s, ci;
-    tap_of(k, k0, g.C, g.KW, r, s, ci);
+    tap_of(k, k0, g.fC, g.fKW, r, s, ci);
     const bool kv = k < K;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int hi = hb_[i] + r * g.dil, wi = wb_[i] + s * g.dil;
-      const bool ok = kv && nb_[i] >= 0 && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-      v[i] = ok ? ld16(x + (((size_t)nb_[i] * g.H + hi) * g.W + wi) * g.C + ci) : zero4();
+    for (int i = 0; i < R / 32; ++i) {
+      const int hi = st.hb[i] + r * g.dil, wi = st.wb[i] + s * g.dil;
+      const bool ok = kv && st.nb[i] >= 0 && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+      v[i] = ok ? ld16(x + (((size_t)st.nb[i] * g.H + hi) * g.W + wi) * g.C + ci) : zero4();
     }
   }
 };
 
-// Row order of a dgrad output: for stride 1 the natural (n, hi, wi) order; for stride
-// S > 1 parity-class-major: class c = ph*S + pw holds pixels hi = i*S+ph, wi = j*S+pw.
+// Row order of a dgrad output: for stride 1 the natural (n, hi, wi) order; for stride 2
+// parity-class-major: class c = ph*2 + pw holds pixels hi = 2i+ph, wi = 2j+pw.
 struct DgradRows {
   int N, H, W, S;
+  int nclass;            // parity classes with at least one contributing filter tap
+  int base[4];           // start row of each listed class (INT_MAX when unused)
+  int cid[4];            // class id (ph*2+pw) of each listed class
+  FastDiv fWc[4], fHc[4];
+  FastDiv fW, fH;
   __device__ __forceinline__ void decode(int m, int& n, int& hi, int& wi, int& cls) const {
+    unsigned t, q, rr;
     if (S == 1) {
-      wi = m % W; const int t = m / W; hi = t % H; n = t / H; cls = 0;
+      fW.divmod((unsigned)m, t, rr); wi = (int)rr;
+      fH.divmod(t, q, rr); hi = (int)rr; n = (int)q; cls = 0;
       return;
     }
-    int base = 0;
-    for (int ph = 0; ph < S; ++ph) {
-      const int Hc = (H - ph + S - 1) / S;
-      for (int pw = 0; pw < S; ++pw) {
-        const int Wc = (W - pw + S - 1) / S;
-        const int sz = N * Hc * Wc;
-        if (m < base + sz) {
-          const int l = m - base;
-          const int j = l % Wc, t = l / Wc, i = t % Hc;
-          n = t / Hc; hi = i * S + ph; wi = j * S + pw; cls = ph * S + pw;
-          return;
-        }
-        base += sz;
-      }
-    }
-    n = N; hi = 0; wi = 0; cls = -1;
+    const int k = (m >= base[1]) + (m >= base[2]) + (m >= base[3]);
+    // explicit selects: a runtime index into these arrays would force them to scratch
+    const int b = k == 0 ? base[0] : k == 1 ? base[1] : k == 2 ? base[2] : base[3];
+    const int c = k == 0 ? cid[0] : k == 1 ? cid[1] : k == 2 ? cid[2] : cid[3];
+    const FastDiv fw = k == 0 ? fWc[0] : k == 1 ? fWc[1] : k == 2 ? fWc[2] : fWc[3];
+    const FastDiv fh = k == 0 ? fHc[0] : k == 1 ? fHc[1] : k == 2 ? fHc[2] : fHc[3];
+    const unsigned l = (unsigned)(m - b);
+    fw.divmod(l, t, rr);
+    const int j = (int)rr;
+    fh.divmod(t, q, rr);
+    n = (int)q; hi = 2 * (int)rr + (c >> 1); wi = 2 * j + (c & 1); cls = c;
   }
 };
 
-// conv dgrad A operand: rows = input pixels q=(n,hi,wi) in DgradRows order,
-// k = (r, s, co), co fastest
+// conv dgrad A operand: rows = input pixels (DgradRows order), k = (r, s, co), co fastest
+template <int R>
 struct ConvDgradA {
   static constexpr bool KC = true;
   const bf16* dy; ConvGeom g; int M, K; DgradRows rows;
-  int h_[4], w_[4], n_[4];
-  int cls_;   // parity class shared by every row of the block, or -1 (mixed)
-  __device__ void init(int m0, int tid) {
+  // per-row coords; cls: parity class shared by every row of the block, or -1
+  struct St { int h[R / 32], w[R / 32], n[R / 32]; int cls; };
+  __device__ void init(St& st, int m0, int tid) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < R / 32; ++i) {
       const int m = m0 + (tid >> 3) + 32 * i;
-      if (m < M) {
-        int n, hi, wi, c;
-        rows.decode(m, n, hi, wi, c);
-        h_[i] = hi + g.pad; w_[i] = wi + g.pad; n_[i] = n;
-      } else { n_[i] = -1; h_[i] = 0; w_[i] = 0; }
+      const bool ok = m < M;
+      int n, hi, wi, c;
+      rows.decode(ok ? m : 0, n, hi, wi, c);
+      st.h[i] = hi + g.pad;
+      st.w[i] = wi + g.pad;
+      st.n[i] = ok ? n : -1;
     }
-    cls_ = -1;
-    if (g.stride > 1 && g.Co % BK == 0) {
+    st.cls = -1;
+    if (g.stride == 2 && g.Co % BK == 0) {
       int n, hi, wi, c0, c1;
       rows.decode(m0, n, hi, wi, c0);
-      rows.decode(min(m0 + BM, M) - 1, n, hi, wi, c1);
-      if (c0 == c1) cls_ = c0;
+      rows.decode(min(m0 + R, M) - 1, n, hi, wi, c1);
+      if (c0 == c1) st.cls = c0;
     }
   }
   // first K-tile >= kt (and < e) whose filter tap can reach this block's class
-  __device__ int next(int kt, int e) const {
-    if (cls_ < 0) return kt;
-    const int S = g.stride, ph = cls_ / S, pw = cls_ % S;
+  __device__ int next(const St& st, int kt, int e) const {
+    if (st.cls < 0) return kt;
+    const int ph = st.cls >> 1, pw = st.cls & 1;
     for (; kt < e; ++kt) {
-      const int rs = (kt * BK) / g.Co, s = rs % g.KW, r = rs / g.KW;
-      const int a = ph + g.pad - r * g.dil, b = pw + g.pad - s * g.dil;
-      if (((a % S) + S) % S == 0 && ((b % S) + S) % S == 0) break;
+      unsigned rs, rem, r, s;
+      g.fCo.divmod((unsigned)(kt * BK), rs, rem);
+      g.fKW.divmod(rs, r, s);
+      if ((((ph + g.pad - (int)r * g.dil) & 1) == 0) && (((pw + g.pad - (int)s * g.dil) & 1) == 0)) break;
     }
     return kt;
   }
-  __device__ void load(int k0, int tid, uint4 (&v)[4]) const {
+  __device__ void load(const St& st, int k0, int tid, uint4 (&v)[R / 32]) const {
     const int k = k0 + (tid & 7) * 8;
     int r, s, co;
-    tap_of(k, k0, g.Co, g.KW, r, s, co);
+    tap_of(k, k0, g.fCo, g.fKW, r, s, co);
     const bool kv = k < K;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int th = h_[i] - r * g.dil, tw = w_[i] - s * g.dil;
-      bool ok = kv && n_[i] >= 0 && th >= 0 && tw >= 0;
+    for (int i = 0; i < R / 32; ++i) {
+      const int th = st.h[i] - r * g.dil, tw = st.w[i] - s * g.dil;
+      bool ok = kv && st.n[i] >= 0 && th >= 0 && tw >= 0;
       int ho = th, wo = tw;
-      if (g.stride != 1) {
+      if (g.stride == 2) {
+        ok = ok && ((th & 1) == 0) && ((tw & 1) == 0);
+        ho = th >> 1; wo = tw >> 1;
+      } else if (g.stride != 1) {
         ok = ok && (th % g.stride == 0) && (tw % g.stride == 0);
         ho = th / g.stride; wo = tw / g.stride;
       }
       ok = ok && ho < g.Ho && wo < g.Wo;
-      v[i] = ok ? ld16(dy + (((size_t)n_[i] * g.Ho + ho) * g.Wo + wo) * g.Co + co) : zero4();
+      v[i] = ok ? ld16(dy + (((size_t)st.n[i] * g.Ho + ho) * g.Wo + wo) * g.Co + co) : zero4();
     }
   }
 };
 
 // conv dgrad B operand: k = (r, s, co) rows, cols = ci; W stored [co][r][s][ci]
+template <int R>
 struct ConvDgradB : AllTiles {
   static constexpr bool KC = false;
   const bf16* w; ConvGeom g; int K;
-  int c_;
-  __device__ void init(int n0, int tid) { c_ = n0 + (tid & 15) * 8; }
-  __device__ void load(int k0, int tid, uint4 (&v)[4]) const {
+  struct St { int c; };
+  __device__ void init(St& st, int n0, int tid) const { st.c = n0 + (tid % (R / 8)) * 8; }
+  __device__ void load(const St& st, int k0, int tid, uint4 (&v)[R / 32]) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = k0 + (tid >> 4) + 16 * i;
+    for (int i = 0; i < R / 32; ++i) {
+      const int k = k0 + tid / (R / 8) + (NTHR / (R / 8)) * i;
       int r, s, co;
-      tap_of(k, k0, g.Co, g.KW, r, s, co);
-      v[i] = (k < K && c_ < g.C) ? ld16(w + (((size_t)co * g.KH + r) * g.KW + s) * g.C + c_) : zero4();
+      tap_of(k, k0, g.fCo, g.fKW, r, s, co);
+      v[i] = (k < K && st.c < g.C) ? ld16(w + (((size_t)co * g.KH + r) * g.KW + s) * g.C + st.c) : zero4();
     }
   }
 };
 
 // conv wgrad B operand: k = output pixel p rows, cols = kk = (r, s, ci)
+template <int R>
 struct ConvWgradB : AllTiles {
   static constexpr bool KC = false;
   const bf16* x; ConvGeom g; int P, KK;
-  int r_, s_, ci_; bool cv_;
-  __device__ void init(int n0, int tid) {
-    const int kk = n0 + (tid & 15) * 8;
-    cv_ = kk < KK;
-    ci_ = kk % g.C; const int rs = kk / g.C; s_ = rs % g.KW; r_ = rs / g.KW;
+  struct St { int r, s, ci; bool cv; };
+  __device__ void init(St& st, int n0, int tid) const {
+    const int kk = n0 + (tid % (R / 8)) * 8;
+    st.cv = kk < KK;
+    unsigned rs, ci, r, s;
+    g.fC.divmod((unsigned)kk, rs, ci);
+    g.fKW.divmod(rs, r, s);
+    st.ci = (int)ci; st.r = (int)r; st.s = (int)s;
   }
-  __device__ void load(int k0, int tid, uint4 (&v)[4]) const {
+  __device__ void load(const St& st, int k0, int tid, uint4 (&v)[R / 32]) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = k0 + (tid >> 4) + 16 * i;
-      const int wo = p % g.Wo, t = p / g.Wo, ho = t % g.Ho, n = t / g.Ho;
-      const int hi = ho * g.stride - g.pad + r_ * g.dil, wi = wo * g.stride - g.pad + s_ * g.dil;
-      const bool ok = cv_ && p < P && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-      v[i] = ok ? ld16(x + (((size_t)n * g.H + hi) * g.W + wi) * g.C + ci_) : zero4();
+    for (int i = 0; i < R / 32; ++i) {
+      const int p = k0 + tid / (R / 8) + (NTHR / (R / 8)) * i;
+      unsigned t, wo, n, ho;
+      g.fWo.divmod((unsigned)p, t, wo);
+      g.fHo.divmod(t, n, ho);
+      const int hi = (int)ho * g.stride - g.pad + st.r * g.dil, wi = (int)wo * g.stride - g.pad + st.s * g.dil;
+      const bool ok = st.cv && p < P && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+      v[i] = ok ? ld16(x + (((size_t)n * g.H + hi) * g.W + wi) * g.C + st.ci) : zero4();
     }
   }
 };
 
 // ---------------------------------------------------------------- epilogues
-// acc[i][j][reg] holds C[m][n] with m = wm*64 + 32i + (reg&3) + 8(reg>>2) + 4(lane>>5),
-// n = wn*64 + 32j + (lane&31)  (gfx950 32x32 C/D map)
+// acc[i][j][reg] of wave (wm, wn) holds C[m][n] with
+//   m = wm*64 + 32i + (reg&3) + 8(reg>>2) + 4(lane>>5),  n = wn*64 + 32j + (lane&31)
 
 struct IdentityRows {
   __device__ __forceinline__ size_t operator()(int m) const { return (size_t)m; }
@@ -301,13 +349,14 @@ struct DgradOutRows {  // DgradRows order -> NHWC pixel index
 };
 
 template <class RowMap = IdentityRows>
-struct EpiBF16 {  // bf16 [M][ld] store, optional per-column sum / sum of squares
-  bf16* out; int ld; float* sum; float* sumsq; RowMap rowmap;
+struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / sum of squares
+  bf16* out; int ld; float* sum; float* sumsq; RowMap rowmap; const bf16* addend = nullptr;
+  template <int BM, int BN>
   __device__ void apply(f32x16 (&acc)[2][2], char* lds, int m0, int n0, int M, int N,
                         int wm, int wn, int lane, int tid) const {
     if (sum) {
       // copy slot spreads the per-channel atomics of different blocks over NSTAT rows
-      const int slot = ((m0 / BM) * 2 + wm) & (NSTAT - 1);
+      const int slot = ((m0 / 64) + wm) & (NSTAT - 1);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         float s1 = 0.f, s2 = 0.f;
@@ -324,8 +373,8 @@ struct EpiBF16 {  // bf16 [M][ld] store, optional per-column sum / sum of square
         }
       }
     }
-    // stage the 128x128 tile through LDS as bf16 rows of 272 B, then 16 B/lane stores
-    constexpr int RS = 272;
+    // stage the BMxBN tile through LDS as bf16 rows of (BN+8)*2 B, then 16 B/lane stores
+    constexpr int RS = (BN + 8) * 2;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -338,19 +387,33 @@ struct EpiBF16 {  // bf16 [M][ld] store, optional per-column sum / sum of square
           *reinterpret_cast<bf16*>(lds + m * RS + n * 2) = (bf16)acc[i][j][r];
         }
     __syncthreads();
-    const int c = tid & 15;
+    constexpr int CPR = BN / 8;              // 16 B chunks per row
+    constexpr int RPI = NTHR / CPR;          // rows per iteration
+    const int c = tid % CPR;
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int row = (tid >> 4) + 16 * it;
+    for (int it = 0; it < BM / RPI; ++it) {
+      const int row = tid / CPR + RPI * it;
       const int m = m0 + row, n = n0 + c * 8;
-      if (m < M && n < N)
-        *reinterpret_cast<uint4*>(out + rowmap(m) * ld + n) = *reinterpret_cast<const uint4*>(lds + row * RS + c * 16);
+      if (m < M && n < N) {
+        const size_t o = rowmap(m) * ld + n;
+        uint4 v = *reinterpret_cast<const uint4*>(lds + row * RS + c * 16);
+        if (addend) {  // fused residual-gradient sum (dx of a branch point)
+          float a[8], b[8];
+          unpack8(v, a);
+          unpack8(*reinterpret_cast<const uint4*>(addend + o), b);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[e] += b[e];
+          v = pack8(a);
+        }
+        *reinterpret_cast<uint4*>(out + o) = v;
+      }
     }
   }
 };
 
 struct EpiF32Atomic {  // fp32 [M][ld] += (split-K partial sums)
   float* out; int ld;
+  template <int BM, int BN>
   __device__ void apply(f32x16 (&acc)[2][2], char*, int m0, int n0, int M, int N,
                         int wm, int wn, int lane, int) const {
 #pragma unroll
@@ -370,6 +433,7 @@ struct EpiF32Atomic {  // fp32 [M][ld] += (split-K partial sums)
 
 struct EpiF32 {  // fp32 [M][ld] = acc (+ bias[n]) (+= if accumulate)
   float* out; int ld; const float* bias; int accumulate;
+  template <int BM, int BN>
   __device__ void apply(f32x16 (&acc)[2][2], char*, int m0, int n0, int M, int N,
                         int wm, int wn, int lane, int) const {
 #pragma unroll
@@ -392,12 +456,15 @@ struct EpiF32 {  // fp32 [M][ld] = acc (+ bias[n]) (+= if accumulate)
 };
 
 // ---------------------------------------------------------------- main loop
-template <class LA, class LB, class EPI>
+template <int BM, int BN, class LA, class LB, class EPI>
 __global__ void __launch_bounds__(NTHR, 2)
-gemm_kernel(LA la, LB lb, EPI epi, int M, int N, int K, int ktiles_per_split) {
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int ktiles_per_split) {
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int WN = BN / 64;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
 
   // tile id: XCD remap, then grouped (8 M-tiles per group) order for L2 reuse
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
@@ -423,52 +490,54 @@ gemm_kernel(LA la, LB lb, EPI epi, int M, int N, int K, int ktiles_per_split) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  la.init(m0, tid);
-  lb.init(n0, tid);
-  int kt = la.next(kt_begin, kt_end);
+  typename LA::St sa;
+  typename LB::St sb;
+  la.init(sa, m0, tid);
+  lb.init(sb, n0, tid);
+  int kt = la.next(sa, kt_begin, kt_end);
   if (kt < kt_end) {
-    uint4 ra[4], rb[4];
-    la.load(kt * BK, tid, ra);
-    lb.load(kt * BK, tid, rb);
-    store_stage<LA::KC>(smem, tid, ra);
-    store_stage<LB::KC>(smem + TILE_BYTES, tid, rb);
+    uint4 ra[BM / 32], rb[BN / 32];
+    la.load(sa, kt * BK, tid, ra);
+    lb.load(sb, kt * BK, tid, rb);
+    store_stage<LA::KC, BM>(smem, tid, ra);
+    store_stage<LB::KC, BN>(smem + A_BYTES, tid, rb);
     __syncthreads();
 
     int cur = 0;
     while (kt < kt_end) {
-      char* As = smem + cur * 2 * TILE_BYTES;
-      char* Bs = As + TILE_BYTES;
-      const int nxt = la.next(kt + 1, kt_end);
+      char* As = smem + cur * STAGE;
+      char* Bs = As + A_BYTES;
+      const int nxt = la.next(sa, kt + 1, kt_end);
       const bool more = nxt < kt_end;
       if (more) {  // issue next tile's global loads before the MFMAs (T14)
-        la.load(nxt * BK, tid, ra);
-        lb.load(nxt * BK, tid, rb);
+        la.load(sa, nxt * BK, tid, ra);
+        lb.load(sb, nxt * BK, tid, rb);
       }
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        bf16x8 a0 = read_frag<LA::KC>(As, wm * 64, s, lane);
-        bf16x8 a1 = read_frag<LA::KC>(As, wm * 64 + 32, s, lane);
-        bf16x8 b0 = read_frag<LB::KC>(Bs, wn * 64, s, lane);
-        bf16x8 b1 = read_frag<LB::KC>(Bs, wn * 64 + 32, s, lane);
+        bf16x8 a0 = read_frag<LA::KC, BM>(As, wm * 64, s, lane);
+        bf16x8 a1 = read_frag<LA::KC, BM>(As, wm * 64 + 32, s, lane);
+        bf16x8 b0 = read_frag<LB::KC, BN>(Bs, wn * 64, s, lane);
+        bf16x8 b1 = read_frag<LB::KC, BN>(Bs, wn * 64 + 32, s, lane);
         acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
         acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
         acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
         acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
       }
       if (more) {
-        char* An = smem + (cur ^ 1) * 2 * TILE_BYTES;
-        store_stage<LA::KC>(An, tid, ra);
-        store_stage<LB::KC>(An + TILE_BYTES, tid, rb);
+        char* An = smem + (cur ^ 1) * STAGE;
+        store_stage<LA::KC, BM>(An, tid, ra);
+        store_stage<LB::KC, BN>(An + A_BYTES, tid, rb);
       }
       __syncthreads();
       cur ^= 1;
       kt = nxt;
     }
   }
-  epi.apply(acc, smem, m0, n0, M, N, wm, wn, lane, tid);
+  epi.template apply<BM, BN>(acc, smem, m0, n0, M, N, wm, wn, lane, tid);
 }
 
-template <class LA, class LB, class EPI>
+template <int BM, int BN, class LA, class LB, class EPI>
 static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K,
                          int splits, hipStream_t st) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
@@ -478,13 +547,22 @@ static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int 
   const int per = (ktiles + splits - 1) / splits;
   splits = (ktiles + per - 1) / per;
   dim3 grid(tiles, 1, splits);
-  hipLaunchKernelGGL((gemm_kernel<LA, LB, EPI>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, EPI>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
   return hipGetLastError();
 }
 
+// tile shape: 0 = 128x128, 1 = 256x64 (narrow N), 2 = 64x256 (narrow M)
+static int pick_tile(int M, int N) {
+  if (N <= 64 && M > 64) return 1;
+  if (M <= 64 && N > 64) return 2;
+  return 0;
+}
+
 // pick a split-K factor so a small-output / long-K GEMM still fills 256 CUs
-static int auto_splits(int M, int N, int K) {
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+static int auto_splits(int M, int N, int K, int tile) {
+  const int BMv = tile == 1 ? 256 : tile == 2 ? 64 : 128;
+  const int BNv = tile == 1 ? 64 : tile == 2 ? 256 : 128;
+  const int tiles = ((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
   const int ktiles = (K + BK - 1) / BK;
   int s = 1;
   while (tiles * s < 768 && ktiles / (s * 2) >= 8) s *= 2;
@@ -500,8 +578,46 @@ static ConvGeom mkgeom(int N, int H, int W, int C, int Co, int KH, int KW, int s
   ConvGeom g;
   g.N = N; g.H = H; g.W = W; g.C = C; g.Co = Co; g.KH = KH; g.KW = KW;
   g.stride = stride; g.pad = pad; g.dil = dil; g.Ho = Ho; g.Wo = Wo;
+  g.fWo = FastDiv(Wo); g.fHo = FastDiv(Ho); g.fW = FastDiv(W); g.fH = FastDiv(H);
+  g.fC = FastDiv(C); g.fCo = FastDiv(Co); g.fKW = FastDiv(KW);
   return g;
 }
+
+// Row plan of a dgrad output.  Stride 2: one row range per parity class that at least
+// one filter tap reaches (a 1x1/s2 conv reaches only class (0,0)); rows of the other
+// classes are structurally zero and are filled by a memset/copy instead of GEMM blocks.
+static DgradRows mkrows(int N, int H, int W, int S, int KH, int KW, int pad, int dil, int* rows_out) {
+  DgradRows r;
+  r.N = N; r.H = H; r.W = W; r.S = S;
+  r.fW = FastDiv(W); r.fH = FastDiv(H);
+  r.nclass = 0;
+  for (int k = 0; k < 4; ++k) { r.base[k] = 0x7fffffff; r.cid[k] = 0; }
+  if (S != 2) { *rows_out = N * H * W; r.nclass = 1; r.base[0] = 0; return r; }
+  int b = 0;
+  for (int c = 0; c < 4; ++c) {
+    const int ph = c >> 1, pw = c & 1;
+    const int Hc = (H - ph + 1) / 2, Wc = (W - pw + 1) / 2;
+    bool rv = false, sv = false;
+    for (int t = 0; t < KH; ++t) rv |= (((ph + pad - t * dil) % 2) + 2) % 2 == 0;
+    for (int t = 0; t < KW; ++t) sv |= (((pw + pad - t * dil) % 2) + 2) % 2 == 0;
+    if (!rv || !sv || Hc <= 0 || Wc <= 0) continue;
+    const int k = r.nclass++;
+    r.base[k] = b; r.cid[k] = c;
+    r.fHc[k] = FastDiv(Hc);
+    r.fWc[k] = FastDiv(Wc);
+    b += N * Hc * Wc;
+  }
+  *rows_out = b;
+  return r;
+}
+
+// dispatch one GEMM over the three tile shapes; MK(R) builds the loaders for R rows
+#define MLC_TILE_DISPATCH(TILE, M, N, K, SPLITS, ST, EPI, MKA, MKB)                              \
+  do {                                                                                         \
+    if ((TILE) == 1) return launch<256, 64>(MKA(256), MKB(64), EPI, M, N, K, SPLITS, ST);      \
+    if ((TILE) == 2) return launch<64, 256>(MKA(64), MKB(256), EPI, M, N, K, SPLITS, ST);      \
+    return launch<128, 128>(MKA(128), MKB(128), EPI, M, N, K, SPLITS, ST);                     \
+  } while (0)
 
 MLC_EXPORT int mlc_bn_stat_copies() { return NSTAT; }
 
@@ -514,37 +630,56 @@ MLC_EXPORT int mlc_conv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, f
                             int pad, int dil, int Ho, int Wo, hipStream_t st) {
   if (C % 8 || Co % 8) return -1;
   const int M = N * Ho * Wo, K = KH * KW * C;
+  const int tile = pick_tile(M, Co);
   EpiBF16<> epi{y, Co, sum, sumsq, IdentityRows{}};
-  MatKC lb{{}, w, K, Co, K};
+#define MKB(R) (MatKC<R>{{}, w, K, Co, K})
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
-    MatKC la{{}, x, C, M, K};
-    return launch(la, lb, epi, M, Co, K, 1, st);
+#define MKA(R) (MatKC<R>{{}, x, C, M, K})
+    MLC_TILE_DISPATCH(tile, M, Co, K, 1, st, epi, MKA, MKB);
+#undef MKA
   }
-  ConvFwdA la{{}, x, mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo), M, K};
-  return launch(la, lb, epi, M, Co, K, 1, st);
+  const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
+#define MKA(R) (ConvFwdA<R>{{}, x, g, M, K})
+  MLC_TILE_DISPATCH(tile, M, Co, K, 1, st, epi, MKA, MKB);
+#undef MKA
+#undef MKB
 }
 
-// dx[N,H,W,C] = conv_transpose(dy[N,Ho,Wo,Co], w)
-MLC_EXPORT int mlc_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, int N, int H, int W,
-                              int C, int Co, int KH, int KW, int stride, int pad, int dil,
-                              int Ho, int Wo, hipStream_t st) {
+// dx[N,H,W,C] = conv_transpose(dy[N,Ho,Wo,Co], w) (+ addend, same layout as dx; may
+// alias dx) -- the addend fuses the gradient sum at a residual branch point.
+MLC_EXPORT int mlc_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, const bf16* addend, int N,
+                              int H, int W, int C, int Co, int KH, int KW, int stride, int pad,
+                              int dil, int Ho, int Wo, hipStream_t st) {
   if (C % 8 || Co % 8) return -1;
-  const int M = N * H * W, K = KH * KW * Co;
-  ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
-  ConvDgradB lb{{}, w, g, K};
+  const int K = KH * KW * Co;
+  const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
+#define MKB(R) (ConvDgradB<R>{{}, w, g, K})
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
-    EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}};
-    MatKC la{{}, dy, Co, M, K};
-    return launch(la, lb, epi, M, C, K, 1, st);
+    const int M = N * H * W;
+    const int tile = pick_tile(M, C);
+    EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}, addend};
+#define MKA(R) (MatKC<R>{{}, dy, Co, M, K})
+    MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB);
+#undef MKA
   }
-  DgradRows rows{N, H, W, stride};
-  ConvDgradA la{dy, g, M, K, rows};
-  if (stride == 1) {
-    EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}};
-    return launch(la, lb, epi, M, C, K, 1, st);
+  int M = 0;
+  const DgradRows rows = mkrows(N, H, W, stride == 2 ? 2 : 1, KH, KW, pad, dil, &M);
+  const int tile = pick_tile(M, C);
+#define MKA(R) (ConvDgradA<R>{dy, g, M, K, rows})
+  if (stride != 2) {
+    EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}, addend};
+    MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB);
   }
-  EpiBF16<DgradOutRows> epi{dx, C, nullptr, nullptr, DgradOutRows{rows}};
-  return launch(la, lb, epi, M, C, K, 1, st);
+  if (M < N * H * W) {  // classes no tap reaches: dx = addend there (or 0)
+    const size_t bytes = (size_t)N * H * W * C * sizeof(bf16);
+    if (addend) { if (addend != dx) (void)hipMemcpyAsync(dx, addend, bytes, hipMemcpyDeviceToDevice, st); }
+    else (void)hipMemsetAsync(dx, 0, bytes, st);
+  }
+  if (M == 0) return hipGetLastError();
+  EpiBF16<DgradOutRows> epi{dx, C, nullptr, nullptr, DgradOutRows{rows}, addend};
+  MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB);
+#undef MKA
+#undef MKB
 }
 
 // dw[Co, KH*KW*C] (fp32) = sum_p dy[p][co] * im2col(x)[p][kk]; zeroes dw first unless
@@ -554,16 +689,21 @@ MLC_EXPORT int mlc_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, i
                               int Ho, int Wo, int splits, int accumulate, hipStream_t st) {
   if (C % 8 || Co % 8) return -1;
   const int P = N * Ho * Wo, KK = KH * KW * C;
+  const int tile = pick_tile(Co, KK);
   if (!accumulate) (void)hipMemsetAsync(dw, 0, (size_t)Co * KK * sizeof(float), st);
-  if (splits <= 0) splits = auto_splits(Co, KK, P);
+  if (splits <= 0) splits = auto_splits(Co, KK, P, tile);
   EpiF32Atomic epi{dw, KK};
-  MatMC la{{}, dy, Co, P, Co};
+#define MKA(R) (MatMC<R>{{}, dy, Co, P, Co})
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
-    MatMC lb{{}, x, C, P, C};
-    return launch(la, lb, epi, Co, KK, P, splits, st);
+#define MKB(R) (MatMC<R>{{}, x, C, P, C})
+    MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
+#undef MKB
   }
-  ConvWgradB lb{{}, x, mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo), P, KK};
-  return launch(la, lb, epi, Co, KK, P, splits, st);
+  const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
+#define MKB(R) (ConvWgradB<R>{{}, x, g, P, KK})
+  MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
+#undef MKB
+#undef MKA
 }
 
 // Generic bf16 GEMM with fp32 output: C[M][N] (+)= op(A) op(B) (+ bias)
@@ -571,32 +711,39 @@ MLC_EXPORT int mlc_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, i
 //   tb=0: B is [K][N] (ldb);  tb=1: B is [N][K]
 // out_mode 0: store (+bias, accumulate flag), 1: atomic add (split-K allowed; the
 // caller zeroes C unless accumulating)
+#define GA_KC(R) (MatKC<R>{{}, A, lda, M, K})
+#define GA_MC(R) (MatMC<R>{{}, A, lda, K, M})
+#define GB_KC(R) (MatKC<R>{{}, B, ldb, N, K})
+#define GB_MC(R) (MatMC<R>{{}, B, ldb, K, N})
+
 MLC_EXPORT int mlc_gemm_f32out(const bf16* A, const bf16* B, float* C, const float* bias,
                                int M, int N, int K, int lda, int ldb, int ldc, int ta, int tb,
                                int out_mode, int accumulate, int splits, hipStream_t st) {
   if (K % 8 || lda % 8 || ldb % 8 || (ta && M % 8) || (!tb && N % 8)) return -1;
+  const int tile = pick_tile(M, N);
   if (out_mode == 1) {
-    if (splits <= 0) splits = auto_splits(M, N, K);
+    if (splits <= 0) splits = auto_splits(M, N, K, tile);
     EpiF32Atomic epi{C, ldc};
-    if (!ta && tb) return launch(MatKC{{}, A, lda, M, K}, MatKC{{}, B, ldb, N, K}, epi, M, N, K, splits, st);
-    if (!ta && !tb) return launch(MatKC{{}, A, lda, M, K}, MatMC{{}, B, ldb, K, N}, epi, M, N, K, splits, st);
-    if (ta && tb) return launch(MatMC{{}, A, lda, K, M}, MatKC{{}, B, ldb, N, K}, epi, M, N, K, splits, st);
-    return launch(MatMC{{}, A, lda, K, M}, MatMC{{}, B, ldb, K, N}, epi, M, N, K, splits, st);
+    if (!ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_KC, GB_KC);
+    if (!ta && !tb) MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_KC, GB_MC);
+    if (ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_MC, GB_KC);
+    MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_MC, GB_MC);
   }
   EpiF32 epi{C, ldc, bias, accumulate};
-  if (!ta && tb) return launch(MatKC{{}, A, lda, M, K}, MatKC{{}, B, ldb, N, K}, epi, M, N, K, 1, st);
-  if (!ta && !tb) return launch(MatKC{{}, A, lda, M, K}, MatMC{{}, B, ldb, K, N}, epi, M, N, K, 1, st);
-  if (ta && tb) return launch(MatMC{{}, A, lda, K, M}, MatKC{{}, B, ldb, N, K}, epi, M, N, K, 1, st);
-  return launch(MatMC{{}, A, lda, K, M}, MatMC{{}, B, ldb, K, N}, epi, M, N, K, 1, st);
+  if (!ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_KC, GB_KC);
+  if (!ta && !tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_KC, GB_MC);
+  if (ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_MC, GB_KC);
+  MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_MC, GB_MC);
 }
 
 // bf16-output GEMM (same layout flags)
 MLC_EXPORT int mlc_gemm_bf16out(const bf16* A, const bf16* B, bf16* C, int M, int N, int K,
                                 int lda, int ldb, int ldc, int ta, int tb, hipStream_t st) {
   if (K % 8 || N % 8 || ldc % 8 || lda % 8 || ldb % 8 || (ta && M % 8)) return -1;
+  const int tile = pick_tile(M, N);
   EpiBF16<> epi{C, ldc, nullptr, nullptr, IdentityRows{}};
-  if (!ta && tb) return launch(MatKC{{}, A, lda, M, K}, MatKC{{}, B, ldb, N, K}, epi, M, N, K, 1, st);
-  if (!ta && !tb) return launch(MatKC{{}, A, lda, M, K}, MatMC{{}, B, ldb, K, N}, epi, M, N, K, 1, st);
-  if (ta && tb) return launch(MatMC{{}, A, lda, K, M}, MatKC{{}, B, ldb, N, K}, epi, M, N, K, 1, st);
-  return launch(MatMC{{}, A, lda, K, M}, MatMC{{}, B, ldb, K, N}, epi, M, N, K, 1, st);
+  if (!ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_KC, GB_KC);
+  if (!ta && !tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_KC, GB_MC);
+  if (ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_MC, GB_KC);
+  MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_MC, GB_MC);
 }

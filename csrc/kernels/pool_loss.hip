@@ -145,9 +145,9 @@ avgpool_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx, int N, in
 __global__ void __launch_bounds__(NT)
 softmax_ce_kernel(const float* __restrict__ logits, const long* __restrict__ labels,
                   bf16* __restrict__ dlogits, float* __restrict__ loss_sum, float* __restrict__ correct,
-                  int V, float scale, float smoothing) {
+                  int V, int ld, float scale, float smoothing) {
   const int row = blockIdx.x;
-  const float* x = logits + (long)row * V;
+  const float* x = logits + (long)row * ld;
   __shared__ float sm[NT / 64], si[NT / 64];
   __shared__ int sarg[NT / 64];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -180,10 +180,14 @@ softmax_ce_kernel(const float* __restrict__ logits, const long* __restrict__ lab
   }
   if (dlogits) {
     const float inv_s = 1.f / s;
-    for (int i = t; i < V; i += NT) {
-      const float p = __expf(x[i] - mx) * inv_s;
-      const float tgt = (i == y ? (1.f - smoothing) : 0.f) + smoothing / (float)V;
-      dlogits[(long)row * V + i] = (bf16)((p - tgt) * scale);
+    for (int i = t; i < ld; i += NT) {
+      float g = 0.f;  // padded columns [V, ld) get zero gradient
+      if (i < V) {
+        const float p = __expf(x[i] - mx) * inv_s;
+        const float tgt = (i == y ? (1.f - smoothing) : 0.f) + smoothing / (float)V;
+        g = (p - tgt) * scale;
+      }
+      dlogits[(long)row * ld + i] = (bf16)g;
     }
   }
 }
@@ -258,11 +262,12 @@ MLC_EXPORT int mlc_avgpool_bwd(const bf16* dy, bf16* dx, int N, int HW, int C, h
   return hipGetLastError();
 }
 
+// logits/dlogits rows have stride ld >= V (columns [V, ld) are padding)
 MLC_EXPORT int mlc_softmax_ce(const float* logits, const long* labels, bf16* dlogits, float* loss_sum,
-                              float* correct, int B, int V, float scale, float smoothing,
+                              float* correct, int B, int V, int ld, float scale, float smoothing,
                               hipStream_t st) {
   hipLaunchKernelGGL(softmax_ce_kernel, dim3(B), dim3(NT), 0, st, logits, labels, dlogits, loss_sum,
-                     correct, V, scale, smoothing);
+                     correct, V, ld, scale, smoothing);
   return hipGetLastError();
 }
 

@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import torch
 
-from mlcomp_amd.ops.layers import ClassifierHead, ConvBN, MaxPool, NativeContext
+from mlcomp_amd.ops.layers import ClassifierHead, ConvBN, MaxPool, NativeContext, ResidualBlock
 from .resnet import BasicBlock, Bottleneck, ResNet
 
 STEM_CIN = 8
@@ -48,7 +48,7 @@ class NativeResNet:
                 if blk.downsample is not None:
                     d = blk.downsample.cb
                     down = ConvBN(ctx, f'{pre}.downsample.cb', d.conv, d.bn, act=False)
-                self.blocks.append((units, down))
+                self.blocks.append(ResidualBlock(units, down))
         self.head = ClassifierHead(ctx, 'fc', model.fc, smoothing)
         ctx.finalize(device)
         for u in self._units():
@@ -58,22 +58,18 @@ class NativeResNet:
 
     def _units(self):
         yield self.stem
-        for units, down in self.blocks:
-            yield from units
-            if down is not None:
-                yield down
+        for blk in self.blocks:
+            yield from blk.units
+            if blk.down is not None:
+                yield blk.down
 
     # ------------------------------------------------------------------ execution
     def features(self, x):
         anchor = self.ctx.anchor
         x = self.stem(x)
         x = self.pool(x, anchor)
-        for units, down in self.blocks:
-            identity = down(x) if down is not None else x
-            y = x
-            for u in units[:-1]:
-                y = u(y)
-            x = units[-1](y, identity)
+        for blk in self.blocks:
+            x = blk(x)
         return x
 
     def loss(self, x, labels):

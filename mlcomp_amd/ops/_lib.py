@@ -20,7 +20,7 @@ vp, i32, i64, f32 = C.c_void_p, C.c_int, C.c_long, C.c_float
 
 _SIGS = {
     'mlc_conv_fwd': [vp, vp, vp, vp, vp] + [i32] * 12 + [vp],
-    'mlc_conv_dgrad': [vp, vp, vp] + [i32] * 12 + [vp],
+    'mlc_conv_dgrad': [vp, vp, vp, vp] + [i32] * 12 + [vp],
     'mlc_conv_wgrad': [vp, vp, vp] + [i32] * 14 + [vp],
     'mlc_gemm_f32out': [vp, vp, vp, vp] + [i32] * 11 + [vp],
     'mlc_gemm_bf16out': [vp, vp, vp] + [i32] * 8 + [vp],
@@ -28,19 +28,30 @@ _SIGS = {
     'mlc_bn_finalize': [vp, vp, i32] + [vp] * 8 + [i64, i32, f32, f32, vp],
     'mlc_bn_fwd_apply': [vp] * 5 + [i64, i32, i32, vp],
     'mlc_bn_bwd_reduce': [vp] * 5 + [i64, i32, vp],
-    'mlc_bn_bwd_apply': [vp] * 11 + [i64, i32, vp],
+    'mlc_bn_bwd_finalize': [vp] * 6 + [i64, i32, vp],
+    'mlc_bn_bwd_apply': [vp] * 7 + [i64, i32, vp],
     'mlc_maxpool_fwd': [vp, vp, vp] + [i32] * 9 + [vp],
     'mlc_maxpool_bwd': [vp, vp, vp] + [i32] * 9 + [vp],
     'mlc_avgpool_fwd': [vp, vp, i32, i32, i32, vp],
     'mlc_avgpool_bwd': [vp, vp, i32, i32, i32, vp],
-    'mlc_softmax_ce': [vp] * 5 + [i32, i32, f32, f32, vp],
+    'mlc_softmax_ce': [vp] * 5 + [i32, i32, i32, f32, f32, vp],
     'mlc_colsum': [vp, vp, i32, i32, vp],
     'mlc_nchw_to_nhwc': [vp, vp, i32, i32, i32, i32, vp],
     'mlc_cast_f32_bf16': [vp, vp, i64, vp],
     'mlc_sgd': [vp] * 5 + [i64, i64, i64, f32, f32, f32, i32, i32, vp],
     'mlc_adam': [vp] * 6 + [i64, i64, i64, f32, f32, f32, f32, i32, vp],
     'mlc_sqnorm': [vp, i64, vp, f32, vp],
+    'mlc_comm_unique_id_bytes': [],
+    'mlc_comm_get_unique_id': [vp],
+    'mlc_comm_init': [vp, i32, i32, i32, vp],
+    'mlc_comm_destroy': [vp],
+    'mlc_allreduce': [vp, vp, vp, i64, i32, i32, vp],
+    'mlc_broadcast': [vp, vp, vp, i64, i32, i32, vp],
+    'mlc_reduce_scatter': [vp, vp, vp, i64, i32, i32, vp],
+    'mlc_allgather': [vp, vp, vp, i64, i32, vp],
+    'mlc_alltoall': [vp, vp, vp, i64, i32, i32, i32, vp],
 }
+_RESTYPE = {'mlc_comm_init': vp}
 
 
 def lib_path():
@@ -64,7 +75,7 @@ def load():
         for name, args in _SIGS.items():
             fn = getattr(lib, name)
             fn.argtypes = args
-            fn.restype = C.c_int
+            fn.restype = _RESTYPE.get(name, C.c_int)
         _LIB = lib
     return _LIB
 

@@ -58,18 +58,28 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, stride=1, pad=0, dil=1,
     return y
 
 
-def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=1, pad=0, dil=1) -> torch.Tensor:
+def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=1, pad=0, dil=1,
+                 addend: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dx = conv_transpose(dy, w) [+ addend] (the addend fuses the gradient sum of a
+    residual branch point into the epilogue; ``out`` may alias ``addend``)."""
     N, H, W, C = x_shape
     Co, KH, KW, Ci = w.shape
     _, Ho, Wo, _ = dy.shape
     if _cuda(dy):
-        dx = torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
-        _lib.call('mlc_conv_dgrad', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(dx), N, H, W, C, Co, KH, KW,
-                  stride, pad, dil, Ho, Wo, _lib.stream())
+        dx = out if out is not None else torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
+        _lib.call('mlc_conv_dgrad', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(dx), _lib.ptr(addend), N, H, W, C,
+                  Co, KH, KW, stride, pad, dil, Ho, Wo, _lib.stream())
         return dx
     dxf = torch.nn.grad.conv2d_input((N, C, H, W), w.permute(0, 3, 1, 2).float(),
                                      dy.permute(0, 3, 1, 2).float(), stride, pad, dil)
-    return dxf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+    dxf = dxf.permute(0, 2, 3, 1)
+    if addend is not None:
+        dxf = dxf + addend.float()
+    dx = dxf.to(torch.bfloat16).contiguous()
+    if out is not None:
+        out.copy_(dx)
+        return out
+    return dx
 
 
 def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride=1, pad=0, dil=1,
@@ -148,24 +158,28 @@ def bn_fwd_apply(y, res, s1, s2, gamma, beta, save_mean, save_invstd, run_mean, 
 
 
 def bn_bwd(dz, z, y, mean, invstd, gamma, want_dres=False, dgamma=None, dbeta=None, sums=None,
-           zero_sums=True):
+           zero_sums=True, coef=None):
     """Backward of z = act(BN(y) [+res]).  ``z`` is the saved output (ReLU mask) or None
     when there is no ReLU.  Returns (dy, dres or None); writes dgamma/dbeta (fp32).
-    ``sums`` (2*C fp32 scratch) must be zero on entry when ``zero_sums`` is False."""
+    ``sums`` is NSTAT*2*C fp32 scratch (must be zero on entry when ``zero_sums`` is
+    False), ``coef`` 3*C fp32 scratch."""
     rows = y.numel() // y.shape[-1]
     C = y.shape[-1]
     if _cuda(dz):
         if sums is None:
-            sums = torch.zeros(2 * C, device=dz.device, dtype=torch.float32)
+            sums = torch.zeros(NSTAT * 2 * C, device=dz.device, dtype=torch.float32)
         elif zero_sums:
             sums.zero_()
+        if coef is None:
+            coef = torch.empty(3 * C, device=dz.device, dtype=torch.float32)
         _lib.call('mlc_bn_bwd_reduce', _lib.ptr(dz), _lib.ptr(z), _lib.ptr(y), _lib.ptr(mean),
                   _lib.ptr(sums), rows, C, _lib.stream())
+        _lib.call('mlc_bn_bwd_finalize', _lib.ptr(sums), _lib.ptr(invstd), _lib.ptr(gamma), _lib.ptr(coef),
+                  _lib.ptr(dgamma), _lib.ptr(dbeta), rows, C, _lib.stream())
         dy = torch.empty_like(y)
         dres = torch.empty_like(y) if want_dres else None
         _lib.call('mlc_bn_bwd_apply', _lib.ptr(dz), _lib.ptr(z), _lib.ptr(y), _lib.ptr(mean),
-                  _lib.ptr(invstd), _lib.ptr(gamma), _lib.ptr(sums), _lib.ptr(dy), _lib.ptr(dres),
-                  _lib.ptr(dgamma), _lib.ptr(dbeta), rows, C, _lib.stream())
+                  _lib.ptr(coef), _lib.ptr(dy), _lib.ptr(dres), rows, C, _lib.stream())
         return dy, dres
     d = dz.float().reshape(rows, C)
     if z is not None:
@@ -284,17 +298,21 @@ def colsum(g, out):
 
 
 # ---------------------------------------------------------------- loss
-def softmax_ce(logits, labels, loss_sum, correct=None, scale=None, smoothing=0.0, want_grad=True):
-    """Fused softmax cross-entropy.  Accumulates the summed loss (and #correct) into
-    fp32 scalars; returns bf16 dlogits = (softmax - target) * scale (scale = 1/B)."""
-    B, V = logits.shape
+def softmax_ce(logits, labels, loss_sum, correct=None, scale=None, smoothing=0.0, want_grad=True,
+               num_classes=None):
+    """Fused softmax cross-entropy over the first ``num_classes`` columns of ``logits``
+    ([B, ld], extra columns are padding).  Accumulates the summed loss (and #correct)
+    into fp32 scalars; returns bf16 dlogits [B, ld] = (softmax - target) * scale
+    (scale defaults to 1/B), zero in the padding columns."""
+    B, ld = logits.shape
+    V = num_classes or ld
     scale = (1.0 / B) if scale is None else scale
     if _cuda(logits):
-        dl = torch.empty(B, V, device=logits.device, dtype=torch.bfloat16) if want_grad else None
+        dl = torch.empty(B, ld, device=logits.device, dtype=torch.bfloat16) if want_grad else None
         _lib.call('mlc_softmax_ce', _lib.ptr(logits), _lib.ptr(labels), _lib.ptr(dl), _lib.ptr(loss_sum),
-                  _lib.ptr(correct), B, V, float(scale), float(smoothing), _lib.stream())
+                  _lib.ptr(correct), B, V, ld, float(scale), float(smoothing), _lib.stream())
         return dl
-    lf = logits.float()
+    lf = logits.float()[:, :V]
     lse = torch.logsumexp(lf, 1)
     nll = lse - lf.gather(1, labels[:, None])[:, 0]
     sm = lse - lf.mean(1)
@@ -306,7 +324,9 @@ def softmax_ce(logits, labels, loss_sum, correct=None, scale=None, smoothing=0.0
     p = torch.softmax(lf, 1)
     tgt = torch.full_like(p, smoothing / V)
     tgt.scatter_add_(1, labels[:, None], torch.full((B, 1), 1 - smoothing, dtype=p.dtype))
-    return ((p - tgt) * scale).to(torch.bfloat16)
+    g = torch.zeros(B, ld)
+    g[:, :V] = (p - tgt) * scale
+    return g.to(torch.bfloat16)
 
 
 # ---------------------------------------------------------------- layout helpers

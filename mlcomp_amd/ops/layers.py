@@ -59,6 +59,9 @@ class NativeContext:
         self.anchor = None
         self.training = True
         self.device = None
+        # True when the step zeroes the whole grad arena once up front: the wgrad kernels
+        # then accumulate (atomics) instead of issuing one memset per layer
+        self.grad_prezeroed = False
 
     def finalize(self, device):
         self.device = torch.device(device)
@@ -93,7 +96,7 @@ class ConvBN:
         self._src = (conv, bn)
         self.k_s1 = ctx.ws.request(f'{name}.s1', Fn.NSTAT * Co)
         self.k_s2 = ctx.ws.request(f'{name}.s2', Fn.NSTAT * Co)
-        self.k_bw = ctx.ws.request(f'{name}.bwd', 2 * Co)
+        self.k_bw = ctx.ws.request(f'{name}.bwd', Fn.NSTAT * 2 * Co)
 
     def load_from_torch(self):
         conv, bn = self._src
@@ -107,8 +110,9 @@ class ConvBN:
         self.run_mean = bn.running_mean.detach().clone().float().to(dev)
         self.run_var = bn.running_var.detach().clone().float().to(dev)
         Co = self.Co
-        b = torch.zeros(4, Co, device=dev)
+        b = torch.zeros(7, Co, device=dev)
         self.save_mean, self.save_invstd, self.scale, self.shift = b[0], b[1], b[2], b[3]
+        self.coef = b[4:7].reshape(-1)
 
     def export_to_torch(self):
         conv, bn = self._src
@@ -122,40 +126,111 @@ class ConvBN:
     def __call__(self, x, res=None):
         return _ConvBNFn.apply(x, res, self.ctx.anchor, self)
 
+    # raw (autograd-free) halves, composed by the block-level Functions
+    def fwd(self, x, res=None):
+        ws = self.ctx.ws
+        s1, s2 = ws[self.k_s1], ws[self.k_s2]
+        y = Fn.conv2d_fwd(x, self.w.bf16, self.stride, self.pad, self.dil, stats=(s1, s2))
+        training = self.ctx.training
+        z = Fn.bn_fwd_apply(y, res, s1, s2, self.gamma.master, self.beta.master, self.save_mean,
+                            self.save_invstd, self.run_mean if training else None,
+                            self.run_var if training else None, self.eps, self.momentum, self.act,
+                            scale=self.scale, shift=self.shift)
+        return z, (x, y, z)
+
+    def bwd(self, dz, rec, want_dres=False, dx_addend=None, need_dx=True, dx_out=None):
+        x, y, z = rec
+        arena = self.ctx.arena
+        dy, dres = Fn.bn_bwd(dz, z if self.act else None, y, self.save_mean, self.save_invstd,
+                             self.gamma.master, want_dres=want_dres, dgamma=self.gamma.grad,
+                             dbeta=self.beta.grad, sums=self.ctx.ws[self.k_bw], zero_sums=False,
+                             coef=self.coef)
+        arena.mark_ready(self.gamma)
+        arena.mark_ready(self.beta)
+        Fn.conv2d_wgrad(dy, x, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad,
+                        accumulate=self.ctx.grad_prezeroed)
+        arena.mark_ready(self.w)
+        dx = None
+        if need_dx:
+            dx = Fn.conv2d_dgrad(dy, self.w.bf16, x.shape, self.stride, self.pad, self.dil,
+                                 addend=dx_addend, out=dx_out)
+        return dx, dres
+
 
 class _ConvBNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, anchor, m: ConvBN):
-        ws = m.ctx.ws
-        s1, s2 = ws[m.k_s1], ws[m.k_s2]
-        y = Fn.conv2d_fwd(x, m.w.bf16, m.stride, m.pad, m.dil, stats=(s1, s2))
-        training = m.ctx.training
-        z = Fn.bn_fwd_apply(y, res, s1, s2, m.gamma.master, m.beta.master, m.save_mean,
-                            m.save_invstd, m.run_mean if training else None,
-                            m.run_var if training else None, m.eps, m.momentum, m.act,
-                            scale=m.scale, shift=m.shift)
+        z, rec = m.fwd(x, res)
         ctx.m = m
         ctx.has_res = res is not None
-        ctx.save_for_backward(x, y, z)
+        ctx.save_for_backward(*rec)
         return z
 
     @staticmethod
     def backward(ctx, dz):
-        x, y, z = ctx.saved_tensors
         m: ConvBN = ctx.m
-        arena = m.ctx.arena
-        dz = dz.contiguous()
-        dy, dres = Fn.bn_bwd(dz, z if m.act else None, y, m.save_mean, m.save_invstd,
-                             m.gamma.master, want_dres=ctx.has_res, dgamma=m.gamma.grad,
-                             dbeta=m.beta.grad, sums=m.ctx.ws[m.k_bw], zero_sums=False)
-        arena.mark_ready(m.gamma)
-        arena.mark_ready(m.beta)
-        Fn.conv2d_wgrad(dy, x, m.w.shape, m.stride, m.pad, m.dil, out=m.w.grad)
-        arena.mark_ready(m.w)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = Fn.conv2d_dgrad(dy, m.w.bf16, x.shape, m.stride, m.pad, m.dil)
+        dx, dres = m.bwd(dz.contiguous(), ctx.saved_tensors, want_dres=ctx.has_res,
+                         need_dx=ctx.needs_input_grad[0])
         return dx, dres, None, None
+
+
+class ResidualBlock:
+    """units[0..n-1] chained, the last one adding the shortcut (identity or ``down(x)``)
+    before its ReLU.  One autograd node for the whole block: backward fuses the gradient
+    sum at the branch point into the dgrad epilogue of the first unit."""
+
+    def __init__(self, units: List[ConvBN], down: Optional[ConvBN]):
+        self.units = units
+        self.down = down
+        self.ctx = units[0].ctx
+
+    def __call__(self, x):
+        return _ResidualBlockFn.apply(x, self.ctx.anchor, self)
+
+
+class _ResidualBlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, blk: ResidualBlock):
+        recs = []
+        if blk.down is not None:
+            identity, rd = blk.down.fwd(x)
+        else:
+            identity, rd = x, None
+        y = x
+        for u in blk.units[:-1]:
+            y, r = u.fwd(y)
+            recs.append(r)
+        out, r = blk.units[-1].fwd(y, identity)
+        recs.append(r)
+        ctx.blk = blk
+        ctx.n = len(recs)
+        flat = [t for r in recs for t in r]
+        if rd is not None:
+            flat += list(rd)
+        ctx.save_for_backward(*flat)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        blk: ResidualBlock = ctx.blk
+        saved = ctx.saved_tensors
+        recs = [saved[3 * i:3 * i + 3] for i in range(ctx.n)]
+        rd = saved[3 * ctx.n:3 * ctx.n + 3] if blk.down is not None else None
+        dout = dout.contiguous()
+        need_dx = ctx.needs_input_grad[0]
+        # last unit: its dres is the shortcut-branch gradient
+        d, dres = blk.units[-1].bwd(dout, recs[-1], want_dres=True)
+        for i in range(len(blk.units) - 2, 0, -1):
+            d, _ = blk.units[i].bwd(d, recs[i])
+        if blk.down is not None:
+            # shortcut conv first; its dx becomes the addend of the first unit's dgrad
+            short, _ = blk.down.bwd(dres, rd, need_dx=need_dx)
+        else:
+            short = dres
+        dx, _ = blk.units[0].bwd(d, recs[0], dx_addend=short if need_dx else None,
+                                 need_dx=need_dx,
+                                 dx_out=short if (need_dx and blk.down is not None) else None)
+        return dx, None, None
 
 
 # ---------------------------------------------------------------------------- pooling
@@ -192,20 +267,23 @@ class ClassifierHead:
         self.name = name
         self.fc = fc
         self.O, self.I = fc.weight.shape
-        self.w = ctx.arena.weight(f'{name}.weight', (self.O, self.I))
-        self.b = ctx.arena.vector(f'{name}.bias', (self.O,))
+        # output rows padded to a multiple of 8 (16-byte MFMA operand chunks); the
+        # padded rows stay zero and the loss ignores their logits
+        self.Op = (self.O + 7) // 8 * 8
+        self.w = ctx.arena.weight(f'{name}.weight', (self.Op, self.I))
+        self.b = ctx.arena.vector(f'{name}.bias', (self.Op,))
         self.smoothing = smoothing
         self.k_loss = ctx.ws.request(f'{name}.loss', 1)
         self.k_correct = ctx.ws.request(f'{name}.correct', 1)
 
     def load_from_torch(self):
         dev = self.ctx.device
-        self.w.master.copy_(self.fc.weight.detach().float().to(dev))
-        self.b.master.copy_(self.fc.bias.detach().float().to(dev))
+        self.w.master[:self.O].copy_(self.fc.weight.detach().float().to(dev))
+        self.b.master[:self.O].copy_(self.fc.bias.detach().float().to(dev))
 
     def export_to_torch(self):
-        self.fc.weight.data.copy_(self.w.master.to(self.fc.weight.device))
-        self.fc.bias.data.copy_(self.b.master.to(self.fc.bias.device))
+        self.fc.weight.data.copy_(self.w.master[:self.O].to(self.fc.weight.device))
+        self.fc.bias.data.copy_(self.b.master[:self.O].to(self.fc.bias.device))
 
     def loss_sum(self):
         return self.ctx.ws[self.k_loss]
@@ -218,7 +296,7 @@ class ClassifierHead:
 
     def logits(self, x):
         pooled = Fn.avgpool_fwd(x)
-        return Fn.linear_fwd(pooled, self.w.bf16, self.b.master)
+        return Fn.linear_fwd(pooled, self.w.bf16, self.b.master)[:, :self.O]
 
 
 class _HeadFn(torch.autograd.Function):
@@ -231,11 +309,11 @@ class _HeadFn(torch.autograd.Function):
         logits = Fn.linear_fwd(pooled, h.w.bf16, h.b.master)
         ws = h.ctx.ws
         dl = Fn.softmax_ce(logits, labels, ws[h.k_loss], ws[h.k_correct],
-                           scale=1.0 / labels.shape[0], smoothing=h.smoothing)
+                           scale=1.0 / labels.shape[0], smoothing=h.smoothing, num_classes=h.O)
         ctx.h = h
         ctx.xshape = tuple(x.shape)
         ctx.save_for_backward(pooled, dl)
-        return ws[h.k_loss]
+        return ws[h.k_loss].clone()
 
     @staticmethod
     def backward(ctx, dloss):

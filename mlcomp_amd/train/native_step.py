@@ -1,0 +1,104 @@
+"""The native training step for image classifiers (the headline ResNet-50 task).
+
+forward (fused conv+BN+ReLU nodes) -> fused avgpool/FC/softmax-CE -> backward (wgrad
+straight into the flat grad arena, bucketed RCCL all-reduce on a side stream as buckets
+fill) -> one fused SGD launch per arena (also refreshing the bf16 weight mirror).
+
+After ``warmup_eager`` eager iterations the whole step is captured into ONE HIP graph
+(``torch.cuda.CUDAGraph``; HIP graph on ROCm) and replayed: ~400 kernel launches per
+step cost one graph launch.  Inputs are static device buffers; ``load_batch`` copies a
+new batch into them (outside the graph) for real-data training.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+from mlcomp_amd.models import build_model
+from mlcomp_amd.models.native_resnet import STEM_CIN, NativeResNet
+from mlcomp_amd.ops import functional as Fn
+from mlcomp_amd.parallel.comm import make_comm
+from mlcomp_amd.parallel.ddp import GradBucketer
+from mlcomp_amd.train.optim import FusedSGD
+
+
+class NativeClassifierStep:
+    def __init__(self, model_name='resnet50', batch=256, image_size=224, device=None,
+                 world_size=1, use_graph=True, num_classes=1000, lr=0.1, momentum=0.9,
+                 weight_decay=5e-5, nesterov=False, smoothing=0.0, seed=0, warmup_eager=2,
+                 torch_model=None):
+        self.device = torch.device(device or 'cuda')
+        torch.manual_seed(seed)
+        tm = torch_model if torch_model is not None else build_model(model_name, num_classes=num_classes)
+        self.net = NativeResNet(tm, self.device, smoothing=smoothing)
+        self.net.ctx.grad_prezeroed = True
+        self.world = world_size
+        self.comm = make_comm(self.device) if world_size > 1 else None
+        self.bucketer = GradBucketer(self.net.arena, self.comm)
+        self.bucketer.broadcast_params()
+        self.opt = FusedSGD(self.net.arena, lr=lr, momentum=momentum, weight_decay=weight_decay,
+                            nesterov=nesterov, grad_scale=1.0 / world_size)
+        self.batch = batch
+        rank = int(os.environ.get('RANK', '0'))
+        g = torch.Generator(device=self.device)
+        g.manual_seed(1234 + rank)
+        img = torch.randn(batch, image_size, image_size, 3, device=self.device, generator=g)
+        self.x = torch.nn.functional.pad(img, (0, STEM_CIN - 3)).to(torch.bfloat16).contiguous()
+        self.y = torch.randint(0, num_classes, (batch,), device=self.device, generator=g)
+        self.use_graph = use_graph and self.device.type == 'cuda'
+        self.warmup_eager = warmup_eager
+        self.graph = None
+        self.calls = 0
+        self._loss = None
+
+    # ------------------------------------------------------------------ data
+    def load_batch(self, images_nchw_or_nhwc: torch.Tensor, labels: torch.Tensor):
+        """Copy a batch into the static input buffers (NCHW float or NHWC bf16)."""
+        x = images_nchw_or_nhwc
+        if x.dim() == 4 and x.shape[1] in (1, 3) and x.dtype != torch.bfloat16:
+            x = Fn.nchw_to_nhwc(x.to(self.device, non_blocking=True).float(), pad_to=STEM_CIN)
+        self.x.copy_(x)
+        self.y.copy_(labels.to(self.device, non_blocking=True))
+
+    # ------------------------------------------------------------------ step
+    def _body(self):
+        self.net.ctx.ws.zero()
+        self.net.arena.zero_grad()   # one memset; wgrad kernels then accumulate
+        self.bucketer.begin()
+        loss = self.net.loss(self.x, self.y)
+        loss.backward()
+        self.bucketer.finish()
+        self.opt.step()
+        self._loss = self.net.head.loss_sum()
+
+    def __call__(self):
+        self.calls += 1
+        if not self.use_graph:
+            self._body()
+            return
+        if self.graph is None:
+            if self.calls <= self.warmup_eager:
+                s = torch.cuda.Stream(self.device)
+                s.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(s):
+                    self._body()
+                torch.cuda.current_stream(self.device).wait_stream(s)
+                return
+            torch.cuda.synchronize(self.device)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._body()
+        self.graph.replay()
+
+    def set_lr(self, lr):
+        self.opt.set_lr(lr)
+
+    def last_loss(self) -> Optional[float]:
+        if self._loss is None:
+            return None
+        return float(self._loss.item()) / self.batch
+
+    def accuracy(self) -> float:
+        return float(self.net.head.correct().item()) / self.batch

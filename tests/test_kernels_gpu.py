@@ -183,3 +183,18 @@ def test_sgd_adam():
     Fn.adam_step(pg, g.to(DEV), mg, vg, None, hyper.to(DEV), nd, 0, wd=0.01)
     torch.cuda.synchronize()
     assert rel_err(pg, pc) < 1e-5
+
+
+@pytest.mark.parametrize('case', [(2, 16, 16, 64, 128, 1, 2, 0), (2, 14, 14, 64, 64, 3, 1, 1),
+                                  (2, 16, 16, 64, 128, 3, 2, 1)])
+def test_conv_dgrad_addend(case):
+    N, H, W, C, Co, K, s, p = case
+    Ho, Wo = Fn.conv_out_hw(H, W, K, K, s, p, 1)
+    dy = _bf(N, Ho, Wo, Co, seed=21)
+    w = _bf(Co, K, K, C, scale=(1.0 / (K * K * C)) ** 0.5, seed=22)
+    add = _bf(N, H, W, C, seed=23)
+    ref = Fn.conv2d_dgrad(dy, w, (N, H, W, C), s, p, addend=add)
+    a = add.to(DEV)
+    out = Fn.conv2d_dgrad(dy.to(DEV), w.to(DEV), (N, H, W, C), s, p, addend=a, out=a)  # in place
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 1e-2

@@ -14,11 +14,11 @@ def _parse():
     decls = {}
     for f in glob.glob(os.path.join(ROOT, 'csrc', 'kernels', '*.hip')):
         src = open(f).read()
-        for m in re.finditer(r'MLC_EXPORT\s+int\s+(\w+)\s*\(([^)]*)\)', src):
+        for m in re.finditer(r'MLC_EXPORT\s+(?:int|void\*)\s+(\w+)\s*\(([^)]*)\)', src):
             args = [a.strip() for a in m.group(2).replace('\n', ' ').split(',') if a.strip()]
             kinds = []
             for a in args:
-                if '*' in a or a.startswith('hipStream_t'):
+                if '*' in a or a.startswith('hipStream_t') or a.startswith('void'):
                     kinds.append('vp')
                 else:
                     kinds.append(_TYPES[a.split()[0]])

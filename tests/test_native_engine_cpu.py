@@ -1,0 +1,71 @@
+"""The native engine (flat arenas, fused conv+BN autograd nodes, fused head, fused SGD)
+against plain PyTorch autograd on the same model, on CPU (reference op paths)."""
+import torch
+import torch.nn.functional as F
+
+from mlcomp_amd.models import build_model
+from mlcomp_amd.models.native_resnet import STEM_CIN
+from mlcomp_amd.train.native_step import NativeClassifierStep
+
+
+def _cos(a, b):
+    a, b = a.flatten().float(), b.flatten().float()
+    return (a @ b / (a.norm() * b.norm() + 1e-12)).item()
+
+
+def test_native_step_matches_torch_autograd():
+    torch.manual_seed(0)
+    tm = build_model('resnet18', num_classes=16)
+    ref = build_model('resnet18', num_classes=16)
+    ref.load_state_dict(tm.state_dict())
+    # give the zero-initialised residual gammas some value so every path carries signal
+    with torch.no_grad():
+        for m in list(tm.modules()):
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.weight.uniform_(0.5, 1.5)
+        ref.load_state_dict(tm.state_dict())
+    step = NativeClassifierStep(torch_model=tm, batch=8, image_size=32, device='cpu',
+                                num_classes=16, lr=0.1, momentum=0.0, weight_decay=0.0,
+                                use_graph=False)
+    x_nhwc = step.x[..., :3].float()
+    x = x_nhwc.permute(0, 3, 1, 2).contiguous()
+    y = step.y
+    ref.train()
+    out = ref(x)
+    loss = F.cross_entropy(out, y)
+    loss.backward()
+    step()
+    assert abs(step.last_loss() - loss.item()) / loss.item() < 0.03
+    arena = step.net.arena
+    # conv weight grads: arena is [Co,KH,KW,Ci]; compare with torch [Co,Ci,KH,KW]
+    # bf16 activations through 18 BN layers over a tiny batch: a pure torch bf16 run of
+    # this same model/batch reaches cosine ~0.87-0.96 vs fp32 (checked when writing this
+    # test), so the bar is "at least as close as stock bf16"
+    g_stem = arena.by_name['stem.conv.weight'].grad[..., :3].permute(0, 3, 1, 2)
+    assert _cos(g_stem, ref.stem.conv.weight.grad) > 0.85
+    g = arena.by_name['layer2.0.cb1.conv.weight'].grad.permute(0, 3, 1, 2)
+    assert _cos(g, ref.layer2[0].cb1.conv.weight.grad) > 0.85
+    assert _cos(arena.by_name['fc.weight'].grad[:16], ref.fc.weight.grad) > 0.99
+    assert _cos(arena.by_name['layer4.1.cb2.bn.weight'].grad, ref.layer4[1].cb2.bn.weight.grad) > 0.95
+    # padded stem input channels never receive gradient
+    assert arena.by_name['stem.conv.weight'].grad[..., 3:].abs().max() == 0
+    # SGD applied: master = old - lr * grad
+    new_fc = arena.by_name['fc.weight'].master[:16]
+    exp = ref.fc.weight.detach() - 0.1 * arena.by_name['fc.weight'].grad[:16]
+    assert torch.allclose(new_fc, exp, atol=1e-6)
+
+
+def test_native_export_roundtrip():
+    torch.manual_seed(1)
+    tm = build_model('resnet18', num_classes=10)   # 10 -> padded to 16 internally
+    sd = {k: v.clone() for k, v in tm.state_dict().items()}
+    step = NativeClassifierStep(torch_model=tm, batch=8, image_size=32, device='cpu',
+                                num_classes=10, use_graph=False)
+    step()  # padded fc rows must stay exactly zero after a step
+    w = step.net.arena.by_name['fc.weight']
+    assert w.master[10:].abs().max() == 0 and w.grad[10:].abs().max() == 0
+    step = NativeClassifierStep(torch_model=tm, batch=8, image_size=32, device='cpu',
+                                num_classes=10, use_graph=False)
+    step.net.export_to_torch()
+    for k, v in tm.state_dict().items():
+        assert torch.allclose(v.float(), sd[k].float()), k
