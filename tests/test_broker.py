@@ -1,0 +1,112 @@
+"""Transport: the native mlcomp-broker daemon (csrc/broker/broker.cpp) and the
+in-process broker obey the same contract (FIFO, blocking pop, lease/ack/requeue on
+disconnect, revoke, result store)."""
+import os
+import socket
+import subprocess
+import threading
+import time
+
+import pytest
+
+from mlcomp_amd.broker import BrokerClient, InProcBroker
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture
+def daemon():
+    from mlcomp_amd.build import build_broker
+    binary = build_broker()
+    port = _free_port()
+    p = subprocess.Popen([binary, '--host', '127.0.0.1', '--port', str(port)], stdout=subprocess.PIPE)
+    p.stdout.readline()
+    yield port
+    p.kill()
+    p.wait()
+
+
+@pytest.fixture(params=['native', 'inproc'])
+def broker_factory(request):
+    if request.param == 'inproc':
+        b = InProcBroker()
+        yield lambda: b
+    else:
+        port = request.getfixturevalue('daemon')
+        clients = []
+
+        def make():
+            c = BrokerClient('127.0.0.1', port)
+            clients.append(c)
+            return c
+        yield make
+        for c in clients:
+            c.close()
+
+
+def test_fifo_ack_revoke_results(broker_factory):
+    b = broker_factory()
+    assert b.ping()
+    ids = [b.push('q1', {'task': 'execute', 'args': [i]}) for i in range(3)]
+    assert b.queue_len('q1') == 3
+    assert b.revoke(ids[1]) is True
+    assert b.revoke('999999') is False
+    q, m = b.pop(['q0', 'q1'], 0.5)
+    assert q == 'q1' and m['args'] == [0] and m['id'] == ids[0]
+    b.ack(m['id'])
+    q, m = b.pop(['q1'], 0.5)
+    assert m['args'] == [2]
+    b.nack(m['id'])                       # back to the head
+    q, m2 = b.pop(['q1'], 0.5)
+    assert m2['args'] == [2]
+    b.ack(m2['id'])
+    assert b.pop(['q1'], 0.05) is None
+    b.set_result('k', {'x': [1, 2]})
+    assert b.get_result('k', 0.5) == {'x': [1, 2]}
+    assert b.get_result('k', 0.05) is None
+
+
+def test_blocking_pop_is_woken(broker_factory):
+    consumer = broker_factory()
+    producer = broker_factory()
+    got = []
+    t = threading.Thread(target=lambda: got.append(consumer.pop(['w'], 5.0)))
+    t.start()
+    time.sleep(0.2)
+    producer.push('w', {'task': 'kill', 'args': [1]})
+    t.join(3)
+    assert got and got[0][1]['task'] == 'kill'
+
+
+def test_rpc_call(broker_factory):
+    server = broker_factory()
+    client = broker_factory()
+
+    def serve():
+        q, m = server.pop(['ctl'], 5.0)
+        server.set_result(m['reply'], sum(m['args']))
+        server.ack(m['id'])
+    t = threading.Thread(target=serve)
+    t.start()
+    assert client.call('ctl', 'add', 2, 3, timeout=5.0) == 5
+    t.join()
+
+
+def test_lease_requeued_when_consumer_dies(daemon):
+    a = BrokerClient('127.0.0.1', daemon)
+    a.push('jobs', {'task': 'execute', 'args': [7]})
+    consumer = BrokerClient('127.0.0.1', daemon)
+    q, m = consumer.pop(['jobs'], 1.0)
+    assert a.queue_len('jobs') == 0
+    consumer.close()                      # dies without ACK
+    deadline = time.time() + 2
+    while a.queue_len('jobs') == 0 and time.time() < deadline:
+        time.sleep(0.02)
+    q, m2 = a.pop(['jobs'], 1.0)
+    assert m2['args'] == [7]
