@@ -1,0 +1,1 @@
+"""Server side: scheduler (supervisor) and REST API."""

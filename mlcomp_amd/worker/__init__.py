@@ -1,0 +1,1 @@
+"""Worker runtime: task lifecycle, executors, code storage, worker pool and daemon."""
