@@ -1,0 +1,63 @@
+"""Extra model families for config-driven training.
+
+* ``Pretrained`` - the reference's classification wrapper
+  (`mlcomp/contrib/model/pretrained.py:8-58`): a registered backbone (``variant``)
+  with its classifier resized to ``num_classes`` and an optional output activation.
+  There is no network access, so ``pretrained`` takes a local checkpoint path
+  (loaded with ``weights_only=True``) instead of downloading.
+* ``SimpleCNN`` - small LeNet-style net for MNIST/CIFAR-shaped smoke configs.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import MODELS, register
+
+
+def _activation(a):
+    if a is None or callable(a):
+        return a
+    if a == 'softmax':
+        return nn.Softmax(dim=1)
+    if a == 'sigmoid':
+        return nn.Sigmoid()
+    raise ValueError('activation should be "sigmoid"/"softmax"/callable/None')
+
+
+@register('Pretrained')
+class Pretrained(nn.Module):
+    def __init__(self, variant: str, num_classes: int, pretrained=None, activation=None, **kw):
+        super().__init__()
+        self.model = MODELS[variant](num_classes=num_classes, **kw)
+        if isinstance(pretrained, str):
+            sd = torch.load(pretrained, map_location='cpu', weights_only=True)
+            sd = sd.get('model_state_dict', sd)
+            own = self.model.state_dict()
+            sd = {k: v for k, v in sd.items() if k in own and own[k].shape == v.shape}
+            self.model.load_state_dict(sd, strict=False)
+        self.activation = _activation(activation)
+
+    def forward(self, x):
+        y = self.model(x)
+        if isinstance(y, tuple):
+            y = y[0]
+        return self.activation(y) if self.activation else y
+
+
+@register('SimpleCNN')
+class SimpleCNN(nn.Module):
+    def __init__(self, in_channels: int = 3, num_classes: int = 10, width: int = 16, image_size: int = 32):
+        super().__init__()
+        self.features = nn.Sequential(
+            nn.Conv2d(in_channels, width, 3, padding=1), nn.BatchNorm2d(width), nn.ReLU(inplace=True),
+            nn.MaxPool2d(2),
+            nn.Conv2d(width, 2 * width, 3, padding=1), nn.BatchNorm2d(2 * width), nn.ReLU(inplace=True),
+            nn.AdaptiveAvgPool2d(1))
+        self.fc = nn.Linear(2 * width, num_classes)
+
+    def forward(self, x):
+        return self.fc(self.features(x).flatten(1))
+
+
+__all__ = ['Pretrained', 'SimpleCNN']

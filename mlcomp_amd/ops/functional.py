@@ -157,6 +157,24 @@ def bn_fwd_apply(y, res, s1, s2, gamma, beta, save_mean, save_invstd, run_mean, 
     return z
 
 
+def bn_apply(y, res, scale, shift, relu=True):
+    """z = act(y*scale + shift [+ res]) with precomputed per-channel scale/shift
+    (inference BatchNorm / frozen BN)."""
+    rows = y.numel() // y.shape[-1]
+    C = y.shape[-1]
+    if _cuda(y):
+        z = torch.empty_like(y)
+        _lib.call('mlc_bn_fwd_apply', _lib.ptr(y), _lib.ptr(res), _lib.ptr(z), _lib.ptr(scale),
+                  _lib.ptr(shift), rows, C, int(relu), _lib.stream())
+        return z
+    zf = y.float() * scale + shift
+    if res is not None:
+        zf = zf + res.float()
+    if relu:
+        zf = zf.clamp_min(0)
+    return zf.to(torch.bfloat16)
+
+
 def bn_bwd(dz, z, y, mean, invstd, gamma, want_dres=False, dgamma=None, dbeta=None, sums=None,
            zero_sums=True, coef=None):
     """Backward of z = act(BN(y) [+res]).  ``z`` is the saved output (ReLU mask) or None

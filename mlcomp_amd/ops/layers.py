@@ -129,6 +129,12 @@ class ConvBN:
     # raw (autograd-free) halves, composed by the block-level Functions
     def fwd(self, x, res=None):
         ws = self.ctx.ws
+        if not self.ctx.training:  # inference BN: running statistics, no stat epilogue
+            y = Fn.conv2d_fwd(x, self.w.bf16, self.stride, self.pad, self.dil)
+            scale = self.gamma.master * torch.rsqrt(self.run_var + self.eps)
+            shift = self.beta.master - self.run_mean * scale
+            z = Fn.bn_apply(y, res, scale.contiguous(), shift.contiguous(), self.act)
+            return z, (x, y, z)
         s1, s2 = ws[self.k_s1], ws[self.k_s2]
         y = Fn.conv2d_fwd(x, self.w.bf16, self.stride, self.pad, self.dil, stats=(s1, s2))
         training = self.ctx.training

@@ -1,0 +1,257 @@
+"""Training callbacks (the Catalyst 20.3 callback set the reference's YAML configs use:
+CriterionCallback, OptimizerCallback, AccuracyCallback, SchedulerCallback,
+CheckpointCallback, plus TimerCallback / EarlyStoppingCallback / InferCallback).
+
+Order (``order`` attribute): timer -> criterion -> optimizer -> metrics -> scheduler ->
+checkpoint -> user callbacks.  Hooks: on_stage_start/end, on_epoch_start/end,
+on_loader_start/end, on_batch_start/end.
+"""
+from __future__ import annotations
+
+import os
+import time
+from collections import OrderedDict
+from typing import Dict, Optional
+
+import torch
+
+CALLBACKS: Dict[str, type] = {}
+
+
+def register_callback(cls):
+    CALLBACKS[cls.__name__] = cls
+    return cls
+
+
+class Callback:
+    order = 50
+    master_only = False   # only run on rank 0 in DDP
+
+    def on_stage_start(self, state): ...
+    def on_stage_end(self, state): ...
+    def on_epoch_start(self, state): ...
+    def on_epoch_end(self, state): ...
+    def on_loader_start(self, state): ...
+    def on_loader_end(self, state): ...
+    def on_batch_start(self, state): ...
+    def on_batch_end(self, state): ...
+    def on_exception(self, state): ...
+
+
+@register_callback
+class TimerCallback(Callback):
+    """``_timer/_fps`` (samples/s of this rank and, under DDP, ``_timer/_fps_node``
+    = whole-node throughput), ``data_time``, ``model_time``, ``batch_time``."""
+    order = 0
+
+    def on_loader_start(self, state):
+        self.t_end = time.time()
+        self.acc = {'data_time': 0.0, 'model_time': 0.0, 'batch_time': 0.0, 'n': 0, 'samples': 0}
+
+    def on_batch_start(self, state):
+        now = time.time()
+        self.t_start = now
+        self.acc['data_time'] += now - self.t_end
+
+    def on_batch_end(self, state):
+        now = time.time()
+        self.acc['model_time'] += now - self.t_start
+        self.acc['batch_time'] += now - self.t_end
+        self.acc['n'] += 1
+        self.acc['samples'] += state.batch_size
+        self.t_end = now
+
+    def on_loader_end(self, state):
+        n = max(1, self.acc['n'])
+        for k in ('data_time', 'model_time', 'batch_time'):
+            state.loader_metrics[f'_timer/{k}'] = self.acc[k] / n
+        fps = self.acc['samples'] / max(1e-9, self.acc['batch_time'])
+        state.loader_metrics['_timer/_fps'] = fps
+        if state.world_size > 1:
+            state.loader_metrics['_timer/_fps_node'] = fps * state.world_size
+
+
+@register_callback
+class CriterionCallback(Callback):
+    order = 10
+
+    def __init__(self, input_key='targets', output_key='logits', prefix='loss', multiplier=1.0):
+        self.input_key, self.output_key, self.prefix, self.multiplier = input_key, output_key, prefix, multiplier
+
+    def on_batch_end(self, state):
+        if state.loss is None and state.output is not None:
+            state.loss = state.criterion(state.output[self.output_key], state.input[self.input_key]) * self.multiplier
+        if state.loss is not None:
+            state.batch_metrics[self.prefix] = float(state.loss.detach())
+
+
+@register_callback
+class OptimizerCallback(Callback):
+    order = 20
+
+    def __init__(self, grad_clip_params=None, accumulation_steps=1):
+        self.accumulation_steps = accumulation_steps
+        self.clip = (grad_clip_params or {}).get('max_norm') if grad_clip_params else None
+
+    def on_batch_end(self, state):
+        if not state.is_train or state.native or state.loss is None:
+            return
+        (state.loss / self.accumulation_steps).backward()
+        state.step_count += 1
+        if state.step_count % self.accumulation_steps == 0:
+            if self.clip:
+                torch.nn.utils.clip_grad_norm_(state.model.parameters(), self.clip)
+            state.optimizer.step()
+            state.optimizer.zero_grad(set_to_none=True)
+
+
+@register_callback
+class AccuracyCallback(Callback):
+    order = 30
+
+    def __init__(self, input_key='targets', output_key='logits', prefix='accuracy', accuracy_args=(1,)):
+        self.input_key, self.output_key, self.prefix = input_key, output_key, prefix
+        self.topk = list(accuracy_args or [1])
+
+    def on_batch_end(self, state):
+        if state.native_correct is not None and self.topk == [1]:
+            state.batch_metrics[f'{self.prefix}01'] = state.native_correct / max(1, state.batch_size)
+            return
+        out = state.output.get(self.output_key) if state.output else None
+        if out is None:
+            return
+        y = state.input[self.input_key]
+        maxk = max(self.topk)
+        pred = out.float().topk(maxk, 1).indices
+        correct = pred.eq(y.view(-1, 1))
+        for k in self.topk:
+            state.batch_metrics[f'{self.prefix}{k:02d}'] = float(correct[:, :k].any(1).float().mean())
+
+
+@register_callback
+class SchedulerCallback(Callback):
+    order = 40
+
+    def __init__(self, reduced_metric='loss', mode='epoch'):
+        self.reduced_metric = reduced_metric
+        self.mode = mode
+
+    def on_batch_end(self, state):
+        if self.mode == 'batch' and state.is_train and state.scheduler is not None:
+            state.scheduler.step()
+            state.sync_lr()
+
+    def on_epoch_end(self, state):
+        if self.mode != 'epoch' or state.scheduler is None:
+            return
+        if isinstance(state.scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
+            state.scheduler.step(state.valid_metrics.get(self.reduced_metric, 0.0))
+        else:
+            state.scheduler.step()
+        state.sync_lr()
+        state.epoch_metrics['lr'] = state.current_lr()
+
+
+@register_callback
+class CheckpointCallback(Callback):
+    """``logdir/checkpoints/{best,last}_full.pth`` (model + optimizer + scheduler +
+    ``stage`` + ``checkpoint_data.epoch``) and ``{best,last}.pth`` (weights only) - the
+    file names and keys the reference's resume logic consumes
+    (`catalyst_.py:267-347`).  Rank 0 only."""
+    order = 90
+    master_only = True
+
+    def __init__(self, save_n_best=1, resume=None, resume_dir=None):
+        self.save_n_best = save_n_best
+        self.resume = resume
+        self.best_score = None
+
+    def on_stage_start(self, state):
+        if self.resume and os.path.exists(self.resume):
+            ckpt = torch.load(self.resume, map_location='cpu', weights_only=True)
+            state.load_checkpoint(ckpt)
+            self.best_score = ckpt.get('best_score')
+            self.resume = None
+
+    def on_epoch_end(self, state):
+        if not state.logdir:
+            return
+        d = os.path.join(state.logdir, 'checkpoints')
+        os.makedirs(d, exist_ok=True)
+        ckpt = state.make_checkpoint()
+        score = state.valid_metrics.get(state.main_metric)
+        is_best = score is not None and (self.best_score is None or
+                                         (score < self.best_score if state.minimize_metric
+                                          else score > self.best_score))
+        if is_best:
+            self.best_score = score
+        ckpt['best_score'] = self.best_score
+        torch.save(ckpt, os.path.join(d, 'last_full.pth'))
+        torch.save({'model_state_dict': ckpt['model_state_dict']}, os.path.join(d, 'last.pth'))
+        if is_best:
+            torch.save(ckpt, os.path.join(d, 'best_full.pth'))
+            torch.save({'model_state_dict': ckpt['model_state_dict']}, os.path.join(d, 'best.pth'))
+
+
+@register_callback
+class EarlyStoppingCallback(Callback):
+    order = 95
+
+    def __init__(self, patience=5, metric='loss', minimize=True, min_delta=1e-6):
+        self.patience, self.metric, self.minimize, self.min_delta = patience, metric, minimize, min_delta
+        self.best, self.bad = None, 0
+
+    def on_epoch_end(self, state):
+        v = state.valid_metrics.get(self.metric)
+        if v is None:
+            return
+        better = self.best is None or (v < self.best - self.min_delta if self.minimize
+                                       else v > self.best + self.min_delta)
+        if better:
+            self.best, self.bad = v, 0
+        else:
+            self.bad += 1
+            if self.bad >= self.patience:
+                state.need_early_stop = True
+
+
+@register_callback
+class InferCallback(Callback):
+    """Collects the ``logits`` of every loader and saves ``<out_dir>/<loader>.npy``
+    (`mlcomp/contrib/catalyst/callbacks/inference.py:10-49`)."""
+    order = 100
+    master_only = True
+
+    def __init__(self, out_dir='infer', out_prefix=None, key='logits'):
+        self.out_dir, self.key = out_dir, key
+        self.store = {}
+
+    def on_loader_start(self, state):
+        self.store[state.loader_name] = []
+
+    def on_batch_end(self, state):
+        if state.output and self.key in state.output:
+            self.store[state.loader_name].append(state.output[self.key].detach().float().cpu())
+
+    def on_loader_end(self, state):
+        import numpy as np
+        out = self.store.get(state.loader_name)
+        if out:
+            os.makedirs(self.out_dir, exist_ok=True)
+            np.save(os.path.join(self.out_dir, f'{state.loader_name}.npy'), torch.cat(out).numpy())
+
+
+def build_callbacks(params: dict) -> 'OrderedDict[str, Callback]':
+    out = OrderedDict()
+    for name, p in (params or {}).items():
+        p = dict(p or {})
+        cls_name = p.pop('callback')
+        if cls_name not in CALLBACKS:
+            raise KeyError(f'unknown callback {cls_name}; known: {sorted(CALLBACKS)}')
+        out[name] = CALLBACKS[cls_name](**p)
+    if not any(isinstance(c, TimerCallback) for c in out.values()):
+        out['_timer'] = TimerCallback()
+    return out
+
+
+__all__ = ['Callback', 'CALLBACKS', 'register_callback', 'build_callbacks'] + list(CALLBACKS)

@@ -1,0 +1,153 @@
+"""Config-driven experiment (replacement for Catalyst's ``ConfigExperiment`` that the
+reference delegates to, `catalyst_.py:365-430`).
+
+Config layout (the YAML the reference's examples use)::
+
+    model_params: {model: <registered name>, ...kwargs}
+    args: {expdir, logdir, seed, engine: auto|native|torch, ...}
+    distributed_params: {...}
+    stages:
+      data_params / state_params / criterion_params / optimizer_params /
+      scheduler_params / callbacks_params   # shared defaults
+      <stage name>: {same sections, overriding the defaults}
+
+User code may subclass :class:`ConfigExperiment` in ``<expdir>/experiment.py`` (class
+``Experiment``) and override ``get_datasets`` / ``get_model`` / ``get_transforms``.
+"""
+from __future__ import annotations
+
+import importlib.util
+import os
+import sys
+from collections import OrderedDict
+from copy import deepcopy
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+from .callbacks import build_callbacks
+
+SECTIONS = ('data_params', 'state_params', 'criterion_params', 'optimizer_params',
+            'scheduler_params', 'callbacks_params')
+
+CRITERIONS = {}
+
+
+def register_criterion(name):
+    def deco(fn):
+        CRITERIONS[name] = fn
+        return fn
+    return deco
+
+
+def _merge(a: dict, b: dict) -> dict:
+    out = deepcopy(a)
+    for k, v in (b or {}).items():
+        if isinstance(v, dict) and isinstance(out.get(k), dict):
+            out[k] = _merge(out[k], v)
+        else:
+            out[k] = deepcopy(v)
+    return out
+
+
+class ConfigExperiment:
+    def __init__(self, config: dict):
+        self._config = deepcopy(config)
+        self.args = self._config.get('args', {}) or {}
+        self.logdir = self.args.get('logdir')
+        self.distributed_params = self._config.get('distributed_params', {}) or {}
+        stages = deepcopy(self._config.get('stages', {}) or {})
+        shared = {k: stages.pop(k) for k in list(stages) if k in SECTIONS}
+        names = [k for k, v in stages.items() if isinstance(v, dict)]
+        if not names:
+            names = ['stage1']
+            stages['stage1'] = {}
+        self.stages_config: 'OrderedDict[str, dict]' = OrderedDict(
+            (n, _merge(shared, stages[n])) for n in names)
+
+    @property
+    def stages(self) -> List[str]:
+        return list(self.stages_config)
+
+    def stage_params(self, stage: str, section: str) -> dict:
+        return deepcopy(self.stages_config[stage].get(section, {}) or {})
+
+    # ------------------------------------------------------------------ components
+    def get_model(self, stage: str = None) -> nn.Module:
+        from mlcomp_amd.models import build_model
+        p = deepcopy(self._config.get('model_params', {}) or {})
+        name = p.pop('model', None) or p.pop('variant', None)
+        if name is None:
+            raise ValueError('model_params.model is required')
+        if 'variant' in p and name in ('Pretrained', 'pretrained'):
+            name = p.pop('variant')
+        return build_model(name, **p)
+
+    def get_criterion(self, stage: str):
+        p = self.stage_params(stage, 'criterion_params')
+        name = p.pop('criterion', 'CrossEntropyLoss')
+        if name in CRITERIONS:
+            return CRITERIONS[name](**p)
+        from mlcomp_amd.contrib import criterion as C
+        if hasattr(C, name):
+            return getattr(C, name)(**p)
+        return getattr(nn, name)(**p)
+
+    def get_optimizer(self, stage: str, model: nn.Module):
+        p = self.stage_params(stage, 'optimizer_params')
+        name = p.pop('optimizer', 'Adam')
+        p.pop('layerwise_params', None)
+        return getattr(torch.optim, name)(model.parameters(), **p)
+
+    def optimizer_spec(self, stage: str) -> dict:
+        return self.stage_params(stage, 'optimizer_params')
+
+    def get_scheduler(self, stage: str, optimizer):
+        p = self.stage_params(stage, 'scheduler_params')
+        name = p.pop('scheduler', None)
+        if not name:
+            return None
+        from mlcomp_amd.contrib import optim as O
+        if hasattr(O, name):
+            return getattr(O, name)(optimizer, **p)
+        return getattr(torch.optim.lr_scheduler, name)(optimizer, **p)
+
+    def get_callbacks(self, stage: str):
+        return build_callbacks(self.stage_params(stage, 'callbacks_params'))
+
+    def get_transforms(self, stage: str = None, dataset: str = None):
+        return None
+
+    def get_datasets(self, stage: str, **data_params) -> 'OrderedDict[str, object]':
+        from .data import DATASETS
+        name = data_params.get('dataset')
+        if name is None:
+            raise NotImplementedError('override get_datasets or set data_params.dataset')
+        cls = DATASETS[name]
+        out = OrderedDict()
+        kw = {k: v for k, v in data_params.items() if k not in ('dataset', 'batch_size', 'num_workers')}
+        out['train'] = cls(**kw)
+        if data_params.get('valid_samples', 0):
+            out['valid'] = cls(**dict(kw, num_samples=data_params['valid_samples'], seed=kw.get('seed', 0) + 1))
+        return out
+
+    def get_state_params(self, stage: str) -> dict:
+        return self.stage_params(stage, 'state_params')
+
+
+def import_experiment(expdir: str) -> type:
+    """``Experiment`` class from ``<expdir>/experiment.py`` if present."""
+    path = os.path.join(expdir or '.', 'experiment.py')
+    if not os.path.exists(path):
+        return ConfigExperiment
+    folder = os.path.abspath(expdir or '.')
+    if folder not in sys.path:   # experiment.py imports its siblings (model.py, dataset.py)
+        sys.path.insert(0, folder)
+    spec = importlib.util.spec_from_file_location('mlcomp_user_experiment', path)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return getattr(m, 'Experiment', ConfigExperiment)
+
+
+__all__ = ['ConfigExperiment', 'import_experiment', 'register_criterion', 'SECTIONS']

@@ -1,0 +1,345 @@
+"""Stage / epoch / loader / batch training loop with callbacks (replacement for the
+Catalyst runner the reference executes, `catalyst_.py:365-430`).
+
+Two engines behind one loop:
+
+* ``torch`` - any ``nn.Module``: autocast(bf16) forward, criterion, backward,
+  ``torch.optim`` step; DDP through ``torch.nn.parallel.DistributedDataParallel``
+  (backend "nccl" == RCCL on ROCm) when ``world_size > 1``.
+* ``native`` - ResNet-family classifiers (``groups == 1``) on a GPU: the whole step
+  runs through :class:`~mlcomp_amd.train.native_step.NativeClassifierStep` (hand-written
+  HIP kernels, flat arenas, fused optimizer, RCCL bucketer, HIP-graph replay).  Loss and
+  accuracy are accumulated on the device and read once per loader, so the graph replays
+  back to back without host syncs.
+
+``engine: auto`` (default) picks native when the model/device qualify.
+"""
+from __future__ import annotations
+
+import time
+from collections import OrderedDict, defaultdict
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+from .callbacks import Callback
+from .data import DeviceSyntheticLoader, make_loader
+from .experiment import ConfigExperiment
+
+
+class State:
+    def __init__(self):
+        self.stage = None
+        self.epoch = 0
+        self.num_epochs = 1
+        self.loader_name = None
+        self.is_train = True
+        self.input = None
+        self.output = None
+        self.loss = None
+        self.batch_size = 0
+        self.batch_metrics: Dict[str, float] = {}
+        self.loader_metrics: Dict[str, float] = {}
+        self.epoch_metrics: Dict[str, float] = {}
+        self.valid_metrics: Dict[str, float] = {}
+        self.loaders = OrderedDict()
+        self.loader_step = 0
+        self.loader_len = 0
+        self.main_metric = 'loss'
+        self.minimize_metric = True
+        self.need_early_stop = False
+        self.step_count = 0
+        self.native = False
+        self.native_correct = None
+        self.world_size = 1
+        self.rank = 0
+        self.logdir = None
+        self.checkpoint_data = {}
+        self.runner = None
+
+    # delegated to the runner
+    @property
+    def model(self):
+        return self.runner.model
+
+    @property
+    def optimizer(self):
+        return self.runner.optimizer
+
+    @property
+    def scheduler(self):
+        return self.runner.scheduler
+
+    @property
+    def criterion(self):
+        return self.runner.criterion
+
+    def make_checkpoint(self) -> dict:
+        return self.runner.make_checkpoint()
+
+    def load_checkpoint(self, ckpt: dict):
+        self.runner.load_checkpoint(ckpt)
+
+    def sync_lr(self):
+        self.runner.sync_lr()
+
+    def current_lr(self) -> float:
+        return self.runner.current_lr()
+
+
+def _native_capable(model: nn.Module, device: torch.device) -> bool:
+    from mlcomp_amd.models.resnet import ResNet
+    return device.type == 'cuda' and isinstance(model, ResNet) and model.groups == 1 and model.include_top
+
+
+class Runner:
+    def __init__(self, experiment: ConfigExperiment, device=None, extra_callbacks=None,
+                 rank: int = 0, world_size: int = 1, engine: Optional[str] = None):
+        self.experiment = experiment
+        self.device = torch.device(device or ('cuda' if torch.cuda.is_available() else 'cpu'))
+        self.extra_callbacks = extra_callbacks or OrderedDict()
+        self.rank, self.world_size = rank, world_size
+        self.engine = engine or experiment.args.get('engine', 'auto')
+        self.model: Optional[nn.Module] = None
+        self.ddp_model = None
+        self.native_step = None
+        self.optimizer = self.scheduler = self.criterion = None
+        self.state = State()
+        self.state.runner = self
+        self.state.rank, self.state.world_size = rank, world_size
+        self.state.logdir = experiment.logdir
+        self.exception = None
+
+    # ------------------------------------------------------------------ setup
+    def _build_model(self, stage):
+        if self.model is None:
+            self.model = self.experiment.get_model(stage)
+        use_native = self.engine == 'native' or (self.engine == 'auto' and _native_capable(self.model, self.device))
+        if self.engine == 'native' and not _native_capable(self.model, self.device):
+            raise RuntimeError('engine: native needs a ResNet-family classifier (groups=1) on a GPU')
+        self.state.native = use_native
+        if not use_native:
+            self.model.to(self.device)
+            if self.device.type == 'cuda':
+                self.model = self.model.to(memory_format=torch.channels_last)
+            if self.world_size > 1:
+                from torch.nn.parallel import DistributedDataParallel as DDP
+                ids = [self.device.index] if self.device.type == 'cuda' else None
+                self.ddp_model = DDP(self.model, device_ids=ids)
+            else:
+                self.ddp_model = self.model
+
+    def _build_native(self, stage, batch):
+        from .native_step import NativeClassifierStep
+        spec = self.experiment.optimizer_spec(stage)
+        name = spec.get('optimizer', 'SGD')
+        x = batch['features']
+        size = x.shape[1] if x.dtype == torch.bfloat16 and x.shape[-1] == 8 else x.shape[-1]
+        self.native_step = NativeClassifierStep(
+            torch_model=self.model, batch=x.shape[0], image_size=size, device=self.device,
+            world_size=self.world_size, num_classes=self.model.fc.out_features,
+            lr=spec.get('lr', 0.1), momentum=spec.get('momentum', 0.9 if name == 'SGD' else 0.0),
+            weight_decay=spec.get('weight_decay', 0.0), nesterov=spec.get('nesterov', False),
+            use_graph=self.experiment.args.get('graph', True), optimizer=name,
+            betas=tuple(spec.get('betas', (0.9, 0.999))), eps=spec.get('eps', 1e-8))
+        # a torch optimizer over one dummy tensor drives torch LR schedulers
+        dummy = torch.zeros(1, requires_grad=True)
+        self.optimizer = torch.optim.SGD([dummy], lr=spec.get('lr', 0.1))
+        self.scheduler = self.experiment.get_scheduler(stage, self.optimizer)
+
+    def sync_lr(self):
+        if self.native_step is not None:
+            self.native_step.set_lr(self.optimizer.param_groups[0]['lr'])
+
+    def current_lr(self) -> float:
+        return float(self.optimizer.param_groups[0]['lr']) if self.optimizer else 0.0
+
+    def _loaders(self, stage) -> 'OrderedDict[str, object]':
+        dp = self.experiment.stage_params(stage, 'data_params')
+        bs = int(dp.get('batch_size', 32))
+        if dp.get('dataset') == 'synthetic_classification' and dp.get('on_device') and self.device.type == 'cuda':
+            from mlcomp_amd.models.native_resnet import STEM_CIN
+            kw = {k: v for k, v in dp.items() if k not in ('dataset', 'batch_size', 'on_device')}
+            steps = int(dp.get('steps', max(1, int(dp.get('num_samples', bs)) // (bs * self.world_size))))
+            out = OrderedDict(train=DeviceSyntheticLoader(bs, steps, device=self.device,
+                                                          nhwc_pad=STEM_CIN if self.state.native else None,
+                                                          seed=self.rank, **kw))
+            return out
+        datasets = self.experiment.get_datasets(stage, **dp)
+        out = OrderedDict()
+        for name, ds in datasets.items():
+            if isinstance(ds, dict):  # {'dataset': ds, 'sampler': ...}
+                ds, sampler = ds['dataset'], ds.get('sampler')
+            else:
+                sampler = None
+            out[name] = make_loader(ds, bs, shuffle=name.startswith('train'), sampler=sampler,
+                                    num_workers=int(dp.get('num_workers', 0)), world_size=self.world_size,
+                                    rank=self.rank, drop_last=self.state.native and name.startswith('train'))
+        return out
+
+    def _callbacks(self, stage) -> List[Callback]:
+        cbs = OrderedDict(self.experiment.get_callbacks(stage))
+        cbs.update(self.extra_callbacks)
+        out = [c for c in cbs.values() if not (c.master_only and self.rank != 0)]
+        return sorted(out, key=lambda c: c.order)
+
+    def _fire(self, event: str):
+        for c in self.callbacks:
+            getattr(c, event)(self.state)
+
+    # ------------------------------------------------------------------ checkpoints
+    def make_checkpoint(self) -> dict:
+        if self.native_step is not None:
+            self.native_step.net.export_to_torch()
+        return {'stage': self.state.stage, 'epoch': self.state.epoch,
+                'model_state_dict': {k: v.detach().cpu() for k, v in self.model.state_dict().items()},
+                'optimizer_state_dict': self.optimizer.state_dict() if self.optimizer else None,
+                'scheduler_state_dict': self.scheduler.state_dict() if self.scheduler else None,
+                'checkpoint_data': dict(self.state.checkpoint_data, epoch=self.state.epoch),
+                'epoch_metrics': dict(self.state.epoch_metrics),
+                'valid_metrics': dict(self.state.valid_metrics)}
+
+    def load_checkpoint(self, ckpt: dict):
+        self.model.load_state_dict(ckpt['model_state_dict'])
+        if self.native_step is not None:
+            self.native_step = None  # rebuilt from the loaded weights on the next batch
+        if ckpt.get('optimizer_state_dict') and self.optimizer is not None and self.native_step is None \
+                and not self.state.native:
+            try:
+                self.optimizer.load_state_dict(ckpt['optimizer_state_dict'])
+            except ValueError:
+                pass
+
+    # ------------------------------------------------------------------ loops
+    def _run_batch_torch(self, batch):
+        st = self.state
+        x = batch['features'].to(self.device, non_blocking=True)
+        y = batch['targets'].to(self.device, non_blocking=True)
+        if self.device.type == 'cuda' and x.dim() == 4:
+            x = x.contiguous(memory_format=torch.channels_last)
+        st.input = {'features': x, 'targets': y}
+        with torch.set_grad_enabled(st.is_train), \
+                torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.device.type == 'cuda'):
+            out = (self.ddp_model if st.is_train else self.model)(x)
+        st.output = {'logits': out.float() if isinstance(out, torch.Tensor) else out}
+        st.batch_size = x.shape[0]
+
+    def _run_loader(self, name, loader):
+        st = self.state
+        st.loader_name = name
+        st.is_train = name.startswith('train')
+        st.loader_len = len(loader)
+        if hasattr(getattr(loader, 'sampler', None), 'set_epoch'):
+            loader.sampler.set_epoch(st.epoch)
+        st.loader_metrics = {}
+        sums, count = defaultdict(float), 0
+        dev_loss = dev_correct = None
+        n_samples = 0
+        if self.model is not None and not st.native:
+            self.model.train(st.is_train)
+        self._fire('on_loader_start')
+        for i, batch in enumerate(loader):
+            st.loader_step = i + 1
+            st.batch_metrics = {}
+            st.loss = None
+            st.output = None
+            st.native_correct = None
+            self._fire('on_batch_start')
+            if st.native and st.is_train:
+                if self.native_step is None:
+                    self._build_native(st.stage, batch)
+                    self.sync_lr()
+                ns = self.native_step
+                ns.load_batch(batch['features'], batch['targets'])
+                ns()
+                st.batch_size = ns.batch
+                if dev_loss is None:
+                    dev_loss = torch.zeros(2, device=self.device)
+                dev_loss[0] += ns.net.head.loss_sum()[0]
+                dev_loss[1] += ns.net.head.correct()[0]
+                n_samples += ns.batch
+            elif st.native:
+                self._run_native_eval(batch)
+            else:
+                self._run_batch_torch(batch)
+            self._fire('on_batch_end')
+            for k, v in st.batch_metrics.items():
+                sums[k] += v * st.batch_size
+            count += st.batch_size
+        if dev_loss is not None:
+            v = dev_loss.tolist()
+            sums['loss'] += v[0]
+            sums['accuracy01'] += v[1]
+            count = max(count, n_samples)
+        for k, v in sums.items():
+            st.loader_metrics[k] = v / max(1, count)
+        self._fire('on_loader_end')
+        for k, v in st.loader_metrics.items():
+            st.epoch_metrics[f'{name}_{k}'] = v
+
+    def _run_native_eval(self, batch):
+        st = self.state
+        ns = self.native_step
+        x = batch['features'].to(self.device)
+        y = batch['targets'].to(self.device)
+        if x.dtype != torch.bfloat16:
+            from mlcomp_amd.ops import functional as Fn
+            from mlcomp_amd.models.native_resnet import STEM_CIN
+            x = Fn.nchw_to_nhwc(x.float(), pad_to=STEM_CIN)
+        net = ns.net if ns is not None else None
+        if net is None:
+            self._run_batch_torch(batch)
+            return
+        net.eval()
+        with torch.no_grad():
+            logits = net.logits(x).float()
+        net.train()
+        st.input = {'features': x, 'targets': y}
+        st.output = {'logits': logits}
+        st.batch_size = x.shape[0]
+        st.loss = torch.nn.functional.cross_entropy(logits, y)
+
+    def run_stage(self, stage: str, start_epoch: int = 0):
+        st = self.state
+        st.stage = stage
+        sp = self.experiment.get_state_params(stage)
+        st.num_epochs = int(sp.get('num_epochs', 1))
+        st.main_metric = sp.get('main_metric', 'loss')
+        st.minimize_metric = bool(sp.get('minimize_metric', True))
+        st.checkpoint_data = sp.get('checkpoint_data', {}) or {}
+        self._build_model(stage)
+        self.criterion = self.experiment.get_criterion(stage)
+        if not st.native:
+            self.optimizer = self.experiment.get_optimizer(stage, self.model)
+            self.scheduler = self.experiment.get_scheduler(stage, self.optimizer)
+        else:
+            self.native_step = None
+        self.loaders = self._loaders(stage)
+        st.loaders = self.loaders
+        self.callbacks = self._callbacks(stage)
+        self._fire('on_stage_start')
+        for epoch in range(start_epoch, st.num_epochs):
+            st.epoch = epoch
+            st.epoch_metrics = {}
+            self._fire('on_epoch_start')
+            for name, loader in self.loaders.items():
+                self._run_loader(name, loader)
+            valid = 'valid' if 'valid' in self.loaders else next(iter(self.loaders))
+            st.valid_metrics = {k[len(valid) + 1:]: v for k, v in st.epoch_metrics.items()
+                                if k.startswith(valid + '_')}
+            self._fire('on_epoch_end')
+            if st.need_early_stop:
+                st.need_early_stop = False
+                break
+        if self.native_step is not None:
+            self.native_step.net.export_to_torch()
+        self._fire('on_stage_end')
+
+    def run_experiment(self, stages: Optional[List[str]] = None, start_epoch: int = 0):
+        for i, s in enumerate(stages or self.experiment.stages):
+            self.run_stage(s, start_epoch if i == 0 else 0)
+        return self.state
+
+
+__all__ = ['Runner', 'State']

@@ -1,0 +1,187 @@
+"""Config-driven training engine on CPU: experiment parsing, runner loop + callbacks,
+checkpoint/resume, contrib losses/schedulers, gloo DDP (world_size 2) and the
+``catalyst``/``train`` executor run end-to-end through a DAG."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+import yaml
+
+from mlcomp_amd.train.experiment import ConfigExperiment
+from mlcomp_amd.train.runner import Runner
+
+
+def _cfg(logdir, epochs=2, stages=('stage1',), sched=None, n=64):
+    st = {
+        'data_params': {'dataset': 'synthetic_classification', 'batch_size': 16, 'num_samples': n,
+                        'valid_samples': 32, 'image_size': 16, 'num_classes': 4},
+        'state_params': {'num_epochs': epochs, 'main_metric': 'accuracy01', 'minimize_metric': False},
+        'criterion_params': {'criterion': 'CrossEntropyLoss'},
+        'optimizer_params': {'optimizer': 'Adam', 'lr': 0.01},
+        'callbacks_params': {
+            'loss': {'callback': 'CriterionCallback'},
+            'optimizer': {'callback': 'OptimizerCallback'},
+            'accuracy': {'callback': 'AccuracyCallback', 'accuracy_args': [1, 2]},
+            'saver': {'callback': 'CheckpointCallback'},
+        },
+    }
+    if sched:
+        st['scheduler_params'] = sched
+        st['callbacks_params']['scheduler'] = {'callback': 'SchedulerCallback', 'reduced_metric': 'accuracy01'}
+    for s in stages:
+        st[s] = {}
+    return {'model_params': {'model': 'SimpleCNN', 'num_classes': 4, 'width': 8},
+            'args': {'expdir': '.', 'logdir': str(logdir), 'engine': 'torch'},
+            'stages': st}
+
+
+def test_experiment_merges_shared_sections(tmp_path):
+    cfg = _cfg(tmp_path, stages=('warm', 'main'))
+    cfg['stages']['main'] = {'optimizer_params': {'lr': 0.5}}
+    e = ConfigExperiment(cfg)
+    assert e.stages == ['warm', 'main']
+    assert e.stage_params('warm', 'optimizer_params')['lr'] == 0.01
+    assert e.stage_params('main', 'optimizer_params') == {'optimizer': 'Adam', 'lr': 0.5}
+    assert e.stage_params('main', 'data_params')['batch_size'] == 16
+
+
+def test_runner_trains_checkpoints_and_resumes(tmp_path):
+    torch.manual_seed(0)
+    cfg = _cfg(tmp_path, epochs=3, sched={'scheduler': 'OneCycleCosineAnnealLR', 'T_max': 2})
+    r = Runner(ConfigExperiment(cfg), device='cpu')
+    st = r.run_experiment()
+    for k in ('train_loss', 'train_accuracy01', 'train_accuracy02', 'valid_loss', 'valid_accuracy01',
+              'train__timer/_fps', 'lr'):
+        assert k in st.epoch_metrics, k
+    assert st.epoch == 2
+    ck = tmp_path / 'checkpoints'
+    for f in ('last_full.pth', 'best_full.pth', 'last.pth', 'best.pth'):
+        assert (ck / f).exists()
+    d = torch.load(ck / 'last_full.pth', map_location='cpu', weights_only=True)
+    assert d['stage'] == 'stage1' and d['checkpoint_data']['epoch'] == 2
+    # resume: a fresh runner restores the weights from the checkpoint
+    r2 = Runner(ConfigExperiment(cfg), device='cpu')
+    r2.model = r2.experiment.get_model('stage1')
+    r2.model.load_state_dict(d['model_state_dict'])
+    for k, v in r.model.state_dict().items():
+        assert torch.equal(v.cpu(), r2.model.state_dict()[k])
+
+
+def test_runner_learns_separable_data(tmp_path):
+    """A learnable synthetic task: class = sign pattern of the first two pixels."""
+    from collections import OrderedDict
+
+    class Sep(torch.utils.data.Dataset):
+        def __init__(self, n, seed):
+            g = torch.Generator().manual_seed(seed)
+            self.x = torch.randn(n, 3, 8, 8, generator=g)
+            self.y = ((self.x[:, 0].mean((1, 2)) > 0).long() * 2 + (self.x[:, 1].mean((1, 2)) > 0).long())
+
+        def __len__(self):
+            return len(self.y)
+
+        def __getitem__(self, i):
+            return self.x[i], int(self.y[i])
+
+    class E(ConfigExperiment):
+        def get_datasets(self, stage, **kw):
+            return OrderedDict(train=Sep(512, 0), valid=Sep(128, 1))
+
+    cfg = _cfg(tmp_path, epochs=6)
+    cfg['stages']['data_params']['batch_size'] = 32
+    r = Runner(E(cfg), device='cpu')
+    st = r.run_experiment()
+    assert st.valid_metrics['accuracy01'] > 0.6, st.valid_metrics
+
+
+def test_contrib_losses_match_definitions():
+    from mlcomp_amd.contrib.criterion import LabelSmoothingCrossEntropy, RingLoss, triplet_loss
+    torch.manual_seed(0)
+    x = torch.randn(16, 5)
+    y = torch.randint(0, 5, (16,))
+    eps = 0.2
+    ref = (1 - eps) * torch.nn.functional.cross_entropy(x, y) + eps * (-torch.log_softmax(x, 1).mean(1)).mean()
+    assert torch.allclose(LabelSmoothingCrossEntropy(eps)(x, y), ref, atol=1e-6)
+    assert torch.allclose(LabelSmoothingCrossEntropy(eps)(x, y),
+                          torch.nn.functional.cross_entropy(x, y, label_smoothing=eps), atol=1e-6)
+    rl = RingLoss(type='l2', loss_weight=1.0)
+    v = rl(x, y)
+    assert torch.allclose(rl.radius.detach(), x.norm(dim=1).mean().reshape(1))
+    assert v.item() >= torch.nn.functional.cross_entropy(x, y).item() - 1e-6
+    # triplet: brute force over all (a, p, n)
+    e = torch.randn(6, 4)
+    lab = torch.tensor([0, 0, 1, 1, 2, 0])
+    en = torch.nn.functional.normalize(e, dim=1)
+    d = 1 - en @ en.t()
+    vals = []
+    for a in range(6):
+        for p in range(6):
+            for n in range(6):
+                if len({a, p, n}) == 3 and lab[a] == lab[p] and lab[a] != lab[n]:
+                    vals.append(torch.relu(d[a, p] - d[a, n] + 0.3))
+    vals = torch.stack(vals)
+    ref = vals.sum() / ((vals > 1e-8).sum() + 1e-8)
+    assert torch.allclose(triplet_loss(e, lab), ref, atol=1e-5)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ddp_worker(rank, world, port, logdir, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    torch.manual_seed(0)
+    cfg = _cfg(logdir, epochs=1)
+    r = Runner(ConfigExperiment(cfg), device='cpu', rank=rank, world_size=world)
+    st = r.run_experiment()
+    w = torch.cat([p.detach().flatten() for p in r.model.parameters()])
+    torch.save({'w': w, 'n': len(r.loaders['train'].sampler), 'fps_node': st.epoch_metrics.get(
+        'train__timer/_fps_node')}, os.path.join(out, f'r{rank}.pt'))
+    dist.destroy_process_group()
+
+
+def test_ddp_gloo_two_ranks_stay_in_sync(tmp_path):
+    mp.spawn(_ddp_worker, args=(2, _free_port(), str(tmp_path / 'log'), str(tmp_path)), nprocs=2)
+    a = torch.load(tmp_path / 'r0.pt', weights_only=True)
+    b = torch.load(tmp_path / 'r1.pt', weights_only=True)
+    assert a['n'] == b['n'] == 32          # 64 samples split over 2 ranks
+    assert torch.allclose(a['w'], b['w'])  # gradients all-reduced -> identical weights
+    assert a['fps_node'] is not None
+    assert (tmp_path / 'log' / 'checkpoints' / 'last_full.pth').exists()
+
+
+# ---------------------------------------------------------------------------- executor
+from test_lifecycle import _submit, _wait, cluster  # noqa: E402,F401
+
+
+def test_train_executor_through_dag(cluster, tmp_path):
+    from mlcomp_amd.db.core import Session
+    from mlcomp_amd.db.enums import TaskStatus
+    from mlcomp_amd.db.models import ReportSeries, Step, Task
+    cat = _cfg('log', epochs=2, stages=('warm', 'main'))
+    cfg = {'info': {'name': 'trn', 'project': 'p_train', 'layout': 'classify'},
+           'executors': {'train': {'type': 'catalyst', 'args': {'config': 'catalyst.yml'}}}}
+    created = _submit(cluster['tmp'], cfg, files={'catalyst.yml': yaml.safe_dump(cat)})
+    ids = [t.id for t in created[1]] if isinstance(created, tuple) else None
+    if ids is None:
+        s = Session.create_session(key='q')
+        ids = [t.id for t in s.query(Task).all()]
+    res = _wait(cluster['sup'], ids, timeout=240)
+    assert all(v == TaskStatus.Success for v in res.values()), res
+    s = Session.create_session(key='q2')
+    tid = ids[0]
+    series = s.query(ReportSeries).filter(ReportSeries.task == tid).all()
+    names = {(r.part, r.name, r.stage) for r in series}
+    assert ('train', 'loss', 'warm') in names and ('valid', 'accuracy01', 'main') in names
+    steps = s.query(Step).filter(Step.task == tid).all()
+    assert {'warm', 'main'} <= {st.name for st in steps}
+    t = s.get(Task, tid)
+    assert t.score is not None and t.loss is not None
