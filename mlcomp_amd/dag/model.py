@@ -60,4 +60,34 @@ def dag_model_start(session, data: dict):
     return dag_standard(session, config, debug=False, upload_files=False, copy_files_from=data['dag'])
 
 
-__all__ = ['dag_model_add', 'dag_model_start']
+def model_start_begin(session, model_id: int) -> dict:
+    """The project's Pipe DAGs (newest first, one per name) with their pipes ordered by
+    the last time a version was used; feeds the UI's "start model" dialog."""
+    from mlcomp_amd.db.enums import DagType
+    from mlcomp_amd.db.models import Dag
+    model = ModelProvider(session).by_id(model_id)
+    dags = session.query(Dag).filter(Dag.type == DagType.Pipe.value).filter(
+        Dag.project == model.project).order_by(Dag.id.desc()).all()
+    versions = yaml_load(model.equations) or {}
+    seen, res, current = set(), [], None
+    for dag in dags:
+        if dag.name in seen:
+            continue
+        seen.add(dag.name)
+        cfg = yaml_load(dag.config) or {}
+        pipes = []
+        for name in (cfg.get('pipes') or {}):
+            vs = [dict(v) for v in versions.get(name, [])]
+            used = max((str(v.get('used', '')) for v in vs), default='')
+            for v in vs:
+                v.pop('used', None)
+            pipes.append((used, {'name': name, 'versions': vs}))
+        pipes.sort(key=lambda x: x[0], reverse=True)
+        d = {'name': dag.name, 'id': dag.id, 'pipes': [p for _, p in pipes]}
+        res.append(d)
+        if dag.id == model.dag:
+            current = d
+    return {'dags': res, 'dag': current, 'model_id': model_id}
+
+
+__all__ = ['dag_model_add', 'dag_model_start', 'model_start_begin']

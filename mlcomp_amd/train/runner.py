@@ -160,7 +160,7 @@ class Runner:
         bs = int(dp.get('batch_size', 32))
         if dp.get('dataset') == 'synthetic_classification' and dp.get('on_device') and self.device.type == 'cuda':
             from mlcomp_amd.models.native_resnet import STEM_CIN
-            kw = {k: v for k, v in dp.items() if k not in ('dataset', 'batch_size', 'on_device')}
+            kw = {k: v for k, v in dp.items() if k not in ('dataset', 'batch_size', 'on_device', 'steps', 'seed')}
             steps = int(dp.get('steps', max(1, int(dp.get('num_samples', bs)) // (bs * self.world_size))))
             out = OrderedDict(train=DeviceSyntheticLoader(bs, steps, device=self.device,
                                                           nhwc_pad=STEM_CIN if self.state.native else None,

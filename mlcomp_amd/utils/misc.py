@@ -13,7 +13,7 @@ from collections import defaultdict
 from glob import glob
 from itertools import product
 from os.path import join
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import yaml
 
@@ -218,6 +218,20 @@ def disk_usage(path='/') -> Tuple[float, float]:
     return d.used / 2 ** 30, d.total / 2 ** 30
 
 
-__all__ = ['now', 'to_snake', 'yaml_load', 'yaml_dump', 'dict_flatten', 'dict_unflatten',
+def default_network_interface() -> Optional[str]:
+    """Interface of the default IPv4 route (``/proc/net/route``), e.g. for
+    NCCL_SOCKET_IFNAME (RCCL reads the same variable)."""
+    try:
+        with open('/proc/net/route') as f:
+            for line in f.readlines()[1:]:
+                parts = line.split()
+                if len(parts) > 2 and parts[1] == '00000000':
+                    return parts[0]
+    except OSError:
+        pass
+    return None
+
+
+__all__ = ['default_network_interface', 'now', 'to_snake', 'yaml_load', 'yaml_dump', 'dict_flatten', 'dict_unflatten',
            'merge_dicts_smart', 'dict_from_list_str', 'grid_cells', 'cell_name', 'set_global_seed',
            'parse_gpu_range', 'kill_child_processes', 'kill_pid', 'memory_gb', 'disk_usage']

@@ -197,5 +197,34 @@ def remove(path: str) -> bool:
 CONTROL_TASKS = {'kill': kill, 'kill_all': kill_all, 'remove': remove}
 
 
+def remove_from_all(session, path: str):
+    """Ask every online computer's supervisor queue to delete ``path`` (fire-and-forget)."""
+    from mlcomp_amd.broker import get_broker, queue_name
+    from mlcomp_amd.db.providers import DockerProvider
+    b = get_broker()
+    for d in DockerProvider(session).get_online():
+        try:
+            b.send_task(queue_name(d.computer, d.name or 'default', 'supervisor'), 'remove', path)
+        except Exception:
+            pass
+    remove(path) if os.path.exists(path) else None
+
+
+def remove_model_files(session, project_name: str, model_name: str):
+    s = config.get()
+    for suffix in ('.pth', '_weight.pth'):
+        remove_from_all(session, os.path.join(s.MODEL_FOLDER, project_name, model_name + suffix))
+
+
+def remove_task_files(session, task_id: int):
+    remove_from_all(session, os.path.join(config.get().TASK_FOLDER, str(task_id)))
+
+
+def remove_dag_files(session, dag_id: int):
+    from mlcomp_amd.db.providers import TaskProvider
+    for t in TaskProvider(session).by_dag(dag_id):
+        remove_task_files(session, t.id)
+
+
 if __name__ == '__main__':  # python -m mlcomp_amd.worker.tasks <task_id>
     execute_by_id(int(sys.argv[1]), exit_process=False)

@@ -64,3 +64,34 @@ def test_rccl_single_rank():
     assert torch.equal(t, torch.arange(1024, device='cuda', dtype=torch.float32))
     assert torch.equal(out, t)
     comm.close()
+
+
+def test_runner_native_engine_on_device_data(tmp_path):
+    """Config-driven runner picks the native engine for a ResNet on the GPU; checkpoints
+    export the native arenas back into the torch module."""
+    from mlcomp_amd.train.experiment import ConfigExperiment
+    from mlcomp_amd.train.runner import Runner
+    cfg = {'model_params': {'model': 'resnet18', 'num_classes': 10},
+           'args': {'logdir': str(tmp_path), 'engine': 'auto'},
+           'stages': {
+               'data_params': {'dataset': 'synthetic_classification', 'on_device': True,
+                               'batch_size': 32, 'steps': 6, 'image_size': 64, 'num_classes': 10},
+               'state_params': {'num_epochs': 2},
+               'optimizer_params': {'optimizer': 'SGD', 'lr': 0.05, 'momentum': 0.9},
+               'scheduler_params': {'scheduler': 'OneCycleCosineAnnealLR', 'T_max': 2},
+               'callbacks_params': {'loss': {'callback': 'CriterionCallback'},
+                                    'opt': {'callback': 'OptimizerCallback'},
+                                    'acc': {'callback': 'AccuracyCallback'},
+                                    'sched': {'callback': 'SchedulerCallback'},
+                                    'saver': {'callback': 'CheckpointCallback'}},
+               'stage1': {}}}
+    r = Runner(ConfigExperiment(cfg), device='cuda')
+    st = r.run_experiment()
+    assert st.native and r.native_step is not None
+    m = st.epoch_metrics
+    assert m['train_loss'] == m['train_loss'] and m['train_loss'] > 0
+    assert 0 <= m['train_accuracy01'] <= 1
+    ck = torch.load(tmp_path / 'checkpoints' / 'last_full.pth', weights_only=True)
+    w = ck['model_state_dict']['fc.weight']
+    assert torch.isfinite(w).all()
+    assert not torch.equal(w, torch.zeros_like(w))
