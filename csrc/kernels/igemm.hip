@@ -348,9 +348,23 @@ struct DgradOutRows {  // DgradRows order -> NHWC pixel index
   }
 };
 
+// BatchNorm-backward reduction fused into the epilogue of the dgrad that produces the
+// final gradient dU of a BN's output (the branch-point sum is already in via addend):
+//   dU <- dU * [mask > 0]   (ReLU of the BN being differentiated; mask = its output z)
+//   sums_k[slot][0][c] += sum dU,  sums_k[slot][1][c] += sum dU*(y_k - mean_k)
+// for up to two BNs sharing the same dU (a block's last BN and its downsample BN).  The
+// masked dU is what gets stored, so the elementwise BN-backward pass needs neither z
+// nor a separate residual-gradient copy.
+struct BnBwdEpi {
+  const bf16* mask = nullptr;
+  const bf16* y0 = nullptr; const float* mean0 = nullptr; float* sums0 = nullptr;
+  const bf16* y1 = nullptr; const float* mean1 = nullptr; float* sums1 = nullptr;
+};
+
 template <class RowMap = IdentityRows>
 struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / sum of squares
   bf16* out; int ld; float* sum; float* sumsq; RowMap rowmap; const bf16* addend = nullptr;
+  BnBwdEpi bn = {};
   template <int BM, int BN>
   __device__ void apply(f32x16 (&acc)[2][2], char* lds, int m0, int n0, int M, int N,
                         int wm, int wn, int lane, int tid) const {
@@ -390,22 +404,118 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
     constexpr int CPR = BN / 8;              // 16 B chunks per row
     constexpr int RPI = NTHR / CPR;          // rows per iteration
     const int c = tid % CPR;
+    const int nc = n0 + c * 8;
+    const bool red = bn.y0 != nullptr;
+    float mu0[8], mu1[8], s1[8], s2[8], t2[8];
+    if (red) {
 #pragma unroll
-    for (int it = 0; it < BM / RPI; ++it) {
-      const int row = tid / CPR + RPI * it;
-      const int m = m0 + row, n = n0 + c * 8;
-      if (m < M && n < N) {
-        const size_t o = rowmap(m) * ld + n;
-        uint4 v = *reinterpret_cast<const uint4*>(lds + row * RS + c * 16);
-        if (addend) {  // fused residual-gradient sum (dx of a branch point)
-          float a[8], b[8];
+      for (int e = 0; e < 8; ++e) {
+        mu0[e] = nc < N ? bn.mean0[nc + e] : 0.f;
+        mu1[e] = (bn.y1 && nc < N) ? bn.mean1[nc + e] : 0.f;
+        s1[e] = 0.f; s2[e] = 0.f; t2[e] = 0.f;
+      }
+    }
+    if (!addend && !red) {  // plain store (forward convs / GEMMs)
+#pragma unroll
+      for (int it = 0; it < BM / RPI; ++it) {
+        const int row = tid / CPR + RPI * it;
+        const int m = m0 + row;
+        if (m < M && nc < N)
+          *reinterpret_cast<uint4*>(out + rowmap(m) * ld + nc) =
+              *reinterpret_cast<const uint4*>(lds + row * RS + c * 16);
+      }
+      return;
+    }
+    // rows are processed U at a time: every global load of a chunk (addend, mask, y) is
+    // issued before the chunk's stores, so the loads overlap instead of serialising
+    // behind stores the compiler must assume alias them (out may alias addend)
+    constexpr int ITERS = BM / RPI;
+    constexpr int U = ITERS < 4 ? ITERS : 4;
+    const bool has_add = addend != nullptr, has_mask = red && bn.mask, has_y1 = red && bn.y1;
+#pragma unroll
+    for (int it0 = 0; it0 < ITERS; it0 += U) {
+      uint4 vv[U], aa[U], zz[U], p0[U], p1[U];
+      size_t off[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int row = tid / CPR + RPI * (it0 + u);
+        const int m = m0 + row;
+        ok[u] = m < M && nc < N;
+        off[u] = ok[u] ? rowmap(m) * ld + nc : 0;
+        vv[u] = *reinterpret_cast<const uint4*>(lds + row * RS + c * 16);
+        const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+        aa[u] = (ok[u] && has_add) ? *reinterpret_cast<const uint4*>(addend + off[u]) : zero;
+        zz[u] = (ok[u] && has_mask) ? *reinterpret_cast<const uint4*>(bn.mask + off[u]) : zero;
+        p0[u] = (ok[u] && red) ? *reinterpret_cast<const uint4*>(bn.y0 + off[u]) : zero;
+        p1[u] = (ok[u] && has_y1) ? *reinterpret_cast<const uint4*>(bn.y1 + off[u]) : zero;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        uint4 v = vv[u];
+        if (has_add || red) {
+          float a[8];
           unpack8(v, a);
-          unpack8(*reinterpret_cast<const uint4*>(addend + o), b);
+          if (has_add) {  // fused residual-gradient sum (dx of a branch point)
+            float b[8];
+            unpack8(aa[u], b);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) a[e] += b[e];
+            for (int e = 0; e < 8; ++e) a[e] += b[e];
+          }
+          if (has_mask) {
+            float z[8];
+            unpack8(zz[u], z);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a[e] = z[e] > 0.f ? a[e] : 0.f;
+          }
           v = pack8(a);
+          if (red) {
+            unpack8(v, a);  // reduce exactly the bf16 values that are stored
+            float y[8];
+            unpack8(p0[u], y);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { s1[e] += a[e]; s2[e] += a[e] * (y[e] - mu0[e]); }
+            if (has_y1) {
+              unpack8(p1[u], y);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) t2[e] += a[e] * (y[e] - mu1[e]);
+            }
+          }
         }
-        *reinterpret_cast<uint4*>(out + o) = v;
+        *reinterpret_cast<uint4*>(out + off[u]) = v;
+      }
+    }
+    if (red) {
+      // combine the RPI threads that own the same 8 columns, then one atomic per
+      // column and quantity into this block's copy slot
+      float* rb = reinterpret_cast<float*>(lds);     // [NTHR][24]
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        rb[tid * 24 + e] = s1[e];
+        rb[tid * 24 + 8 + e] = s2[e];
+        rb[tid * 24 + 16 + e] = t2[e];
+      }
+      __syncthreads();
+      if (tid < BN) {
+        const int col = tid, cc = col >> 3, e = col & 7, n = n0 + col;
+        float a = 0.f, b = 0.f, d = 0.f;
+        for (int r = 0; r < RPI; ++r) {
+          const float* q = rb + (cc + CPR * r) * 24;
+          a += q[e]; b += q[8 + e]; d += q[16 + e];
+        }
+        if (n < N) {
+          const int slot = (m0 / BM) & (NSTAT - 1);
+          float* d0 = bn.sums0 + (size_t)slot * 2 * N;
+          atomicAdd(d0 + n, a);
+          atomicAdd(d0 + N + n, b);
+          if (bn.y1) {
+            float* d1 = bn.sums1 + (size_t)slot * 2 * N;
+            atomicAdd(d1 + n, a);
+            atomicAdd(d1 + N + n, d);
+          }
+        }
       }
     }
   }
@@ -647,17 +757,25 @@ MLC_EXPORT int mlc_conv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, f
 
 // dx[N,H,W,C] = conv_transpose(dy[N,Ho,Wo,Co], w) (+ addend, same layout as dx; may
 // alias dx) -- the addend fuses the gradient sum at a residual branch point.
+// bn_y0 != null additionally fuses the backward reduction of the BatchNorm(s) whose
+// output gradient dx is (see BnBwdEpi): dx is stored masked by bn_mask > 0 and the
+// partial sums go to bn_sums{0,1}[NSTAT][2][C] (zeroed by the caller).  Only valid when
+// every dx row is produced by the GEMM (not for stride-2 convs with unreachable taps).
 MLC_EXPORT int mlc_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, const bf16* addend, int N,
                               int H, int W, int C, int Co, int KH, int KW, int stride, int pad,
-                              int dil, int Ho, int Wo, hipStream_t st) {
+                              int dil, int Ho, int Wo, const bf16* bn_mask, const bf16* bn_y0,
+                              const float* bn_mean0, float* bn_sums0, const bf16* bn_y1,
+                              const float* bn_mean1, float* bn_sums1, hipStream_t st) {
   if (C % 8 || Co % 8) return -1;
   const int K = KH * KW * Co;
   const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
+  BnBwdEpi bn{bn_mask, bn_y0, bn_mean0, bn_sums0, bn_y1, bn_mean1, bn_sums1};
+  if (bn_y0 && (!bn_mean0 || !bn_sums0 || (bn_y1 && (!bn_mean1 || !bn_sums1)))) return -1;
 #define MKB(R) (ConvDgradB<R>{{}, w, g, K})
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
     const int M = N * H * W;
     const int tile = pick_tile(M, C);
-    EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}, addend};
+    EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}, addend, bn};
 #define MKA(R) (MatKC<R>{{}, dy, Co, M, K})
     MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB);
 #undef MKA
@@ -667,16 +785,17 @@ MLC_EXPORT int mlc_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, const bf1
   const int tile = pick_tile(M, C);
 #define MKA(R) (ConvDgradA<R>{dy, g, M, K, rows})
   if (stride != 2) {
-    EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}, addend};
+    EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}, addend, bn};
     MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB);
   }
   if (M < N * H * W) {  // classes no tap reaches: dx = addend there (or 0)
+    if (bn_y0) return -1;
     const size_t bytes = (size_t)N * H * W * C * sizeof(bf16);
     if (addend) { if (addend != dx) (void)hipMemcpyAsync(dx, addend, bytes, hipMemcpyDeviceToDevice, st); }
     else (void)hipMemsetAsync(dx, 0, bytes, st);
   }
   if (M == 0) return hipGetLastError();
-  EpiBF16<DgradOutRows> epi{dx, C, nullptr, nullptr, DgradOutRows{rows}, addend};
+  EpiBF16<DgradOutRows> epi{dx, C, nullptr, nullptr, DgradOutRows{rows}, addend, bn};
   MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB);
 #undef MKA
 #undef MKB

@@ -48,7 +48,9 @@ class NativeResNet:
                 if blk.downsample is not None:
                     d = blk.downsample.cb
                     down = ConvBN(ctx, f'{pre}.downsample.cb', d.conv, d.bn, act=False)
-                self.blocks.append(ResidualBlock(units, down))
+                rb = ResidualBlock(units, down)
+                rb.prev = self.blocks[-1] if self.blocks else None
+                self.blocks.append(rb)
         self.head = ClassifierHead(ctx, 'fc', model.fc, smoothing)
         ctx.finalize(device)
         for u in self._units():

@@ -58,23 +58,50 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, stride=1, pad=0, dil=1,
     return y
 
 
+class BnBwdSpec:
+    """Backward reduction of up to two BatchNorms fused into a dgrad epilogue: the dgrad
+    output is their (shared) output gradient dU.  ``mask`` (the BN output z, or None)
+    applies the ReLU; ``ys`` = [(y, mean, sums)] with ``sums`` the NSTAT*2*C scratch
+    :func:`bn_bwd` later consumes with ``prereduced=True``."""
+
+    def __init__(self, mask, ys):
+        assert 1 <= len(ys) <= 2
+        self.mask = mask
+        self.ys = list(ys)
+
+
 def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=1, pad=0, dil=1,
-                 addend: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 addend: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+                 bn: Optional[BnBwdSpec] = None) -> torch.Tensor:
     """dx = conv_transpose(dy, w) [+ addend] (the addend fuses the gradient sum of a
-    residual branch point into the epilogue; ``out`` may alias ``addend``)."""
+    residual branch point into the epilogue; ``out`` may alias ``addend``).  With ``bn``
+    the epilogue also masks dx by ``bn.mask > 0`` and accumulates the BN-backward sums."""
     N, H, W, C = x_shape
     Co, KH, KW, Ci = w.shape
     _, Ho, Wo, _ = dy.shape
     if _cuda(dy):
         dx = out if out is not None else torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
+        b = [None] * 7
+        if bn is not None:
+            b[0] = bn.mask
+            for k, (yk, mk, sk) in enumerate(bn.ys):
+                b[1 + 3 * k:4 + 3 * k] = [yk, mk, sk]
         _lib.call('mlc_conv_dgrad', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(dx), _lib.ptr(addend), N, H, W, C,
-                  Co, KH, KW, stride, pad, dil, Ho, Wo, _lib.stream())
+                  Co, KH, KW, stride, pad, dil, Ho, Wo, *[_lib.ptr(t) for t in b], _lib.stream())
         return dx
     dxf = torch.nn.grad.conv2d_input((N, C, H, W), w.permute(0, 3, 1, 2).float(),
                                      dy.permute(0, 3, 1, 2).float(), stride, pad, dil)
     dxf = dxf.permute(0, 2, 3, 1)
     if addend is not None:
         dxf = dxf + addend.float()
+    if bn is not None:
+        if bn.mask is not None:
+            dxf = dxf * (bn.mask.float() > 0)
+        d = dxf.to(torch.bfloat16).float().reshape(-1, C)
+        for yk, mk, sk in bn.ys:
+            sv = sk.view(NSTAT, 2, C)
+            sv[0, 0] += d.sum(0)
+            sv[0, 1] += (d * (yk.float().reshape(-1, C) - mk)).sum(0)
     dx = dxf.to(torch.bfloat16).contiguous()
     if out is not None:
         out.copy_(dx)
@@ -176,42 +203,57 @@ def bn_apply(y, res, scale, shift, relu=True):
 
 
 def bn_bwd(dz, z, y, mean, invstd, gamma, want_dres=False, dgamma=None, dbeta=None, sums=None,
-           zero_sums=True, coef=None):
+           zero_sums=True, coef=None, prereduced=False):
     """Backward of z = act(BN(y) [+res]).  ``z`` is the saved output (ReLU mask) or None
     when there is no ReLU.  Returns (dy, dres or None); writes dgamma/dbeta (fp32).
     ``sums`` is NSTAT*2*C fp32 scratch (must be zero on entry when ``zero_sums`` is
-    False), ``coef`` 3*C fp32 scratch."""
+    False), ``coef`` 3*C fp32 scratch.  ``prereduced``: the producer of ``dz`` (a dgrad
+    epilogue, :class:`BnBwdSpec`) already applied the ReLU mask and filled ``sums``; the
+    residual-branch gradient is then ``dz`` itself."""
     rows = y.numel() // y.shape[-1]
     C = y.shape[-1]
+    if prereduced:
+        assert sums is not None
+        z = None
     if _cuda(dz):
         if sums is None:
             sums = torch.zeros(NSTAT * 2 * C, device=dz.device, dtype=torch.float32)
-        elif zero_sums:
+        elif zero_sums and not prereduced:
             sums.zero_()
         if coef is None:
             coef = torch.empty(3 * C, device=dz.device, dtype=torch.float32)
-        _lib.call('mlc_bn_bwd_reduce', _lib.ptr(dz), _lib.ptr(z), _lib.ptr(y), _lib.ptr(mean),
-                  _lib.ptr(sums), rows, C, _lib.stream())
+        if not prereduced:
+            _lib.call('mlc_bn_bwd_reduce', _lib.ptr(dz), _lib.ptr(z), _lib.ptr(y), _lib.ptr(mean),
+                      _lib.ptr(sums), rows, C, _lib.stream())
         _lib.call('mlc_bn_bwd_finalize', _lib.ptr(sums), _lib.ptr(invstd), _lib.ptr(gamma), _lib.ptr(coef),
                   _lib.ptr(dgamma), _lib.ptr(dbeta), rows, C, _lib.stream())
         dy = torch.empty_like(y)
-        dres = torch.empty_like(y) if want_dres else None
+        dres = None
+        if want_dres:
+            dres = dz if prereduced else torch.empty_like(y)
         _lib.call('mlc_bn_bwd_apply', _lib.ptr(dz), _lib.ptr(z), _lib.ptr(y), _lib.ptr(mean),
-                  _lib.ptr(coef), _lib.ptr(dy), _lib.ptr(dres), rows, C, _lib.stream())
+                  _lib.ptr(coef), _lib.ptr(dy), _lib.ptr(None if prereduced else dres), rows, C,
+                  _lib.stream())
         return dy, dres
     d = dz.float().reshape(rows, C)
     if z is not None:
         d = d * (z.reshape(rows, C).float() > 0)
     yc = y.float().reshape(rows, C) - mean
-    S1 = d.sum(0)
-    S2 = (d * yc).sum(0)
+    if prereduced:
+        sv = sums.view(NSTAT, 2, C).sum(0)
+        S1, S2 = sv[0], sv[1]
+    else:
+        S1 = d.sum(0)
+        S2 = (d * yc).sum(0)
     if dgamma is not None:
         dgamma.copy_(S2 * invstd)
         dbeta.copy_(S1)
     k1 = gamma * invstd
     dyf = k1 * d - k1 * S1 / rows - k1 * invstd * invstd * S2 / rows * yc
     dy = dyf.reshape(y.shape).to(torch.bfloat16)
-    dres = d.reshape(y.shape).to(torch.bfloat16) if want_dres else None
+    dres = None
+    if want_dres:
+        dres = dz if prereduced else d.reshape(y.shape).to(torch.bfloat16)
     return dy, dres
 
 

@@ -144,13 +144,30 @@ class ConvBN:
                             scale=self.scale, shift=self.shift)
         return z, (x, y, z)
 
-    def bwd(self, dz, rec, want_dres=False, dx_addend=None, need_dx=True, dx_out=None):
+    def dgrad_covers_all(self) -> bool:
+        """True when the dgrad GEMM writes every dx row (no structurally-zero stride-2
+        parity classes), i.e. a BN-backward reduction can be fused into its epilogue."""
+        if self.stride == 1:
+            return True
+        if self.stride != 2:
+            return False
+        KH, KW = self.k
+        ok = lambda p, K: any((p + self.pad - t * self.dil) % 2 == 0 for t in range(K))  # noqa: E731
+        return all(ok(p, KH) for p in (0, 1)) and all(ok(p, KW) for p in (0, 1))
+
+    def bn_target(self, rec):
+        """(y, mean, sums) of this unit's BN for a fused dgrad epilogue."""
+        x, y, z = rec
+        return (y, self.save_mean, self.ctx.ws[self.k_bw])
+
+    def bwd(self, dz, rec, want_dres=False, dx_addend=None, need_dx=True, dx_out=None,
+            prereduced=False, dgrad_bn=None):
         x, y, z = rec
         arena = self.ctx.arena
         dy, dres = Fn.bn_bwd(dz, z if self.act else None, y, self.save_mean, self.save_invstd,
                              self.gamma.master, want_dres=want_dres, dgamma=self.gamma.grad,
                              dbeta=self.beta.grad, sums=self.ctx.ws[self.k_bw], zero_sums=False,
-                             coef=self.coef)
+                             coef=self.coef, prereduced=prereduced)
         arena.mark_ready(self.gamma)
         arena.mark_ready(self.beta)
         Fn.conv2d_wgrad(dy, x, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad,
@@ -159,7 +176,7 @@ class ConvBN:
         dx = None
         if need_dx:
             dx = Fn.conv2d_dgrad(dy, self.w.bf16, x.shape, self.stride, self.pad, self.dil,
-                                 addend=dx_addend, out=dx_out)
+                                 addend=dx_addend, out=dx_out, bn=dgrad_bn)
         return dx, dres
 
 
@@ -183,15 +200,33 @@ class _ConvBNFn(torch.autograd.Function):
 class ResidualBlock:
     """units[0..n-1] chained, the last one adding the shortcut (identity or ``down(x)``)
     before its ReLU.  One autograd node for the whole block: backward fuses the gradient
-    sum at the branch point into the dgrad epilogue of the first unit."""
+    sum at the branch point into the dgrad epilogue of the first unit.
+
+    BN-backward fusion: the dgrad that produces a BN's output gradient also masks it by
+    the ReLU and accumulates that BN's backward sums (``Fn.BnBwdSpec``), so no separate
+    reduction pass runs.  Inside a block, unit i+1's dgrad serves unit i; the first
+    unit's dgrad (the block's input gradient) serves the PREVIOUS block's last BN and its
+    downsample BN, linked through ``prev`` and flagged by ``dout_prereduced``."""
 
     def __init__(self, units: List[ConvBN], down: Optional[ConvBN]):
         self.units = units
         self.down = down
         self.ctx = units[0].ctx
+        self.prev: Optional['ResidualBlock'] = None
+        self.fuse_bn_bwd = True
+        self.dout_prereduced = False
+        self._last = None   # (rec of the last unit, rec of down) of the latest forward
 
     def __call__(self, x):
         return _ResidualBlockFn.apply(x, self.ctx.anchor, self)
+
+    def output_bn_spec(self):
+        """BnBwdSpec for the gradient of this block's output (used by the next block)."""
+        rec, rd = self._last
+        ys = [self.units[-1].bn_target(rec)]
+        if self.down is not None:
+            ys.append(self.down.bn_target(rd))
+        return Fn.BnBwdSpec(rec[2], ys)
 
 
 class _ResidualBlockFn(torch.autograd.Function):
@@ -208,6 +243,7 @@ class _ResidualBlockFn(torch.autograd.Function):
             recs.append(r)
         out, r = blk.units[-1].fwd(y, identity)
         recs.append(r)
+        blk._last = (r, rd)
         ctx.blk = blk
         ctx.n = len(recs)
         flat = [t for r in recs for t in r]
@@ -224,18 +260,39 @@ class _ResidualBlockFn(torch.autograd.Function):
         rd = saved[3 * ctx.n:3 * ctx.n + 3] if blk.down is not None else None
         dout = dout.contiguous()
         need_dx = ctx.needs_input_grad[0]
+        pre = blk.dout_prereduced
+        blk.dout_prereduced = False
+        units = blk.units
+        fuse = blk.fuse_bn_bwd
+
+        def spec_for(i):  # fused reduction of unit i's BN in unit i+1's dgrad
+            u = units[i]
+            if not fuse or not units[i + 1].dgrad_covers_all():
+                return None
+            return Fn.BnBwdSpec(recs[i][2] if u.act else None, [u.bn_target(recs[i])])
+
         # last unit: its dres is the shortcut-branch gradient
-        d, dres = blk.units[-1].bwd(dout, recs[-1], want_dres=True)
-        for i in range(len(blk.units) - 2, 0, -1):
-            d, _ = blk.units[i].bwd(d, recs[i])
+        sp = spec_for(len(units) - 2) if len(units) > 1 else None
+        d, dres = units[-1].bwd(dout, recs[-1], want_dres=True, prereduced=pre, dgrad_bn=sp)
+        fused = sp is not None
+        for i in range(len(units) - 2, 0, -1):
+            sp = spec_for(i - 1)
+            d, _ = units[i].bwd(d, recs[i], prereduced=fused, dgrad_bn=sp)
+            fused = sp is not None
         if blk.down is not None:
             # shortcut conv first; its dx becomes the addend of the first unit's dgrad
-            short, _ = blk.down.bwd(dres, rd, need_dx=need_dx)
+            short, _ = blk.down.bwd(dres, rd, need_dx=need_dx, prereduced=pre)
         else:
             short = dres
-        dx, _ = blk.units[0].bwd(d, recs[0], dx_addend=short if need_dx else None,
-                                 need_dx=need_dx,
-                                 dx_out=short if (need_dx and blk.down is not None) else None)
+        prev_spec = None
+        if need_dx and fuse and blk.prev is not None and blk.prev._last is not None \
+                and units[0].dgrad_covers_all():
+            prev_spec = blk.prev.output_bn_spec()
+        dx, _ = units[0].bwd(d, recs[0], dx_addend=short if need_dx else None, need_dx=need_dx,
+                             dx_out=short if (need_dx and blk.down is not None) else None,
+                             prereduced=fused, dgrad_bn=prev_spec)
+        if prev_spec is not None:
+            blk.prev.dout_prereduced = True
         return dx, None, None
 
 

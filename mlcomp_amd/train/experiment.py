@@ -132,6 +132,22 @@ class ConfigExperiment:
             out['valid'] = cls(**dict(kw, num_samples=data_params['valid_samples'], seed=kw.get('seed', 0) + 1))
         return out
 
+    def get_native_batch(self, stage: str = None, loader: int = 0) -> torch.Tensor:
+        """One input batch (batch size 1) of the stage's first dataset, used to trace the
+        model; falls back to a random image of ``data_params.image_size``."""
+        stage = stage or self.stages[0]
+        dp = self.stage_params(stage, 'data_params')
+        try:
+            ds = list(self.get_datasets(stage, **dp).values())[loader]
+            if isinstance(ds, dict):
+                ds = ds['dataset']
+            item = ds[0]
+            x = item['features'] if isinstance(item, dict) else item[0]
+            return torch.as_tensor(x).float().unsqueeze(0)
+        except Exception:
+            s = int(dp.get('image_size', 224))
+            return torch.randn(1, int(dp.get('channels', 3)), s, s)
+
     def get_state_params(self, stage: str) -> dict:
         return self.stage_params(stage, 'state_params')
 

@@ -336,7 +336,19 @@ class Runner:
             self.native_step.net.export_to_torch()
         self._fire('on_stage_end')
 
+    def save_config(self):
+        """``logdir/configs/_config.json`` - what model tracing / model_add rebuild from."""
+        if self.rank != 0 or not self.experiment.logdir:
+            return
+        import json
+        import os
+        d = os.path.join(self.experiment.logdir, 'configs')
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, '_config.json'), 'w') as f:
+            json.dump(self.experiment._config, f, indent=2, default=str)
+
     def run_experiment(self, stages: Optional[List[str]] = None, start_epoch: int = 0):
+        self.save_config()
         for i, s in enumerate(stages or self.experiment.stages):
             self.run_stage(s, start_epoch if i == 0 else 0)
         return self.state

@@ -11,7 +11,7 @@ def load_builtin_executors():
         return
     _LOADED = True
     from . import bash, click_, split  # noqa: F401
-    for mod in ('train', 'model', 'kaggle', 'infer'):
+    for mod in ('train', 'model', 'kaggle', 'equation', 'valid', 'infer'):
         try:
             __import__(f'{__name__}.{mod}')
         except ImportError:

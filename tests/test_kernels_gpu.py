@@ -198,3 +198,64 @@ def test_conv_dgrad_addend(case):
     out = Fn.conv2d_dgrad(dy.to(DEV), w.to(DEV), (N, H, W, C), s, p, addend=a, out=a)  # in place
     torch.cuda.synchronize()
     assert rel_err(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize('case,two', [((2, 14, 14, 64, 64, 1, 1, 0), False),
+                                      ((2, 14, 14, 64, 64, 1, 1, 0), True),
+                                      ((2, 14, 14, 64, 128, 3, 1, 1), True),
+                                      ((2, 16, 16, 64, 128, 3, 2, 1), False),
+                                      ((2, 15, 13, 128, 64, 3, 2, 1), True),
+                                      ((1, 7, 7, 2048, 512, 1, 1, 0), True)])
+def test_conv_dgrad_bn_epilogue(case, two):
+    """Fused BN-backward reduction in the dgrad epilogue: masked dx and per-channel
+    sums match the CPU reference (which reduces the same bf16-rounded values)."""
+    N, H, W, C, Co, K, s, p = case
+    Ho, Wo = Fn.conv_out_hw(H, W, K, K, s, p, 1)
+    dy = _bf(N, Ho, Wo, Co, seed=31)
+    w = _bf(Co, K, K, C, scale=(1.0 / (K * K * C)) ** 0.5, seed=32)
+    add = _bf(N, H, W, C, seed=33)
+    z = _bf(N, H, W, C, seed=34)
+    y0, y1 = _bf(N, H, W, C, seed=35), _bf(N, H, W, C, seed=36)
+    m0, m1 = torch.randn(C) * 0.1, torch.randn(C) * 0.1
+
+    def run(dev):
+        t = lambda v: v.to(dev)  # noqa: E731
+        sums = [torch.zeros(Fn.NSTAT * 2 * C, device=dev) for _ in range(2)]
+        ys = [(t(y0), t(m0), sums[0])] + ([(t(y1), t(m1), sums[1])] if two else [])
+        spec = Fn.BnBwdSpec(t(z), ys)
+        dx = Fn.conv2d_dgrad(t(dy), t(w), (N, H, W, C), s, p, addend=t(add), bn=spec)
+        return dx, [x.view(Fn.NSTAT, 2, C).sum(0).cpu() for x in sums]
+
+    ref_dx, ref_s = run('cpu')
+    dx, sg = run(DEV)
+    torch.cuda.synchronize()
+    assert rel_err(dx, ref_dx) < 1e-2
+    assert ((dx.cpu().float() != 0) <= (z.float() > 0)).all()    # masked
+    for k in range(2 if two else 1):
+        assert rel_err(sg[k][0], ref_s[k][0]) < 2e-2, k
+        assert rel_err(sg[k][1], ref_s[k][1]) < 2e-2, k
+
+
+def test_native_fused_bn_bwd_matches_unfused():
+    """Engine-level: gradients with the BN-backward reduction fused into dgrad epilogues
+    equal (up to float-atomic order) the ones from the separate reduction kernel."""
+    torch.manual_seed(5)
+    from mlcomp_amd.models import build_model
+    from mlcomp_amd.train.native_step import NativeClassifierStep
+    tm1 = build_model('resnet50', num_classes=16)
+    tm2 = build_model('resnet50', num_classes=16)
+    tm2.load_state_dict(tm1.state_dict())
+    a = NativeClassifierStep(torch_model=tm1, batch=8, image_size=64, device=DEV, num_classes=16,
+                             use_graph=False, lr=0.0, momentum=0.0)
+    b = NativeClassifierStep(torch_model=tm2, batch=8, image_size=64, device=DEV, num_classes=16,
+                             use_graph=False, lr=0.0, momentum=0.0)
+    for blk in b.net.blocks:
+        blk.fuse_bn_bwd = False
+    b.load_batch(a.x, a.y)
+    a()
+    b()
+    torch.cuda.synchronize()
+    ga, gb = a.net.arena.decay.grad, b.net.arena.decay.grad
+    assert ((ga - gb).norm() / gb.norm()).item() < 2e-2
+    na, nb = a.net.arena.nodecay.grad, b.net.arena.nodecay.grad
+    assert ((na - nb).norm() / nb.norm()).item() < 2e-2
