@@ -60,4 +60,48 @@ class SimpleCNN(nn.Module):
         return self.fc(self.features(x).flatten(1))
 
 
-__all__ = ['Pretrained', 'SimpleCNN']
+class EncoderClassifier(nn.Module):
+    """Any segmentation encoder (densenet / se_resnet / senet154 / dpn / vgg / mobilenet
+    ...) as an image classifier: deepest feature -> global average pool -> linear.  Gives
+    ``Pretrained`` / ``Timm`` the pretrainedmodels-style variants without that package."""
+
+    def __init__(self, encoder_name: str, num_classes: int = 1000, in_channels: int = 3):
+        super().__init__()
+        from mlcomp_amd.contrib.segmentation.encoders import get_encoder
+        self.encoder = get_encoder(encoder_name)
+        self.fc = nn.Linear(self.encoder.out_shapes[0], num_classes)
+
+    def forward(self, x):
+        f = self.encoder(x)[0]
+        return self.fc(torch.flatten(torch.nn.functional.adaptive_avg_pool2d(f, 1), 1))
+
+
+def _register_encoder_classifiers():
+    from mlcomp_amd.contrib.segmentation.encoders import ENCODERS
+    for name in ENCODERS:
+        if name not in MODELS:
+            register(name)((lambda n: (lambda num_classes=1000, **kw: EncoderClassifier(n, num_classes, **kw)))(name))
+
+
+_TIMM_ALIASES = {f'efficientnet_b{i}': f'efficientnet-b{i}' for i in range(8)}
+_TIMM_ALIASES.update({f'tf_efficientnet_b{i}': f'efficientnet-b{i}' for i in range(8)})
+_TIMM_ALIASES.update({'mobilenetv2_100': 'mobilenet_v2', 'seresnet50': 'se_resnet50',
+                      'seresnext50_32x4d': 'se_resnext50_32x4d', 'dpn68b': 'dpn68'})
+
+
+@register('Timm')
+class Timm(Pretrained):
+    """The reference's timm wrapper (`mlcomp/contrib/model/timm.py:5-40`): timm is not in
+    this stack, so timm variant names are mapped onto the native registry."""
+
+    def __init__(self, variant: str, num_classes: int, pretrained=None, activation=None, **kw):
+        _register_encoder_classifiers()
+        name = _TIMM_ALIASES.get(variant, variant)
+        if name not in MODELS:
+            raise KeyError(f'timm variant {variant!r} has no native equivalent; registered: {sorted(MODELS)}')
+        super().__init__(name, num_classes, pretrained if isinstance(pretrained, str) else None, activation, **kw)
+
+
+_register_encoder_classifiers()
+
+__all__ = ['Pretrained', 'SimpleCNN', 'EncoderClassifier', 'Timm']
