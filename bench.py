@@ -35,7 +35,8 @@ def parse():
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=5)
-    p.add_argument('--batch', type=int, default=256, help='per-GPU batch')
+    p.add_argument('--batch', type=int, default=None, help='per-GPU batch (256 images / 32 sequences)')
+    p.add_argument('--seq-len', type=int, default=128, help='BERT sequence length')
     p.add_argument('--model', default='resnet50')
     p.add_argument('--impl', default='native', choices=['native', 'torch'])
     p.add_argument('--image-size', type=int, default=224)
@@ -64,11 +65,20 @@ def main():
     if world > 1:
         dist.init_process_group('nccl', device_id=device)
 
-    from mlcomp_amd.train.imagenet import build_train_step
-    step = build_train_step(args.model, batch=args.batch, impl=args.impl,
-                            image_size=args.image_size, device=device,
-                            world_size=world,
-                            use_graph=(args.graph if args.graph >= 0 else None))
+    is_bert = args.model.startswith('bert')
+    if args.batch is None:
+        args.batch = 32 if is_bert else 256
+    if is_bert:
+        from mlcomp_amd.train.bert import build_bert_step
+        step = build_bert_step(args.model, batch=args.batch, seq_len=args.seq_len, impl=args.impl,
+                               device=device, world_size=world,
+                               use_graph=(args.graph if args.graph >= 0 else None))
+    else:
+        from mlcomp_amd.train.imagenet import build_train_step
+        step = build_train_step(args.model, batch=args.batch, impl=args.impl,
+                                image_size=args.image_size, device=device,
+                                world_size=world,
+                                use_graph=(args.graph if args.graph >= 0 else None))
 
     for _ in range(args.warmup):
         step()
@@ -94,7 +104,19 @@ def main():
     images = args.batch * world * args.steps
     value = images / elapsed
     loss = step.last_loss()
-    if rank == 0:
+    if rank == 0 and is_bert:
+        out = {
+            'metric': 'sequences/sec (whole node) BERT fine-tune DAG train task',
+            'value': round(value, 2), 'unit': 'sequences/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'bf16',
+            'data': f'synthetic (random token ids, seq_len {args.seq_len}, 2 labels, random-init weights)',
+            'config': {'model': args.model, 'global_batch': args.batch * world, 'per_gpu_batch': args.batch,
+                       'seq_len': args.seq_len, 'parallelism': f'dp{world}', 'impl': args.impl,
+                       'optimizer': 'AdamW lr 2e-5 wd 0.01, fp32 master weights', 'dropout': 0.1,
+                       'final_loss': loss}}
+        print(json.dumps(out), flush=True)
+    elif rank == 0:
         out = {
             'metric': 'images/sec (whole node) ResNet-50 DAG train task',
             'value': round(value, 2),

@@ -365,6 +365,9 @@ template <class RowMap = IdentityRows>
 struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / sum of squares
   bf16* out; int ld; float* sum; float* sumsq; RowMap rowmap; const bf16* addend = nullptr;
   BnBwdEpi bn = {};
+  // dense-layer extras: out = act(acc + bias) (pre-activation stored to preact), or
+  // out = acc * act'(dact) for the backward of an activation (act 1 = exact-erf GELU)
+  const float* bias = nullptr; int act = 0; bf16* preact = nullptr; const bf16* dact = nullptr;
   template <int BM, int BN>
   __device__ void apply(f32x16 (&acc)[2][2], char* lds, int m0, int n0, int M, int N,
                         int wm, int wn, int lane, int tid) const {
@@ -415,7 +418,8 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
         s1[e] = 0.f; s2[e] = 0.f; t2[e] = 0.f;
       }
     }
-    if (!addend && !red) {  // plain store (forward convs / GEMMs)
+    const bool dense = bias || act || dact;
+    if (!addend && !red && !dense) {  // plain store (forward convs / GEMMs)
 #pragma unroll
       for (int it = 0; it < BM / RPI; ++it) {
         const int row = tid / CPR + RPI * it;
@@ -434,7 +438,7 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
     const bool has_add = addend != nullptr, has_mask = red && bn.mask, has_y1 = red && bn.y1;
 #pragma unroll
     for (int it0 = 0; it0 < ITERS; it0 += U) {
-      uint4 vv[U], aa[U], zz[U], p0[U], p1[U];
+      uint4 vv[U], aa[U], zz[U], p0[U], p1[U], du[U];
       size_t off[U];
       bool ok[U];
 #pragma unroll
@@ -449,14 +453,34 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
         zz[u] = (ok[u] && has_mask) ? *reinterpret_cast<const uint4*>(bn.mask + off[u]) : zero;
         p0[u] = (ok[u] && red) ? *reinterpret_cast<const uint4*>(bn.y0 + off[u]) : zero;
         p1[u] = (ok[u] && has_y1) ? *reinterpret_cast<const uint4*>(bn.y1 + off[u]) : zero;
+        du[u] = (ok[u] && dact) ? *reinterpret_cast<const uint4*>(dact + off[u]) : zero;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (!ok[u]) continue;
         uint4 v = vv[u];
-        if (has_add || red) {
+        if (has_add || red || dense) {
           float a[8];
           unpack8(v, a);
+          if (bias) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a[e] += bias[nc + e];
+          }
+          if (preact) *reinterpret_cast<uint4*>(preact + off[u]) = pack8(a);
+          if (act == 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a[e] = 0.5f * a[e] * (1.f + erff(a[e] * 0.70710678118654752f));
+          }
+          if (dact) {
+            float z[8];
+            unpack8(du[u], z);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float cdf = 0.5f * (1.f + erff(z[e] * 0.70710678118654752f));
+              const float pdf = 0.3989422804014327f * __expf(-0.5f * z[e] * z[e]);
+              a[e] *= cdf + z[e] * pdf;
+            }
+          }
           if (has_add) {  // fused residual-gradient sum (dx of a branch point)
             float b[8];
             unpack8(aa[u], b);
@@ -849,6 +873,21 @@ MLC_EXPORT int mlc_gemm_f32out(const bf16* A, const bf16* B, float* C, const flo
     MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_MC, GB_MC);
   }
   EpiF32 epi{C, ldc, bias, accumulate};
+  if (!ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_KC, GB_KC);
+  if (!ta && !tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_KC, GB_MC);
+  if (ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_MC, GB_KC);
+  MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_MC, GB_MC);
+}
+
+// bf16-output GEMM with a dense-layer epilogue: C = act(op(A) op(B) + bias) (pre-
+// activation to preact when given), or C = (op(A) op(B)) * act'(dact) (+ addend).
+MLC_EXPORT int mlc_gemm_bf16_ex(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int lda, int ldb,
+                                int ldc, int ta, int tb, const float* bias, int act, bf16* preact,
+                                const bf16* addend, const bf16* dact, hipStream_t st) {
+  if (K % 8 || N % 8 || ldc % 8 || lda % 8 || ldb % 8 || (ta && M % 8)) return -1;
+  const int tile = pick_tile(M, N);
+  EpiBF16<> epi{C, ldc, nullptr, nullptr, IdentityRows{}, addend};
+  epi.bias = bias; epi.act = act; epi.preact = preact; epi.dact = dact;
   if (!ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_KC, GB_KC);
   if (!ta && !tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_KC, GB_MC);
   if (ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_MC, GB_KC);

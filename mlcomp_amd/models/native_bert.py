@@ -1,0 +1,314 @@
+"""BERT on the native kernels: every dense layer is the MFMA GEMM with a fused
+bias / exact-GELU epilogue (pre-activation kept for backward), the GELU derivative and
+the residual-gradient sum are fused into the dgrad epilogues, LayerNorm is one kernel
+fused with the residual add and hidden dropout, attention softmax is one kernel fused
+with scale + key mask + attention dropout; the QK^T and PV batched products go to the
+library batched GEMM (``torch.bmm`` -> hipBLASLt).
+
+Parameters live in the flat arenas (``ops.arena``): matmul weights and embedding tables
+in the decay arena (bf16 mirror for the kernels), biases and LayerNorm affine in the
+no-decay arena - so AdamW is one fused launch per arena and the RCCL bucketer all-reduces
+arena slices as gradients complete during backward.
+
+Activations are token-major [T = B*S, H] bf16.  Dropout masks come from a hash of
+(step seed, site salt, element): the seed is a device scalar the step advances, so a
+captured HIP graph draws fresh masks every replay and backward regenerates them.
+"""
+from __future__ import annotations
+
+import math
+from typing import List
+
+import torch
+
+from mlcomp_amd.ops import functional as Fn
+from mlcomp_amd.ops import transformer as Tx
+from mlcomp_amd.ops.layers import NativeContext
+from .bert import BertForSequenceClassification
+
+
+class _Dense:
+    def __init__(self, ctx: NativeContext, name: str, lin: torch.nn.Linear):
+        self.ctx = ctx
+        self.lin = lin
+        self.w = ctx.arena.weight(f'{name}.weight', tuple(lin.weight.shape))
+        self.b = ctx.arena.vector(f'{name}.bias', tuple(lin.bias.shape))
+
+    def load(self):
+        self.w.master.copy_(self.lin.weight.detach().float())
+        self.b.master.copy_(self.lin.bias.detach().float())
+
+    def export(self):
+        self.lin.weight.data.copy_(self.w.master.to(self.lin.weight.device))
+        self.lin.bias.data.copy_(self.b.master.to(self.lin.bias.device))
+
+    def fwd(self, x, act=0, want_preact=False):
+        return Tx.dense_fwd(x, self.w.bf16, self.b.master, act, want_preact)
+
+    def bwd_params(self, dy, x):
+        """dW += dy^T x, db += colsum(dy) (straight into the grad arena)."""
+        a = self.ctx.arena
+        Fn.linear_wgrad(dy, x, out=self.w.grad, accumulate=True)
+        Tx.colsum_acc(dy, self.b.grad)
+        a.mark_ready(self.w)
+        a.mark_ready(self.b)
+
+
+class _LN:
+    def __init__(self, ctx: NativeContext, name: str, ln: torch.nn.LayerNorm):
+        self.ctx = ctx
+        self.ln = ln
+        self.g = ctx.arena.vector(f'{name}.weight', tuple(ln.weight.shape))
+        self.b = ctx.arena.vector(f'{name}.bias', tuple(ln.bias.shape))
+        self.k_sums = ctx.ws.request(f'{name}.sums', Fn.NSTAT * 2 * ln.weight.numel())
+
+    def load(self):
+        self.g.master.copy_(self.ln.weight.detach().float())
+        self.b.master.copy_(self.ln.bias.detach().float())
+
+    def export(self):
+        self.ln.weight.data.copy_(self.g.master.to(self.ln.weight.device))
+        self.ln.bias.data.copy_(self.b.master.to(self.ln.bias.device))
+
+    def mark(self):
+        self.ctx.arena.mark_ready(self.g)
+        self.ctx.arena.mark_ready(self.b)
+
+
+class NativeBertLayer:
+    def __init__(self, net: 'NativeBert', idx: int, layer):
+        ctx = net.ctx
+        self.net, self.idx = net, idx
+        n = f'layers.{idx}'
+        self.qkv = _Dense(ctx, f'{n}.qkv', layer.qkv)
+        self.out = _Dense(ctx, f'{n}.out', layer.out)
+        self.ln1 = _LN(ctx, f'{n}.ln1', layer.ln1)
+        self.ffn1 = _Dense(ctx, f'{n}.ffn1', layer.ffn1)
+        self.ffn2 = _Dense(ctx, f'{n}.ffn2', layer.ffn2)
+        self.ln2 = _LN(ctx, f'{n}.ln2', layer.ln2)
+        self.salt = 16 + 8 * idx     # dropout sites: +0 attn probs, +1 attn-out, +2 ffn-out
+
+    def parts(self):
+        return [self.qkv, self.out, self.ln1, self.ffn1, self.ffn2, self.ln2]
+
+    def __call__(self, x, key_bias):
+        return _BertLayerFn.apply(x, self.net.ctx.anchor, key_bias, self)
+
+    # -------------------------------------------------------------- forward / backward
+    def fwd(self, x, key_bias):
+        net = self.net
+        B, S, nh, dh = net.B, net.S, net.c.heads, net.c.head_dim
+        pa, ph = net.p_attn, net.p_hidden
+        qkv, _ = self.qkv.fwd(x)
+        q, k, v = qkv.view(B, S, 3, nh, dh).permute(2, 0, 3, 1, 4).reshape(3, B * nh, S, dh).unbind(0)
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        scores = torch.bmm(q, k.transpose(1, 2))
+        P, Pd = Tx.softmax_fwd(scores.view(-1, S), key_bias, nh * S, 1.0 / math.sqrt(dh), pa, net.seed, self.salt)
+        ctxv = torch.bmm(Pd.view(B * nh, S, S), v)
+        ctx2 = ctxv.view(B, nh, S, dh).transpose(1, 2).reshape(B * S, nh * dh)
+        ao, _ = self.out.fwd(ctx2)
+        h1, s1, m1, r1 = Tx.ln_fwd(x, ao, self.ln1.g.master, self.ln1.b.master, net.c.eps, p_in=ph,
+                                   seed=net.seed, salt_in=self.salt + 1)
+        g, u = self.ffn1.fwd(h1, act=1, want_preact=True)
+        f, _ = self.ffn2.fwd(g)
+        h2, s2, m2, r2 = Tx.ln_fwd(h1, f, self.ln2.g.master, self.ln2.b.master, net.c.eps, p_in=ph,
+                                   seed=net.seed, salt_in=self.salt + 2)
+        return h2, (x, q, k, v, P, Pd, ctx2, s1, m1, r1, h1, u, g, s2, m2, r2)
+
+    def bwd(self, dh2, saved, key_bias):
+        net = self.net
+        ws = net.ctx.ws
+        B, S, nh, dh = net.B, net.S, net.c.heads, net.c.head_dim
+        pa, ph = net.p_attn, net.p_hidden
+        x, q, k, v, P, Pd, ctx2, s1, m1, r1, h1, u, g, s2, m2, r2 = saved
+        ds2, df = Tx.ln_bwd(dh2, s2, m2, r2, self.ln2.g.master, self.ln2.g.grad, self.ln2.b.grad,
+                            ws[self.ln2.k_sums], p_in=ph, seed=net.seed, salt_in=self.salt + 2, want_dr=True)
+        self.ln2.mark()
+        self.ffn2.bwd_params(df, g)
+        du = Tx.dense_dgrad(df, self.ffn2.w.bf16, dact_u=u)          # grad of the GELU input
+        self.ffn1.bwd_params(du, h1)
+        dh1 = Tx.dense_dgrad(du, self.ffn1.w.bf16, addend=ds2)       # + residual branch
+        ds1, dao = Tx.ln_bwd(dh1, s1, m1, r1, self.ln1.g.master, self.ln1.g.grad, self.ln1.b.grad,
+                             ws[self.ln1.k_sums], p_in=ph, seed=net.seed, salt_in=self.salt + 1, want_dr=True)
+        self.ln1.mark()
+        self.out.bwd_params(dao, ctx2)
+        dctx2 = Tx.dense_dgrad(dao, self.out.w.bf16)
+        dctx = dctx2.view(B, S, nh, dh).transpose(1, 2).reshape(B * nh, S, dh)
+        dPd = torch.bmm(dctx, v.transpose(1, 2))
+        dv = torch.bmm(Pd.view(B * nh, S, S).transpose(1, 2), dctx)
+        dS = Tx.softmax_bwd(P, dPd.view(-1, S), 1.0 / math.sqrt(dh), pa, net.seed, self.salt).view(B * nh, S, S)
+        dq = torch.bmm(dS, k)
+        dk = torch.bmm(dS.transpose(1, 2), q)
+        dqkv = torch.stack([dq, dk, dv]).view(3, B, nh, S, dh).permute(1, 3, 0, 2, 4).reshape(B * S, 3 * nh * dh)
+        self.qkv.bwd_params(dqkv, x)
+        return Tx.dense_dgrad(dqkv, self.qkv.w.bf16, addend=ds1)
+
+
+class _BertLayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, key_bias, layer: NativeBertLayer):
+        h, saved = layer.fwd(x, key_bias)
+        ctx.layer = layer
+        ctx.kb = key_bias
+        ctx.save_for_backward(*saved)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        return ctx.layer.bwd(dh.contiguous(), ctx.saved_tensors, ctx.kb), None, None, None
+
+
+class _EmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, tt, anchor, net: 'NativeBert'):
+        B, S = ids.shape
+        e = (net.word.bf16[ids].float() + net.pos.bf16[:S][None].float() + net.tok_type.bf16[tt].float())
+        e = e.to(torch.bfloat16).view(B * S, -1)
+        y, s, m, r = Tx.ln_fwd(e, None, net.ln.g.master, net.ln.b.master, net.c.eps, p_out=net.p_hidden,
+                               seed=net.seed, salt_out=1)
+        ctx.net = net
+        ctx.save_for_backward(ids, tt, s, m, r)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        net = ctx.net
+        ids, tt, s, m, r = ctx.saved_tensors
+        ds, _ = Tx.ln_bwd(dy.contiguous(), s, m, r, net.ln.g.master, net.ln.g.grad, net.ln.b.grad,
+                          net.ctx.ws[net.ln.k_sums], p_out=net.p_hidden, seed=net.seed, salt_out=1)
+        net.ln.mark()
+        B, S = ids.shape
+        d = ds.float().view(B, S, -1)
+        net.word.grad.index_add_(0, ids.reshape(-1), d.reshape(B * S, -1))
+        net.pos.grad[:S].add_(d.sum(0))
+        net.tok_type.grad.index_add_(0, tt.reshape(-1), d.reshape(B * S, -1))
+        for sl in (net.word, net.pos, net.tok_type):
+            net.ctx.arena.mark_ready(sl)
+        return None, None, None, None
+
+
+class _HeadFn(torch.autograd.Function):
+    """[CLS] -> tanh pooler -> (dropout) -> classifier -> fused softmax-CE (sum reduced)."""
+
+    @staticmethod
+    def forward(ctx, h, anchor, labels, net: 'NativeBert'):
+        B, S = net.B, net.S
+        cls = h.view(B, S, -1)[:, 0].contiguous()
+        z, _ = net.pooler.fwd(cls)
+        pooled = torch.tanh(z.float()).to(torch.bfloat16)
+        pd = Tx.dropout(pooled, net.p_hidden, net.seed, 2)
+        logits = Fn.linear_fwd(pd, net.cls_w.bf16, net.cls_b.master)
+        dl = Fn.softmax_ce(logits, labels, net.loss_sum(), net.correct(), scale=1.0 / B,
+                           num_classes=net.c.num_labels)
+        ctx.net = net
+        ctx.save_for_backward(cls, pooled, pd, dl)
+        net._logits = logits
+        return (net.loss_sum() / B).sum()
+
+    @staticmethod
+    def backward(ctx, g):
+        net = ctx.net
+        cls, pooled, pd, dl = ctx.saved_tensors
+        a = net.ctx.arena
+        Fn.linear_wgrad(dl, pd, out=net.cls_w.grad, accumulate=True)
+        Tx.colsum_acc(dl, net.cls_b.grad) if dl.shape[1] % 8 == 0 else net.cls_b.grad.add_(dl.float().sum(0))
+        a.mark_ready(net.cls_w)
+        a.mark_ready(net.cls_b)
+        dpd = Fn.linear_dgrad(dl, net.cls_w.bf16)
+        dpooled = Tx.dropout(dpd, net.p_hidden, net.seed, 2)   # same mask, same scale
+        dz = (dpooled.float() * (1 - pooled.float() ** 2)).to(torch.bfloat16)
+        net.pooler.bwd_params(dz, cls)
+        dcls = Tx.dense_dgrad(dz, net.pooler.w.bf16)
+        dh = torch.zeros(net.B, net.S, dcls.shape[1], device=dcls.device, dtype=torch.bfloat16)
+        dh[:, 0] = dcls
+        return dh.view(net.B * net.S, -1), None, None, None
+
+
+class NativeBert:
+    def __init__(self, model: BertForSequenceClassification, device, batch: int, seq_len: int):
+        c = model.config
+        assert c.hidden % 8 == 0 and c.intermediate % 8 == 0 and seq_len % 4 == 0
+        self.model, self.c = model, c
+        self.B, self.S = batch, seq_len
+        self.p_hidden, self.p_attn = c.hidden_dropout, c.attention_dropout
+        ctx = self.ctx = NativeContext()
+        a = ctx.arena
+        # registration order == forward order (the arena lays slots out backward-first)
+        self.word = a.weight('word', tuple(model.word.weight.shape))
+        self.pos = a.weight('pos', tuple(model.pos.weight.shape))
+        self.tok_type = a.weight('tok_type', tuple(model.tok_type.weight.shape))
+        self.ln = _LN(ctx, 'ln', model.ln)
+        self.layers: List[NativeBertLayer] = [NativeBertLayer(self, i, l) for i, l in enumerate(model.layers)]
+        self.pooler = _Dense(ctx, 'pooler', model.pooler)
+        self.Lp = (c.num_labels + 7) // 8 * 8   # classifier rows padded for 16 B MFMA chunks
+        self.cls_w = a.weight('classifier.weight', (self.Lp, c.hidden))
+        self.cls_b = a.vector('classifier.bias', (self.Lp,))
+        self.k_loss = ctx.ws.request('loss', 1)
+        self.k_correct = ctx.ws.request('correct', 1)
+        ctx.finalize(device)
+        self.device = ctx.device
+        self.seed = torch.zeros(1, device=self.device, dtype=torch.int32)
+        self.load_from_torch()
+
+    # ------------------------------------------------------------------ weights
+    def _dense_parts(self):
+        for l in self.layers:
+            yield from l.parts()
+        yield self.pooler
+        yield self.ln
+
+    def load_from_torch(self):
+        m = self.model
+        with torch.no_grad():
+            self.word.master.copy_(m.word.weight.float())
+            self.pos.master.copy_(m.pos.weight.float())
+            self.tok_type.master.copy_(m.tok_type.weight.float())
+            for p in self._dense_parts():
+                p.load()
+            self.cls_w.master.zero_()
+            self.cls_b.master.zero_()
+            self.cls_w.master[:self.c.num_labels].copy_(m.classifier.weight.float())
+            self.cls_b.master[:self.c.num_labels].copy_(m.classifier.bias.float())
+        self.ctx.arena.decay.refresh_mirror()
+
+    def export_to_torch(self):
+        m = self.model
+        with torch.no_grad():
+            m.word.weight.copy_(self.word.master.to(m.word.weight.device))
+            m.pos.weight.copy_(self.pos.master.to(m.pos.weight.device))
+            m.tok_type.weight.copy_(self.tok_type.master.to(m.tok_type.weight.device))
+            for p in self._dense_parts():
+                p.export()
+            m.classifier.weight.copy_(self.cls_w.master[:self.c.num_labels].to(m.classifier.weight.device))
+            m.classifier.bias.copy_(self.cls_b.master[:self.c.num_labels].to(m.classifier.bias.device))
+
+    @property
+    def arena(self):
+        return self.ctx.arena
+
+    def loss_sum(self):
+        return self.ctx.ws[self.k_loss]
+
+    def correct(self):
+        return self.ctx.ws[self.k_correct]
+
+    def train(self, mode=True):
+        self.ctx.training = mode
+        self.p_hidden = self.c.hidden_dropout if mode else 0.0
+        self.p_attn = self.c.attention_dropout if mode else 0.0
+
+    def eval(self):
+        self.train(False)
+
+    # ------------------------------------------------------------------ graph
+    def loss(self, ids, tt, key_bias, labels):
+        h = _EmbedFn.apply(ids, tt, self.ctx.anchor, self)
+        for layer in self.layers:
+            h = layer(h, key_bias)
+        return _HeadFn.apply(h, self.ctx.anchor, labels, self)
+
+    def logits(self):
+        return self._logits[:, :self.c.num_labels]
+
+
+__all__ = ['NativeBert']

@@ -1,0 +1,222 @@
+"""Python entry points of the transformer kernels (``csrc/kernels/transformer.hip`` and the
+dense-layer GEMM epilogue of ``igemm.hip``), each with an fp32 PyTorch reference used on
+CPU (and by the numerics tests).  Dropout uses the kernels' counter-based hash, which the
+CPU path reproduces bit-exactly, so masks agree between the two."""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+from .functional import NSTAT, _cuda
+
+_M32 = 0xFFFFFFFF
+
+
+def _hash(seed: int, salt: int, idx: torch.Tensor) -> torch.Tensor:
+    x = (idx * 0x9E3779B9) & _M32
+    x = x ^ ((seed * 0x85EBCA6B + salt * 0xC2B2AE35) & _M32)
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    x = x ^ (x >> 16)
+    return x
+
+
+def keep_mask(shape, p: float, seed: int, salt: int, device=None) -> torch.Tensor:
+    """Same keep decisions as the kernels for a contiguous tensor of ``shape``."""
+    n = 1
+    for s in shape:
+        n *= s
+    idx = torch.arange(n, dtype=torch.int64, device=device)
+    thr = int(p * 16777216.0)
+    return ((_hash(seed, salt, idx) >> 8) >= thr).reshape(shape)
+
+
+def _seed_val(seed) -> int:
+    return int(seed.item()) if torch.is_tensor(seed) else int(seed or 0)
+
+
+# ---------------------------------------------------------------------------- LayerNorm
+def ln_fwd(x, r, gamma, beta, eps=1e-12, p_in=0.0, p_out=0.0, seed=None, salt_in=0, salt_out=0):
+    """y = dropout_out(LN(x + dropout_in(r))).  Returns (y, s, mean, rstd) where s is the
+    normalised input (``x`` itself when there is no ``r``)."""
+    T, H = x.shape
+    if _cuda(x):
+        y = torch.empty_like(x)
+        s = torch.empty_like(x) if r is not None else x
+        mean = torch.empty(T, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(T, device=x.device, dtype=torch.float32)
+        _lib.call('mlc_ln_fwd', _lib.ptr(x), _lib.ptr(r), _lib.ptr(s if r is not None else None), _lib.ptr(y),
+                  _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(gamma), _lib.ptr(beta), T, H, float(eps), float(p_in),
+                  float(p_out), _lib.ptr(seed), salt_in, salt_out, _lib.stream())
+        return y, s, mean, rstd
+    sd = _seed_val(seed)
+    v = x.float()
+    if r is not None:
+        rr = r.float()
+        if p_in > 0:
+            rr = torch.where(keep_mask((T, H), p_in, sd, salt_in), rr / (1 - p_in), torch.zeros_like(rr))
+        v = v + rr
+    s = v.to(torch.bfloat16) if r is not None else x
+    mean = v.mean(1)
+    var = ((v - mean[:, None]) ** 2).mean(1)
+    rstd = torch.rsqrt(var + eps)
+    y = (v - mean[:, None]) * rstd[:, None] * gamma + beta
+    if p_out > 0:
+        y = torch.where(keep_mask((T, H), p_out, sd, salt_out), y / (1 - p_out), torch.zeros_like(y))
+    return y.to(torch.bfloat16), s, mean, rstd
+
+
+def ln_bwd(dy, s, mean, rstd, gamma, dgamma, dbeta, sums=None, p_in=0.0, p_out=0.0, seed=None, salt_in=0,
+           salt_out=0, want_dr=False):
+    """Returns (ds, dr): ds = dLoss/ds, dr = dropout_in'(ds) (None unless ``want_dr``).
+    dgamma / dbeta are ACCUMULATED (+=)."""
+    T, H = dy.shape
+    if _cuda(dy):
+        ds = torch.empty_like(dy)
+        dr = torch.empty_like(dy) if want_dr else None
+        if sums is None:
+            sums = torch.zeros(NSTAT * 2 * H, device=dy.device, dtype=torch.float32)
+        _lib.call('mlc_ln_bwd', _lib.ptr(dy), _lib.ptr(s), _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(gamma),
+                  _lib.ptr(ds), _lib.ptr(dr), _lib.ptr(sums), _lib.ptr(dgamma), _lib.ptr(dbeta), T, H, float(p_in),
+                  float(p_out), _lib.ptr(seed), salt_in, salt_out, _lib.stream())
+        return ds, dr
+    sd = _seed_val(seed)
+    d = dy.float()
+    if p_out > 0:
+        d = torch.where(keep_mask((T, H), p_out, sd, salt_out), d / (1 - p_out), torch.zeros_like(d))
+    xh = (s.float() - mean[:, None]) * rstd[:, None]
+    dgamma.add_((d * xh).sum(0))
+    dbeta.add_(d.sum(0))
+    g = d * gamma
+    a = g.mean(1, keepdim=True)
+    b = (g * xh).mean(1, keepdim=True)
+    dsf = rstd[:, None] * (g - a - xh * b)
+    ds = dsf.to(torch.bfloat16)
+    dr = None
+    if want_dr:
+        drf = dsf
+        if p_in > 0:
+            drf = torch.where(keep_mask((T, H), p_in, sd, salt_in), dsf / (1 - p_in), torch.zeros_like(dsf))
+        dr = drf.to(torch.bfloat16)
+    return ds, dr
+
+
+# ---------------------------------------------------------------------------- softmax
+def softmax_fwd(S, key_bias, rows_per_batch, scale, p=0.0, seed=None, salt=0):
+    """S [R, L] bf16 scores; key_bias [B, L] fp32 (0 / -inf) or None.  Returns (P, Pd)."""
+    R, L = S.shape
+    if _cuda(S):
+        P = torch.empty_like(S)
+        Pd = torch.empty_like(S) if p > 0 else P
+        _lib.call('mlc_softmax_fwd', _lib.ptr(S), _lib.ptr(key_bias), _lib.ptr(P),
+                  _lib.ptr(Pd if p > 0 else None), R, L, rows_per_batch, float(scale), float(p), _lib.ptr(seed),
+                  salt, _lib.stream())
+        return P, Pd
+    v = S.float() * scale
+    if key_bias is not None:
+        v = v + key_bias.repeat_interleave(rows_per_batch, 0)
+    Pf = torch.softmax(v, 1).nan_to_num(0.0)
+    P = Pf.to(torch.bfloat16)
+    if p > 0:
+        m = keep_mask((R, L), p, _seed_val(seed), salt)
+        Pd = torch.where(m, Pf / (1 - p), torch.zeros_like(Pf)).to(torch.bfloat16)
+    else:
+        Pd = P
+    return P, Pd
+
+
+def softmax_bwd(P, dPd, scale, p=0.0, seed=None, salt=0):
+    R, L = P.shape
+    if _cuda(P):
+        dS = torch.empty_like(P)
+        _lib.call('mlc_softmax_bwd', _lib.ptr(P), _lib.ptr(dPd), _lib.ptr(dS), R, L, float(scale), float(p),
+                  _lib.ptr(seed), salt, _lib.stream())
+        return dS
+    d = dPd.float()
+    if p > 0:
+        d = torch.where(keep_mask((R, L), p, _seed_val(seed), salt), d / (1 - p), torch.zeros_like(d))
+    Pf = P.float()
+    dot = (Pf * d).sum(1, keepdim=True)
+    return (scale * Pf * (d - dot)).to(torch.bfloat16)
+
+
+# ---------------------------------------------------------------------------- dense layers
+def _gelu(u):
+    return 0.5 * u * (1.0 + torch.erf(u / math.sqrt(2.0)))
+
+
+def _dgelu(u):
+    return 0.5 * (1.0 + torch.erf(u / math.sqrt(2.0))) + u * torch.exp(-0.5 * u * u) / math.sqrt(2 * math.pi)
+
+
+def dense_fwd(x, w, bias=None, act: int = 0, want_preact: bool = False):
+    """y = act(x @ w^T + bias): x [M, K] bf16, w [N, K] bf16, bias fp32 [N].  Returns
+    (y, u) with u the bf16 pre-activation (when ``want_preact``)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if _cuda(x):
+        y = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
+        u = torch.empty_like(y) if want_preact else None
+        _lib.call('mlc_gemm_bf16_ex', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), M, N, K, K, K, N, 0, 1,
+                  _lib.ptr(bias), act, _lib.ptr(u), None, None, _lib.stream())
+        return y, u
+    z = x.float() @ w.float().t()
+    if bias is not None:
+        z = z + bias
+    u = z.to(torch.bfloat16) if want_preact else None
+    if act == 1:
+        z = _gelu(z)
+    return z.to(torch.bfloat16), u
+
+
+def dense_dgrad(dy, w, dact_u=None, addend=None):
+    """dx = (dy @ w) [* gelu'(dact_u)] [+ addend]: dy [M, N], w [N, K] -> [M, K] bf16."""
+    M, N = dy.shape
+    K = w.shape[1]
+    if _cuda(dy):
+        dx = torch.empty(M, K, device=dy.device, dtype=torch.bfloat16)
+        _lib.call('mlc_gemm_bf16_ex', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(dx), M, K, N, N, K, K, 0, 0, None, 0,
+                  None, _lib.ptr(addend), _lib.ptr(dact_u), _lib.stream())
+        return dx
+    z = dy.float() @ w.float()
+    z = z.to(torch.bfloat16).float()
+    if dact_u is not None:
+        z = z * _dgelu(dact_u.float())
+    if addend is not None:
+        z = z + addend.float()
+    return z.to(torch.bfloat16)
+
+
+def dact_gelu(dy, u):
+    """dy * gelu'(u) as a standalone op (used when the GEMM producing dy cannot fuse it)."""
+    return (dy.float() * _dgelu(u.float())).to(torch.bfloat16)
+
+
+def colsum_acc(g, out):
+    """out += column sums of g [R, C] bf16."""
+    R, C = g.shape
+    if _cuda(g):
+        _lib.call('mlc_colsum_acc', _lib.ptr(g), _lib.ptr(out), R, C, _lib.stream())
+        return out
+    out.add_(g.float().sum(0))
+    return out
+
+
+def dropout(x, p, seed, salt):
+    if p <= 0:
+        return x
+    if _cuda(x):
+        y = torch.empty_like(x)
+        _lib.call('mlc_dropout', _lib.ptr(x), _lib.ptr(y), x.numel(), float(p), _lib.ptr(seed), salt, _lib.stream())
+        return y
+    m = keep_mask(tuple(x.shape), p, _seed_val(seed), salt)
+    return torch.where(m, x.float() / (1 - p), torch.zeros_like(x, dtype=torch.float32)).to(x.dtype)
+
+
+__all__ = ['ln_fwd', 'ln_bwd', 'softmax_fwd', 'softmax_bwd', 'dense_fwd', 'dense_dgrad', 'dact_gelu', 'colsum_acc',
+           'dropout', 'keep_mask']

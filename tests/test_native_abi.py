@@ -7,7 +7,7 @@ import re
 from mlcomp_amd.ops import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-_TYPES = {'int': 'i32', 'long': 'i64', 'float': 'f32'}
+_TYPES = {'int': 'i32', 'long': 'i64', 'float': 'f32', 'uint32_t': 'u32'}
 
 
 def _parse():
@@ -28,7 +28,7 @@ def _parse():
 
 def test_signatures_match():
     decls = _parse()
-    names = {_lib.vp: 'vp', _lib.i32: 'i32', _lib.i64: 'i64', _lib.f32: 'f32'}
+    names = {_lib.vp: 'vp', _lib.i32: 'i32', _lib.i64: 'i64', _lib.f32: 'f32', _lib.u32: 'u32'}
     assert set(decls) == set(_lib._SIGS), set(decls) ^ set(_lib._SIGS)
     for name, kinds in decls.items():
         got = [names[t] for t in _lib._SIGS[name]]

@@ -1,0 +1,119 @@
+"""Transformer kernels (LayerNorm, softmax, dense GEMM epilogues, dropout) on the GPU vs
+their fp32 PyTorch references (which reproduce the dropout hash bit-exactly), and the
+native BERT step."""
+import pytest
+import torch
+
+from mlcomp_amd.ops import transformer as Tx
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _bf(*s, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*s, generator=g) * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize('H,p', [(768, 0.0), (768, 0.1), (1024, 0.1), (128, 0.0), (2048, 0.2)])
+def test_layernorm_fwd_bwd(H, p):
+    T = 333
+    x, r, dy = _bf(T, H, seed=1), _bf(T, H, seed=2), _bf(T, H, seed=3)
+    g = torch.rand(H) + 0.5
+    b = torch.randn(H) * 0.1
+    seed = torch.tensor([7], dtype=torch.int32)
+    ref = Tx.ln_fwd(x, r, g, b, 1e-12, p_in=p, p_out=p / 2, seed=seed, salt_in=3, salt_out=4)
+    got = Tx.ln_fwd(x.to(DEV), r.to(DEV), g.to(DEV), b.to(DEV), 1e-12, p_in=p, p_out=p / 2, seed=seed.to(DEV),
+                    salt_in=3, salt_out=4)
+    assert rel(got[0], ref[0]) < 1e-2 and rel(got[1], ref[1]) < 1e-2
+    assert rel(got[2], ref[2]) < 1e-4 and rel(got[3], ref[3]) < 1e-4
+    dg_r, db_r = torch.zeros(H), torch.zeros(H)
+    dg_g, db_g = torch.zeros(H, device=DEV), torch.zeros(H, device=DEV)
+    rb = Tx.ln_bwd(dy, ref[1], ref[2], ref[3], g, dg_r, db_r, p_in=p, p_out=p / 2, seed=seed, salt_in=3,
+                   salt_out=4, want_dr=True)
+    gb = Tx.ln_bwd(dy.to(DEV), got[1], got[2], got[3], g.to(DEV), dg_g, db_g, p_in=p, p_out=p / 2,
+                   seed=seed.to(DEV), salt_in=3, salt_out=4, want_dr=True)
+    torch.cuda.synchronize()
+    assert rel(gb[0], rb[0]) < 2e-2 and rel(gb[1], rb[1]) < 2e-2
+    assert rel(dg_g, dg_r) < 1e-2 and rel(db_g, db_r) < 1e-2
+
+
+@pytest.mark.parametrize('L,p,masked', [(128, 0.0, False), (128, 0.1, True), (512, 0.1, True), (64, 0.0, True)])
+def test_softmax_fwd_bwd(L, p, masked):
+    B, nh = 3, 4
+    R = B * nh * L
+    S, dPd = _bf(R, L, seed=4, scale=3.0), _bf(R, L, seed=5)
+    kb = None
+    if masked:
+        am = torch.ones(B, L)
+        am[0, L // 2:] = 0
+        kb = torch.zeros(B, L).masked_fill(am == 0, float('-inf'))
+    seed = torch.tensor([11], dtype=torch.int32)
+    P_r, Pd_r = Tx.softmax_fwd(S, kb, nh * L, 0.125, p, seed, 9)
+    P_g, Pd_g = Tx.softmax_fwd(S.to(DEV), kb.to(DEV) if kb is not None else None, nh * L, 0.125, p, seed.to(DEV), 9)
+    assert rel(P_g, P_r) < 1e-2 and rel(Pd_g, Pd_r) < 1e-2
+    dS_r = Tx.softmax_bwd(P_r, dPd, 0.125, p, seed, 9)
+    dS_g = Tx.softmax_bwd(P_g, dPd.to(DEV), 0.125, p, seed.to(DEV), 9)
+    torch.cuda.synchronize()
+    assert rel(dS_g, dS_r) < 2e-2
+
+
+@pytest.mark.parametrize('M,N,K', [(512, 3072, 768), (300, 768, 3072), (4096, 2304, 768), (64, 8, 128)])
+def test_dense_epilogues(M, N, K):
+    x, w = _bf(M, K, seed=6), _bf(N, K, seed=7, scale=K ** -0.5)
+    bias = torch.randn(N) * 0.1
+    y_r, u_r = Tx.dense_fwd(x, w, bias, act=1, want_preact=True)
+    y_g, u_g = Tx.dense_fwd(x.to(DEV), w.to(DEV), bias.to(DEV), act=1, want_preact=True)
+    assert rel(y_g, y_r) < 1e-2 and rel(u_g, u_r) < 1e-2
+    dy, add = _bf(M, N, seed=8), _bf(M, K, seed=9)
+    dx_r = Tx.dense_dgrad(dy, w, dact_u=None, addend=add)
+    dx_g = Tx.dense_dgrad(dy.to(DEV), w.to(DEV), addend=add.to(DEV))
+    assert rel(dx_g, dx_r) < 1e-2
+    # GELU-derivative epilogue: (dy2 @ w2) * gelu'(u)
+    w2 = _bf(K, N, seed=10, scale=N ** -0.5)
+    dy2 = _bf(M, K, seed=11)
+    r = Tx.dense_dgrad(dy2, w2, dact_u=u_r)
+    g = Tx.dense_dgrad(dy2.to(DEV), w2.to(DEV), dact_u=u_g)
+    torch.cuda.synchronize()
+    assert rel(g, r) < 2e-2
+    o_r, o_g = torch.zeros(N), torch.zeros(N, device=DEV)
+    Tx.colsum_acc(dy, o_r)
+    Tx.colsum_acc(dy.to(DEV), o_g)
+    assert rel(o_g, o_r) < 1e-4
+
+
+def test_dropout_kernel_matches_hash():
+    x = _bf(1000, 64, seed=12)
+    seed = torch.tensor([3], dtype=torch.int32)
+    assert torch.equal(Tx.dropout(x.to(DEV), 0.3, seed.to(DEV), 5).cpu(), Tx.dropout(x, 0.3, seed, 5))
+
+
+def test_native_bert_step_trains_and_graph_matches():
+    from mlcomp_amd.models import build_model
+    from mlcomp_amd.train.native_bert_step import NativeBertStep
+    torch.manual_seed(0)
+    st = NativeBertStep('bert-small', batch=16, seq_len=128, device=DEV, use_graph=False, lr=1e-4)
+    losses = []
+    for _ in range(25):
+        st()
+        losses.append(st.last_loss())
+    assert all(l == l for l in losses)
+    assert min(losses[-5:]) < losses[0], losses
+    tm1 = build_model('bert-small', num_labels=2)
+    tm2 = build_model('bert-small', num_labels=2)
+    tm2.load_state_dict(tm1.state_dict())
+    a = NativeBertStep(torch_model=tm1, batch=8, seq_len=64, device=DEV, use_graph=False, lr=1e-4)
+    b = NativeBertStep(torch_model=tm2, batch=8, seq_len=64, device=DEV, use_graph=True, lr=1e-4, warmup_eager=2)
+    for _ in range(5):
+        a()
+        b()
+    torch.cuda.synchronize()
+    assert b.graph is not None
+    assert abs(a.last_loss() - b.last_loss()) < 1e-2 * max(1.0, abs(a.last_loss()))
+    pa, pb = a.net.arena.decay.master, b.net.arena.decay.master
+    assert ((pa - pb).norm() / pa.norm()).item() < 1e-3
