@@ -361,7 +361,7 @@ struct BnBwdEpi {
   const bf16* y1 = nullptr; const float* mean1 = nullptr; float* sums1 = nullptr;
 };
 
-template <class RowMap = IdentityRows>
+template <class RowMap = IdentityRows, bool kDense = false>
 struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / sum of squares
   bf16* out; int ld; float* sum; float* sumsq; RowMap rowmap; const bf16* addend = nullptr;
   BnBwdEpi bn = {};
@@ -408,7 +408,7 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
     constexpr int RPI = NTHR / CPR;          // rows per iteration
     const int c = tid % CPR;
     const int nc = n0 + c * 8;
-    const bool red = bn.y0 != nullptr;
+    const bool red = !kDense && bn.y0 != nullptr;
     float mu0[8], mu1[8], s1[8], s2[8], t2[8];
     if (red) {
 #pragma unroll
@@ -418,7 +418,7 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
         s1[e] = 0.f; s2[e] = 0.f; t2[e] = 0.f;
       }
     }
-    const bool dense = bias || act || dact;
+    const bool dense = kDense && (bias || act || dact);
     if (!addend && !red && !dense) {  // plain store (forward convs / GEMMs)
 #pragma unroll
       for (int it = 0; it < BM / RPI; ++it) {
@@ -438,7 +438,9 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
     const bool has_add = addend != nullptr, has_mask = red && bn.mask, has_y1 = red && bn.y1;
 #pragma unroll
     for (int it0 = 0; it0 < ITERS; it0 += U) {
-      uint4 vv[U], aa[U], zz[U], p0[U], p1[U], du[U];
+      constexpr int UB = kDense ? 1 : U;   // BN-reduction operands (conv dgrad only)
+      constexpr int UD = kDense ? U : 1;   // activation-derivative operand (dense only)
+      uint4 vv[U], aa[U], zz[UB], p0[UB], p1[UB], du[UD];
       size_t off[U];
       bool ok[U];
 #pragma unroll
@@ -450,10 +452,12 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
         vv[u] = *reinterpret_cast<const uint4*>(lds + row * RS + c * 16);
         const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
         aa[u] = (ok[u] && has_add) ? *reinterpret_cast<const uint4*>(addend + off[u]) : zero;
-        zz[u] = (ok[u] && has_mask) ? *reinterpret_cast<const uint4*>(bn.mask + off[u]) : zero;
-        p0[u] = (ok[u] && red) ? *reinterpret_cast<const uint4*>(bn.y0 + off[u]) : zero;
-        p1[u] = (ok[u] && has_y1) ? *reinterpret_cast<const uint4*>(bn.y1 + off[u]) : zero;
-        du[u] = (ok[u] && dact) ? *reinterpret_cast<const uint4*>(dact + off[u]) : zero;
+        if constexpr (!kDense) {
+          zz[u] = (ok[u] && has_mask) ? *reinterpret_cast<const uint4*>(bn.mask + off[u]) : zero;
+          p0[u] = (ok[u] && red) ? *reinterpret_cast<const uint4*>(bn.y0 + off[u]) : zero;
+          p1[u] = (ok[u] && has_y1) ? *reinterpret_cast<const uint4*>(bn.y1 + off[u]) : zero;
+        }
+        if constexpr (kDense) du[u] = (ok[u] && dact) ? *reinterpret_cast<const uint4*>(dact + off[u]) : zero;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -462,6 +466,7 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
         if (has_add || red || dense) {
           float a[8];
           unpack8(v, a);
+          if constexpr (kDense) {
           if (bias) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) a[e] += bias[nc + e];
@@ -481,20 +486,21 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
               a[e] *= cdf + z[e] * pdf;
             }
           }
+          }
           if (has_add) {  // fused residual-gradient sum (dx of a branch point)
             float b[8];
             unpack8(aa[u], b);
 #pragma unroll
             for (int e = 0; e < 8; ++e) a[e] += b[e];
           }
-          if (has_mask) {
+          if constexpr (!kDense) if (has_mask) {
             float z[8];
             unpack8(zz[u], z);
 #pragma unroll
             for (int e = 0; e < 8; ++e) a[e] = z[e] > 0.f ? a[e] : 0.f;
           }
           v = pack8(a);
-          if (red) {
+          if constexpr (!kDense) if (red) {
             unpack8(v, a);  // reduce exactly the bf16 values that are stored
             float y[8];
             unpack8(p0[u], y);
@@ -699,7 +705,7 @@ static int auto_splits(int M, int N, int K, int tile) {
   const int tiles = ((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
   const int ktiles = (K + BK - 1) / BK;
   int s = 1;
-  while (tiles * s < 768 && ktiles / (s * 2) >= 8) s *= 2;
+  while (tiles * s < 768 && ktiles / (s * 2) >= 4) s *= 2;
   return s;
 }
 
@@ -886,7 +892,7 @@ MLC_EXPORT int mlc_gemm_bf16_ex(const bf16* A, const bf16* B, bf16* C, int M, in
                                 const bf16* addend, const bf16* dact, hipStream_t st) {
   if (K % 8 || N % 8 || ldc % 8 || lda % 8 || ldb % 8 || (ta && M % 8)) return -1;
   const int tile = pick_tile(M, N);
-  EpiBF16<> epi{C, ldc, nullptr, nullptr, IdentityRows{}, addend};
+  EpiBF16<IdentityRows, true> epi{C, ldc, nullptr, nullptr, IdentityRows{}, addend};
   epi.bias = bias; epi.act = act; epi.preact = preact; epi.dact = dact;
   if (!ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_KC, GB_KC);
   if (!ta && !tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_KC, GB_MC);

@@ -421,7 +421,10 @@ MLC_EXPORT int mlc_softmax_bwd(const bf16* P, const bf16* dPd, bf16* dS, long R,
 // out[C] += column sums of g[R][C] (C % 8 == 0)
 MLC_EXPORT int mlc_colsum_acc(const bf16* g, float* out, int R, int C, hipStream_t st) {
   if (C % 8) return -1;
-  const int RB = 128;
+  // enough row blocks for ~1024 workgroups, at least 8 rows each (atomics per block = C)
+  const int xb = (C / 8 + NT - 1) / NT;
+  int RB = (R * xb + 1023) / 1024;
+  if (RB < 8) RB = 8;
   dim3 grid((C / 8 + NT - 1) / NT, (R + RB - 1) / RB);
   hipLaunchKernelGGL(colsum_atomic_kernel, grid, dim3(NT), 0, st, g, out, R, C, RB);
   return hipGetLastError();

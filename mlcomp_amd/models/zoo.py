@@ -45,6 +45,26 @@ class Pretrained(nn.Module):
         return self.activation(y) if self.activation else y
 
 
+@register('LeNet')
+class LeNet(nn.Module):
+    """The digit-recognizer example net (`examples/digit-recognizer/model.py:8-25`):
+    conv5(20) -> pool -> conv5(50) -> pool -> fc(500) -> fc(classes), log-softmax out."""
+
+    def __init__(self, in_channels: int = 1, num_classes: int = 10, image_size: int = 28):
+        super().__init__()
+        self.conv1 = nn.Conv2d(in_channels, 20, 5)
+        self.conv2 = nn.Conv2d(20, 50, 5)
+        s = ((image_size - 4) // 2 - 4) // 2
+        self.fc1 = nn.Linear(50 * s * s, 500)
+        self.fc2 = nn.Linear(500, num_classes)
+
+    def forward(self, x):
+        x = torch.nn.functional.max_pool2d(torch.relu(self.conv1(x)), 2)
+        x = torch.nn.functional.max_pool2d(torch.relu(self.conv2(x)), 2)
+        x = torch.relu(self.fc1(x.flatten(1)))
+        return torch.log_softmax(self.fc2(x), dim=1)
+
+
 @register('SimpleCNN')
 class SimpleCNN(nn.Module):
     def __init__(self, in_channels: int = 3, num_classes: int = 10, width: int = 16, image_size: int = 32):
@@ -104,4 +124,4 @@ class Timm(Pretrained):
 
 _register_encoder_classifiers()
 
-__all__ = ['Pretrained', 'SimpleCNN', 'EncoderClassifier', 'Timm']
+__all__ = ['Pretrained', 'SimpleCNN', 'LeNet', 'EncoderClassifier', 'Timm']

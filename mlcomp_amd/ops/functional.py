@@ -330,13 +330,19 @@ def linear_dgrad(dout, w):
 
 
 def linear_wgrad(dout, x, out=None, accumulate=False):
-    """dW [O, I] fp32 = dout^T x."""
+    """dW [O, I] fp32 = dout^T x (+= into ``out`` when ``accumulate``).  Accumulation
+    uses split-K with fp32 atomics, so small weight matrices (M x N tiles << CUs) still
+    spread the long token reduction over the whole chip."""
     B, O = dout.shape
     I = x.shape[1]
     if _cuda(dout):
         dw = out if out is not None else torch.empty(O, I, device=dout.device, dtype=torch.float32)
-        _lib.call('mlc_gemm_f32out', _lib.ptr(dout), _lib.ptr(x), _lib.ptr(dw), None, O, I, B, O, I, I,
-                  1, 0, 0, int(accumulate), 1, _lib.stream())
+        if accumulate:
+            _lib.call('mlc_gemm_f32out', _lib.ptr(dout), _lib.ptr(x), _lib.ptr(dw), None, O, I, B, O, I, I,
+                      1, 0, 1, 1, 0, _lib.stream())
+        else:
+            _lib.call('mlc_gemm_f32out', _lib.ptr(dout), _lib.ptr(x), _lib.ptr(dw), None, O, I, B, O, I, I,
+                      1, 0, 0, 0, 1, _lib.stream())
         return dw
     g = dout.float().t() @ x.float()
     if out is not None:

@@ -129,6 +129,27 @@ class AccuracyCallback(Callback):
 
 
 @register_callback
+class DiceCallback(Callback):
+    """Batch Dice of thresholded sigmoid (or argmax-softmax one-hot) predictions."""
+    order = 30
+
+    def __init__(self, input_key='targets', output_key='logits', prefix='dice', threshold=0.5, activation='sigmoid',
+                 eps=1e-7):
+        self.input_key, self.output_key, self.prefix = input_key, output_key, prefix
+        self.threshold, self.activation, self.eps = threshold, activation, eps
+
+    def on_batch_end(self, state):
+        out = state.output.get(self.output_key) if state.output else None
+        if out is None:
+            return
+        from mlcomp_amd.contrib.metrics import dice
+        with torch.no_grad():
+            state.batch_metrics[self.prefix] = float(dice(out.detach(), state.input[self.input_key],
+                                                          eps=self.eps, threshold=self.threshold,
+                                                          activation=self.activation))
+
+
+@register_callback
 class SchedulerCallback(Callback):
     order = 40
 

@@ -42,6 +42,59 @@ class SyntheticClassification(Dataset):
         return {'features': x, 'targets': y}
 
 
+@register_dataset('synthetic_text_classification')
+class SyntheticTextClassification(Dataset):
+    """Random token ids (two segments) with labels; ``learnable`` makes the label a
+    function of the first token so fine-tuning has signal."""
+
+    def __init__(self, num_samples=256, seq_len=128, vocab_size=30522, num_classes=2, seed=0, learnable=True,
+                 pad_fraction=0.0, **_):
+        g = torch.Generator().manual_seed(seed)
+        self.ids = torch.randint(1, vocab_size, (num_samples, seq_len), generator=g)
+        self.y = (self.ids[:, 1] % num_classes) if learnable else torch.randint(0, num_classes, (num_samples,),
+                                                                                 generator=g)
+        self.tt = torch.zeros(num_samples, seq_len, dtype=torch.long)
+        self.tt[:, seq_len // 2:] = 1
+        self.mask = torch.ones(num_samples, seq_len, dtype=torch.long)
+        if pad_fraction > 0:
+            lens = torch.randint(int(seq_len * (1 - pad_fraction)), seq_len + 1, (num_samples,), generator=g)
+            self.mask = (torch.arange(seq_len)[None] < lens[:, None]).long()
+
+    def __len__(self):
+        return len(self.y)
+
+    def __getitem__(self, i):
+        return {'input_ids': self.ids[i], 'token_type_ids': self.tt[i], 'attention_mask': self.mask[i],
+                'targets': int(self.y[i])}
+
+
+@register_dataset('synthetic_segmentation')
+class SyntheticSegmentation(Dataset):
+    """Images with 1-3 random filled discs per class; targets are the one-hot masks
+    (learnable: the disc colour encodes its class)."""
+
+    def __init__(self, num_samples=64, image_size=128, num_classes=1, seed=0, **_):
+        self.n, self.size, self.k, self.seed = num_samples, image_size, num_classes, seed
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        g = torch.Generator().manual_seed(self.seed * 1000003 + i)
+        s = self.size
+        yy, xx = torch.meshgrid(torch.arange(s), torch.arange(s), indexing='ij')
+        img = torch.randn(3, s, s, generator=g) * 0.3
+        mask = torch.zeros(self.k, s, s)
+        for c in range(self.k):
+            for _ in range(int(torch.randint(1, 4, (1,), generator=g))):
+                cy, cx = torch.randint(0, s, (2,), generator=g).tolist()
+                r = int(torch.randint(s // 16 + 1, s // 5 + 2, (1,), generator=g))
+                disc = ((yy - cy) ** 2 + (xx - cx) ** 2) <= r * r
+                mask[c][disc] = 1.0
+                img[c % 3][disc] += 1.0 + 0.5 * (c // 3)
+        return {'features': img, 'targets': mask}
+
+
 class DeviceSyntheticLoader:
     """Fixed random batches resident on the device (NHWC bf16 when ``nhwc_pad`` is set
     for the native engine, NCHW fp32 otherwise); ``steps`` batches per epoch."""
@@ -122,5 +175,6 @@ def make_loader(dataset, batch_size, shuffle, num_workers=0, world_size=1, rank=
                       persistent_workers=num_workers > 0)
 
 
-__all__ = ['DATASETS', 'register_dataset', 'SyntheticClassification', 'DeviceSyntheticLoader',
+__all__ = ['DATASETS', 'register_dataset', 'SyntheticClassification', 'SyntheticTextClassification',
+           'SyntheticSegmentation', 'DeviceSyntheticLoader',
            'DistributedSamplerIndices', 'make_loader', 'collate_dict']

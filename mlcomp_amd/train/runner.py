@@ -88,9 +88,21 @@ class State:
         return self.runner.current_lr()
 
 
-def _native_capable(model: nn.Module, device: torch.device) -> bool:
+def _native_kind(model: nn.Module, device: torch.device) -> Optional[str]:
+    """'resnet' / 'bert' when the model runs on a native engine on this device."""
+    if device.type != 'cuda':
+        return None
+    from mlcomp_amd.models.bert import BertForSequenceClassification
     from mlcomp_amd.models.resnet import ResNet
-    return device.type == 'cuda' and isinstance(model, ResNet) and model.groups == 1 and model.include_top
+    if isinstance(model, ResNet) and model.groups == 1 and model.include_top:
+        return 'resnet'
+    if isinstance(model, BertForSequenceClassification):
+        return 'bert'
+    return None
+
+
+def _native_capable(model: nn.Module, device: torch.device) -> bool:
+    return _native_kind(model, device) is not None
 
 
 class Runner:
@@ -117,8 +129,9 @@ class Runner:
             self.model = self.experiment.get_model(stage)
         use_native = self.engine == 'native' or (self.engine == 'auto' and _native_capable(self.model, self.device))
         if self.engine == 'native' and not _native_capable(self.model, self.device):
-            raise RuntimeError('engine: native needs a ResNet-family classifier (groups=1) on a GPU')
+            raise RuntimeError('engine: native needs a ResNet-family classifier (groups=1) or BERT on a GPU')
         self.state.native = use_native
+        self.native_kind = _native_kind(self.model, self.device) if use_native else None
         if not use_native:
             self.model.to(self.device)
             if self.device.type == 'cuda':
@@ -131,8 +144,21 @@ class Runner:
                 self.ddp_model = self.model
 
     def _build_native(self, stage, batch):
-        from .native_step import NativeClassifierStep
         spec = self.experiment.optimizer_spec(stage)
+        if self.native_kind == 'bert':
+            from .native_bert_step import NativeBertStep
+            ids = batch['input_ids']
+            self.model.to(self.device)
+            self.native_step = NativeBertStep(
+                torch_model=self.model, batch=ids.shape[0], seq_len=ids.shape[1], device=self.device,
+                world_size=self.world_size, num_labels=self.model.config.num_labels, lr=spec.get('lr', 2e-5),
+                weight_decay=spec.get('weight_decay', 0.01), betas=tuple(spec.get('betas', (0.9, 0.999))),
+                eps=spec.get('eps', 1e-6), use_graph=self.experiment.args.get('graph', True))
+            dummy = torch.zeros(1, requires_grad=True)
+            self.optimizer = torch.optim.SGD([dummy], lr=spec.get('lr', 2e-5))
+            self.scheduler = self.experiment.get_scheduler(stage, self.optimizer)
+            return
+        from .native_step import NativeClassifierStep
         name = spec.get('optimizer', 'SGD')
         x = batch['features']
         size = x.shape[1] if x.dtype == torch.bfloat16 and x.shape[-1] == 8 else x.shape[-1]
@@ -214,6 +240,17 @@ class Runner:
     # ------------------------------------------------------------------ loops
     def _run_batch_torch(self, batch):
         st = self.state
+        if 'input_ids' in batch:   # text classification (BERT family)
+            dev = lambda k: batch[k].to(self.device, non_blocking=True) if batch.get(k) is not None else None  # noqa
+            ids, y = dev('input_ids'), dev('targets')
+            st.input = {'input_ids': ids, 'targets': y}
+            with torch.set_grad_enabled(st.is_train), \
+                    torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.device.type == 'cuda'):
+                out = (self.ddp_model if st.is_train else self.model)(ids, dev('token_type_ids'),
+                                                                     dev('attention_mask'))
+            st.output = {'logits': out.float()}
+            st.batch_size = ids.shape[0]
+            return
         x = batch['features'].to(self.device, non_blocking=True)
         y = batch['targets'].to(self.device, non_blocking=True)
         if self.device.type == 'cuda' and x.dim() == 4:
@@ -251,13 +288,20 @@ class Runner:
                     self._build_native(st.stage, batch)
                     self.sync_lr()
                 ns = self.native_step
-                ns.load_batch(batch['features'], batch['targets'])
+                if self.native_kind == 'bert':
+                    ns.load_batch(batch['input_ids'], batch['targets'], batch.get('token_type_ids'),
+                                  batch.get('attention_mask'))
+                    head = ns.net
+                else:
+                    ns.load_batch(batch['features'], batch['targets'])
+                    head = ns.net.head
                 ns()
+                self._exported = False
                 st.batch_size = ns.batch
                 if dev_loss is None:
                     dev_loss = torch.zeros(2, device=self.device)
-                dev_loss[0] += ns.net.head.loss_sum()[0]
-                dev_loss[1] += ns.net.head.correct()[0]
+                dev_loss[0] += head.loss_sum()[0]
+                dev_loss[1] += head.correct()[0]
                 n_samples += ns.batch
             elif st.native:
                 self._run_native_eval(batch)
@@ -281,6 +325,15 @@ class Runner:
     def _run_native_eval(self, batch):
         st = self.state
         ns = self.native_step
+        if self.native_kind == 'bert' or ns is None and 'input_ids' in batch:
+            if ns is not None and not getattr(self, '_exported', False):
+                ns.net.export_to_torch()
+                self._exported = True
+            self.model.to(self.device).eval()
+            self._run_batch_torch(batch)
+            self.model.train()
+            st.loss = torch.nn.functional.cross_entropy(st.output['logits'], st.input['targets'])
+            return
         x = batch['features'].to(self.device)
         y = batch['targets'].to(self.device)
         if x.dtype != torch.bfloat16:

@@ -18,3 +18,5 @@ timeout -k 10 300 python bench.py --steps 30 --warmup 5 > $OUT/resnet_native.log
 tail -1 $OUT/resnet_native.log; fatal $rc resnet
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bert -- python bench.py --model bert-base --steps 5 --warmup 3 --graph 0 > $OUT/prof.log 2>&1
 echo "exit $?"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_resnet -o native -- python bench.py --steps 5 --warmup 3 --graph 0 > $OUT/prof_resnet.log 2>&1
+echo "exit $?"

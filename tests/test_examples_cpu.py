@@ -1,0 +1,78 @@
+"""The shipped examples: every DAG config builds, and the CPU-runnable ones (bash, grid,
+click, hierarchical logging, progress bar, MNIST LeNet = BASELINE config 1) run to
+completion through scheduler -> broker -> worker pool -> task processes."""
+import os
+import shutil
+
+import pytest
+import yaml
+
+from test_lifecycle import _wait, cluster  # noqa: F401
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EX = os.path.join(ROOT, 'examples')
+
+
+def _run_example(tmp, rel_config, params=None):
+    from mlcomp_amd.dag import dag_from_config
+    from mlcomp_amd.db.core import Session
+    folder = os.path.dirname(rel_config)
+    dst = tmp / f'{folder}_{len(os.listdir(tmp))}'
+    shutil.copytree(os.path.join(EX, folder), dst)
+    cfg_path = dst / os.path.basename(rel_config)
+    text = cfg_path.read_text()
+    cwd = os.getcwd()
+    os.chdir(dst)
+    try:
+        return dag_from_config(Session.create_session(key='ex'), yaml.safe_load(text), config_path=str(cfg_path),
+                               config_text=text, params=params)
+    finally:
+        os.chdir(cwd)
+
+
+def _ids(created):
+    return [i for d in created for ids in d.values() for i in ids]
+
+
+ALL_CONFIGS = ['bash/config.yml', 'bash/config_error.yml', 'bash/config_grid.yml', 'grid/dag.yml', 'grid/task.yml',
+               'click/config.yml', 'hierarchical_logging/config.yml', 'progress_bar/config.yml',
+               'mnist_lenet/config.yml', 'resnet50_ddp/config.yml', 'unet_segmentation/config.yml',
+               'bert_finetune/config.yml', 'multi_branch/config.yml']
+
+
+def test_all_example_dags_build(cluster):
+    counts = {}
+    for c in ALL_CONFIGS:
+        counts[c] = len(_ids(_run_example(cluster['tmp'], c)))
+    assert counts['bash/config_grid.yml'] == 11
+    assert counts['grid/dag.yml'] == 6          # 3 DAGs x 2 tasks
+    assert counts['unet_segmentation/config.yml'] == 2
+    assert counts['multi_branch/config.yml'] == 3
+
+
+@pytest.mark.parametrize('cfg,expect', [('bash/config.yml', 'success'), ('bash/config_error.yml', 'failed'),
+                                        ('grid/task.yml', 'success'), ('click/config.yml', 'success'),
+                                        ('hierarchical_logging/config.yml', 'success'),
+                                        ('progress_bar/config.yml', 'success')])
+def test_cpu_examples_run(cluster, cfg, expect):
+    from mlcomp_amd.db.enums import TaskStatus
+    ids = _ids(_run_example(cluster['tmp'], cfg))
+    res = _wait(cluster['sup'], ids, timeout=120)
+    want = TaskStatus.Success if expect == 'success' else TaskStatus.Failed
+    assert all(v == want for v in res.values()), res
+
+
+def test_mnist_lenet_dag_trains_on_cpu(cluster):
+    """BASELINE.json config 1: MNIST LeNet single-task train DAG, 1 worker, CPU."""
+    from mlcomp_amd.db.core import Session
+    from mlcomp_amd.db.enums import TaskStatus
+    from mlcomp_amd.db.models import ReportSeries, Task
+    ids = _ids(_run_example(cluster['tmp'], 'mnist_lenet/config.yml',
+                            params={'executors/train/args/config': 'catalyst.yml'}))
+    res = _wait(cluster['sup'], ids, timeout=300)
+    assert all(v == TaskStatus.Success for v in res.values()), res
+    s = Session.create_session(key='mn')
+    t = s.get(Task, ids[0])
+    assert t.score is not None
+    names = {(r.part, r.name) for r in s.query(ReportSeries).filter(ReportSeries.task == t.id)}
+    assert ('valid', 'accuracy01') in names and ('train', 'loss') in names
