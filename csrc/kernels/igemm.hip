@@ -887,11 +887,96 @@ MLC_EXPORT int mlc_gemm_f32out(const bf16* A, const bf16* B, float* C, const flo
 
 // bf16-output GEMM with a dense-layer epilogue: C = act(op(A) op(B) + bias) (pre-
 // activation to preact when given), or C = (op(A) op(B)) * act'(dact) (+ addend).
+
+// non-returning tile dispatch (for callers that continue after the GEMM)
+template <class EPI, class FA, class FB>
+static hipError_t launch_tiles(int tile, int M, int N, int K, int splits, hipStream_t st, const EPI& epi, FA fa,
+                               FB fb) {
+  if (tile == 1) return launch<256, 64>(fa.template make<256>(), fb.template make<64>(), epi, M, N, K, splits, st);
+  if (tile == 2) return launch<64, 256>(fa.template make<64>(), fb.template make<256>(), epi, M, N, K, splits, st);
+  return launch<128, 128>(fa.template make<128>(), fb.template make<128>(), epi, M, N, K, splits, st);
+}
+struct MkMatKC { const bf16* p; int ld, rows, K; template <int R> MatKC<R> make() const { return MatKC<R>{{}, p, ld, rows, K}; } };
+struct MkMatMC { const bf16* p; int ld, K, cols; template <int R> MatMC<R> make() const { return MatMC<R>{{}, p, ld, K, cols}; } };
+#define GA_KC_F (MkMatKC{A, lda, M, K})
+#define GA_MC_F (MkMatMC{A, lda, K, M})
+#define GB_KC_F (MkMatKC{B, ldb, N, K})
+#define GB_MC_F (MkMatMC{B, ldb, K, N})
+
+namespace {
+// Split-K finish for the dense GEMM: ws [M][N] fp32 holds the split-K sums (zero on
+// entry; re-zeroed here so the next call can reuse it), C = epilogue(ws) in bf16.
+__global__ void __launch_bounds__(256)
+dense_finalize_kernel(float* __restrict__ ws, bf16* __restrict__ C, int ldc, const float* __restrict__ bias,
+                      int act, bf16* __restrict__ preact, const bf16* __restrict__ addend,
+                      const bf16* __restrict__ dact, int M, int N) {
+  const long n8 = (long)M * (N / 8);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    const int m = (int)(i / (N / 8)), c = (int)(i % (N / 8)) * 8;
+    float4* w4 = reinterpret_cast<float4*>(ws + (size_t)m * N + c);
+    const float4 p = w4[0], q = w4[1];
+    w4[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+    w4[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float a[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+    const size_t o = (size_t)m * ldc + c;
+    if (bias) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += bias[c + e];
+    }
+    if (preact) *reinterpret_cast<uint4*>(preact + o) = pack8(a);
+    if (act == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = 0.5f * a[e] * (1.f + erff(a[e] * 0.70710678118654752f));
+    }
+    if (dact) {
+      float z[8];
+      unpack8(*reinterpret_cast<const uint4*>(dact + o), z);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float cdf = 0.5f * (1.f + erff(z[e] * 0.70710678118654752f));
+        a[e] *= cdf + z[e] * 0.3989422804014327f * __expf(-0.5f * z[e] * z[e]);
+      }
+    }
+    if (addend) {
+      float b[8];
+      unpack8(*reinterpret_cast<const uint4*>(addend + o), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += b[e];
+    }
+    *reinterpret_cast<uint4*>(C + o) = pack8(a);
+  }
+}
+}  // namespace
+
+// bf16-output GEMM with a dense-layer epilogue: C = act(op(A) op(B) + bias) (pre-
+// activation to preact when given), or C = (op(A) op(B)) * act'(dact) (+ addend).
+// ws (optional, M*N fp32, zero on entry and on exit): when the output has too few tiles
+// to fill the chip, the K reduction is split across workgroups into ws with fp32 atomics
+// and the epilogue runs in a finishing pass.
 MLC_EXPORT int mlc_gemm_bf16_ex(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int lda, int ldb,
                                 int ldc, int ta, int tb, const float* bias, int act, bf16* preact,
-                                const bf16* addend, const bf16* dact, hipStream_t st) {
+                                const bf16* addend, const bf16* dact, float* ws, hipStream_t st) {
   if (K % 8 || N % 8 || ldc % 8 || lda % 8 || ldb % 8 || (ta && M % 8)) return -1;
   const int tile = pick_tile(M, N);
+  const int BMv = tile == 1 ? 256 : tile == 2 ? 64 : 128, BNv = tile == 1 ? 64 : tile == 2 ? 256 : 128;
+  const int tiles = ((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
+  const int ktiles = (K + BK - 1) / BK;
+  int splits = 1;
+  if (ws) while (tiles * splits < 640 && ktiles / (splits * 2) >= 4) splits *= 2;
+  if (splits > 1) {
+    EpiF32Atomic epi{ws, N};
+    hipError_t e;
+    if (!ta && tb) e = launch_tiles(tile, M, N, K, splits, st, epi, GA_KC_F, GB_KC_F);
+    else if (!ta && !tb) e = launch_tiles(tile, M, N, K, splits, st, epi, GA_KC_F, GB_MC_F);
+    else if (ta && tb) e = launch_tiles(tile, M, N, K, splits, st, epi, GA_MC_F, GB_KC_F);
+    else e = launch_tiles(tile, M, N, K, splits, st, epi, GA_MC_F, GB_MC_F);
+    if (e != hipSuccess) return e;
+    long blocks = ((long)M * (N / 8) + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(dense_finalize_kernel, dim3(blocks), dim3(256), 0, st, ws, C, ldc, bias, act, preact,
+                       addend, dact, M, N);
+    return hipGetLastError();
+  }
   EpiBF16<IdentityRows, true> epi{C, ldc, nullptr, nullptr, IdentityRows{}, addend};
   epi.bias = bias; epi.act = act; epi.preact = preact; epi.dact = dact;
   if (!ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_KC, GB_KC);

@@ -9,7 +9,7 @@
 //   into one of NSTAT copies) + a finalize that writes them into the grad arena.
 // * Attention softmax: P = softmax(scale*S + key_bias) with attention dropout; backward
 //   dS = scale * P * (dP - sum(P*dP)).
-// * Column sums for bias gradients (2D grid + atomics).
+// * Column sums for bias gradients (2D grid, partials into NSTAT copies, finalize).
 //
 // Dropout masks are a counter-based hash of (seed, site salt, element index): nothing is
 // stored, backward regenerates the mask, and the seed lives in device memory so a
@@ -312,9 +312,11 @@ softmax_bwd_kernel(const bf16* __restrict__ P, const bf16* __restrict__ dPd, bf1
 }
 
 // ------------------------------------------------------------------ bias grads
-// out[c] += sum_r g[r][c]; 8 columns per thread, RB rows per block, atomics across blocks
+// partial column sums: block (x, y) sums rows [y*RB, (y+1)*RB) of 8*NT columns and adds
+// them into copy (y % NSTAT) of scratch[NSTAT][C] (8 adds per address at most per
+// NSTAT blocks); colsum_finalize folds the copies into out (+=)
 __global__ void __launch_bounds__(NT)
-colsum_atomic_kernel(const bf16* __restrict__ g, float* __restrict__ out, int R, int C, int RB) {
+colsum_partial_kernel(const bf16* __restrict__ g, float* __restrict__ scratch, int R, int C, int RB) {
   const int c8 = blockIdx.x * NT + threadIdx.x;
   if (c8 * 8 >= C) return;
   const int r0 = blockIdx.y * RB, r1 = min(R, r0 + RB);
@@ -325,8 +327,18 @@ colsum_atomic_kernel(const bf16* __restrict__ g, float* __restrict__ out, int R,
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] += f[e];
   }
+  float* dst = scratch + (size_t)(blockIdx.y % NSTAT) * C + c8 * 8;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) atomicAdd(out + c8 * 8 + e, acc[e]);
+  for (int e = 0; e < 8; ++e) atomicAdd(dst + e, acc[e]);
+}
+
+__global__ void __launch_bounds__(NT)
+colsum_finalize_kernel(float* __restrict__ scratch, float* __restrict__ out, int C) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int k = 0; k < NSTAT; ++k) { s += scratch[(size_t)k * C + c]; scratch[(size_t)k * C + c] = 0.f; }
+  out[c] += s;
 }
 
 // ------------------------------------------------------------------ dropout (standalone)
@@ -418,15 +430,16 @@ MLC_EXPORT int mlc_softmax_bwd(const bf16* P, const bf16* dPd, bf16* dS, long R,
   });
 }
 
-// out[C] += column sums of g[R][C] (C % 8 == 0)
-MLC_EXPORT int mlc_colsum_acc(const bf16* g, float* out, int R, int C, hipStream_t st) {
+// out[C] += column sums of g[R][C] (C % 8 == 0).  scratch: NSTAT*C fp32, zero on entry
+// (left zeroed on exit, so one buffer can serve every call of a step).
+MLC_EXPORT int mlc_colsum_acc(const bf16* g, float* out, float* scratch, int R, int C, hipStream_t st) {
   if (C % 8) return -1;
-  // enough row blocks for ~1024 workgroups, at least 8 rows each (atomics per block = C)
   const int xb = (C / 8 + NT - 1) / NT;
-  int RB = (R * xb + 1023) / 1024;
-  if (RB < 8) RB = 8;
-  dim3 grid((C / 8 + NT - 1) / NT, (R + RB - 1) / RB);
-  hipLaunchKernelGGL(colsum_atomic_kernel, grid, dim3(NT), 0, st, g, out, R, C, RB);
+  int RB = (R * xb + 511) / 512;       // ~512 blocks
+  if (RB < 16) RB = 16;
+  dim3 grid(xb, (R + RB - 1) / RB);
+  hipLaunchKernelGGL(colsum_partial_kernel, grid, dim3(NT), 0, st, g, scratch, R, C, RB);
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, st, scratch, out, C);
   return hipGetLastError();
 }
 

@@ -371,6 +371,90 @@ for _v in ('b0', 'b1', 'b2', 'b3', 'b4', 'b5', 'b6', 'b7'):
     register_encoder(f'efficientnet-{_v}')((lambda v: (lambda: EfficientNetEncoder(v)))(_v))
 
 
+# ---------------------------------------------------------------------------- inception-resnet-v2
+def _bcr(cin, cout, k, stride=1, padding=0):
+    return nn.Sequential(nn.Conv2d(cin, cout, k, stride, padding, bias=False), nn.BatchNorm2d(cout, eps=1e-3),
+                         nn.ReLU(inplace=True))
+
+
+class _Block35(nn.Module):
+    def __init__(self, scale=0.17):
+        super().__init__()
+        self.scale = scale
+        self.b0 = _bcr(320, 32, 1)
+        self.b1 = nn.Sequential(_bcr(320, 32, 1), _bcr(32, 32, 3, padding=1))
+        self.b2 = nn.Sequential(_bcr(320, 32, 1), _bcr(32, 48, 3, padding=1), _bcr(48, 64, 3, padding=1))
+        self.conv = nn.Conv2d(128, 320, 1)
+
+    def forward(self, x):
+        y = self.conv(torch.cat([self.b0(x), self.b1(x), self.b2(x)], 1))
+        return F.relu(x + self.scale * y)
+
+
+class _Block17(nn.Module):
+    def __init__(self, scale=0.10):
+        super().__init__()
+        self.scale = scale
+        self.b0 = _bcr(1088, 192, 1)
+        self.b1 = nn.Sequential(_bcr(1088, 128, 1), _bcr(128, 160, (1, 7), padding=(0, 3)),
+                                _bcr(160, 192, (7, 1), padding=(3, 0)))
+        self.conv = nn.Conv2d(384, 1088, 1)
+
+    def forward(self, x):
+        return F.relu(x + self.scale * self.conv(torch.cat([self.b0(x), self.b1(x)], 1)))
+
+
+class _Block8(nn.Module):
+    def __init__(self, scale=0.20, relu=True):
+        super().__init__()
+        self.scale, self.relu = scale, relu
+        self.b0 = _bcr(2080, 192, 1)
+        self.b1 = nn.Sequential(_bcr(2080, 192, 1), _bcr(192, 224, (1, 3), padding=(0, 1)),
+                                _bcr(224, 256, (3, 1), padding=(1, 0)))
+        self.conv = nn.Conv2d(448, 2080, 1)
+
+    def forward(self, x):
+        y = x + self.scale * self.conv(torch.cat([self.b0(x), self.b1(x)], 1))
+        return F.relu(y) if self.relu else y
+
+
+class InceptionResNetV2Encoder(nn.Module):
+    """Inception-ResNet-v2 (Szegedy et al. 2016) with 'same' padding on the strided
+    layers so the five features sit exactly at strides 2..32."""
+
+    def __init__(self, in_channels=3):
+        super().__init__()
+        self.s2 = nn.Sequential(_bcr(in_channels, 32, 3, 2, 1), _bcr(32, 32, 3, padding=1), _bcr(32, 64, 3, padding=1))
+        self.s4 = nn.Sequential(nn.MaxPool2d(3, 2, 1), _bcr(64, 80, 1), _bcr(80, 192, 3, padding=1))
+        self.pool8 = nn.MaxPool2d(3, 2, 1)
+        self.m5b = nn.ModuleList([_bcr(192, 96, 1),
+                                  nn.Sequential(_bcr(192, 48, 1), _bcr(48, 64, 5, padding=2)),
+                                  nn.Sequential(_bcr(192, 64, 1), _bcr(64, 96, 3, padding=1), _bcr(96, 96, 3, padding=1)),
+                                  nn.Sequential(nn.AvgPool2d(3, 1, 1, count_include_pad=False), _bcr(192, 64, 1))])
+        self.r35 = nn.Sequential(*[_Block35() for _ in range(10)])
+        self.m6a = nn.ModuleList([_bcr(320, 384, 3, 2, 1),
+                                  nn.Sequential(_bcr(320, 256, 1), _bcr(256, 256, 3, padding=1), _bcr(256, 384, 3, 2, 1)),
+                                  nn.MaxPool2d(3, 2, 1)])
+        self.r17 = nn.Sequential(*[_Block17() for _ in range(20)])
+        self.m7a = nn.ModuleList([nn.Sequential(_bcr(1088, 256, 1), _bcr(256, 384, 3, 2, 1)),
+                                  nn.Sequential(_bcr(1088, 256, 1), _bcr(256, 288, 3, 2, 1)),
+                                  nn.Sequential(_bcr(1088, 256, 1), _bcr(256, 288, 3, padding=1), _bcr(288, 320, 3, 2, 1)),
+                                  nn.MaxPool2d(3, 2, 1)])
+        self.r8 = nn.Sequential(*[_Block8() for _ in range(9)], _Block8(relu=False))
+        self.head = _bcr(2080, 1536, 1)
+
+    def forward(self, x):
+        x2 = self.s2(x)
+        x4 = self.s4(x2)
+        x8 = self.r35(torch.cat([b(self.pool8(x4)) for b in self.m5b], 1))
+        x16 = self.r17(torch.cat([b(x8) for b in self.m6a], 1))
+        x32 = self.head(self.r8(torch.cat([b(x16) for b in self.m7a], 1)))
+        return [x32, x16, x8, x4, x2]
+
+
+register_encoder('inceptionresnetv2')(lambda: InceptionResNetV2Encoder())
+
+
 # ---------------------------------------------------------------------------- api
 def _measure_out_shapes(enc: nn.Module) -> tuple:
     was = enc.training

@@ -24,12 +24,12 @@ _SIGS = {
     'mlc_conv_wgrad': [vp, vp, vp] + [i32] * 14 + [vp],
     'mlc_gemm_f32out': [vp, vp, vp, vp] + [i32] * 11 + [vp],
     'mlc_gemm_bf16out': [vp, vp, vp] + [i32] * 8 + [vp],
-    'mlc_gemm_bf16_ex': [vp, vp, vp] + [i32] * 8 + [vp, i32, vp, vp, vp, vp],
+    'mlc_gemm_bf16_ex': [vp, vp, vp] + [i32] * 8 + [vp, i32, vp, vp, vp, vp, vp],
     'mlc_ln_fwd': [vp] * 8 + [i32, i32, f32, f32, f32, vp, u32, u32, vp],
     'mlc_ln_bwd': [vp] * 10 + [i32, i32, f32, f32, vp, u32, u32, vp],
     'mlc_softmax_fwd': [vp] * 4 + [i64, i32, i32, f32, f32, vp, u32, vp],
     'mlc_softmax_bwd': [vp] * 3 + [i64, i32, f32, f32, vp, u32, vp],
-    'mlc_colsum_acc': [vp, vp, i32, i32, vp],
+    'mlc_colsum_acc': [vp, vp, vp, i32, i32, vp],
     'mlc_dropout': [vp, vp, i64, f32, vp, u32, vp],
     'mlc_bn_stat_copies': [],
     'mlc_bn_finalize': [vp, vp, i32] + [vp] * 8 + [i64, i32, f32, f32, vp],

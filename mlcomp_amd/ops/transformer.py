@@ -146,6 +146,23 @@ def softmax_bwd(P, dPd, scale, p=0.0, seed=None, salt=0):
 
 
 # ---------------------------------------------------------------------------- dense layers
+_WS = {}
+_WS_OLD = []   # superseded buffers stay alive: a captured graph may still point at them
+
+
+def gemm_workspace(device, n: int) -> torch.Tensor:
+    """Zeroed fp32 split-K workspace per device (the finishing kernel re-zeroes what it
+    used), grown on demand - first during eager warm-up, so graph capture reuses it."""
+    key = str(device)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < n:
+        if buf is not None:
+            _WS_OLD.append(buf)
+        buf = torch.zeros(max(n, 1 << 20), device=device, dtype=torch.float32)
+        _WS[key] = buf
+    return buf
+
+
 def _gelu(u):
     return 0.5 * u * (1.0 + torch.erf(u / math.sqrt(2.0)))
 
@@ -163,7 +180,8 @@ def dense_fwd(x, w, bias=None, act: int = 0, want_preact: bool = False):
         y = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
         u = torch.empty_like(y) if want_preact else None
         _lib.call('mlc_gemm_bf16_ex', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), M, N, K, K, K, N, 0, 1,
-                  _lib.ptr(bias), act, _lib.ptr(u), None, None, _lib.stream())
+                  _lib.ptr(bias), act, _lib.ptr(u), None, None, _lib.ptr(gemm_workspace(x.device, M * N)),
+                  _lib.stream())
         return y, u
     z = x.float() @ w.float().t()
     if bias is not None:
@@ -181,7 +199,8 @@ def dense_dgrad(dy, w, dact_u=None, addend=None):
     if _cuda(dy):
         dx = torch.empty(M, K, device=dy.device, dtype=torch.bfloat16)
         _lib.call('mlc_gemm_bf16_ex', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(dx), M, K, N, N, K, K, 0, 0, None, 0,
-                  None, _lib.ptr(addend), _lib.ptr(dact_u), _lib.stream())
+                  None, _lib.ptr(addend), _lib.ptr(dact_u), _lib.ptr(gemm_workspace(dy.device, M * K)),
+                  _lib.stream())
         return dx
     z = dy.float() @ w.float()
     z = z.to(torch.bfloat16).float()
@@ -197,11 +216,28 @@ def dact_gelu(dy, u):
     return (dy.float() * _dgelu(u.float())).to(torch.bfloat16)
 
 
-def colsum_acc(g, out):
+_SCRATCH = {}
+
+
+def colsum_scratch(device, C: int) -> torch.Tensor:
+    """A zeroed NSTAT*C fp32 buffer per device, grown on demand; the kernel leaves it
+    zeroed, so every call of a step (and a captured graph) can share it."""
+    key = str(device)
+    buf = _SCRATCH.get(key)
+    if buf is None or buf.numel() < NSTAT * C:
+        if buf is not None:
+            _WS_OLD.append(buf)
+        buf = torch.zeros(NSTAT * max(C, 4096), device=device, dtype=torch.float32)
+        _SCRATCH[key] = buf
+    return buf
+
+
+def colsum_acc(g, out, scratch=None):
     """out += column sums of g [R, C] bf16."""
     R, C = g.shape
     if _cuda(g):
-        _lib.call('mlc_colsum_acc', _lib.ptr(g), _lib.ptr(out), R, C, _lib.stream())
+        sc = scratch if scratch is not None else colsum_scratch(g.device, C)
+        _lib.call('mlc_colsum_acc', _lib.ptr(g), _lib.ptr(out), _lib.ptr(sc), R, C, _lib.stream())
         return out
     out.add_(g.float().sum(0))
     return out

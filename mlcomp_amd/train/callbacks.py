@@ -262,6 +262,34 @@ class InferCallback(Callback):
             np.save(os.path.join(self.out_dir, f'{state.loader_name}.npy'), torch.cat(out).numpy())
 
 
+@register_callback
+class InferBestCallback(InferCallback):
+    """``InferCallback`` that only keeps the outputs of the best epoch so far (by the
+    stage's main metric): every epoch's outputs are collected, and saved only when the
+    epoch improves the metric (`contrib/catalyst/callbacks/inference.py:10-49`)."""
+
+    def __init__(self, out_dir='infer', out_prefix=None, key='logits'):
+        super().__init__(out_dir, out_prefix, key)
+        self.best = None
+        self.pending = {}
+
+    def on_loader_end(self, state):
+        out = self.store.get(state.loader_name)
+        if out:
+            self.pending[state.loader_name] = torch.cat(out)
+
+    def on_epoch_end(self, state):
+        import numpy as np
+        v = state.valid_metrics.get(state.main_metric)
+        better = v is not None and (self.best is None or (v < self.best if state.minimize_metric else v > self.best))
+        if better:
+            self.best = v
+            os.makedirs(self.out_dir, exist_ok=True)
+            for name, t in self.pending.items():
+                np.save(os.path.join(self.out_dir, f'{name}.npy'), t.numpy())
+        self.pending = {}
+
+
 def build_callbacks(params: dict) -> 'OrderedDict[str, Callback]':
     out = OrderedDict()
     for name, p in (params or {}).items():

@@ -50,6 +50,19 @@ class ClassificationReportBuilder(ReportBuilderBase):
                                            size=len(blob)), commit=False)
             self.session.commit()
             self.plot_count -= 1
+        if targets is not None:
+            self._plot_items(np.asarray(targets), preds)
+
+    def _plot_items(self, targets, preds):
+        """``f1`` (per-class precision/recall/F1 heatmap) and ``precision_recall`` items."""
+        from mlcomp_amd.utils.plot import plot_classification_report, plot_precision_recall
+        for kind, fn in (('f1', lambda: plot_classification_report(targets, preds.argmax(1), preds.shape[1])),
+                         ('precision_recall', lambda: plot_precision_recall(targets, preds))):
+            for key, item in self.items(kind):
+                data = fn()
+                self.session.add(ReportImg(group=key, epoch=0, task=self.task.id, img=data, dag=self.task.dag,
+                                           part=self.part, project=self.project, size=len(data)), commit=False)
+        self.session.commit()
 
 
 __all__ = ['ClassificationReportBuilder', 'confusion_matrix']

@@ -1,0 +1,45 @@
+"""GEMM throughput of the native MFMA kernel (dense-layer entry point, with and without
+split-K) vs the library GEMM behind torch.matmul (hipBLASLt), on BERT-base / ResNet
+shapes.  python scripts/bench_gemm.py"""
+import time
+
+import torch
+
+from mlcomp_amd.ops import transformer as Tx
+
+SHAPES = [  # (M, N, K, name)
+    (4096, 2304, 768, 'bert qkv'), (4096, 768, 768, 'bert out'), (4096, 3072, 768, 'bert ffn1'),
+    (4096, 768, 3072, 'bert ffn2'), (4096, 768, 2304, 'bert qkv dgrad'), (4096, 4096, 4096, 'square 4k'),
+    (8192, 8192, 8192, 'square 8k'), (802816, 256, 64, 'r50 l1 1x1 64->256'), (200704, 512, 128, 'r50 l2 1x1'),
+]
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / iters
+
+
+def main():
+    for M, N, K, name in SHAPES:
+        x = torch.randn(M, K, device='cuda').to(torch.bfloat16)
+        w = (torch.randn(N, K, device='cuda') * K ** -0.5).to(torch.bfloat16)
+        b = torch.zeros(N, device='cuda')
+        fl = 2.0 * M * N * K
+        t_lib = timeit(lambda: torch.matmul(x, w.t()))
+        t_nat = timeit(lambda: Tx.dense_fwd(x, w, b))
+        dy = torch.randn(M, N, device='cuda').to(torch.bfloat16)
+        t_dg = timeit(lambda: Tx.dense_dgrad(dy, w))
+        t_dgl = timeit(lambda: torch.matmul(dy, w))
+        print(f'{name:22s} M={M:7d} N={N:5d} K={K:5d}  fwd native {fl / t_nat / 1e12:7.1f} TF/s  lib '
+              f'{fl / t_lib / 1e12:7.1f} | dgrad native {fl / t_dg / 1e12:7.1f} lib {fl / t_dgl / 1e12:7.1f}',
+              flush=True)
+
+
+if __name__ == '__main__':
+    main()

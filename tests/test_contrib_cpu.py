@@ -27,6 +27,7 @@ def test_encoder_out_shapes_match_reference_table():
     assert get_encoder('resnet34').out_shapes == (512, 256, 128, 64, 64)
     assert get_encoder('densenet121').out_shapes == (1024, 1024, 512, 256, 64)
     assert get_encoder('dpn92').out_shapes == (2688, 1552, 704, 336, 64)
+    assert get_encoder('inceptionresnetv2').out_shapes == (1536, 1088, 320, 192, 64)
 
 
 def test_unet_scse_trains():

@@ -172,3 +172,19 @@ def test_segmentation_report_and_rle(dbtask):
     from mlcomp_amd.db.models import ReportImg
     rows = s.query(ReportImg).filter(ReportImg.task == task.id).all()
     assert len(rows) == 2 and rows[0].score == 0.5
+
+
+def test_report_plots_and_describe(dbtask):
+    from mlcomp_amd.utils.plot import classification_report_table, plot_classification_report, plot_precision_recall
+    y = np.array([0, 1, 2, 1, 0, 2])
+    p = np.eye(3)[[0, 1, 1, 1, 0, 2]] * 0.9 + 0.03
+    t = classification_report_table(y, p.argmax(1), 3)
+    assert t[2, 1] == 0.5 and t[0, 0] == 1.0
+    assert plot_classification_report(y, p.argmax(1), 3)[:2] == b'\xff\xd8'
+    assert plot_precision_recall(y, p)[:2] == b'\xff\xd8'
+    s, task, tp, _ = dbtask
+    from mlcomp_amd.utils.describe import draw, task_table
+    rows = task_table(task.dag)
+    assert rows and rows[0]['status'] == 'in_progress'
+    fig = draw(task.dag, metrics=['loss'])
+    assert fig is not None
