@@ -596,7 +596,7 @@ struct EpiF32 {  // fp32 [M][ld] = acc (+ bias[n]) (+= if accumulate)
 };
 
 // ---------------------------------------------------------------- main loop
-template <int BM, int BN, class LA, class LB, class EPI>
+template <int BM, int BN, class LA, class LB, class EPI, int PF>
 __global__ void __launch_bounds__(NTHR, 2)
 gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int ktiles_per_split) {
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
@@ -634,6 +634,20 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
   typename LB::St sb;
   la.init(sa, m0, tid);
   lb.init(sb, n0, tid);
+  auto mfma_tile = [&](const char* As, const char* Bs) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 a0 = read_frag<LA::KC, BM>(As, wm * 64, s, lane);
+      bf16x8 a1 = read_frag<LA::KC, BM>(As, wm * 64 + 32, s, lane);
+      bf16x8 b0 = read_frag<LB::KC, BN>(Bs, wn * 64, s, lane);
+      bf16x8 b1 = read_frag<LB::KC, BN>(Bs, wn * 64 + 32, s, lane);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+    }
+  };
+  if constexpr (PF == 1) {
   int kt = la.next(sa, kt_begin, kt_end);
   if (kt < kt_end) {
     uint4 ra[BM / 32], rb[BN / 32];
@@ -653,17 +667,7 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
         la.load(sa, nxt * BK, tid, ra);
         lb.load(sb, nxt * BK, tid, rb);
       }
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        bf16x8 a0 = read_frag<LA::KC, BM>(As, wm * 64, s, lane);
-        bf16x8 a1 = read_frag<LA::KC, BM>(As, wm * 64 + 32, s, lane);
-        bf16x8 b0 = read_frag<LB::KC, BN>(Bs, wn * 64, s, lane);
-        bf16x8 b1 = read_frag<LB::KC, BN>(Bs, wn * 64 + 32, s, lane);
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
-      }
+      mfma_tile(As, Bs);
       if (more) {
         char* An = smem + (cur ^ 1) * STAGE;
         store_stage<LA::KC, BM>(An, tid, ra);
@@ -674,8 +678,63 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
       kt = nxt;
     }
   }
+  } else {
+    // PF == 2: two register sets, global loads issued two K-tiles ahead.  The loop
+    // body is unrolled twice so each set's role is static (no runtime-indexed arrays).
+    int kt = la.next(sa, kt_begin, kt_end);
+    if (kt < kt_end) {
+      uint4 a0[BM / 32], b0[BN / 32], a1[BM / 32], b1[BN / 32];
+      la.load(sa, kt * BK, tid, a0);
+      lb.load(sb, kt * BK, tid, b0);
+      store_stage<LA::KC, BM>(smem, tid, a0);
+      store_stage<LB::KC, BN>(smem + A_BYTES, tid, b0);
+      int k1 = la.next(sa, kt + 1, kt_end);
+      if (k1 < kt_end) {
+        la.load(sa, k1 * BK, tid, a1);
+        lb.load(sb, k1 * BK, tid, b1);
+      }
+      __syncthreads();
+      int cur = 0;
+      while (true) {
+        // phase A: compute kt; set 1 holds k1 (in flight); set 0 is free
+        int k2 = k1 < kt_end ? la.next(sa, k1 + 1, kt_end) : kt_end;
+        if (k2 < kt_end) {
+          la.load(sa, k2 * BK, tid, a0);
+          lb.load(sb, k2 * BK, tid, b0);
+        }
+        mfma_tile(smem + cur * STAGE, smem + cur * STAGE + A_BYTES);
+        if (k1 < kt_end) {
+          store_stage<LA::KC, BM>(smem + (cur ^ 1) * STAGE, tid, a1);
+          store_stage<LB::KC, BN>(smem + (cur ^ 1) * STAGE + A_BYTES, tid, b1);
+        }
+        __syncthreads();
+        cur ^= 1;
+        kt = k1;
+        if (kt >= kt_end) break;
+        // phase B: compute kt; set 0 holds k2; set 1 is free
+        k1 = k2 < kt_end ? la.next(sa, k2 + 1, kt_end) : kt_end;
+        if (k1 < kt_end) {
+          la.load(sa, k1 * BK, tid, a1);
+          lb.load(sb, k1 * BK, tid, b1);
+        }
+        mfma_tile(smem + cur * STAGE, smem + cur * STAGE + A_BYTES);
+        if (k2 < kt_end) {
+          store_stage<LA::KC, BM>(smem + (cur ^ 1) * STAGE, tid, a0);
+          store_stage<LB::KC, BN>(smem + (cur ^ 1) * STAGE + A_BYTES, tid, b0);
+        }
+        __syncthreads();
+        cur ^= 1;
+        kt = k2;
+        if (kt >= kt_end) break;
+      }
+    }
+  }
   epi.template apply<BM, BN>(acc, smem, m0, n0, M, N, wm, wn, lane, tid);
 }
+
+// K-tile prefetch depth of the main loop (1 = next tile, 2 = two tiles ahead); set by
+// mlc_gemm_config for A/B measurements, default chosen from the microbenchmarks
+static int g_prefetch = 1;
 
 template <int BM, int BN, class LA, class LB, class EPI>
 static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K,
@@ -687,7 +746,10 @@ static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int 
   const int per = (ktiles + splits - 1) / splits;
   splits = (ktiles + per - 1) / per;
   dim3 grid(tiles, 1, splits);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, EPI>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
+  if (g_prefetch >= 2 && per >= 3)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, EPI, 2>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
+  else
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, EPI, 1>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
   return hipGetLastError();
 }
 
@@ -760,6 +822,12 @@ static DgradRows mkrows(int N, int H, int W, int S, int KH, int KW, int pad, int
   } while (0)
 
 MLC_EXPORT int mlc_bn_stat_copies() { return NSTAT; }
+
+MLC_EXPORT int mlc_gemm_config(int prefetch) {
+  const int old = igemm::g_prefetch;
+  if (prefetch == 1 || prefetch == 2) igemm::g_prefetch = prefetch;
+  return old;
+}
 
 // y[N,Ho,Wo,Co] = conv(x[N,H,W,C], w[Co,KH,KW,C]).  If sum/sumsq are given they must
 // hold NSTAT*Co fp32 (zeroed by the caller); per-channel partial sums of y and y^2 are
@@ -962,7 +1030,7 @@ MLC_EXPORT int mlc_gemm_bf16_ex(const bf16* A, const bf16* B, bf16* C, int M, in
   const int tiles = ((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
   const int ktiles = (K + BK - 1) / BK;
   int splits = 1;
-  if (ws) while (tiles * splits < 640 && ktiles / (splits * 2) >= 4) splits *= 2;
+  if (ws) while (tiles * splits < 384 && ktiles / (splits * 2) >= 4) splits *= 2;
   if (splits > 1) {
     EpiF32Atomic epi{ws, N};
     hipError_t e;

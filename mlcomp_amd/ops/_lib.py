@@ -32,6 +32,7 @@ _SIGS = {
     'mlc_colsum_acc': [vp, vp, vp, i32, i32, vp],
     'mlc_dropout': [vp, vp, i64, f32, vp, u32, vp],
     'mlc_bn_stat_copies': [],
+    'mlc_gemm_config': [i32],
     'mlc_bn_finalize': [vp, vp, i32] + [vp] * 8 + [i64, i32, f32, f32, vp],
     'mlc_bn_fwd_apply': [vp] * 5 + [i64, i32, i32, vp],
     'mlc_bn_bwd_reduce': [vp] * 5 + [i64, i32, vp],

@@ -1,10 +1,15 @@
 """GEMM throughput of the native MFMA kernel (dense-layer entry point, with and without
 split-K) vs the library GEMM behind torch.matmul (hipBLASLt), on BERT-base / ResNet
 shapes.  python scripts/bench_gemm.py"""
+import os
+import sys
 import time
 
 import torch
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from mlcomp_amd.ops import _lib
 from mlcomp_amd.ops import transformer as Tx
 
 SHAPES = [  # (M, N, K, name)
@@ -32,13 +37,17 @@ def main():
         b = torch.zeros(N, device='cuda')
         fl = 2.0 * M * N * K
         t_lib = timeit(lambda: torch.matmul(x, w.t()))
-        t_nat = timeit(lambda: Tx.dense_fwd(x, w, b))
         dy = torch.randn(M, N, device='cuda').to(torch.bfloat16)
-        t_dg = timeit(lambda: Tx.dense_dgrad(dy, w))
         t_dgl = timeit(lambda: torch.matmul(dy, w))
-        print(f'{name:22s} M={M:7d} N={N:5d} K={K:5d}  fwd native {fl / t_nat / 1e12:7.1f} TF/s  lib '
-              f'{fl / t_lib / 1e12:7.1f} | dgrad native {fl / t_dg / 1e12:7.1f} lib {fl / t_dgl / 1e12:7.1f}',
-              flush=True)
+        res = []
+        for pf in (1, 2):
+            _lib.call('mlc_gemm_config', pf)
+            t_nat = timeit(lambda: Tx.dense_fwd(x, w, b))
+            t_dg = timeit(lambda: Tx.dense_dgrad(dy, w))
+            res.append(f'pf{pf} fwd {fl / t_nat / 1e12:6.1f} dgrad {fl / t_dg / 1e12:6.1f}')
+        _lib.call('mlc_gemm_config', 1)
+        print(f'{name:20s} M={M:7d} N={N:5d} K={K:5d} | lib fwd {fl / t_lib / 1e12:6.1f} dgrad '
+              f'{fl / t_dgl / 1e12:6.1f} | ' + ' | '.join(res) + '  TF/s', flush=True)
 
 
 if __name__ == '__main__':
