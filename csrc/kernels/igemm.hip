@@ -59,16 +59,11 @@ __device__ __forceinline__ int mc_off(int k, int c) {
   return k * (R * 2) + ((c ^ ((k & 3) << 2)) << 4);
 }
 
-// tile of R rows (KC) / R cols (MC): NCH = R/32 chunks of 16 B per thread
-template <bool KC, int R>
+// write a loader's R/32 register chunks into its LDS image
+template <class L, int R>
 __device__ __forceinline__ void store_stage(char* lds, int tid, const uint4 (&v)[R / 32]) {
 #pragma unroll
-  for (int i = 0; i < R / 32; ++i) {
-    int off;
-    if (KC) off = kc_off((tid >> 3) + 32 * i, tid & 7);
-    else off = mc_off<R>(tid / (R / 8) + (NTHR / (R / 8)) * i, tid % (R / 8));
-    *reinterpret_cast<uint4*>(lds + off) = v[i];
-  }
+  for (int i = 0; i < R / 32; ++i) *reinterpret_cast<uint4*>(lds + L::lds_off(i, tid)) = v[i];
 }
 
 // fragment of a 32-row (KC) / 32-col (MC) sub-tile for k-step s (16 deep)
@@ -91,14 +86,22 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int base, int s, in
   }
 }
 
-__device__ __forceinline__ uint4 ld16(const bf16* p) { return *reinterpret_cast<const uint4*>(p); }
-__device__ __forceinline__ uint4 zero4() { return make_uint4(0, 0, 0, 0); }
-
-// Default K-tile iteration: every tile in [b, e).
-struct AllTiles {
-  template <class S>
-  __device__ int next(const S&, int kt, int) const { return kt; }
-};
+// ---------------------------------------------------------------- buffer loads
+// Every operand load is a branch-free raw buffer load: the per-thread 32-bit voffset is
+// precomputed (relative to a wave-uniform base that moves per block / K-tile), and a
+// load that must read zero (padding tap, row past M, K tail) gets voffset OOB, past
+// num_records, so the hardware returns 0.  No exec-mask branches around loads means the
+// compiler sees a fixed number of loads per K-tile and can wait with counted vmcnt
+// instead of draining all of them, which is what lets loads stay in flight across the
+// MFMA phase (two tiles deep with PF=2).
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+constexpr unsigned OOB = 0x80000000u;
+__device__ __forceinline__ Rsrc rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7ffffff0, 0x00020000);
+}
+__device__ __forceinline__ uint4 bload(Rsrc r, unsigned voff) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+}
 
 // ---------------------------------------------------------------- geometry
 struct ConvGeom {
@@ -108,226 +111,250 @@ struct ConvGeom {
   FastDiv fWo, fHo, fW, fH, fC, fCo, fKW;
 };
 
-// decompose k = ((r*KW)+s)*CC + c; if CC % BK == 0 a whole K-tile shares one tap, so
-// only the (wave-uniform) tile base is decomposed.
-__device__ __forceinline__ void tap_of(int k, int k0, const FastDiv& fCC, const FastDiv& fKW,
-                                       int& r, int& s, int& c) {
-  unsigned rs, cc, rr, ss;
-  if (fCC.d % BK == 0) {
-    fCC.divmod((unsigned)k0, rs, cc);
-    c = (int)cc + (k - k0);
-  } else {
-    fCC.divmod((unsigned)k, rs, cc);
-    c = (int)cc;
-  }
-  fKW.divmod(rs, rr, ss);
-  r = (int)rr; s = (int)ss;
-}
-
 // ---------------------------------------------------------------- loaders
-// KC loader of R rows: thread t owns rows (t>>3)+32i, chunk t&7 (8 k per chunk).
-// MC loader of R cols: thread t owns chunk t%(R/8) (8 mn), k-rows t/(R/8) + (256/(R/8))i.
+// Thread -> 16 B chunk mapping (chunk i of R/32 per thread), unless a loader overrides
+// lds_off: KC tile of R rows: row (t>>3)+32i, chunk t&7 (8 k per chunk); MC tile of R
+// cols: chunk t%(R/8) (8 mn), k-row t/(R/8) + (256/(R/8))i.  Loaders take the K-tile
+// index kt (k0 = kt*BK).
 
 template <int R>
-struct MatKC : AllTiles {
+struct MatKC {  // [rows][K] row-major, ld elements per row
   static constexpr bool KC = true;
   const bf16* p; int ld, rows, K;
-  struct St { int r[R / 32]; };
+  struct St { unsigned off[R / 32]; int m0; };
+  __device__ static int lds_off(int i, int tid) { return kc_off((tid >> 3) + 32 * i, tid & 7); }
   __device__ void init(St& st, int m0, int tid) const {
+    st.m0 = m0;
 #pragma unroll
-    for (int i = 0; i < R / 32; ++i) st.r[i] = m0 + (tid >> 3) + 32 * i;
+    for (int i = 0; i < R / 32; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      st.off[i] = m0 + r < rows ? (unsigned)(r * ld + (tid & 7) * 8) * 2u : OOB;
+    }
   }
-  __device__ void load(const St& st, int k0, int tid, uint4 (&v)[R / 32]) const {
-    const int k = k0 + (tid & 7) * 8;
+  __device__ void load(const St& st, int kt, int tid, uint4 (&v)[R / 32]) const {
+    const int k0 = kt * BK;
+    const Rsrc rs = rsrc(p + (size_t)st.m0 * ld + k0);
+    const bool kv = (tid & 7) * 8 < K - k0;
 #pragma unroll
-    for (int i = 0; i < R / 32; ++i)
-      v[i] = (st.r[i] < rows && k < K) ? ld16(p + (size_t)st.r[i] * ld + k) : zero4();
+    for (int i = 0; i < R / 32; ++i) v[i] = bload(rs, kv ? st.off[i] : OOB);
   }
 };
 
 template <int R>
-struct MatMC : AllTiles {
+struct MatMC {  // [K][cols] row-major, ld elements per row
   static constexpr bool KC = false;
   const bf16* p; int ld, K, cols;
-  struct St { int c; };
-  __device__ void init(St& st, int n0, int tid) const { st.c = n0 + (tid % (R / 8)) * 8; }
-  __device__ void load(const St& st, int k0, int tid, uint4 (&v)[R / 32]) const {
+  struct St { unsigned off[R / 32]; int n0; };
+  __device__ static int kr(int i, int tid) { return tid / (R / 8) + (NTHR / (R / 8)) * i; }
+  __device__ static int lds_off(int i, int tid) { return mc_off<R>(kr(i, tid), tid % (R / 8)); }
+  __device__ void init(St& st, int n0, int tid) const {
+    st.n0 = n0;
+    const int c = (tid % (R / 8)) * 8;
 #pragma unroll
-    for (int i = 0; i < R / 32; ++i) {
-      const int k = k0 + tid / (R / 8) + (NTHR / (R / 8)) * i;
-      v[i] = (k < K && st.c < cols) ? ld16(p + (size_t)k * ld + st.c) : zero4();
-    }
+    for (int i = 0; i < R / 32; ++i) st.off[i] = n0 + c < cols ? (unsigned)(kr(i, tid) * ld + c) * 2u : OOB;
+  }
+  __device__ void load(const St& st, int kt, int tid, uint4 (&v)[R / 32]) const {
+    const int k0 = kt * BK;
+    const Rsrc rs = rsrc(p + (size_t)k0 * ld + st.n0);
+    const int left = K - k0;
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) v[i] = bload(rs, kr(i, tid) < left ? st.off[i] : OOB);
   }
 };
 
-// conv fwd A operand: rows = output pixels, k = (r, s, ci) with ci fastest (C % 8 == 0)
+// Per-row tap mask: bit r (r < 15) = filter row r lands inside the input, bit 16+s =
+// filter column s does; a K chunk of tap (r, s) is loaded iff (mask & P) == P with
+// P = 1<<r | 1<<(16+s).  P = 1<<15 (never set) marks a chunk past K.
+__device__ __forceinline__ unsigned tap_pat(int r, int s) { return (1u << r) | (1u << (16 + s)); }
+constexpr unsigned NO_TAP = 1u << 15;
+
+// conv fwd A operand: rows = output pixels (n, ho, wo), k = (r, s, ci), ci fastest.
+// Row offsets are relative to the block's first row; the tap offset is per chunk.
 template <int R>
-struct ConvFwdA : AllTiles {
+struct ConvFwdA {
   static constexpr bool KC = true;
   const bf16* x; ConvGeom g; int M, K;
-  struct St { int hb[R / 32], wb[R / 32], nb[R / 32]; };  // per-row base input coords, nb=-1 if row >= M
+  struct St { unsigned off[R / 32], msk[R / 32]; long long b0; };
+  __device__ static int lds_off(int i, int tid) { return kc_off((tid >> 3) + 32 * i, tid & 7); }
+  __device__ long long rowoff(int m, int& hb, int& wb) const {
+    unsigned t, wo, n, ho;
+    g.fWo.divmod((unsigned)m, t, wo);
+    g.fHo.divmod(t, n, ho);
+    hb = (int)ho * g.stride - g.pad;
+    wb = (int)wo * g.stride - g.pad;
+    return (((long long)n * g.H + hb) * g.W + wb) * g.C;
+  }
   __device__ void init(St& st, int m0, int tid) const {
+    int hb, wb;
+    st.b0 = rowoff(m0, hb, wb);
 #pragma unroll
     for (int i = 0; i < R / 32; ++i) {
-      // branch-free: a conditional store into st.* is sunk into a dynamic-index store
-      // by the compiler, which moves the whole array to scratch
       const int m = m0 + (tid >> 3) + 32 * i;
       const bool ok = m < M;
-      unsigned t, wo, n, ho;
-      g.fWo.divmod((unsigned)(ok ? m : 0), t, wo);
-      g.fHo.divmod(t, n, ho);
-      st.hb[i] = (int)ho * g.stride - g.pad;
-      st.wb[i] = (int)wo * g.stride - g.pad;
-      st.nb[i] = ok ? (int)n : -1;
+      const long long o = rowoff(ok ? m : m0, hb, wb);
+      st.off[i] = (unsigned)(o - st.b0) * 2u;
+      unsigned mk = 0;
+      for (int r = 0; r < g.KH; ++r) mk |= ((unsigned)(hb + r * g.dil) < (unsigned)g.H) ? (1u << r) : 0u;
+      for (int s = 0; s < g.KW; ++s) mk |= ((unsigned)(wb + s * g.dil) < (unsigned)g.W) ? (1u << (16 + s)) : 0u;
+      st.msk[i] = ok ? mk : 0u;
     }
   }
-  __device__ void load(const St& st, int k0, int tid, uint4 (&v)[R / 32]) const {
-    const int k = k0 + (tid & 7) * 8;
-    int r, s, ci;
-    tap_of(k, k0, g.fC, g.fKW, r, s, ci);
-    const bool kv = k < K;
-#pragma unroll
-    for (int i = 0; i < R / 32; ++i) {
-      const int hi = st.hb[i] + r * g.dil, wi = st.wb[i] + s * g.dil;
-      const bool ok = kv && st.nb[i] >= 0 && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-      v[i] = ok ? ld16(x + (((size_t)st.nb[i] * g.H + hi) * g.W + wi) * g.C + ci) : zero4();
+  __device__ void load(const St& st, int kt, int tid, uint4 (&v)[R / 32]) const {
+    const int k0 = kt * BK, k = k0 + (tid & 7) * 8;
+    unsigned rs_, cc, rr, ss;
+    if (g.C % BK == 0) {  // whole K-tile = one tap (uniform decomposition)
+      g.fC.divmod((unsigned)k0, rs_, cc);
+      cc += (unsigned)(k - k0);
+    } else {
+      g.fC.divmod((unsigned)k, rs_, cc);
     }
+    g.fKW.divmod(rs_, rr, ss);
+    const unsigned P = k < K ? tap_pat((int)rr, (int)ss) : NO_TAP;
+    const unsigned toff = (unsigned)(((int)rr * g.dil * g.W + (int)ss * g.dil) * g.C + (int)cc) * 2u;
+    const Rsrc rsr = rsrc(x + st.b0);
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) v[i] = bload(rsr, (st.msk[i] & P) == P ? st.off[i] + toff : OOB);
   }
 };
 
-// Row order of a dgrad output: for stride 1 the natural (n, hi, wi) order; for stride 2
-// parity-class-major: class c = ph*2 + pw holds pixels hi = 2i+ph, wi = 2j+pw.
-struct DgradRows {
-  int N, H, W, S;
-  int nclass;            // parity classes with at least one contributing filter tap
-  int base[4];           // start row of each listed class (INT_MAX when unused)
-  int cid[4];            // class id (ph*2+pw) of each listed class
-  FastDiv fWc[4], fHc[4];
-  FastDiv fW, fH;
-  __device__ __forceinline__ void decode(int m, int& n, int& hi, int& wi, int& cls) const {
+// Transposed-conv (dgrad) geometry of ONE stride-parity class: output rows are the input
+// pixels (n, hi = i*S+ph, wi = j*S+pw), i < Hc, j < Wc.  Only filter taps r = r0 +
+// rstep*a (a < nr), s = s0 + sstep*b (b < ns) reach the class; for them the dy pixel is
+// (i + dh0 - a*dhs, j + dw0 - b*dws).  The K loop runs over (a, b, 64-channel block of
+// Co): K = nr*ns*ncb*64, channels past Co read as zero.
+struct DgradClass {
+  int S, ph, pw, Hc, Wc;
+  FastDiv fWc, fHc;
+  int r0, s0, rstep, sstep, nr, ns, ncb;
+  FastDiv fns, fncb;
+  int dh0, dhs, dw0, dws;
+  long long tmin;      // smallest tap offset (elements), folded into the base
+  __device__ __forceinline__ void decode(int m, int& n, int& i, int& j) const {
     unsigned t, q, rr;
-    if (S == 1) {
-      fW.divmod((unsigned)m, t, rr); wi = (int)rr;
-      fH.divmod(t, q, rr); hi = (int)rr; n = (int)q; cls = 0;
-      return;
-    }
-    const int k = (m >= base[1]) + (m >= base[2]) + (m >= base[3]);
-    // explicit selects: a runtime index into these arrays would force them to scratch
-    const int b = k == 0 ? base[0] : k == 1 ? base[1] : k == 2 ? base[2] : base[3];
-    const int c = k == 0 ? cid[0] : k == 1 ? cid[1] : k == 2 ? cid[2] : cid[3];
-    const FastDiv fw = k == 0 ? fWc[0] : k == 1 ? fWc[1] : k == 2 ? fWc[2] : fWc[3];
-    const FastDiv fh = k == 0 ? fHc[0] : k == 1 ? fHc[1] : k == 2 ? fHc[2] : fHc[3];
-    const unsigned l = (unsigned)(m - b);
-    fw.divmod(l, t, rr);
-    const int j = (int)rr;
-    fh.divmod(t, q, rr);
-    n = (int)q; hi = 2 * (int)rr + (c >> 1); wi = 2 * j + (c & 1); cls = c;
+    fWc.divmod((unsigned)m, t, rr); j = (int)rr;
+    fHc.divmod(t, q, rr); i = (int)rr; n = (int)q;
+  }
+  // K-tile -> (a, b, first channel)
+  __device__ __forceinline__ void tap(int kt, int& a, int& b, int& co0) const {
+    unsigned t, cb, aa, bb;
+    fncb.divmod((unsigned)kt, t, cb);
+    fns.divmod(t, aa, bb);
+    a = (int)aa; b = (int)bb; co0 = (int)cb * BK;
   }
 };
 
-// conv dgrad A operand: rows = input pixels (DgradRows order), k = (r, s, co), co fastest
 template <int R>
-struct ConvDgradA {
+struct ConvDgradA {  // rows = class pixels, k = (a, b, co)
   static constexpr bool KC = true;
-  const bf16* dy; ConvGeom g; int M, K; DgradRows rows;
-  // per-row coords; cls: parity class shared by every row of the block, or -1
-  struct St { int h[R / 32], w[R / 32], n[R / 32]; int cls; };
+  const bf16* dy; ConvGeom g; int M, K; DgradClass cl;
+  struct St { unsigned off[R / 32], msk[R / 32]; long long b0; };
+  __device__ static int lds_off(int i, int tid) { return kc_off((tid >> 3) + 32 * i, tid & 7); }
+  __device__ long long rowoff(int m, int& i, int& j) const {
+    int n;
+    cl.decode(m, n, i, j);
+    return (((long long)n * g.Ho + i) * g.Wo + j) * g.Co;
+  }
   __device__ void init(St& st, int m0, int tid) const {
+    int i0, j0;
+    st.b0 = rowoff(m0, i0, j0) + cl.tmin;
 #pragma unroll
-    for (int i = 0; i < R / 32; ++i) {
-      const int m = m0 + (tid >> 3) + 32 * i;
+    for (int u = 0; u < R / 32; ++u) {
+      const int m = m0 + (tid >> 3) + 32 * u;
       const bool ok = m < M;
-      int n, hi, wi, c;
-      rows.decode(ok ? m : 0, n, hi, wi, c);
-      st.h[i] = hi + g.pad;
-      st.w[i] = wi + g.pad;
-      st.n[i] = ok ? n : -1;
-    }
-    st.cls = -1;
-    if (g.stride == 2 && g.Co % BK == 0) {
-      int n, hi, wi, c0, c1;
-      rows.decode(m0, n, hi, wi, c0);
-      rows.decode(min(m0 + R, M) - 1, n, hi, wi, c1);
-      if (c0 == c1) st.cls = c0;
+      int i, j;
+      const long long o = rowoff(ok ? m : m0, i, j);
+      st.off[u] = (unsigned)(o + cl.tmin - st.b0) * 2u;
+      unsigned mk = 0;
+      for (int a = 0; a < cl.nr; ++a) mk |= ((unsigned)(i + cl.dh0 - a * cl.dhs) < (unsigned)g.Ho) ? (1u << a) : 0u;
+      for (int b = 0; b < cl.ns; ++b) mk |= ((unsigned)(j + cl.dw0 - b * cl.dws) < (unsigned)g.Wo) ? (1u << (16 + b)) : 0u;
+      st.msk[u] = ok ? mk : 0u;
     }
   }
-  // first K-tile >= kt (and < e) whose filter tap can reach this block's class
-  __device__ int next(const St& st, int kt, int e) const {
-    if (st.cls < 0) return kt;
-    const int ph = st.cls >> 1, pw = st.cls & 1;
-    for (; kt < e; ++kt) {
-      unsigned rs, rem, r, s;
-      g.fCo.divmod((unsigned)(kt * BK), rs, rem);
-      g.fKW.divmod(rs, r, s);
-      if ((((ph + g.pad - (int)r * g.dil) & 1) == 0) && (((pw + g.pad - (int)s * g.dil) & 1) == 0)) break;
-    }
-    return kt;
-  }
-  __device__ void load(const St& st, int k0, int tid, uint4 (&v)[R / 32]) const {
-    const int k = k0 + (tid & 7) * 8;
-    int r, s, co;
-    tap_of(k, k0, g.fCo, g.fKW, r, s, co);
-    const bool kv = k < K;
+  __device__ void load(const St& st, int kt, int tid, uint4 (&v)[R / 32]) const {
+    int a, b, co0;
+    cl.tap(kt, a, b, co0);
+    const int co = co0 + (tid & 7) * 8;
+    const unsigned P = co < g.Co ? tap_pat(a, b) : NO_TAP;
+    const long long toff = ((long long)(cl.dh0 - a * cl.dhs) * g.Wo + (cl.dw0 - b * cl.dws)) * g.Co + co - cl.tmin;
+    const unsigned t2 = (unsigned)toff * 2u;
+    const Rsrc rsr = rsrc(dy + st.b0);
 #pragma unroll
-    for (int i = 0; i < R / 32; ++i) {
-      const int th = st.h[i] - r * g.dil, tw = st.w[i] - s * g.dil;
-      bool ok = kv && st.n[i] >= 0 && th >= 0 && tw >= 0;
-      int ho = th, wo = tw;
-      if (g.stride == 2) {
-        ok = ok && ((th & 1) == 0) && ((tw & 1) == 0);
-        ho = th >> 1; wo = tw >> 1;
-      } else if (g.stride != 1) {
-        ok = ok && (th % g.stride == 0) && (tw % g.stride == 0);
-        ho = th / g.stride; wo = tw / g.stride;
-      }
-      ok = ok && ho < g.Ho && wo < g.Wo;
-      v[i] = ok ? ld16(dy + (((size_t)st.n[i] * g.Ho + ho) * g.Wo + wo) * g.Co + co) : zero4();
-    }
+    for (int u = 0; u < R / 32; ++u) v[u] = bload(rsr, (st.msk[u] & P) == P ? st.off[u] + t2 : OOB);
   }
 };
 
-// conv dgrad B operand: k = (r, s, co) rows, cols = ci; W stored [co][r][s][ci]
+// conv dgrad B operand: k = (a, b, co) rows, cols = ci; W stored [co][r][s][ci]
 template <int R>
-struct ConvDgradB : AllTiles {
+struct ConvDgradB {
   static constexpr bool KC = false;
-  const bf16* w; ConvGeom g; int K;
-  struct St { int c; };
-  __device__ void init(St& st, int n0, int tid) const { st.c = n0 + (tid % (R / 8)) * 8; }
-  __device__ void load(const St& st, int k0, int tid, uint4 (&v)[R / 32]) const {
-#pragma unroll
-    for (int i = 0; i < R / 32; ++i) {
-      const int k = k0 + tid / (R / 8) + (NTHR / (R / 8)) * i;
-      int r, s, co;
-      tap_of(k, k0, g.fCo, g.fKW, r, s, co);
-      v[i] = (k < K && st.c < g.C) ? ld16(w + (((size_t)co * g.KH + r) * g.KW + s) * g.C + st.c) : zero4();
-    }
-  }
-};
-
-// conv wgrad B operand: k = output pixel p rows, cols = kk = (r, s, ci)
-template <int R>
-struct ConvWgradB : AllTiles {
-  static constexpr bool KC = false;
-  const bf16* x; ConvGeom g; int P, KK;
-  struct St { int r, s, ci; bool cv; };
+  const bf16* w; ConvGeom g; DgradClass cl;
+  struct St { unsigned off[R / 32]; int n0; };
+  __device__ static int kr(int i, int tid) { return tid / (R / 8) + (NTHR / (R / 8)) * i; }
+  __device__ static int lds_off(int i, int tid) { return mc_off<R>(kr(i, tid), tid % (R / 8)); }
   __device__ void init(St& st, int n0, int tid) const {
-    const int kk = n0 + (tid % (R / 8)) * 8;
-    st.cv = kk < KK;
-    unsigned rs, ci, r, s;
-    g.fC.divmod((unsigned)kk, rs, ci);
-    g.fKW.divmod(rs, r, s);
-    st.ci = (int)ci; st.r = (int)r; st.s = (int)s;
-  }
-  __device__ void load(const St& st, int k0, int tid, uint4 (&v)[R / 32]) const {
+    st.n0 = n0;
+    const int c = (tid % (R / 8)) * 8;
+    const int T = g.KH * g.KW;
 #pragma unroll
-    for (int i = 0; i < R / 32; ++i) {
-      const int p = k0 + tid / (R / 8) + (NTHR / (R / 8)) * i;
-      unsigned t, wo, n, ho;
-      g.fWo.divmod((unsigned)p, t, wo);
-      g.fHo.divmod(t, n, ho);
-      const int hi = (int)ho * g.stride - g.pad + st.r * g.dil, wi = (int)wo * g.stride - g.pad + st.s * g.dil;
-      const bool ok = st.cv && p < P && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-      v[i] = ok ? ld16(x + (((size_t)n * g.H + hi) * g.W + wi) * g.C + st.ci) : zero4();
+    for (int i = 0; i < R / 32; ++i) st.off[i] = n0 + c < g.C ? (unsigned)(kr(i, tid) * T * g.C + c) * 2u : OOB;
+  }
+  __device__ void load(const St& st, int kt, int tid, uint4 (&v)[R / 32]) const {
+    int a, b, co0;
+    cl.tap(kt, a, b, co0);
+    const int r = cl.r0 + a * cl.rstep, s = cl.s0 + b * cl.sstep;
+    const Rsrc rsr = rsrc(w + (((size_t)co0 * g.KH + r) * g.KW + s) * g.C + st.n0);
+    const int left = g.Co - co0;
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) v[i] = bload(rsr, kr(i, tid) < left ? st.off[i] : OOB);
+  }
+};
+
+// conv wgrad B operand: k = output pixel p rows, cols = kk = (r, s, ci).  Thread t loads
+// pixels (t>>3) and (t>>3)+32 of the K-tile and column chunks (t&7)+8c (c < R/64): two
+// pixel decompositions per thread and K-tile, shared by its column chunks.
+template <int R>
+struct ConvWgradB {
+  static constexpr bool KC = false;
+  static constexpr int NC = R / 64;
+  const bf16* x; ConvGeom g; int P, KK;
+  struct St { unsigned coff[NC]; int rd[NC], sd[NC]; };
+  __device__ static int lds_off(int i, int tid) {
+    return mc_off<R>((tid >> 3) + 32 * (i & 1), (tid & 7) + 8 * (i >> 1));
+  }
+  __device__ void init(St& st, int n0, int tid) const {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int kk = n0 + ((tid & 7) + 8 * c) * 8;
+      unsigned rs_, ci, r, s;
+      g.fC.divmod((unsigned)(kk < KK ? kk : 0), rs_, ci);
+      g.fKW.divmod(rs_, r, s);
+      st.coff[c] = (unsigned)(((int)r * g.dil * g.W + (int)s * g.dil) * g.C + (int)ci) * 2u;
+      st.rd[c] = kk < KK ? (int)r * g.dil : (1 << 28);   // an invalid column never passes the bounds test
+      st.sd[c] = (int)s * g.dil;
+    }
+  }
+  __device__ void load(const St& st, int kt, int tid, uint4 (&v)[R / 32]) const {
+    const int p0 = kt * BK;
+    unsigned t, w0, n0, h0;
+    g.fWo.divmod((unsigned)p0, t, w0);
+    g.fHo.divmod(t, n0, h0);
+    const long long b0 = (((long long)n0 * g.H + (int)h0 * g.stride - g.pad) * g.W + (int)w0 * g.stride - g.pad) * g.C;
+    const Rsrc rsr = rsrc(x + b0);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kr = (tid >> 3) + 32 * j;
+      unsigned cw, wo, ch, ho;
+      g.fWo.divmod(w0 + (unsigned)kr, cw, wo);
+      g.fHo.divmod(h0 + cw, ch, ho);
+      const int hb = p0 + kr < P ? (int)ho * g.stride - g.pad : -(1 << 29);
+      const int wb = (int)wo * g.stride - g.pad;
+      const unsigned rel = (unsigned)((((int)ch * g.H + ((int)ho - (int)h0) * g.stride) * g.W +
+                                       ((int)wo - (int)w0) * g.stride) * g.C) * 2u;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const bool ok = (unsigned)(hb + st.rd[c]) < (unsigned)g.H && (unsigned)(wb + st.sd[c]) < (unsigned)g.W;
+        v[2 * c + j] = bload(rsr, ok ? rel + st.coff[c] : OOB);
+      }
     }
   }
 };
@@ -339,12 +366,12 @@ struct ConvWgradB : AllTiles {
 struct IdentityRows {
   __device__ __forceinline__ size_t operator()(int m) const { return (size_t)m; }
 };
-struct DgradOutRows {  // DgradRows order -> NHWC pixel index
-  DgradRows r;
+struct ClassRows {  // dgrad class row (n, i, j) -> NHWC pixel (n, i*S+ph, j*S+pw)
+  DgradClass c; int H, W;
   __device__ __forceinline__ size_t operator()(int m) const {
-    int n, hi, wi, c;
-    r.decode(m, n, hi, wi, c);
-    return ((size_t)n * r.H + hi) * r.W + wi;
+    int n, i, j;
+    c.decode(m, n, i, j);
+    return ((size_t)n * H + i * c.S + c.ph) * W + j * c.S + c.pw;
   }
 };
 
@@ -596,6 +623,11 @@ struct EpiF32 {  // fp32 [M][ld] = acc (+ bias[n]) (+= if accumulate)
 };
 
 // ---------------------------------------------------------------- main loop
+// PF = 1: the next K-tile's loads are issued before the MFMAs of the current one.
+// PF = 2: two register sets, loads issued two K-tiles ahead (the last tiles' prefetches
+// are clamped to the final tile, so every iteration issues the same loads and the
+// compiler can wait for the older set with a counted vmcnt).  The body is unrolled twice
+// so each set's role is static (no runtime-indexed register arrays).
 template <int BM, int BN, class LA, class LB, class EPI, int PF>
 __global__ void __launch_bounds__(NTHR, 2)
 gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int ktiles_per_split) {
@@ -619,8 +651,8 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int ktiles = (K + BK - 1) / BK;
-  const int kt_begin = blockIdx.z * ktiles_per_split;
-  const int kt_end = min(ktiles, kt_begin + ktiles_per_split);
+  const int kt0 = blockIdx.z * ktiles_per_split;
+  const int nt = min(ktiles, kt0 + ktiles_per_split) - kt0;
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -647,94 +679,62 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
     }
   };
-  if constexpr (PF == 1) {
-  int kt = la.next(sa, kt_begin, kt_end);
-  if (kt < kt_end) {
-    uint4 ra[BM / 32], rb[BN / 32];
-    la.load(sa, kt * BK, tid, ra);
-    lb.load(sb, kt * BK, tid, rb);
-    store_stage<LA::KC, BM>(smem, tid, ra);
-    store_stage<LB::KC, BN>(smem + A_BYTES, tid, rb);
-    __syncthreads();
-
-    int cur = 0;
-    while (kt < kt_end) {
-      char* As = smem + cur * STAGE;
-      char* Bs = As + A_BYTES;
-      const int nxt = la.next(sa, kt + 1, kt_end);
-      const bool more = nxt < kt_end;
-      if (more) {  // issue next tile's global loads before the MFMAs (T14)
-        la.load(sa, nxt * BK, tid, ra);
-        lb.load(sb, nxt * BK, tid, rb);
-      }
-      mfma_tile(As, Bs);
-      if (more) {
-        char* An = smem + (cur ^ 1) * STAGE;
-        store_stage<LA::KC, BM>(An, tid, ra);
-        store_stage<LB::KC, BN>(An + A_BYTES, tid, rb);
-      }
+  auto stage = [&](char* buf, const uint4 (&ra)[BM / 32], const uint4 (&rb)[BN / 32]) {
+    store_stage<LA, BM>(buf, tid, ra);
+    store_stage<LB, BN>(buf + A_BYTES, tid, rb);
+  };
+  if (nt > 0) {
+    if constexpr (PF == 1) {
+      uint4 ra[BM / 32], rb[BN / 32];
+      la.load(sa, kt0, tid, ra);
+      lb.load(sb, kt0, tid, rb);
+      stage(smem, ra, rb);
       __syncthreads();
-      cur ^= 1;
-      kt = nxt;
-    }
-  }
-  } else {
-    // PF == 2: two register sets, global loads issued two K-tiles ahead.  The loop
-    // body is unrolled twice so each set's role is static (no runtime-indexed arrays).
-    int kt = la.next(sa, kt_begin, kt_end);
-    if (kt < kt_end) {
+      for (int t = 0; t < nt; ++t) {
+        const char* cur = smem + (t & 1) * STAGE;
+        const bool more = t + 1 < nt;
+        if (more) {  // issue next tile's global loads before the MFMAs
+          la.load(sa, kt0 + t + 1, tid, ra);
+          lb.load(sb, kt0 + t + 1, tid, rb);
+        }
+        mfma_tile(cur, cur + A_BYTES);
+        if (more) stage(smem + ((t + 1) & 1) * STAGE, ra, rb);
+        __syncthreads();
+      }
+    } else {
+      const int last = kt0 + nt - 1;
       uint4 a0[BM / 32], b0[BN / 32], a1[BM / 32], b1[BN / 32];
-      la.load(sa, kt * BK, tid, a0);
-      lb.load(sb, kt * BK, tid, b0);
-      store_stage<LA::KC, BM>(smem, tid, a0);
-      store_stage<LB::KC, BN>(smem + A_BYTES, tid, b0);
-      int k1 = la.next(sa, kt + 1, kt_end);
-      if (k1 < kt_end) {
-        la.load(sa, k1 * BK, tid, a1);
-        lb.load(sb, k1 * BK, tid, b1);
-      }
+      la.load(sa, kt0, tid, a0);
+      lb.load(sb, kt0, tid, b0);
+      la.load(sa, min(kt0 + 1, last), tid, a1);
+      lb.load(sb, min(kt0 + 1, last), tid, b1);
+      stage(smem, a0, b0);
       __syncthreads();
-      int cur = 0;
-      while (true) {
-        // phase A: compute kt; set 1 holds k1 (in flight); set 0 is free
-        int k2 = k1 < kt_end ? la.next(sa, k1 + 1, kt_end) : kt_end;
-        if (k2 < kt_end) {
-          la.load(sa, k2 * BK, tid, a0);
-          lb.load(sb, k2 * BK, tid, b0);
-        }
-        mfma_tile(smem + cur * STAGE, smem + cur * STAGE + A_BYTES);
-        if (k1 < kt_end) {
-          store_stage<LA::KC, BM>(smem + (cur ^ 1) * STAGE, tid, a1);
-          store_stage<LB::KC, BN>(smem + (cur ^ 1) * STAGE + A_BYTES, tid, b1);
-        }
+      for (int t = 0;; t += 2) {
+        // compute t from buffer 0; set 1 (tile t+1) in flight; set 0 free
+        la.load(sa, min(kt0 + t + 2, last), tid, a0);
+        lb.load(sb, min(kt0 + t + 2, last), tid, b0);
+        mfma_tile(smem, smem + A_BYTES);
+        stage(smem + STAGE, a1, b1);
         __syncthreads();
-        cur ^= 1;
-        kt = k1;
-        if (kt >= kt_end) break;
-        // phase B: compute kt; set 0 holds k2; set 1 is free
-        k1 = k2 < kt_end ? la.next(sa, k2 + 1, kt_end) : kt_end;
-        if (k1 < kt_end) {
-          la.load(sa, k1 * BK, tid, a1);
-          lb.load(sb, k1 * BK, tid, b1);
-        }
-        mfma_tile(smem + cur * STAGE, smem + cur * STAGE + A_BYTES);
-        if (k2 < kt_end) {
-          store_stage<LA::KC, BM>(smem + (cur ^ 1) * STAGE, tid, a0);
-          store_stage<LB::KC, BN>(smem + (cur ^ 1) * STAGE + A_BYTES, tid, b0);
-        }
+        if (t + 1 >= nt) break;
+        // compute t+1 from buffer 1; set 0 (tile t+2) in flight; set 1 free
+        la.load(sa, min(kt0 + t + 3, last), tid, a1);
+        lb.load(sb, min(kt0 + t + 3, last), tid, b1);
+        mfma_tile(smem + STAGE, smem + STAGE + A_BYTES);
+        stage(smem, a0, b0);
         __syncthreads();
-        cur ^= 1;
-        kt = k2;
-        if (kt >= kt_end) break;
+        if (t + 2 >= nt) break;
       }
     }
   }
   epi.template apply<BM, BN>(acc, smem, m0, n0, M, N, wm, wn, lane, tid);
 }
 
-// K-tile prefetch depth of the main loop (1 = next tile, 2 = two tiles ahead); set by
-// mlc_gemm_config for A/B measurements, default chosen from the microbenchmarks
-static int g_prefetch = 1;
+// K-tile prefetch depth of the main loop (1 = next tile, 2 = two tiles ahead, used for the
+// 128x128 tile when a split has at least 4 K-tiles); mlc_gemm_config switches it for A/B
+// measurements
+static int g_prefetch = 2;
 
 template <int BM, int BN, class LA, class LB, class EPI>
 static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K,
@@ -742,14 +742,18 @@ static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int 
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const int ktiles = (K + BK - 1) / BK;
   if (splits < 1) splits = 1;
-  if (splits > ktiles) splits = ktiles;
-  const int per = (ktiles + splits - 1) / splits;
-  splits = (ktiles + per - 1) / per;
+  if (splits > ktiles) splits = ktiles > 0 ? ktiles : 1;
+  const int per = ktiles > 0 ? (ktiles + splits - 1) / splits : 0;
+  splits = per > 0 ? (ktiles + per - 1) / per : 1;
   dim3 grid(tiles, 1, splits);
-  if (g_prefetch >= 2 && per >= 3)
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, EPI, 2>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
-  else
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, EPI, 1>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
+  // the second register set only fits the square tile without spilling
+  if constexpr (BM == BN) {
+    if (g_prefetch >= 2 && per >= 4) {
+      hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, EPI, 2>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, EPI, 1>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
   return hipGetLastError();
 }
 
@@ -785,32 +789,34 @@ static ConvGeom mkgeom(int N, int H, int W, int C, int Co, int KH, int KW, int s
   return g;
 }
 
-// Row plan of a dgrad output.  Stride 2: one row range per parity class that at least
-// one filter tap reaches (a 1x1/s2 conv reaches only class (0,0)); rows of the other
-// classes are structurally zero and are filled by a memset/copy instead of GEMM blocks.
-static DgradRows mkrows(int N, int H, int W, int S, int KH, int KW, int pad, int dil, int* rows_out) {
-  DgradRows r;
-  r.N = N; r.H = H; r.W = W; r.S = S;
-  r.fW = FastDiv(W); r.fH = FastDiv(H);
-  r.nclass = 0;
-  for (int k = 0; k < 4; ++k) { r.base[k] = 0x7fffffff; r.cid[k] = 0; }
-  if (S != 2) { *rows_out = N * H * W; r.nclass = 1; r.base[0] = 0; return r; }
-  int b = 0;
-  for (int c = 0; c < 4; ++c) {
-    const int ph = c >> 1, pw = c & 1;
-    const int Hc = (H - ph + 1) / 2, Wc = (W - pw + 1) / 2;
-    bool rv = false, sv = false;
-    for (int t = 0; t < KH; ++t) rv |= (((ph + pad - t * dil) % 2) + 2) % 2 == 0;
-    for (int t = 0; t < KW; ++t) sv |= (((pw + pad - t * dil) % 2) + 2) % 2 == 0;
-    if (!rv || !sv || Hc <= 0 || Wc <= 0) continue;
-    const int k = r.nclass++;
-    r.base[k] = b; r.cid[k] = c;
-    r.fHc[k] = FastDiv(Hc);
-    r.fWc[k] = FastDiv(Wc);
-    b += N * Hc * Wc;
-  }
-  *rows_out = b;
-  return r;
+static int gcd_i(int a, int b) { while (b) { const int t = a % b; a = b; b = t; } return a; }
+
+// The stride-parity class (ph, pw) of a dgrad output: the filter taps that reach it form
+// arithmetic progressions r = r0 + rstep*a, s = s0 + sstep*b.  A class no tap reaches has
+// nr*ns == 0 and is still launched (K = 0) so its rows get the epilogue (0 + addend, BN).
+static DgradClass mkclass(int S, int ph, int pw, int H, int W, int Ho, int Wo, int Co, int KH, int KW,
+                          int pad, int dil) {
+  DgradClass c;
+  c.S = S; c.ph = ph; c.pw = pw;
+  c.Hc = (H - ph + S - 1) / S; c.Wc = (W - pw + S - 1) / S;
+  c.fWc = FastDiv(c.Wc > 0 ? c.Wc : 1); c.fHc = FastDiv(c.Hc > 0 ? c.Hc : 1);
+  auto axis = [&](int p, int KK, int& r0, int& step, int& n, int& d0, int& ds) {
+    r0 = -1; n = 0;
+    for (int r = 0; r < KK; ++r)
+      if ((((p + pad - r * dil) % S) + S) % S == 0) { if (r0 < 0) r0 = r; ++n; }
+    step = S / gcd_i(S, dil);
+    if (n == 0) { r0 = 0; d0 = 0; ds = 0; return; }
+    d0 = (p + pad - r0 * dil) / S;
+    ds = step * dil / S;
+  };
+  axis(ph, KH, c.r0, c.rstep, c.nr, c.dh0, c.dhs);
+  axis(pw, KW, c.s0, c.sstep, c.ns, c.dw0, c.dws);
+  c.ncb = (Co + BK - 1) / BK;
+  c.fns = FastDiv(c.ns > 0 ? c.ns : 1); c.fncb = FastDiv(c.ncb);
+  c.tmin = (c.nr > 0 && c.ns > 0)
+               ? ((long long)(c.dh0 - (c.nr - 1) * c.dhs) * Wo + (c.dw0 - (c.ns - 1) * c.dws)) * Co : 0;
+  (void)Ho;
+  return c;
 }
 
 // dispatch one GEMM over the three tile shapes; MK(R) builds the loaders for R rows
@@ -836,18 +842,18 @@ MLC_EXPORT int mlc_gemm_config(int prefetch) {
 MLC_EXPORT int mlc_conv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, float* sumsq,
                             int N, int H, int W, int C, int Co, int KH, int KW, int stride,
                             int pad, int dil, int Ho, int Wo, hipStream_t st) {
-  if (C % 8 || Co % 8) return -1;
+  if (C % 8 || Co % 8 || KH > 15 || KW > 16) return -1;
   const int M = N * Ho * Wo, K = KH * KW * C;
   const int tile = pick_tile(M, Co);
   EpiBF16<> epi{y, Co, sum, sumsq, IdentityRows{}};
-#define MKB(R) (MatKC<R>{{}, w, K, Co, K})
+#define MKB(R) (MatKC<R>{w, K, Co, K})
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
-#define MKA(R) (MatKC<R>{{}, x, C, M, K})
+#define MKA(R) (MatKC<R>{x, C, M, K})
     MLC_TILE_DISPATCH(tile, M, Co, K, 1, st, epi, MKA, MKB);
 #undef MKA
   }
   const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
-#define MKA(R) (ConvFwdA<R>{{}, x, g, M, K})
+#define MKA(R) (ConvFwdA<R>{x, g, M, K})
   MLC_TILE_DISPATCH(tile, M, Co, K, 1, st, epi, MKA, MKB);
 #undef MKA
 #undef MKB
@@ -857,45 +863,49 @@ MLC_EXPORT int mlc_conv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, f
 // alias dx) -- the addend fuses the gradient sum at a residual branch point.
 // bn_y0 != null additionally fuses the backward reduction of the BatchNorm(s) whose
 // output gradient dx is (see BnBwdEpi): dx is stored masked by bn_mask > 0 and the
-// partial sums go to bn_sums{0,1}[NSTAT][2][C] (zeroed by the caller).  Only valid when
-// every dx row is produced by the GEMM (not for stride-2 convs with unreachable taps).
+// partial sums go to bn_sums{0,1}[NSTAT][2][C] (zeroed by the caller).
+// A strided conv runs one GEMM per stride-parity class of dx (only the filter taps that
+// reach the class are in its K loop; a class no tap reaches gets K = 0), so every dx row
+// is written by a GEMM epilogue and no structurally-zero products are computed.
 MLC_EXPORT int mlc_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, const bf16* addend, int N,
                               int H, int W, int C, int Co, int KH, int KW, int stride, int pad,
                               int dil, int Ho, int Wo, const bf16* bn_mask, const bf16* bn_y0,
                               const float* bn_mean0, float* bn_sums0, const bf16* bn_y1,
                               const float* bn_mean1, float* bn_sums1, hipStream_t st) {
-  if (C % 8 || Co % 8) return -1;
-  const int K = KH * KW * Co;
+  if (C % 8 || Co % 8 || KH > 15 || KW > 16 || stride < 1) return -1;
   const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
   BnBwdEpi bn{bn_mask, bn_y0, bn_mean0, bn_sums0, bn_y1, bn_mean1, bn_sums1};
   if (bn_y0 && (!bn_mean0 || !bn_sums0 || (bn_y1 && (!bn_mean1 || !bn_sums1)))) return -1;
-#define MKB(R) (ConvDgradB<R>{{}, w, g, K})
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
-    const int M = N * H * W;
+    const DgradClass cl = mkclass(1, 0, 0, H, W, Ho, Wo, Co, 1, 1, 0, dil);
+    const int M = N * H * W, K = cl.ncb * BK;
     const int tile = pick_tile(M, C);
     EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}, addend, bn};
-#define MKA(R) (MatKC<R>{{}, dy, Co, M, K})
+#define MKA(R) (MatKC<R>{dy, Co, M, Co})
+#define MKB(R) (ConvDgradB<R>{w, g, cl})
     MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB);
 #undef MKA
   }
-  int M = 0;
-  const DgradRows rows = mkrows(N, H, W, stride == 2 ? 2 : 1, KH, KW, pad, dil, &M);
-  const int tile = pick_tile(M, C);
-#define MKA(R) (ConvDgradA<R>{dy, g, M, K, rows})
-  if (stride != 2) {
-    EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}, addend, bn};
-    MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB);
-  }
-  if (M < N * H * W) {  // classes no tap reaches: dx = addend there (or 0)
-    if (bn_y0) return -1;
-    const size_t bytes = (size_t)N * H * W * C * sizeof(bf16);
-    if (addend) { if (addend != dx) (void)hipMemcpyAsync(dx, addend, bytes, hipMemcpyDeviceToDevice, st); }
-    else (void)hipMemsetAsync(dx, 0, bytes, st);
-  }
-  if (M == 0) return hipGetLastError();
-  EpiBF16<DgradOutRows> epi{dx, C, nullptr, nullptr, DgradOutRows{rows}, addend, bn};
-  MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB);
+  hipError_t err = hipSuccess;
+  for (int ph = 0; ph < stride && ph < H; ++ph)
+    for (int pw = 0; pw < stride && pw < W; ++pw) {
+      const DgradClass cl = mkclass(stride, ph, pw, H, W, Ho, Wo, Co, KH, KW, pad, dil);
+      if (cl.nr > 15 || cl.ns > 16) return -1;
+      const int M = N * cl.Hc * cl.Wc, K = cl.nr * cl.ns * cl.ncb * BK;
+      if (M <= 0) continue;
+      const int tile = pick_tile(M, C);
+#define MKA(R) (ConvDgradA<R>{dy, g, M, K, cl})
+      if (stride == 1) {
+        EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}, addend, bn};
+        err = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB); }();
+      } else {
+        EpiBF16<ClassRows> epi{dx, C, nullptr, nullptr, ClassRows{cl, H, W}, addend, bn};
+        err = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB); }();
+      }
 #undef MKA
+      if (err != hipSuccess) return err;
+    }
+  return err;
 #undef MKB
 }
 
@@ -910,14 +920,14 @@ MLC_EXPORT int mlc_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, i
   if (!accumulate) (void)hipMemsetAsync(dw, 0, (size_t)Co * KK * sizeof(float), st);
   if (splits <= 0) splits = auto_splits(Co, KK, P, tile);
   EpiF32Atomic epi{dw, KK};
-#define MKA(R) (MatMC<R>{{}, dy, Co, P, Co})
+#define MKA(R) (MatMC<R>{dy, Co, P, Co})
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
-#define MKB(R) (MatMC<R>{{}, x, C, P, C})
+#define MKB(R) (MatMC<R>{x, C, P, C})
     MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
 #undef MKB
   }
   const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
-#define MKB(R) (ConvWgradB<R>{{}, x, g, P, KK})
+#define MKB(R) (ConvWgradB<R>{x, g, P, KK})
   MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
 #undef MKB
 #undef MKA
@@ -928,10 +938,10 @@ MLC_EXPORT int mlc_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, i
 //   tb=0: B is [K][N] (ldb);  tb=1: B is [N][K]
 // out_mode 0: store (+bias, accumulate flag), 1: atomic add (split-K allowed; the
 // caller zeroes C unless accumulating)
-#define GA_KC(R) (MatKC<R>{{}, A, lda, M, K})
-#define GA_MC(R) (MatMC<R>{{}, A, lda, K, M})
-#define GB_KC(R) (MatKC<R>{{}, B, ldb, N, K})
-#define GB_MC(R) (MatMC<R>{{}, B, ldb, K, N})
+#define GA_KC(R) (MatKC<R>{A, lda, M, K})
+#define GA_MC(R) (MatMC<R>{A, lda, K, M})
+#define GB_KC(R) (MatKC<R>{B, ldb, N, K})
+#define GB_MC(R) (MatMC<R>{B, ldb, K, N})
 
 MLC_EXPORT int mlc_gemm_f32out(const bf16* A, const bf16* B, float* C, const float* bias,
                                int M, int N, int K, int lda, int ldb, int ldc, int ta, int tb,
@@ -964,8 +974,8 @@ static hipError_t launch_tiles(int tile, int M, int N, int K, int splits, hipStr
   if (tile == 2) return launch<64, 256>(fa.template make<64>(), fb.template make<256>(), epi, M, N, K, splits, st);
   return launch<128, 128>(fa.template make<128>(), fb.template make<128>(), epi, M, N, K, splits, st);
 }
-struct MkMatKC { const bf16* p; int ld, rows, K; template <int R> MatKC<R> make() const { return MatKC<R>{{}, p, ld, rows, K}; } };
-struct MkMatMC { const bf16* p; int ld, K, cols; template <int R> MatMC<R> make() const { return MatMC<R>{{}, p, ld, K, cols}; } };
+struct MkMatKC { const bf16* p; int ld, rows, K; template <int R> MatKC<R> make() const { return MatKC<R>{p, ld, rows, K}; } };
+struct MkMatMC { const bf16* p; int ld, K, cols; template <int R> MatMC<R> make() const { return MatMC<R>{p, ld, K, cols}; } };
 #define GA_KC_F (MkMatKC{A, lda, M, K})
 #define GA_MC_F (MkMatMC{A, lda, K, M})
 #define GB_KC_F (MkMatKC{B, ldb, N, K})
