@@ -18,7 +18,10 @@ namespace {
 constexpr int NT = 256;
 
 // per-channel finalize: reduce the conv epilogue's NSTAT partial copies, publish batch
-// mean / invstd, the fused affine (scale, shift) and update the running statistics
+// mean / invstd, the fused affine (scale, shift) and update the running statistics.
+// 8 lanes per channel (32 channels per block) each sum every 8th copy, then a shuffle
+// reduction: the copies are all in flight at once instead of one dependent load chain.
+constexpr int FL = 8;
 __global__ void __launch_bounds__(NT)
 bn_finalize_kernel(const float* __restrict__ sum, const float* __restrict__ sumsq, int ncopy,
                    const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -26,10 +29,15 @@ bn_finalize_kernel(const float* __restrict__ sum, const float* __restrict__ sums
                    float* __restrict__ scale, float* __restrict__ shift,
                    float* __restrict__ run_mean, float* __restrict__ run_var,
                    long rows, int C, float eps, float momentum) {
-  const int c = blockIdx.x * NT + threadIdx.x;
-  if (c >= C) return;
+  const int c = blockIdx.x * (NT / FL) + (threadIdx.x / FL), q = threadIdx.x % FL;
   float s1 = 0.f, s2 = 0.f;
-  for (int k = 0; k < ncopy; ++k) { s1 += sum[(long)k * C + c]; s2 += sumsq[(long)k * C + c]; }
+  if (c < C) {
+#pragma unroll 4
+    for (int k = q; k < ncopy; k += FL) { s1 += sum[(long)k * C + c]; s2 += sumsq[(long)k * C + c]; }
+  }
+#pragma unroll
+  for (int o = 1; o < FL; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+  if (c >= C || q != 0) return;
   const float inv_count = 1.f / (float)rows;
   const float mean = s1 * inv_count;
   const float var = fmaxf(s2 * inv_count - mean * mean, 0.f);
@@ -46,19 +54,24 @@ bn_finalize_kernel(const float* __restrict__ sum, const float* __restrict__ sums
   }
 }
 
-// z = act(y*scale + shift [+ res])
+// z = act(y*scale + shift [+ res*rscale + rshift]) -- the residual's own affine lets a
+// block's downsample-branch BatchNorm be applied here instead of in a pass of its own
 __global__ void __launch_bounds__(NT)
 bn_fwd_apply_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf16* __restrict__ z,
                     const float* __restrict__ scale_, const float* __restrict__ shift_,
+                    const float* __restrict__ rscale_, const float* __restrict__ rshift_,
                     long rows, int C, int relu) {
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
   const long stride = (long)gridDim.x * NT;
   const int cg = (int)(gtid % G);
   const int c0 = cg * 8;
-  float scale[8], shift[8];
+  float scale[8], shift[8], rscale[8], rshift[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { scale[j] = scale_[c0 + j]; shift[j] = shift_[c0 + j]; }
+  for (int j = 0; j < 8; ++j) {
+    scale[j] = scale_[c0 + j]; shift[j] = shift_[c0 + j];
+    rscale[j] = rscale_ ? rscale_[c0 + j] : 1.f; rshift[j] = rscale_ ? rshift_[c0 + j] : 0.f;
+  }
   const long total = rows * G;
   for (long i = gtid; i < total; i += stride) {
     const long off = i * 8;  // row*C + c0 since i = row*G + cg
@@ -70,7 +83,7 @@ bn_fwd_apply_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf
       float r[8];
       unpack8(*reinterpret_cast<const uint4*>(res + off), r);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += r[j];
+      for (int j = 0; j < 8; ++j) f[j] += r[j] * rscale[j] + rshift[j];
     }
     if (relu) {
 #pragma unroll
@@ -138,18 +151,24 @@ bn_bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, co
 }
 
 // per-channel: reduce the NSTAT copies, publish dgamma/dbeta and the three
-// coefficients of  dy = k1*dU + k2 + k3*(y-mean)  (coef[0:C]=k1, [C:2C]=k2, [2C:3C]=k3)
+// coefficients of  dy = k1*dU + k2 + k3*(y-mean)  (coef[0:C]=k1, [C:2C]=k2, [2C:3C]=k3);
+// 8 lanes per channel as in bn_finalize_kernel
 __global__ void __launch_bounds__(NT)
 bn_bwd_finalize_kernel(const float* __restrict__ sums, const float* __restrict__ invstd,
                        const float* __restrict__ gamma, float* __restrict__ coef,
                        float* __restrict__ dgamma, float* __restrict__ dbeta, long rows, int C) {
-  const int c = blockIdx.x * NT + threadIdx.x;
-  if (c >= C) return;
+  const int c = blockIdx.x * (NT / FL) + (threadIdx.x / FL), q = threadIdx.x % FL;
   float S1 = 0.f, S2 = 0.f;
-  for (int k = 0; k < NSTAT; ++k) {
-    S1 += sums[(size_t)k * 2 * C + c];
-    S2 += sums[(size_t)k * 2 * C + C + c];
+  if (c < C) {
+#pragma unroll
+    for (int k = q; k < NSTAT; k += FL) {
+      S1 += sums[(size_t)k * 2 * C + c];
+      S2 += sums[(size_t)k * 2 * C + C + c];
+    }
   }
+#pragma unroll
+  for (int o = 1; o < FL; o <<= 1) { S1 += __shfl_xor(S1, o, 64); S2 += __shfl_xor(S2, o, 64); }
+  if (c >= C || q != 0) return;
   const float invM = 1.f / (float)rows;
   const float is = invstd[c];
   const float k1 = gamma[c] * is;
@@ -224,18 +243,24 @@ MLC_EXPORT int mlc_bn_finalize(const float* sum, const float* sumsq, int ncopy, 
                                const float* beta, float* save_mean, float* save_invstd, float* scale,
                                float* shift, float* run_mean, float* run_var, long rows, int C,
                                float eps, float momentum, hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, st, sum, sumsq, ncopy,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + NT / FL - 1) / (NT / FL)), dim3(NT), 0, st, sum, sumsq, ncopy,
                      gamma, beta, save_mean, save_invstd, scale, shift, run_mean, run_var, rows, C, eps,
                      momentum);
   return hipGetLastError();
 }
 
+MLC_EXPORT int mlc_bn_fwd_apply2(const bf16* y, const bf16* res, bf16* z, const float* scale,
+                                 const float* shift, const float* rscale, const float* rshift, long rows,
+                                 int C, int relu, hipStream_t st) {
+  if (!shape_ok(C) || (rscale && !rshift)) return -1;
+  hipLaunchKernelGGL(bn_fwd_apply_kernel, dim3(grid_for(rows, C)), dim3(NT), 0, st, y, res, z, scale,
+                     shift, rscale, rshift, rows, C, relu);
+  return hipGetLastError();
+}
+
 MLC_EXPORT int mlc_bn_fwd_apply(const bf16* y, const bf16* res, bf16* z, const float* scale,
                                 const float* shift, long rows, int C, int relu, hipStream_t st) {
-  if (!shape_ok(C)) return -1;
-  hipLaunchKernelGGL(bn_fwd_apply_kernel, dim3(grid_for(rows, C)), dim3(NT), 0, st, y, res, z, scale,
-                     shift, rows, C, relu);
-  return hipGetLastError();
+  return mlc_bn_fwd_apply2(y, res, z, scale, shift, nullptr, nullptr, rows, C, relu, st);
 }
 
 // sums must hold NSTAT*2*C floats, zeroed by the caller
@@ -251,7 +276,7 @@ MLC_EXPORT int mlc_bn_bwd_reduce(const bf16* dz, const bf16* z, const bf16* y, c
 MLC_EXPORT int mlc_bn_bwd_finalize(const float* sums, const float* invstd, const float* gamma,
                                    float* coef, float* dgamma, float* dbeta, long rows, int C,
                                    hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, st, sums, invstd,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + NT / FL - 1) / (NT / FL)), dim3(NT), 0, st, sums, invstd,
                      gamma, coef, dgamma, dbeta, rows, C);
   return hipGetLastError();
 }

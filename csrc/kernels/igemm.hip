@@ -578,6 +578,27 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
   }
 };
 
+struct EpiF32Slab {  // split-K partial tile -> slab blockIdx.z of ws ([splits][M][ld] fp32, plain stores)
+  float* ws; int ld; size_t slab;
+  template <int BM, int BN>
+  __device__ void apply(f32x16 (&acc)[2][2], char*, int m0, int n0, int M, int N,
+                        int wm, int wn, int lane, int) const {
+    float* out = ws + (size_t)blockIdx.z * slab;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wn * 64 + 32 * j + (lane & 31);
+        if (n >= N) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (m < M) out[(size_t)m * ld + n] = acc[i][j][r];
+        }
+      }
+  }
+};
+
 struct EpiF32Atomic {  // fp32 [M][ld] += (split-K partial sums)
   float* out; int ld;
   template <int BM, int BN>
@@ -735,6 +756,13 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
 // 128x128 tile when a split has at least 4 K-tiles); mlc_gemm_config switches it for A/B
 // measurements
 static int g_prefetch = 2;
+// split-K weight gradients: grow the split until tiles*splits reaches this many blocks.
+// Plain-matrix operands (1x1 convs, dense layers) prefer fewer splits: their K loop is
+// cheap, so the fp32 atomic traffic of extra splits costs more than the lost occupancy
+// (measured on every ResNet-50 wgrad shape: 256 vs 768 blocks saves 10-30 %); gathered
+// operands (3x3 / 7x7 convs) want the occupancy.
+static int g_split_target = 768;
+static int g_split_target_mat = 256;
 
 template <int BM, int BN, class LA, class LB, class EPI>
 static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K,
@@ -765,13 +793,13 @@ static int pick_tile(int M, int N) {
 }
 
 // pick a split-K factor so a small-output / long-K GEMM still fills 256 CUs
-static int auto_splits(int M, int N, int K, int tile) {
+static int auto_splits(int M, int N, int K, int tile, int target = g_split_target) {
   const int BMv = tile == 1 ? 256 : tile == 2 ? 64 : 128;
   const int BNv = tile == 1 ? 64 : tile == 2 ? 256 : 128;
   const int tiles = ((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
   const int ktiles = (K + BK - 1) / BK;
   int s = 1;
-  while (tiles * s < 768 && ktiles / (s * 2) >= 4) s *= 2;
+  while (tiles * s < target && ktiles / (s * 2) >= 4) s *= 2;
   return s;
 }
 
@@ -832,6 +860,18 @@ MLC_EXPORT int mlc_bn_stat_copies() { return NSTAT; }
 MLC_EXPORT int mlc_gemm_config(int prefetch) {
   const int old = igemm::g_prefetch;
   if (prefetch == 1 || prefetch == 2) igemm::g_prefetch = prefetch;
+  return old;
+}
+
+// tuning knobs for A/B measurements: key 0 = prefetch depth (1, 2), key 1 / 2 = split-K
+// block target of gathered / plain-matrix weight-gradient GEMMs; returns the previous
+// value (-1: bad key)
+MLC_EXPORT int mlc_gemm_get_set(int key, int value) {
+  int* k = key == 0 ? &igemm::g_prefetch : key == 1 ? &igemm::g_split_target
+          : key == 2 ? &igemm::g_split_target_mat : nullptr;
+  if (!k) return -1;
+  const int old = *k;
+  if (value > 0) *k = value;
   return old;
 }
 
@@ -911,22 +951,86 @@ MLC_EXPORT int mlc_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, const bf1
 
 // dw[Co, KH*KW*C] (fp32) = sum_p dy[p][co] * im2col(x)[p][kk]; zeroes dw first unless
 // accumulate != 0.  splits <= 0 picks a split-K factor automatically.
+namespace {
+// out[i] (+)= sum over splits of ws[s][i]  (float4 per thread)
+__global__ void __launch_bounds__(256)
+splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n4, int splits,
+                     long slab4, int accumulate) {
+  const float4* w4 = reinterpret_cast<const float4*>(ws);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 a = accumulate ? reinterpret_cast<const float4*>(out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+    int k = 0;
+    for (; k + 4 <= splits; k += 4) {  // four independent loads in flight
+      const float4 u0 = w4[(k + 0) * slab4 + i], u1 = w4[(k + 1) * slab4 + i];
+      const float4 u2 = w4[(k + 2) * slab4 + i], u3 = w4[(k + 3) * slab4 + i];
+      a.x += u0.x + u1.x; a.y += u0.y + u1.y; a.z += u0.z + u1.z; a.w += u0.w + u1.w;
+      b.x += u2.x + u3.x; b.y += u2.y + u3.y; b.z += u2.z + u3.z; b.w += u2.w + u3.w;
+    }
+    for (; k < splits; ++k) {
+      const float4 u = w4[k * slab4 + i];
+      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  }
+}
+}  // namespace
+
+// dw[Co, KH*KW*C] (fp32) = sum_p dy[p][co] * im2col(x)[p][kk]; written, or added to dw
+// when accumulate != 0.  splits <= 0 picks a split-K factor automatically.  With a
+// workspace (ws_floats >= splits*Co*KK) the split-K partial tiles go to fp32 slabs with
+// plain stores and one reduction pass sums them into dw; without, they are added into dw
+// with fp32 atomics (memory-side, ~1.3 TB/s: the slab round trip is ~4x cheaper).
 MLC_EXPORT int mlc_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, int H, int W,
                               int C, int Co, int KH, int KW, int stride, int pad, int dil,
-                              int Ho, int Wo, int splits, int accumulate, hipStream_t st) {
+                              int Ho, int Wo, int splits, int accumulate, float* ws, long ws_floats,
+                              hipStream_t st) {
   if (C % 8 || Co % 8) return -1;
   const int P = N * Ho * Wo, KK = KH * KW * C;
   const int tile = pick_tile(Co, KK);
-  if (!accumulate) (void)hipMemsetAsync(dw, 0, (size_t)Co * KK * sizeof(float), st);
-  if (splits <= 0) splits = auto_splits(Co, KK, P, tile);
-  EpiF32Atomic epi{dw, KK};
+  const bool plain = KH == 1 && KW == 1 && stride == 1 && pad == 0;
+  const size_t slab = (size_t)Co * KK;
+  // slabs pay when the partial sums are large (>= 8 MB: atomics ~1.3 TB/s vs two plain
+  // passes ~5 TB/s each) and the reduction has enough elements to fill the chip
+  bool use_slab = false;
+  if (splits <= 0) {
+    const int ss = auto_splits(Co, KK, P, tile, g_split_target);
+    use_slab = ws && slab >= (1u << 18) && (double)ss * slab * 4 >= 8e6 && (long)(ss * slab) <= ws_floats;
+    splits = use_slab ? ss : auto_splits(Co, KK, P, tile, plain ? g_split_target_mat : g_split_target);
+  } else {
+    use_slab = ws && (long)(splits * slab) <= ws_floats;
+  }
+  const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
 #define MKA(R) (MatMC<R>{dy, Co, P, Co})
-  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
+  if (use_slab) {
+    {  // the launch rounds splits so that no split is empty: size the reduction to it
+      const int ktiles = (P + BK - 1) / BK;
+      const int per = (ktiles + splits - 1) / splits;
+      splits = (ktiles + per - 1) / per;
+    }
+    EpiF32Slab epi{ws, KK, slab};
+    hipError_t e;
+#define MKB(R) (MatMC<R>{x, C, P, C})
+    if (plain) e = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB); }();
+#undef MKB
+#define MKB(R) (ConvWgradB<R>{x, g, P, KK})
+    else e = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB); }();
+#undef MKB
+    if (e != hipSuccess) return e;
+    const long n4 = (long)slab / 4;
+    long blocks = (n4 + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, dw, n4, splits,
+                       (long)slab / 4, accumulate);
+    return hipGetLastError();
+  }
+  if (!accumulate) (void)hipMemsetAsync(dw, 0, slab * sizeof(float), st);
+  EpiF32Atomic epi{dw, KK};
+  if (plain) {
 #define MKB(R) (MatMC<R>{x, C, P, C})
     MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
 #undef MKB
   }
-  const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
 #define MKB(R) (ConvWgradB<R>{x, g, P, KK})
   MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
 #undef MKB
@@ -949,7 +1053,7 @@ MLC_EXPORT int mlc_gemm_f32out(const bf16* A, const bf16* B, float* C, const flo
   if (K % 8 || lda % 8 || ldb % 8 || (ta && M % 8) || (!tb && N % 8)) return -1;
   const int tile = pick_tile(M, N);
   if (out_mode == 1) {
-    if (splits <= 0) splits = auto_splits(M, N, K, tile);
+    if (splits <= 0) splits = auto_splits(M, N, K, tile, g_split_target_mat);
     EpiF32Atomic epi{C, ldc};
     if (!ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_KC, GB_KC);
     if (!ta && !tb) MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_KC, GB_MC);

@@ -21,7 +21,7 @@ vp, i32, i64, f32, u32 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_uint
 _SIGS = {
     'mlc_conv_fwd': [vp, vp, vp, vp, vp] + [i32] * 12 + [vp],
     'mlc_conv_dgrad': [vp, vp, vp, vp] + [i32] * 12 + [vp] * 7 + [vp],
-    'mlc_conv_wgrad': [vp, vp, vp] + [i32] * 14 + [vp],
+    'mlc_conv_wgrad': [vp, vp, vp] + [i32] * 14 + [vp, i64, vp],
     'mlc_gemm_f32out': [vp, vp, vp, vp] + [i32] * 11 + [vp],
     'mlc_gemm_bf16out': [vp, vp, vp] + [i32] * 8 + [vp],
     'mlc_gemm_bf16_ex': [vp, vp, vp] + [i32] * 8 + [vp, i32, vp, vp, vp, vp, vp],
@@ -33,8 +33,10 @@ _SIGS = {
     'mlc_dropout': [vp, vp, i64, f32, vp, u32, vp],
     'mlc_bn_stat_copies': [],
     'mlc_gemm_config': [i32],
+    'mlc_gemm_get_set': [i32, i32],
     'mlc_bn_finalize': [vp, vp, i32] + [vp] * 8 + [i64, i32, f32, f32, vp],
     'mlc_bn_fwd_apply': [vp] * 5 + [i64, i32, i32, vp],
+    'mlc_bn_fwd_apply2': [vp] * 7 + [i64, i32, i32, vp],
     'mlc_bn_bwd_reduce': [vp] * 5 + [i64, i32, vp],
     'mlc_bn_bwd_finalize': [vp] * 6 + [i64, i32, vp],
     'mlc_bn_bwd_apply': [vp] * 7 + [i64, i32, vp],

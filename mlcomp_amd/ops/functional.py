@@ -14,6 +14,8 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -109,16 +111,37 @@ def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=1, pad=0, di
     return dx
 
 
+_USE_SLAB = os.environ.get('MLC_WGRAD_SLAB', '1') != '0'
+_SLAB = {}
+_SLAB_OLD = []   # superseded buffers stay alive: a captured graph may still point at them
+
+
+def slab_workspace(device, n: int) -> torch.Tensor:
+    """fp32 split-K slab workspace (no zeroing needed), grown on demand - first during
+    eager warm-up, so graph capture reuses it."""
+    key = str(device)
+    buf = _SLAB.get(key)
+    if buf is None or buf.numel() < n:
+        if buf is not None:
+            _SLAB_OLD.append(buf)
+        buf = torch.empty(max(n, 1 << 20), device=device, dtype=torch.float32)
+        _SLAB[key] = buf
+    return buf
+
+
 def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride=1, pad=0, dil=1,
                  out: Optional[torch.Tensor] = None, accumulate=False) -> torch.Tensor:
-    """fp32 weight gradient in [Co, KH, KW, Ci] order (written into ``out`` if given)."""
+    """fp32 weight gradient in [Co, KH, KW, Ci] order (written into ``out`` if given).
+    Split-K partial sums go through a slab workspace and one reduction pass."""
     Co, KH, KW, Ci = w_shape
     N, H, W, C = x.shape
     _, Ho, Wo, _ = dy.shape
     if _cuda(dy):
         dw = out if out is not None else torch.empty(Co, KH, KW, Ci, device=dy.device, dtype=torch.float32)
+        ws = slab_workspace(dy.device, min(32 * Co * KH * KW * Ci, 64 << 20)) if _USE_SLAB else None
         _lib.call('mlc_conv_wgrad', _lib.ptr(dy), _lib.ptr(x), _lib.ptr(dw), N, H, W, C, Co, KH, KW,
-                  stride, pad, dil, Ho, Wo, 0, int(accumulate), _lib.stream())
+                  stride, pad, dil, Ho, Wo, 0, int(accumulate), _lib.ptr(ws),
+                  ws.numel() if ws is not None else 0, _lib.stream())
         return dw
     dwf = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).float(), (Co, Ci, KH, KW),
                                       dy.permute(0, 3, 1, 2).float(), stride, pad, dil)
@@ -143,14 +166,17 @@ def stat_buffers(C, device):
 
 
 def bn_fwd_apply(y, res, s1, s2, gamma, beta, save_mean, save_invstd, run_mean, run_var,
-                 eps=1e-5, momentum=0.1, relu=True, out=None, scale=None, shift=None):
+                 eps=1e-5, momentum=0.1, relu=True, out=None, scale=None, shift=None,
+                 res_affine=None, apply=True):
     """z = act(BN_train(y) [+ res]) given the conv epilogue's partial sums s1/s2
-    ([NSTAT*C] each).  Writes save_mean/save_invstd and updates running stats."""
+    ([NSTAT*C] each).  Writes save_mean/save_invstd and updates running stats.
+    ``res_affine=(rscale, rshift)`` applies a per-channel affine to the residual first (a
+    downsample branch's BN folded into this pass).  ``apply=False`` only finalizes the
+    statistics into ``scale``/``shift`` (required then) and returns None."""
     rows = y.numel() // y.shape[-1]
     C = y.shape[-1]
     ncopy = s1.numel() // C
     if _cuda(y):
-        z = out if out is not None else torch.empty_like(y)
         if scale is None:
             scale = torch.empty(2, C, device=y.device, dtype=torch.float32)
             scale, shift = scale[0], scale[1]
@@ -158,8 +184,12 @@ def bn_fwd_apply(y, res, s1, s2, gamma, beta, save_mean, save_invstd, run_mean, 
                   _lib.ptr(save_mean), _lib.ptr(save_invstd), _lib.ptr(scale), _lib.ptr(shift),
                   _lib.ptr(run_mean), _lib.ptr(run_var), rows, C, float(eps), float(momentum),
                   _lib.stream())
-        _lib.call('mlc_bn_fwd_apply', _lib.ptr(y), _lib.ptr(res), _lib.ptr(z), _lib.ptr(scale),
-                  _lib.ptr(shift), rows, C, int(relu), _lib.stream())
+        if not apply:
+            return None
+        z = out if out is not None else torch.empty_like(y)
+        rs, rh = res_affine if res_affine is not None else (None, None)
+        _lib.call('mlc_bn_fwd_apply2', _lib.ptr(y), _lib.ptr(res), _lib.ptr(z), _lib.ptr(scale),
+                  _lib.ptr(shift), _lib.ptr(rs), _lib.ptr(rh), rows, C, int(relu), _lib.stream())
         return z
     s1t = s1.reshape(ncopy, C).sum(0)
     s2t = s2.reshape(ncopy, C).sum(0)
@@ -172,9 +202,17 @@ def bn_fwd_apply(y, res, s1, s2, gamma, beta, save_mean, save_invstd, run_mean, 
         unb = var * rows / max(rows - 1, 1)
         run_mean.mul_(1 - momentum).add_(momentum * mean)
         run_var.mul_(1 - momentum).add_(momentum * unb)
+    if scale is not None:
+        scale.copy_(inv * gamma)
+        shift.copy_(beta - mean * inv * gamma)
+    if not apply:
+        return None
     zf = (y.float() - mean) * (inv * gamma) + beta
     if res is not None:
-        zf = zf + res.float()
+        rf = res.float()
+        if res_affine is not None:
+            rf = rf * res_affine[0] + res_affine[1]
+        zf = zf + rf
     if relu:
         zf = zf.clamp_min(0)
     z = zf.to(torch.bfloat16)
@@ -184,19 +222,23 @@ def bn_fwd_apply(y, res, s1, s2, gamma, beta, save_mean, save_invstd, run_mean, 
     return z
 
 
-def bn_apply(y, res, scale, shift, relu=True):
-    """z = act(y*scale + shift [+ res]) with precomputed per-channel scale/shift
-    (inference BatchNorm / frozen BN)."""
+def bn_apply(y, res, scale, shift, relu=True, res_affine=None):
+    """z = act(y*scale + shift [+ res (*rscale + rshift)]) with precomputed per-channel
+    scale/shift (inference BatchNorm / frozen BN)."""
     rows = y.numel() // y.shape[-1]
     C = y.shape[-1]
     if _cuda(y):
         z = torch.empty_like(y)
-        _lib.call('mlc_bn_fwd_apply', _lib.ptr(y), _lib.ptr(res), _lib.ptr(z), _lib.ptr(scale),
-                  _lib.ptr(shift), rows, C, int(relu), _lib.stream())
+        rs, rh = res_affine if res_affine is not None else (None, None)
+        _lib.call('mlc_bn_fwd_apply2', _lib.ptr(y), _lib.ptr(res), _lib.ptr(z), _lib.ptr(scale),
+                  _lib.ptr(shift), _lib.ptr(rs), _lib.ptr(rh), rows, C, int(relu), _lib.stream())
         return z
     zf = y.float() * scale + shift
     if res is not None:
-        zf = zf + res.float()
+        rf = res.float()
+        if res_affine is not None:
+            rf = rf * res_affine[0] + res_affine[1]
+        zf = zf + rf
     if relu:
         zf = zf.clamp_min(0)
     return zf.to(torch.bfloat16)

@@ -127,13 +127,22 @@ class ConvBN:
         return _ConvBNFn.apply(x, res, self.ctx.anchor, self)
 
     # raw (autograd-free) halves, composed by the block-level Functions
-    def fwd(self, x, res=None):
+    def fwd(self, x, res=None, defer=False):
+        """z = act(BN(conv(x)) [+ res]); ``res`` is a tensor or a deferred BN output
+        ``(y, scale, shift)`` (applied in the same pass).  ``defer=True`` stops after the
+        statistics: z is not materialised (returns None; scale/shift are ready)."""
         ws = self.ctx.ws
+        raff = None
+        if isinstance(res, tuple):
+            res, rs, rh = res
+            raff = (rs, rh)
         if not self.ctx.training:  # inference BN: running statistics, no stat epilogue
             y = Fn.conv2d_fwd(x, self.w.bf16, self.stride, self.pad, self.dil)
-            scale = self.gamma.master * torch.rsqrt(self.run_var + self.eps)
-            shift = self.beta.master - self.run_mean * scale
-            z = Fn.bn_apply(y, res, scale.contiguous(), shift.contiguous(), self.act)
+            torch.rsqrt(self.run_var + self.eps, out=self.scale).mul_(self.gamma.master)
+            torch.sub(self.beta.master, self.run_mean * self.scale, out=self.shift)
+            if defer:
+                return None, (x, y, None)
+            z = Fn.bn_apply(y, res, self.scale, self.shift, self.act, res_affine=raff)
             return z, (x, y, z)
         s1, s2 = ws[self.k_s1], ws[self.k_s2]
         y = Fn.conv2d_fwd(x, self.w.bf16, self.stride, self.pad, self.dil, stats=(s1, s2))
@@ -141,7 +150,7 @@ class ConvBN:
         z = Fn.bn_fwd_apply(y, res, s1, s2, self.gamma.master, self.beta.master, self.save_mean,
                             self.save_invstd, self.run_mean if training else None,
                             self.run_var if training else None, self.eps, self.momentum, self.act,
-                            scale=self.scale, shift=self.shift)
+                            scale=self.scale, shift=self.shift, res_affine=raff, apply=not defer)
         return z, (x, y, z)
 
     def dgrad_covers_all(self) -> bool:
@@ -230,7 +239,9 @@ class _ResidualBlockFn(torch.autograd.Function):
     def forward(ctx, x, anchor, blk: ResidualBlock):
         recs = []
         if blk.down is not None:
-            identity, rd = blk.down.fwd(x)
+            # the downsample BN (no activation) is applied inside the last unit's pass
+            _, rd = blk.down.fwd(x, defer=not blk.down.act)
+            identity = rd[2] if blk.down.act else (rd[1], blk.down.scale, blk.down.shift)
         else:
             identity, rd = x, None
         y = x

@@ -61,7 +61,12 @@ def main():
     ap.add_argument('--batch', type=int, default=256)
     ap.add_argument('--iters', type=int, default=10)
     ap.add_argument('--torch', type=int, default=1)
+    ap.add_argument('--split-targets', default='',
+                    help='comma list: also time wgrad at these split-K block targets')
     a = ap.parse_args()
+    targets = [int(t) for t in a.split_targets.split(',') if t]
+    from mlcomp_amd.ops import _lib
+    sweep = {t: 0.0 for t in targets}
     N = a.batch
     tot = {'nf': 0.0, 'nd': 0.0, 'nw': 0.0, 'tf': 0.0, 'td': 0.0, 'tw': 0.0}
     print(f'{"shape":24s} {"us fwd/dgrad/wgrad (native)":>30s} {"TF/s":>17s} {"GB/s fwd":>8s} | '
@@ -86,6 +91,15 @@ def main():
         line = (f'{name:24s} {tf * 1e6:9.1f} {td * 1e6:9.1f} {tw * 1e6:9.1f}   '
                 f'{fl / tf / 1e12:5.0f} {fl / td / 1e12 if td else 0:5.0f} {fl / tw / 1e12:5.0f} '
                 f'{byts / tf / 1e9:8.0f}')
+        if targets:
+            parts = []
+            for tg in targets:
+                old = _lib.load().mlc_gemm_get_set(1, tg)
+                tt = timeit(lambda: Fn.conv2d_wgrad(dy, x, w.shape, s, p, out=dw), a.iters)
+                _lib.load().mlc_gemm_get_set(1, old)
+                sweep[tg] += cnt * tt
+                parts.append(f'{tg}:{tt * 1e6:.1f}')
+            line += ' | wgrad@' + ' '.join(parts)
         if a.torch:
             xt = x.permute(0, 3, 1, 2)          # channels_last views
             wt = w.permute(0, 3, 1, 2)
@@ -104,6 +118,8 @@ def main():
     print(f'weighted per step (ms): native fwd {tot["nf"] * 1e3:.2f} dgrad {tot["nd"] * 1e3:.2f} '
           f'wgrad {tot["nw"] * 1e3:.2f} | MIOpen fwd {tot["tf"] * 1e3:.2f} dgrad {tot["td"] * 1e3:.2f} '
           f'wgrad {tot["tw"] * 1e3:.2f}', flush=True)
+    if targets:
+        print('wgrad per step by split target (ms): ' + ' '.join(f'{t}:{v * 1e3:.2f}' for t, v in sweep.items()))
 
 
 if __name__ == '__main__':

@@ -37,6 +37,7 @@ CONV_CASES = [
     (2, 16, 16, 64, 128, 3, 2, 1),
     (2, 15, 13, 128, 64, 3, 2, 1),
     (3, 15, 15, 64, 128, 1, 2, 0),
+    (2, 13, 11, 64, 72, 3, 3, 1),     # stride 3: nine parity classes, Co % 64 != 0
 ]
 
 
@@ -85,6 +86,40 @@ def test_conv_wgrad(case):
     out = Fn.conv2d_wgrad(dy.to(DEV), x.to(DEV), (Co, K, K, C), s, p)
     torch.cuda.synchronize()
     assert rel_err(out, ref) < 5e-3
+
+
+@pytest.mark.parametrize('case', [CONV_CASES[0], CONV_CASES[-1]])
+def test_conv_wgrad_accumulate_slab_and_atomic(case):
+    """split-K slab reduction (default) and the atomic fallback (no workspace) both
+    accumulate into an existing gradient"""
+    from mlcomp_amd.ops import _lib
+    N, H, W, C, Co, K, s, p = case
+    Ho, Wo = Fn.conv_out_hw(H, W, K, K, s, p, 1)
+    x = _bf(N, H, W, C, seed=15)
+    dy = _bf(N, Ho, Wo, Co, seed=16)
+    ref = Fn.conv2d_wgrad(dy, x, (Co, K, K, C), s, p) + 1.0
+    out = torch.ones(Co, K, K, C, device=DEV)
+    Fn.conv2d_wgrad(dy.to(DEV), x.to(DEV), (Co, K, K, C), s, p, out=out, accumulate=True)
+    out2 = torch.ones(Co, K, K, C, device=DEV)
+    xd, dyd = x.to(DEV), dy.to(DEV)
+    _lib.call('mlc_conv_wgrad', _lib.ptr(dyd), _lib.ptr(xd), _lib.ptr(out2), N, H, W, C, Co, K, K, s, p, 1,
+              Ho, Wo, 0, 1, None, 0, _lib.stream())
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 5e-3
+    assert rel_err(out2, ref) < 5e-3
+
+
+def test_bn_apply_residual_affine():
+    C = 64
+    y = _bf(2, 3, 4, C, seed=17)
+    r = _bf(2, 3, 4, C, seed=18)
+    sc, sh = torch.rand(C) + 0.5, torch.randn(C) * 0.1
+    rs, rh = torch.rand(C) + 0.5, torch.randn(C) * 0.1
+    ref = Fn.bn_apply(y, r, sc, sh, True, res_affine=(rs, rh))
+    out = Fn.bn_apply(y.to(DEV), r.to(DEV), sc.to(DEV), sh.to(DEV), True,
+                      res_affine=(rs.to(DEV), rh.to(DEV)))
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 1e-2
 
 
 @pytest.mark.parametrize('relu,res', [(True, True), (True, False), (False, False)])
