@@ -382,10 +382,15 @@ struct ClassRows {  // dgrad class row (n, i, j) -> NHWC pixel (n, i*S+ph, j*S+p
 // for up to two BNs sharing the same dU (a block's last BN and its downsample BN).  The
 // masked dU is what gets stored, so the elementwise BN-backward pass needs neither z
 // nor a separate residual-gradient copy.
+// Without a mask tensor the ReLU mask can be recomputed from the pre-BN values the
+// reduction reads anyway: [y0*msc0 + msh0 (+ y1*msc1 + msh1) > 0] with the forward's
+// (scale, shift) -- exactly the forward's z > 0 -- so z is not read at all.
 struct BnBwdEpi {
   const bf16* mask = nullptr;
   const bf16* y0 = nullptr; const float* mean0 = nullptr; float* sums0 = nullptr;
   const bf16* y1 = nullptr; const float* mean1 = nullptr; float* sums1 = nullptr;
+  const float* msc0 = nullptr; const float* msh0 = nullptr;
+  const float* msc1 = nullptr; const float* msh1 = nullptr;
 };
 
 template <class RowMap = IdentityRows, bool kDense = false>
@@ -436,13 +441,18 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
     const int c = tid % CPR;
     const int nc = n0 + c * 8;
     const bool red = !kDense && bn.y0 != nullptr;
-    float mu0[8], mu1[8], s1[8], s2[8], t2[8];
+    float mu0[8], mu1[8], s1[8], s2[8], t2[8], ma0[8], mb0[8], ma1[8], mb1[8];
+    const bool aff = red && !bn.mask && bn.msc0, aff1 = aff && bn.msc1;
     if (red) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         mu0[e] = nc < N ? bn.mean0[nc + e] : 0.f;
         mu1[e] = (bn.y1 && nc < N) ? bn.mean1[nc + e] : 0.f;
         s1[e] = 0.f; s2[e] = 0.f; t2[e] = 0.f;
+        ma0[e] = (aff && nc < N) ? bn.msc0[nc + e] : 0.f;
+        mb0[e] = (aff && nc < N) ? bn.msh0[nc + e] : 0.f;
+        ma1[e] = (aff1 && nc < N) ? bn.msc1[nc + e] : 0.f;
+        mb1[e] = (aff1 && nc < N) ? bn.msh1[nc + e] : 0.f;
       }
     }
     const bool dense = kDense && (bias || act || dact);
@@ -520,11 +530,25 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
 #pragma unroll
             for (int e = 0; e < 8; ++e) a[e] += b[e];
           }
-          if constexpr (!kDense) if (has_mask) {
-            float z[8];
-            unpack8(zz[u], z);
+          if constexpr (!kDense) {
+            if (has_mask) {
+              float z[8];
+              unpack8(zz[u], z);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) a[e] = z[e] > 0.f ? a[e] : 0.f;
+              for (int e = 0; e < 8; ++e) a[e] = z[e] > 0.f ? a[e] : 0.f;
+            } else if (aff) {  // z > 0 recomputed from the pre-BN value(s)
+              float y[8], q[8];
+              unpack8(p0[u], y);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) q[e] = y[e] * ma0[e] + mb0[e];
+              if (aff1) {
+                unpack8(p1[u], y);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) q[e] += y[e] * ma1[e] + mb1[e];
+              }
+#pragma unroll
+              for (int e = 0; e < 8; ++e) a[e] = q[e] > 0.f ? a[e] : 0.f;
+            }
           }
           v = pack8(a);
           if constexpr (!kDense) if (red) {
@@ -902,8 +926,9 @@ MLC_EXPORT int mlc_conv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, f
 // dx[N,H,W,C] = conv_transpose(dy[N,Ho,Wo,Co], w) (+ addend, same layout as dx; may
 // alias dx) -- the addend fuses the gradient sum at a residual branch point.
 // bn_y0 != null additionally fuses the backward reduction of the BatchNorm(s) whose
-// output gradient dx is (see BnBwdEpi): dx is stored masked by bn_mask > 0 and the
-// partial sums go to bn_sums{0,1}[NSTAT][2][C] (zeroed by the caller).
+// output gradient dx is (see BnBwdEpi): dx is stored masked by bn_mask > 0 (or by the
+// mask recomputed from bn_y0/bn_y1 with bn_msc/bn_msh) and the partial sums go to
+// bn_sums{0,1}[NSTAT][2][C] (zeroed by the caller).
 // A strided conv runs one GEMM per stride-parity class of dx (only the filter taps that
 // reach the class are in its K loop; a class no tap reaches gets K = 0), so every dx row
 // is written by a GEMM epilogue and no structurally-zero products are computed.
@@ -911,10 +936,14 @@ MLC_EXPORT int mlc_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, const bf1
                               int H, int W, int C, int Co, int KH, int KW, int stride, int pad,
                               int dil, int Ho, int Wo, const bf16* bn_mask, const bf16* bn_y0,
                               const float* bn_mean0, float* bn_sums0, const bf16* bn_y1,
-                              const float* bn_mean1, float* bn_sums1, hipStream_t st) {
+                              const float* bn_mean1, float* bn_sums1, const float* bn_msc0,
+                              const float* bn_msh0, const float* bn_msc1, const float* bn_msh1,
+                              hipStream_t st) {
   if (C % 8 || Co % 8 || KH > 15 || KW > 16 || stride < 1) return -1;
   const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
-  BnBwdEpi bn{bn_mask, bn_y0, bn_mean0, bn_sums0, bn_y1, bn_mean1, bn_sums1};
+  BnBwdEpi bn{bn_mask, bn_y0, bn_mean0, bn_sums0, bn_y1, bn_mean1, bn_sums1,
+              bn_msc0, bn_msh0, bn_msc1, bn_msh1};
+  if (bn_msc0 && (!bn_msh0 || !bn_y0 || (bn_msc1 && (!bn_msh1 || !bn_y1)))) return -1;
   if (bn_y0 && (!bn_mean0 || !bn_sums0 || (bn_y1 && (!bn_mean1 || !bn_sums1)))) return -1;
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
     const DgradClass cl = mkclass(1, 0, 0, H, W, Ho, Wo, Co, 1, 1, 0, dil);

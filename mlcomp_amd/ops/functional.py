@@ -64,12 +64,16 @@ class BnBwdSpec:
     """Backward reduction of up to two BatchNorms fused into a dgrad epilogue: the dgrad
     output is their (shared) output gradient dU.  ``mask`` (the BN output z, or None)
     applies the ReLU; ``ys`` = [(y, mean, sums)] with ``sums`` the NSTAT*2*C scratch
-    :func:`bn_bwd` later consumes with ``prereduced=True``."""
+    :func:`bn_bwd` later consumes with ``prereduced=True``.  ``affine`` = [(scale,
+    shift)] per y recomputes the ReLU mask as  sum_k y_k*scale_k + shift_k > 0  instead
+    of reading z (valid when z = relu(that sum), i.e. no residual tensor input)."""
 
-    def __init__(self, mask, ys):
+    def __init__(self, mask, ys, affine=None):
         assert 1 <= len(ys) <= 2
+        assert affine is None or (mask is None and len(affine) == len(ys))
         self.mask = mask
         self.ys = list(ys)
+        self.affine = list(affine) if affine is not None else None
 
 
 def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=1, pad=0, dil=1,
@@ -83,11 +87,13 @@ def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=1, pad=0, di
     _, Ho, Wo, _ = dy.shape
     if _cuda(dy):
         dx = out if out is not None else torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
-        b = [None] * 7
+        b = [None] * 11
         if bn is not None:
             b[0] = bn.mask
             for k, (yk, mk, sk) in enumerate(bn.ys):
                 b[1 + 3 * k:4 + 3 * k] = [yk, mk, sk]
+            for k, (ak, hk) in enumerate(bn.affine or []):
+                b[7 + 2 * k:9 + 2 * k] = [ak, hk]
         _lib.call('mlc_conv_dgrad', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(dx), _lib.ptr(addend), N, H, W, C,
                   Co, KH, KW, stride, pad, dil, Ho, Wo, *[_lib.ptr(t) for t in b], _lib.stream())
         return dx
@@ -99,6 +105,9 @@ def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=1, pad=0, di
     if bn is not None:
         if bn.mask is not None:
             dxf = dxf * (bn.mask.float() > 0)
+        elif bn.affine is not None:
+            q = sum(yk.float() * ak + hk for (yk, _, _), (ak, hk) in zip(bn.ys, bn.affine))
+            dxf = dxf * (q > 0)
         d = dxf.to(torch.bfloat16).float().reshape(-1, C)
         for yk, mk, sk in bn.ys:
             sv = sk.view(NSTAT, 2, C)

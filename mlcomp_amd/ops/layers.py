@@ -226,9 +226,16 @@ class ResidualBlock:
         return _ResidualBlockFn.apply(x, self.ctx.anchor, self)
 
     def output_bn_spec(self):
-        """BnBwdSpec for the gradient of this block's output (used by the next block)."""
+        """BnBwdSpec for the gradient of this block's output (used by the next block).
+        With a downsample branch the output is relu(bn3(y3) + bn_d(y_d)), so the ReLU
+        mask is recomputed from the two pre-BN tensors the reduction reads anyway."""
         rec, rd = self._last
-        ys = [self.units[-1].bn_target(rec)]
+        last = self.units[-1]
+        ys = [last.bn_target(rec)]
+        if self.down is not None and not self.down.act:
+            ys.append(self.down.bn_target(rd))
+            return Fn.BnBwdSpec(None, ys, affine=[(last.scale, last.shift),
+                                                  (self.down.scale, self.down.shift)])
         if self.down is not None:
             ys.append(self.down.bn_target(rd))
         return Fn.BnBwdSpec(rec[2], ys)
@@ -276,7 +283,9 @@ class _ResidualBlockFn(torch.autograd.Function):
             u = units[i]
             if not fuse or not units[i + 1].dgrad_covers_all():
                 return None
-            return Fn.BnBwdSpec(recs[i][2] if u.act else None, [u.bn_target(recs[i])])
+            if u.act:   # z = relu(y*scale + shift): mask recomputed from y, z not read
+                return Fn.BnBwdSpec(None, [u.bn_target(recs[i])], affine=[(u.scale, u.shift)])
+            return Fn.BnBwdSpec(None, [u.bn_target(recs[i])])
 
         # last unit: its dres is the shortcut-branch gradient
         sp = spec_for(len(units) - 2) if len(units) > 1 else None

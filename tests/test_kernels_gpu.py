@@ -235,13 +235,14 @@ def test_conv_dgrad_addend(case):
     assert rel_err(out, ref) < 1e-2
 
 
+@pytest.mark.parametrize('aff', [False, True])
 @pytest.mark.parametrize('case,two', [((2, 14, 14, 64, 64, 1, 1, 0), False),
                                       ((2, 14, 14, 64, 64, 1, 1, 0), True),
                                       ((2, 14, 14, 64, 128, 3, 1, 1), True),
                                       ((2, 16, 16, 64, 128, 3, 2, 1), False),
                                       ((2, 15, 13, 128, 64, 3, 2, 1), True),
                                       ((1, 7, 7, 2048, 512, 1, 1, 0), True)])
-def test_conv_dgrad_bn_epilogue(case, two):
+def test_conv_dgrad_bn_epilogue(case, two, aff):
     """Fused BN-backward reduction in the dgrad epilogue: masked dx and per-channel
     sums match the CPU reference (which reduces the same bf16-rounded values)."""
     N, H, W, C, Co, K, s, p = case
@@ -257,15 +258,23 @@ def test_conv_dgrad_bn_epilogue(case, two):
         t = lambda v: v.to(dev)  # noqa: E731
         sums = [torch.zeros(Fn.NSTAT * 2 * C, device=dev) for _ in range(2)]
         ys = [(t(y0), t(m0), sums[0])] + ([(t(y1), t(m1), sums[1])] if two else [])
-        spec = Fn.BnBwdSpec(t(z), ys)
+        if aff:   # ReLU mask recomputed from y0 (and y1) with per-channel affines
+            spec = Fn.BnBwdSpec(None, ys, affine=[(t(a0), t(h0))] + ([(t(a1), t(h1))] if two else []))
+        else:
+            spec = Fn.BnBwdSpec(t(z), ys)
         dx = Fn.conv2d_dgrad(t(dy), t(w), (N, H, W, C), s, p, addend=t(add), bn=spec)
         return dx, [x.view(Fn.NSTAT, 2, C).sum(0).cpu() for x in sums]
 
+    a0, h0, a1, h1 = torch.rand(C) + 0.5, torch.randn(C) * 0.2, torch.rand(C) + 0.5, torch.randn(C) * 0.2
     ref_dx, ref_s = run('cpu')
     dx, sg = run(DEV)
     torch.cuda.synchronize()
     assert rel_err(dx, ref_dx) < 1e-2
-    assert ((dx.cpu().float() != 0) <= (z.float() > 0)).all()    # masked
+    if aff:
+        q = y0.float() * a0 + h0 + ((y1.float() * a1 + h1) if two else 0)
+        assert ((dx.cpu().float() != 0) <= (q > 0)).all()
+    else:
+        assert ((dx.cpu().float() != 0) <= (z.float() > 0)).all()    # masked
     for k in range(2 if two else 1):
         assert rel_err(sg[k][0], ref_s[k][0]) < 2e-2, k
         assert rel_err(sg[k][1], ref_s[k][1]) < 2e-2, k
