@@ -23,7 +23,7 @@ from mlcomp_amd.train.optim import FusedAdam
 class NativeBertStep:
     def __init__(self, model_name='bert-base', batch=32, seq_len=128, device=None, world_size=1, use_graph=True,
                  num_labels=2, lr=2e-5, weight_decay=0.01, betas=(0.9, 0.999), eps=1e-6, seed=0, warmup_eager=2,
-                 torch_model=None, dropout: Optional[float] = None):
+                 torch_model=None, dropout: Optional[float] = None, comm=None):
         self.device = torch.device(device or 'cuda')
         torch.manual_seed(seed)
         kw = {'num_labels': num_labels}
@@ -33,7 +33,7 @@ class NativeBertStep:
         self.net = NativeBert(tm, self.device, batch, seq_len)
         self.net.ctx.grad_prezeroed = True
         self.world = world_size
-        self.comm = make_comm(self.device) if world_size > 1 else None
+        self.comm = comm if comm is not None else (make_comm(self.device) if world_size > 1 else None)
         self.bucketer = GradBucketer(self.net.arena, self.comm)
         self.bucketer.broadcast_params()
         self.opt = FusedAdam(self.net.arena, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, decoupled=True,

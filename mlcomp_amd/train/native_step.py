@@ -28,14 +28,17 @@ class NativeClassifierStep:
     def __init__(self, model_name='resnet50', batch=256, image_size=224, device=None,
                  world_size=1, use_graph=True, num_classes=1000, lr=0.1, momentum=0.9,
                  weight_decay=5e-5, nesterov=False, smoothing=0.0, seed=0, warmup_eager=2,
-                 torch_model=None, optimizer='SGD', betas=(0.9, 0.999), eps=1e-8):
+                 torch_model=None, optimizer='SGD', betas=(0.9, 0.999), eps=1e-8,
+                 comm=None):
         self.device = torch.device(device or 'cuda')
         torch.manual_seed(seed)
         tm = torch_model if torch_model is not None else build_model(model_name, num_classes=num_classes)
         self.net = NativeResNet(tm, self.device, smoothing=smoothing)
         self.net.ctx.grad_prezeroed = True
         self.world = world_size
-        self.comm = make_comm(self.device) if world_size > 1 else None
+        # comm: an explicit communicator (tests inject a 1-rank RCCL one to exercise
+        # bucketed all-reduce inside graph capture on a single GPU)
+        self.comm = comm if comm is not None else (make_comm(self.device) if world_size > 1 else None)
         self.bucketer = GradBucketer(self.net.arena, self.comm)
         self.bucketer.broadcast_params()
         if optimizer in ('Adam', 'AdamW'):
