@@ -365,7 +365,326 @@ int pick_maxc(int cols, K&& launch) {
   return -1;
 }
 
+// ------------------------------------------------------------------ fused attention
+// One workgroup per (batch, head), S/32 waves; wave w owns query rows 32w..32w+31.  Q, K, V
+// are read in place from the QKV projection output [B*S][3*E] (head h = columns h*64..),
+// the context is written straight into [B*S][E] and the backward writes dQ/dK/dV straight
+// into dQKV [B*S][3*E]: no head split / merge copies, no S x S tensor in HBM (the backward
+// recomputes P from the saved per-row log-sum-exp).
+//
+// Scores are computed transposed, S^T = K Q^T (v_mfma_f32_32x32x16_bf16: A = K rows,
+// B = Q rows, both K-contiguous fragments loaded from global), so each lane holds ONE
+// query's scores for half of the keys: the softmax row reductions are in-register plus a
+// single lane^32 exchange.  The probabilities then feed the next MFMA as its B operand
+// directly from the accumulator registers: in the 32x32 C layout lane half hh holds keys
+// 16s + {0..3, 8..11} + 4hh of a 16-key step, i.e. the natural key order with bits 2 and 3
+// swapped, so the A operand (V^T / K^T, read with ds_read_b64_tr_b16 from LDS) is staged
+// with its key rows permuted the same way (swap23).  Dropout masks reuse the counter hash
+// of the softmax kernel at the same element index ((b*H + h)*S + q)*S + key.
+namespace attn {
+constexpr int D = 64;  // head dim
+
+// [rows][64] / [rows][128] bf16 LDS images, 16-B chunks XOR-swizzled for tr16 column reads
+template <int W>
+__device__ __forceinline__ int img_off(int r, int c) {
+  if (W == 64) return r * 128 + ((c ^ (((r >> 1) & 1) << 2)) << 4);
+  return r * 256 + ((c ^ ((r & 3) << 2)) << 4);
+}
+__device__ __forceinline__ int swap23(int k) { return (k & ~12) | ((k >> 1) & 4) | ((k << 1) & 8); }
+
+// MFMA operand fragment (row/col base+(lane&31), k = k0 + 8*(lane>>5) + 0..7) read
+// transposed from a [k][W] image
+template <int W>
+__device__ __forceinline__ bf16x8 tr_frag(const char* lds, int base, int k0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = base + 16 * (g & 1) + 4 * p;
+  const int kr = k0 + 8 * (g >> 1);
+  const int a0 = img_off<W>(kr + q, col >> 3) + (col & 7) * 2;
+  const int a1 = img_off<W>(kr + 4 + q, col >> 3) + (col & 7) * 2;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(lds + a0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(lds + a1));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+// K-contiguous fragment of row `row` straight from global (ld elements per row)
+__device__ __forceinline__ bf16x8 g_frag(const bf16* base, int ld, int row, int s, int lane) {
+  return *reinterpret_cast<const bf16x8*>(base + (size_t)row * ld + 16 * s + 8 * (lane >> 5));
+}
+// accumulator registers 8s..8s+7 as a bf16 B fragment
+__device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) r[t] = (bf16)a[8 * s + t];
+  return r;
+}
+// copy a [rows][64] head slice (row stride ld) into an LDS image; rows permuted by swap23
+template <int ROWS, bool PERM>
+__device__ __forceinline__ void stage64(char* img, const bf16* src, int ld, int tid, int nthr) {
+  for (int c = tid; c < ROWS * 8; c += nthr) {
+    const int r = c >> 3, ch = c & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)r * ld + ch * 8);
+    *reinterpret_cast<uint4*>(img + img_off<64>(PERM ? swap23(r) : r, ch)) = v;
+  }
+}
+// store a transposed C tile pair: acc[j][r] = X[row][d = 32j + (r&3) + 8(r>>2) + 4hh] for
+// this lane's row, as 8-byte pieces
+__device__ __forceinline__ void store_rows(bf16* dst, const f32x16 (&acc)[2], int lane) {
+  const int hh = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float f[4] = {acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]};
+      store4(dst + 32 * j + 8 * g + 4 * hh, f);
+    }
+}
+__device__ __forceinline__ int key_of(int i, int r, int hh) { return 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh; }
+
+template <int S>
+__global__ void __launch_bounds__(2 * S)
+fwd_kernel(const bf16* __restrict__ qkv, const float* __restrict__ key_bias, bf16* __restrict__ out,
+           float* __restrict__ lse, int H, float scale, uint32_t thr, float inv_keep,
+           const uint32_t* __restrict__ seedp, uint32_t salt) {
+  constexpr int NKT = S / 32, NTH = 2 * S;
+  __shared__ __attribute__((aligned(16))) char smem[S * 128];   // V image, key rows swap23
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, l32 = lane & 31;
+  const int bh = blockIdx.x, b = bh / H, hd = bh - b * H;
+  const int E = H * D, ld = 3 * E;
+  const bf16* Qg = qkv + (size_t)b * S * ld + hd * D;
+  const bf16* Kg = Qg + E;
+  stage64<S, true>(smem, Qg + 2 * E, ld, tid, NTH);
+  const int q = 32 * w + l32;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = g_frag(Qg, ld, q, s, lane);
+  f32x16 acc[NKT];
+#pragma unroll
+  for (int i = 0; i < NKT; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(g_frag(Kg, ld, 32 * i + l32, s, lane), qf[s], acc[i], 0, 0, 0);
+  }
+  // softmax over this lane's query (keys split between lane and lane^32)
+  const float* kb = key_bias ? key_bias + (size_t)b * S : nullptr;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NKT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float x = acc[i][r] * scale + (kb ? kb[key_of(i, r, hh)] : 0.f);
+      acc[i][r] = x;
+      mx = fmaxf(mx, x);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < NKT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = acc[i][r] == -INFINITY ? 0.f : __expf(acc[i][r] - mx);
+      acc[i][r] = e;
+      sum += e;
+    }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = sum > 0.f ? 1.f / sum : 0.f;
+  if (hh == 0) lse[(size_t)bh * S + q] = sum > 0.f ? mx + __logf(sum) : INFINITY;
+  const uint32_t seed = seedp ? *seedp : 0u;
+  const uint32_t rowidx = ((uint32_t)bh * S + q) * S;
+#pragma unroll
+  for (int i = 0; i < NKT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = acc[i][r] * inv;
+      acc[i][r] = (thr && !keep(seed, salt, rowidx + key_of(i, r, hh), thr)) ? 0.f : p * inv_keep;
+    }
+  __syncthreads();
+  // O^T = V^T Pd^T
+  f32x16 o[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[j][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < NKT; ++i)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 pb = acc_frag(acc[i], s);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        o[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<64>(smem, 32 * j, 32 * i + 16 * s, lane), pb, o[j], 0,
+                                                       0, 0);
+    }
+  store_rows(out + ((size_t)b * S + q) * E + hd * D, o, lane);
+}
+
+template <int S>
+__global__ void __launch_bounds__(2 * S)
+bwd_kernel(const bf16* __restrict__ qkv, const float* __restrict__ key_bias, const bf16* __restrict__ dout,
+           const float* __restrict__ lse, bf16* __restrict__ dqkv, int H, float scale, uint32_t thr, float inv_keep,
+           const uint32_t* __restrict__ seedp, uint32_t salt) {
+  constexpr int NKT = S / 32, NTH = 2 * S, IMG = S * 128;
+  // K (key rows swap23), Q, dO images [*][64]; Pd, dS images [q][key]
+  __shared__ __attribute__((aligned(16))) char smem[3 * IMG + 2 * S * S * 2];
+  char* Ki = smem;
+  char* Qi = smem + IMG;
+  char* Oi = smem + 2 * IMG;
+  char* Pi = smem + 3 * IMG;
+  char* Si = Pi + S * S * 2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, l32 = lane & 31;
+  const int bh = blockIdx.x, b = bh / H, hd = bh - b * H;
+  const int E = H * D, ld = 3 * E;
+  const bf16* Qg = qkv + (size_t)b * S * ld + hd * D;
+  const bf16* Kg = Qg + E;
+  const bf16* Vg = Qg + 2 * E;
+  const bf16* dOg = dout + (size_t)b * S * E + hd * D;
+  bf16* dQg = dqkv + (size_t)b * S * ld + hd * D;
+  stage64<S, true>(Ki, Kg, ld, tid, NTH);
+  stage64<S, false>(Qi, Qg, ld, tid, NTH);
+  stage64<S, false>(Oi, dOg, E, tid, NTH);
+  const int q = 32 * w + l32;
+  // recompute S^T and dPd^T = V dO^T
+  f32x16 sp[NKT], dp[NKT];
+  {
+    bf16x8 qf[4], of[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = g_frag(Qg, ld, q, s, lane);
+      of[s] = g_frag(dOg, E, q, s, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < NKT; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sp[i][r] = 0.f; dp[i][r] = 0.f; }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sp[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(g_frag(Kg, ld, 32 * i + l32, s, lane), qf[s], sp[i], 0, 0, 0);
+        dp[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(g_frag(Vg, ld, 32 * i + l32, s, lane), of[s], dp[i], 0, 0, 0);
+      }
+    }
+  }
+  const float* kb = key_bias ? key_bias + (size_t)b * S : nullptr;
+  const float l = lse[(size_t)bh * S + q];
+  const uint32_t seed = seedp ? *seedp : 0u;
+  const uint32_t rowidx = ((uint32_t)bh * S + q) * S;
+  float dot = 0.f;
+  uint64_t kept = 0;   // dropout keep bit of register (i, r) at bit 16i + r
+#pragma unroll
+  for (int i = 0; i < NKT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = key_of(i, r, hh);
+      const float x = sp[i][r] * scale + (kb ? kb[key] : 0.f);
+      const float p = x == -INFINITY ? 0.f : __expf(x - l);
+      const bool kp = !thr || keep(seed, salt, rowidx + key, thr);
+      kept |= (uint64_t)kp << (16 * i + r);
+      const float d = kp ? dp[i][r] * inv_keep : 0.f;    // dP
+      sp[i][r] = p;
+      dp[i][r] = d;
+      dot += p * d;
+    }
+  dot += __shfl_xor(dot, 32, 64);
+  // Pd and dS into registers (sp, dp) and into the [q][key] images for dK / dV
+#pragma unroll
+  for (int i = 0; i < NKT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const bool kp = (kept >> (16 * i + r)) & 1;
+      const float p = sp[i][r];
+      dp[i][r] = scale * p * (dp[i][r] - dot);
+      sp[i][r] = kp ? p * inv_keep : 0.f;
+    }
+#pragma unroll
+  for (int i = 0; i < NKT; ++i)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int key0 = 32 * i + 8 * g + 4 * hh;
+      const int off = img_off<S>(q, key0 >> 3) + (key0 & 7) * 2;
+      float f[4] = {sp[i][4 * g], sp[i][4 * g + 1], sp[i][4 * g + 2], sp[i][4 * g + 3]};
+      float e[4] = {dp[i][4 * g], dp[i][4 * g + 1], dp[i][4 * g + 2], dp[i][4 * g + 3]};
+      store4(reinterpret_cast<bf16*>(Pi + off), f);
+      store4(reinterpret_cast<bf16*>(Si + off), e);
+    }
+  __syncthreads();
+  // dQ^T = K^T dS^T  (dS^T straight from registers)
+  {
+    f32x16 dq[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dq[j][r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < NKT; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 sb = acc_frag(dp[i], s);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          dq[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<64>(Ki, 32 * j, 32 * i + 16 * s, lane), sb, dq[j], 0,
+                                                          0, 0);
+      }
+    store_rows(dQg + (size_t)q * ld, dq, lane);
+  }
+  // dV^T = dO^T Pd and dK^T = Q^T dS for this wave's 32 keys, summed over all queries
+  f32x16 dv[2], dk[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dv[j][r] = 0.f; dk[j][r] = 0.f; }
+#pragma unroll
+  for (int s = 0; s < S / 16; ++s) {
+    const bf16x8 pb = tr_frag<S>(Pi, 32 * w, 16 * s, lane);
+    const bf16x8 sb = tr_frag<S>(Si, 32 * w, 16 * s, lane);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      dv[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<64>(Oi, 32 * j, 16 * s, lane), pb, dv[j], 0, 0, 0);
+      dk[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<64>(Qi, 32 * j, 16 * s, lane), sb, dk[j], 0, 0, 0);
+    }
+  }
+  const int key = 32 * w + l32;
+  store_rows(dQg + (size_t)key * ld + E, dk, lane);
+  store_rows(dQg + (size_t)key * ld + 2 * E, dv, lane);
+}
+}  // namespace attn
+
 }  // namespace
+
+// Fused multi-head attention (head dim 64, S in {64, 128}).  qkv [B*S][3*H*64] bf16;
+// key_bias [B][S] fp32 (0 / -inf) or null; out [B*S][H*64]; lse [B*H*S] fp32 (saved for
+// the backward).  Attention-probability dropout p with the softmax kernel's mask indexing.
+MLC_EXPORT int mlc_attn_fwd(const bf16* qkv, const float* key_bias, bf16* out, float* lse, int B, int S, int H,
+                            float scale, float p, const uint32_t* seed, uint32_t salt, hipStream_t st) {
+  const uint32_t t = p > 0.f ? drop_threshold(p) : 0u;
+  const float k = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  if (S == 128)
+    hipLaunchKernelGGL(attn::fwd_kernel<128>, dim3(B * H), dim3(256), 0, st, qkv, key_bias, out, lse, H, scale, t, k,
+                       seed, salt);
+  else if (S == 64)
+    hipLaunchKernelGGL(attn::fwd_kernel<64>, dim3(B * H), dim3(128), 0, st, qkv, key_bias, out, lse, H, scale, t, k,
+                       seed, salt);
+  else
+    return -1;
+  return hipGetLastError();
+}
+
+// dqkv [B*S][3*H*64] is fully overwritten (dQ | dK | dV)
+MLC_EXPORT int mlc_attn_bwd(const bf16* qkv, const float* key_bias, const bf16* dout, const float* lse, bf16* dqkv,
+                            int B, int S, int H, float scale, float p, const uint32_t* seed, uint32_t salt,
+                            hipStream_t st) {
+  const uint32_t t = p > 0.f ? drop_threshold(p) : 0u;
+  const float k = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  if (S == 128)
+    hipLaunchKernelGGL(attn::bwd_kernel<128>, dim3(B * H), dim3(256), 0, st, qkv, key_bias, dout, lse, dqkv, H, scale,
+                       t, k, seed, salt);
+  else if (S == 64)
+    hipLaunchKernelGGL(attn::bwd_kernel<64>, dim3(B * H), dim3(128), 0, st, qkv, key_bias, dout, lse, dqkv, H, scale,
+                       t, k, seed, salt);
+  else
+    return -1;
+  return hipGetLastError();
+}
 
 // y = dropout_out(LN(x + dropout_in(r)) * gamma + beta); s_out = x + dropout_in(r) when r
 // is given (needed by the backward); mean/rstd [T].  H % 4 == 0, H <= 2048.

@@ -1,9 +1,11 @@
 """BERT on the native kernels: every dense layer is the MFMA GEMM with a fused
 bias / exact-GELU epilogue (pre-activation kept for backward), the GELU derivative and
 the residual-gradient sum are fused into the dgrad epilogues, LayerNorm is one kernel
-fused with the residual add and hidden dropout, attention softmax is one kernel fused
-with scale + key mask + attention dropout; the QK^T and PV batched products go to the
-library batched GEMM (``torch.bmm`` -> hipBLASLt).
+fused with the residual add and hidden dropout, and attention (QK^T, scale + key mask,
+softmax, attention dropout, PV; backward recomputing P from the saved log-sum-exp) is one
+MFMA kernel per direction that reads Q/K/V in place from the QKV projection and writes
+dQ/dK/dV straight into its gradient (``Tx.attn_fwd`` / ``Tx.attn_bwd``, head dim 64,
+S in {64, 128}); other shapes fall back to library batched GEMMs around the softmax kernel.
 
 Parameters live in the flat arenas (``ops.arena``): matmul weights and embedding tables
 in the decay arena (bf16 mirror for the kernels), biases and LayerNorm affine in the
@@ -100,12 +102,19 @@ class NativeBertLayer:
         B, S, nh, dh = net.B, net.S, net.c.heads, net.c.head_dim
         pa, ph = net.p_attn, net.p_hidden
         qkv, _ = self.qkv.fwd(x)
-        q, k, v = qkv.view(B, S, 3, nh, dh).permute(2, 0, 3, 1, 4).reshape(3, B * nh, S, dh).unbind(0)
-        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
-        scores = torch.bmm(q, k.transpose(1, 2))
-        P, Pd = Tx.softmax_fwd(scores.view(-1, S), key_bias, nh * S, 1.0 / math.sqrt(dh), pa, net.seed, self.salt)
-        ctxv = torch.bmm(Pd.view(B * nh, S, S), v)
-        ctx2 = ctxv.view(B, nh, S, dh).transpose(1, 2).reshape(B * S, nh * dh)
+        if Tx.attn_supported(S, dh):
+            # fused attention: reads q/k/v in place, writes the merged-head context
+            ctx2, lse = Tx.attn_fwd(qkv, key_bias, B, S, nh, 1.0 / math.sqrt(dh), pa, net.seed, self.salt)
+            att = (qkv, lse)
+        else:
+            q, k, v = qkv.view(B, S, 3, nh, dh).permute(2, 0, 3, 1, 4).reshape(3, B * nh, S, dh).unbind(0)
+            q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+            scores = torch.bmm(q, k.transpose(1, 2))
+            P, Pd = Tx.softmax_fwd(scores.view(-1, S), key_bias, nh * S, 1.0 / math.sqrt(dh), pa, net.seed,
+                                   self.salt)
+            ctxv = torch.bmm(Pd.view(B * nh, S, S), v)
+            ctx2 = ctxv.view(B, nh, S, dh).transpose(1, 2).reshape(B * S, nh * dh)
+            att = (q, k, v, P, Pd)
         ao, _ = self.out.fwd(ctx2)
         h1, s1, m1, r1 = Tx.ln_fwd(x, ao, self.ln1.g.master, self.ln1.b.master, net.c.eps, p_in=ph,
                                    seed=net.seed, salt_in=self.salt + 1)
@@ -113,14 +122,16 @@ class NativeBertLayer:
         f, _ = self.ffn2.fwd(g)
         h2, s2, m2, r2 = Tx.ln_fwd(h1, f, self.ln2.g.master, self.ln2.b.master, net.c.eps, p_in=ph,
                                    seed=net.seed, salt_in=self.salt + 2)
-        return h2, (x, q, k, v, P, Pd, ctx2, s1, m1, r1, h1, u, g, s2, m2, r2)
+        return h2, (x, *att, ctx2, s1, m1, r1, h1, u, g, s2, m2, r2)
 
     def bwd(self, dh2, saved, key_bias):
         net = self.net
         ws = net.ctx.ws
         B, S, nh, dh = net.B, net.S, net.c.heads, net.c.head_dim
         pa, ph = net.p_attn, net.p_hidden
-        x, q, k, v, P, Pd, ctx2, s1, m1, r1, h1, u, g, s2, m2, r2 = saved
+        fused = Tx.attn_supported(S, dh)
+        x, att = saved[0], saved[1:3] if fused else saved[1:6]
+        ctx2, s1, m1, r1, h1, u, g, s2, m2, r2 = saved[len(att) + 1:]
         ds2, df = Tx.ln_bwd(dh2, s2, m2, r2, self.ln2.g.master, self.ln2.g.grad, self.ln2.b.grad,
                             ws[self.ln2.k_sums], p_in=ph, seed=net.seed, salt_in=self.salt + 2, want_dr=True)
         self.ln2.mark()
@@ -133,13 +144,18 @@ class NativeBertLayer:
         self.ln1.mark()
         self.out.bwd_params(dao, ctx2)
         dctx2 = Tx.dense_dgrad(dao, self.out.w.bf16)
-        dctx = dctx2.view(B, S, nh, dh).transpose(1, 2).reshape(B * nh, S, dh)
-        dPd = torch.bmm(dctx, v.transpose(1, 2))
-        dv = torch.bmm(Pd.view(B * nh, S, S).transpose(1, 2), dctx)
-        dS = Tx.softmax_bwd(P, dPd.view(-1, S), 1.0 / math.sqrt(dh), pa, net.seed, self.salt).view(B * nh, S, S)
-        dq = torch.bmm(dS, k)
-        dk = torch.bmm(dS.transpose(1, 2), q)
-        dqkv = torch.stack([dq, dk, dv]).view(3, B, nh, S, dh).permute(1, 3, 0, 2, 4).reshape(B * S, 3 * nh * dh)
+        if fused:
+            qkv, lse = att
+            dqkv = Tx.attn_bwd(qkv, key_bias, dctx2, lse, B, S, nh, 1.0 / math.sqrt(dh), pa, net.seed, self.salt)
+        else:
+            q, k, v, P, Pd = att
+            dctx = dctx2.view(B, S, nh, dh).transpose(1, 2).reshape(B * nh, S, dh)
+            dPd = torch.bmm(dctx, v.transpose(1, 2))
+            dv = torch.bmm(Pd.view(B * nh, S, S).transpose(1, 2), dctx)
+            dS = Tx.softmax_bwd(P, dPd.view(-1, S), 1.0 / math.sqrt(dh), pa, net.seed, self.salt).view(B * nh, S, S)
+            dq = torch.bmm(dS, k)
+            dk = torch.bmm(dS.transpose(1, 2), q)
+            dqkv = torch.stack([dq, dk, dv]).view(3, B, nh, S, dh).permute(1, 3, 0, 2, 4).reshape(B * S, 3 * nh * dh)
         self.qkv.bwd_params(dqkv, x)
         return Tx.dense_dgrad(dqkv, self.qkv.w.bf16, addend=ds1)
 

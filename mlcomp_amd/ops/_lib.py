@@ -29,6 +29,8 @@ _SIGS = {
     'mlc_ln_bwd': [vp] * 10 + [i32, i32, f32, f32, vp, u32, u32, vp],
     'mlc_softmax_fwd': [vp] * 4 + [i64, i32, i32, f32, f32, vp, u32, vp],
     'mlc_softmax_bwd': [vp] * 3 + [i64, i32, f32, f32, vp, u32, vp],
+    'mlc_attn_fwd': [vp] * 4 + [i32, i32, i32, f32, f32, vp, u32, vp],
+    'mlc_attn_bwd': [vp] * 5 + [i32, i32, i32, f32, f32, vp, u32, vp],
     'mlc_colsum_acc': [vp, vp, vp, i32, i32, vp],
     'mlc_dropout': [vp, vp, i64, f32, vp, u32, vp],
     'mlc_bn_stat_copies': [],

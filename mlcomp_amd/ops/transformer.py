@@ -145,6 +145,72 @@ def softmax_bwd(P, dPd, scale, p=0.0, seed=None, salt=0):
     return (scale * Pf * (d - dot)).to(torch.bfloat16)
 
 
+# ---------------------------------------------------------------------------- fused attention
+def attn_supported(S: int, head_dim: int) -> bool:
+    """Shapes the fused attention kernels take (``mlc_attn_fwd`` / ``mlc_attn_bwd``)."""
+    return head_dim == 64 and S in (64, 128)
+
+
+def _attn_ref_probs(qkv, key_bias, B, S, H, scale):
+    E = H * 64
+    q, k, v = qkv.float().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4).unbind(0)   # [B, H, S, 64]
+    x = torch.matmul(q, k.transpose(-1, -2)) * scale
+    if key_bias is not None:
+        x = x + key_bias.float()[:, None, None, :]
+    P = torch.softmax(x, -1).nan_to_num(0.0)
+    return q, k, v, P, E
+
+
+def attn_fwd(qkv, key_bias, B, S, H, scale, p=0.0, seed=None, salt=0):
+    """Fused multi-head attention over the QKV projection output ``qkv`` [B*S, 3*H*64]
+    (columns q | k | v, head h at h*64).  Returns (ctx [B*S, H*64] bf16, lse [B*H*S] fp32).
+    Attention-probability dropout uses the softmax kernel's mask indexing
+    (((b*H + h)*S + q)*S + key), so both paths drop the same elements."""
+    if _cuda(qkv):
+        assert attn_supported(S, 64) and qkv.is_contiguous() and tuple(qkv.shape) == (B * S, 3 * H * 64)
+        assert key_bias is None or (key_bias.is_contiguous() and tuple(key_bias.shape) == (B, S))
+        ctx = torch.empty(B * S, H * 64, device=qkv.device, dtype=torch.bfloat16)
+        lse = torch.empty(B * H * S, device=qkv.device, dtype=torch.float32)
+        _lib.call('mlc_attn_fwd', _lib.ptr(qkv), _lib.ptr(key_bias), _lib.ptr(ctx), _lib.ptr(lse), B, S, H,
+                  float(scale), float(p), _lib.ptr(seed), salt, _lib.stream())
+        return ctx, lse
+    q, k, v, P, E = _attn_ref_probs(qkv, key_bias, B, S, H, scale)
+    Pd = P
+    if p > 0:
+        m = keep_mask((B, H, S, S), p, _seed_val(seed), salt)
+        Pd = torch.where(m, P / (1 - p), torch.zeros_like(P))
+    ctx = torch.matmul(Pd, v).permute(0, 2, 1, 3).reshape(B * S, E)
+    x = torch.matmul(q, k.transpose(-1, -2)) * scale
+    if key_bias is not None:
+        x = x + key_bias.float()[:, None, None, :]
+    lse = torch.logsumexp(x, -1).reshape(-1)
+    return ctx.to(torch.bfloat16), lse
+
+
+def attn_bwd(qkv, key_bias, dctx, lse, B, S, H, scale, p=0.0, seed=None, salt=0):
+    """Gradient of :func:`attn_fwd` wrt ``qkv``: returns dqkv [B*S, 3*H*64] bf16."""
+    if _cuda(qkv):
+        assert attn_supported(S, 64) and qkv.is_contiguous() and tuple(qkv.shape) == (B * S, 3 * H * 64)
+        assert dctx.is_contiguous() and tuple(dctx.shape) == (B * S, H * 64) and lse.numel() == B * H * S
+        assert key_bias is None or (key_bias.is_contiguous() and tuple(key_bias.shape) == (B, S))
+        dqkv = torch.empty_like(qkv)
+        _lib.call('mlc_attn_bwd', _lib.ptr(qkv), _lib.ptr(key_bias), _lib.ptr(dctx), _lib.ptr(lse), _lib.ptr(dqkv),
+                  B, S, H, float(scale), float(p), _lib.ptr(seed), salt, _lib.stream())
+        return dqkv
+    q, k, v, P, E = _attn_ref_probs(qkv, key_bias, B, S, H, scale)
+    do = dctx.float().view(B, S, H, 64).permute(0, 2, 1, 3)
+    m = keep_mask((B, H, S, S), p, _seed_val(seed), salt) if p > 0 else None
+    Pd = torch.where(m, P / (1 - p), torch.zeros_like(P)) if m is not None else P
+    dv = torch.matmul(Pd.transpose(-1, -2), do)
+    dPd = torch.matmul(do, v.transpose(-1, -2))
+    dP = torch.where(m, dPd / (1 - p), torch.zeros_like(dPd)) if m is not None else dPd
+    dS = scale * P * (dP - (P * dP).sum(-1, keepdim=True))
+    dq = torch.matmul(dS, k)
+    dk = torch.matmul(dS.transpose(-1, -2), q)
+    dqkv = torch.stack([dq, dk, dv]).permute(1, 3, 0, 2, 4).reshape(B * S, 3 * E)
+    return dqkv.to(torch.bfloat16)
+
+
 # ---------------------------------------------------------------------------- dense layers
 _WS = {}
 _WS_OLD = []   # superseded buffers stay alive: a captured graph may still point at them

@@ -11,7 +11,7 @@ fatal() {  # rc -> 0 when it is safe to keep using the GPU
     case $1 in 0|1|2) return 0;; *) echo "step $2 ended with rc=$1: stopping"; exit $1;; esac
 }
 
-timeout -k 10 500 python -m pytest tests -m gpu -x -q > $OUT/pytest.log 2>&1; rc=$?
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1; rc=$?
 echo "pytest rc=$rc" >> $OUT/pytest.log; tail -3 $OUT/pytest.log; fatal $rc pytest
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?
 tail -1 $OUT/smoke.log; fatal $rc smoke

@@ -1,5 +1,8 @@
 """Native BERT engine on CPU (kernel entry points fall back to their fp32 references):
 gradients match the plain PyTorch BERT, dropout hash masks are reproducible."""
+import math
+
+import pytest
 import torch
 
 from mlcomp_amd.models import build_model
@@ -12,19 +15,20 @@ def _cos(a, b):
     return (a @ b / (a.norm() * b.norm() + 1e-12)).item()
 
 
-def test_native_bert_matches_torch_autograd():
+@pytest.mark.parametrize('S', [16, 64])     # 64: fused-attention path (head dim 64)
+def test_native_bert_matches_torch_autograd(S):
     torch.manual_seed(0)
     tm = build_model('bert-tiny', num_classes=3, hidden_dropout=0.0, attention_dropout=0.0)
     ref = build_model('bert-tiny', num_classes=3, hidden_dropout=0.0, attention_dropout=0.0)
     ref.load_state_dict(tm.state_dict())
-    B, S = 4, 16
+    B = 4
     net = NativeBert(tm, 'cpu', B, S)
     ids = torch.randint(0, 1024, (B, S))
     tt = torch.zeros(B, S, dtype=torch.long)
-    tt[:, 8:] = 1
+    tt[:, S // 2:] = 1
     y = torch.randint(0, 3, (B,))
     am = torch.ones(B, S, dtype=torch.long)
-    am[0, 12:] = 0                       # one padded sequence
+    am[0, S - 4:] = 0                      # one padded sequence
     kb = ref.key_bias(am)
     net.ctx.ws.zero()
     net.arena.zero_grad()
@@ -76,3 +80,28 @@ def test_native_bert_dropout_trains():
         opt.step()
         losses.append(l.item())
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize('p', [0.0, 0.1])
+def test_fused_attention_reference_matches_unfused_path(p):
+    """attn_fwd / attn_bwd (the fused kernels' reference) == bmm + softmax kernels path."""
+    torch.manual_seed(3)
+    B, S, H = 2, 64, 3
+    qkv = (torch.randn(B * S, 3 * H * 64) * 0.5).to(torch.bfloat16)
+    dctx = torch.randn(B * S, H * 64).to(torch.bfloat16)
+    kb = torch.zeros(B, S)
+    kb[1, 50:] = float('-inf')
+    seed, salt, scale = torch.tensor([9]), 5, 1.0 / math.sqrt(64)
+    ctx, lse = Tx.attn_fwd(qkv, kb, B, S, H, scale, p, seed, salt)
+    dqkv = Tx.attn_bwd(qkv, kb, dctx, lse, B, S, H, scale, p, seed, salt)
+    # unfused reference: autograd through the softmax-kernel references
+    x = qkv.float().requires_grad_(True)
+    q, k, v = x.view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4).reshape(3, B * H, S, 64).unbind(0)
+    sc = torch.bmm(q, k.transpose(1, 2)).reshape(-1, S) * scale + kb.repeat_interleave(H * S, 0)
+    P = torch.softmax(sc, 1)
+    if p > 0:
+        P = torch.where(Tx.keep_mask(P.shape, p, 9, salt), P / (1 - p), torch.zeros_like(P))
+    o = torch.bmm(P.view(B * H, S, S), v).view(B, H, S, 64).transpose(1, 2).reshape(B * S, H * 64)
+    o.backward(dctx.float())
+    assert (ctx.float() - o).abs().max().item() < 2e-2
+    assert _cos(dqkv, x.grad) > 0.999

@@ -87,6 +87,32 @@ def test_dense_epilogues(M, N, K):
     assert rel(o_g, o_r) < 1e-4
 
 
+@pytest.mark.parametrize('B,S,H,p,masked', [(2, 128, 3, 0.0, False), (3, 128, 12, 0.1, True),
+                                             (2, 64, 4, 0.1, True), (1, 64, 2, 0.0, False)])
+def test_fused_attention_fwd_bwd(B, S, H, p, masked):
+    import math
+    qkv = _bf(B * S, 3 * H * 64, seed=6, scale=0.7)
+    dctx = _bf(B * S, H * 64, seed=7)
+    kb = None
+    if masked:
+        kb = torch.zeros(B, S)
+        kb[0, S - 37:] = float('-inf')
+    seed = torch.tensor([13], dtype=torch.int32)
+    scale = 1.0 / math.sqrt(64)
+    ctx_r, lse_r = Tx.attn_fwd(qkv, kb, B, S, H, scale, p, seed, 21)
+    dq_r = Tx.attn_bwd(qkv, kb, dctx, lse_r, B, S, H, scale, p, seed, 21)
+    kbg = kb.to(DEV) if kb is not None else None
+    ctx_g, lse_g = Tx.attn_fwd(qkv.to(DEV), kbg, B, S, H, scale, p, seed.to(DEV), 21)
+    dq_g = Tx.attn_bwd(qkv.to(DEV), kbg, dctx.to(DEV), lse_g, B, S, H, scale, p, seed.to(DEV), 21)
+    torch.cuda.synchronize()
+    assert rel(ctx_g, ctx_r) < 1e-2
+    assert rel(lse_g, lse_r) < 1e-4
+    E = H * 64
+    for part in range(3):   # dQ, dK, dV separately
+        sl = slice(part * E, (part + 1) * E)
+        assert rel(dq_g[:, sl], dq_r[:, sl]) < 2e-2, part
+
+
 def test_dropout_kernel_matches_hash():
     x = _bf(1000, 64, seed=12)
     seed = torch.tensor([3], dtype=torch.int32)
