@@ -162,6 +162,48 @@ struct MatMC {  // [K][cols] row-major, ld elements per row
   }
 };
 
+// MatMC that also sums every column over the K rows it stages (A operand of a dense
+// weight gradient dW = dY^T X: the column sums of dY are the bias gradient).  The sums are
+// taken from the staged registers (after the loads landed, only for real K-tiles) and
+// flushed by the N-tile-0 blocks with one fp32 atomic per column per wave.
+template <int R>
+struct MatMCSum {
+  static constexpr bool KC = false, SUM = true;
+  const bf16* p; int ld, K, cols; float* colsum;
+  struct St { typename MatMC<R>::St b; float s[8]; };
+  __device__ MatMC<R> base() const { return MatMC<R>{p, ld, K, cols}; }
+  __device__ static int lds_off(int i, int tid) { return MatMC<R>::lds_off(i, tid); }
+  __device__ void init(St& st, int n0, int tid) const {
+    base().init(st.b, n0, tid);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) st.s[e] = 0.f;
+  }
+  __device__ void load(const St& st, int kt, int tid, uint4 (&v)[R / 32]) const { base().load(st.b, kt, tid, v); }
+  __device__ void accum(St& st, const uint4 (&v)[R / 32]) const {
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) {
+      float f[8];
+      unpack8(v[i], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) st.s[e] += f[e];
+    }
+  }
+  __device__ void finish(St& st, bool owner, int tid) const {
+    const int lane = tid & 63;
+#pragma unroll
+    for (int o = R / 8; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) st.s[e] += __shfl_xor(st.s[e], o, 64);
+    const int c = st.b.n0 + 8 * (tid % (R / 8));
+    if (owner && lane < R / 8 && c < cols) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(colsum + c + e, st.s[e]);
+    }
+  }
+};
+template <class L, class = void> struct HasSum { static constexpr bool value = false; };
+template <class L> struct HasSum<L, decltype((void)L::SUM)> { static constexpr bool value = L::SUM; };
+
 // Per-row tap mask: bit r (r < 15) = filter row r lands inside the input, bit 16+s =
 // filter column s does; a K chunk of tap (r, s) is loaded iff (mask & P) == P with
 // P = 1<<r | 1<<(16+s).  P = 1<<15 (never set) marks a chunk past K.
@@ -400,22 +442,22 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
   // dense-layer extras: out = act(acc + bias) (pre-activation stored to preact), or
   // out = acc * act'(dact) for the backward of an activation (act 1 = exact-erf GELU)
   const float* bias = nullptr; int act = 0; bf16* preact = nullptr; const bf16* dact = nullptr;
-  template <int BM, int BN>
-  __device__ void apply(f32x16 (&acc)[2][2], char* lds, int m0, int n0, int M, int N,
+  template <int BM, int BN, int MI, int NI>
+  __device__ void apply(f32x16 (&acc)[MI][NI], char* lds, int m0, int n0, int M, int N,
                         int wm, int wn, int lane, int tid) const {
     if (sum) {
       // copy slot spreads the per-channel atomics of different blocks over NSTAT rows
       const int slot = ((m0 / 64) + wm) & (NSTAT - 1);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NI; ++j) {
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int r = 0; r < 16; ++r) { const float v = acc[i][j][r]; s1 += v; s2 += v * v; }
         s1 += __shfl_xor(s1, 32, 64);
         s2 += __shfl_xor(s2, 32, 64);
-        const int n = n0 + wn * 64 + 32 * j + lane;
+        const int n = n0 + wn * 32 * NI + 32 * j + lane;
         if (lane < 32 && n < N) {
           atomicAdd(sum + (size_t)slot * N + n, s1);
           atomicAdd(sumsq + (size_t)slot * N + n, s2);
@@ -426,13 +468,13 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
     constexpr int RS = (BN + 8) * 2;
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NI; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          const int n = wn * 64 + 32 * j + (lane & 31);
+          const int m = wm * 32 * MI + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int n = wn * 32 * NI + 32 * j + (lane & 31);
           *reinterpret_cast<bf16*>(lds + m * RS + n * 2) = (bf16)acc[i][j][r];
         }
     __syncthreads();
@@ -473,7 +515,7 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
     constexpr int ITERS = BM / RPI;
     constexpr int U = ITERS < 4 ? ITERS : 4;
     const bool has_add = addend != nullptr, has_mask = red && bn.mask, has_y1 = red && bn.y1;
-#pragma unroll
+#pragma unroll 1
     for (int it0 = 0; it0 < ITERS; it0 += U) {
       constexpr int UB = kDense ? 1 : U;   // BN-reduction operands (conv dgrad only)
       constexpr int UD = kDense ? U : 1;   // activation-derivative operand (dense only)
@@ -604,19 +646,19 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
 
 struct EpiF32Slab {  // split-K partial tile -> slab blockIdx.z of ws ([splits][M][ld] fp32, plain stores)
   float* ws; int ld; size_t slab;
-  template <int BM, int BN>
-  __device__ void apply(f32x16 (&acc)[2][2], char*, int m0, int n0, int M, int N,
+  template <int BM, int BN, int MI, int NI>
+  __device__ void apply(f32x16 (&acc)[MI][NI], char*, int m0, int n0, int M, int N,
                         int wm, int wn, int lane, int) const {
     float* out = ws + (size_t)blockIdx.z * slab;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = n0 + wn * 64 + 32 * j + (lane & 31);
+      for (int j = 0; j < NI; ++j) {
+        const int n = n0 + wn * 32 * NI + 32 * j + (lane & 31);
         if (n >= N) continue;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int m = m0 + wm * 32 * MI + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           if (m < M) out[(size_t)m * ld + n] = acc[i][j][r];
         }
       }
@@ -625,18 +667,18 @@ struct EpiF32Slab {  // split-K partial tile -> slab blockIdx.z of ws ([splits][
 
 struct EpiF32Atomic {  // fp32 [M][ld] += (split-K partial sums)
   float* out; int ld;
-  template <int BM, int BN>
-  __device__ void apply(f32x16 (&acc)[2][2], char*, int m0, int n0, int M, int N,
+  template <int BM, int BN, int MI, int NI>
+  __device__ void apply(f32x16 (&acc)[MI][NI], char*, int m0, int n0, int M, int N,
                         int wm, int wn, int lane, int) const {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = n0 + wn * 64 + 32 * j + (lane & 31);
+      for (int j = 0; j < NI; ++j) {
+        const int n = n0 + wn * 32 * NI + 32 * j + (lane & 31);
         if (n >= N) continue;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int m = m0 + wm * 32 * MI + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           if (m < M) atomicAdd(out + (size_t)m * ld + n, acc[i][j][r]);
         }
       }
@@ -645,19 +687,19 @@ struct EpiF32Atomic {  // fp32 [M][ld] += (split-K partial sums)
 
 struct EpiF32 {  // fp32 [M][ld] = acc (+ bias[n]) (+= if accumulate)
   float* out; int ld; const float* bias; int accumulate;
-  template <int BM, int BN>
-  __device__ void apply(f32x16 (&acc)[2][2], char*, int m0, int n0, int M, int N,
+  template <int BM, int BN, int MI, int NI>
+  __device__ void apply(f32x16 (&acc)[MI][NI], char*, int m0, int n0, int M, int N,
                         int wm, int wn, int lane, int) const {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = n0 + wn * 64 + 32 * j + (lane & 31);
+      for (int j = 0; j < NI; ++j) {
+        const int n = n0 + wn * 32 * NI + 32 * j + (lane & 31);
         if (n >= N) continue;
         const float b = bias ? bias[n] : 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int m = m0 + wm * 32 * MI + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           if (m < M) {
             float* o = out + (size_t)m * ld + n;
             *o = (accumulate ? *o : 0.f) + acc[i][j][r] + b;
@@ -673,12 +715,23 @@ struct EpiF32 {  // fp32 [M][ld] = acc (+ bias[n]) (+= if accumulate)
 // are clamped to the final tile, so every iteration issues the same loads and the
 // compiler can wait for the older set with a counted vmcnt).  The body is unrolled twice
 // so each set's role is static (no runtime-indexed register arrays).
+// Block tile -> per-wave tile (MI x NI MFMA 32x32 sub-tiles, 4 waves) and occupancy.  The
+// 64x64 wave tile (2x2) reads one LDS fragment per MFMA; the 128x64 wave tile of the
+// 256x128 / 128x256 blocks reads 0.75 and halves the global->LDS bytes per MFMA, at one
+// block per CU (96 KB of double-buffered LDS).
+template <int BM, int BN> struct TileCfg {
+  static constexpr bool BIG = BM * BN > 128 * 128;
+  static constexpr int MI = (BIG && BM > BN) ? 4 : 2, NI = (BIG && BN > BM) ? 4 : 2;
+  static constexpr int OCC = BIG ? 1 : 2;
+};
+
 template <int BM, int BN, class LA, class LB, class EPI, int PF>
-__global__ void __launch_bounds__(NTHR, 2)
+__global__ void __launch_bounds__(NTHR, (TileCfg<BM, BN>::OCC))
 gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int ktiles_per_split) {
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int WN = BN / 64;
+  constexpr int MI = TileCfg<BM, BN>::MI, NI = TileCfg<BM, BN>::NI;
+  constexpr int WN = BN / (32 * NI);
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -699,11 +752,11 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
   const int kt0 = blockIdx.z * ktiles_per_split;
   const int nt = min(ktiles, kt0 + ktiles_per_split) - kt0;
 
-  f32x16 acc[2][2];
+  f32x16 acc[MI][NI];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NI; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -714,26 +767,32 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
   auto mfma_tile = [&](const char* As, const char* Bs) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      bf16x8 a0 = read_frag<LA::KC, BM>(As, wm * 64, s, lane);
-      bf16x8 a1 = read_frag<LA::KC, BM>(As, wm * 64 + 32, s, lane);
-      bf16x8 b0 = read_frag<LB::KC, BN>(Bs, wn * 64, s, lane);
-      bf16x8 b1 = read_frag<LB::KC, BN>(Bs, wn * 64 + 32, s, lane);
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+      bf16x8 a[MI], b[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = read_frag<LA::KC, BM>(As, wm * 32 * MI + 32 * i, s, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b[j] = read_frag<LB::KC, BN>(Bs, wn * 32 * NI + 32 * j, s, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
   };
-  auto stage = [&](char* buf, const uint4 (&ra)[BM / 32], const uint4 (&rb)[BN / 32]) {
+  // real: the tile is inside this split (PF=2 re-stages the clamped last tile)
+  auto stage = [&](char* buf, const uint4 (&ra)[BM / 32], const uint4 (&rb)[BN / 32], bool real) {
     store_stage<LA, BM>(buf, tid, ra);
     store_stage<LB, BN>(buf + A_BYTES, tid, rb);
+    if constexpr (HasSum<LA>::value) {
+      if (real) la.accum(sa, ra);
+    }
   };
   if (nt > 0) {
     if constexpr (PF == 1) {
       uint4 ra[BM / 32], rb[BN / 32];
       la.load(sa, kt0, tid, ra);
       lb.load(sb, kt0, tid, rb);
-      stage(smem, ra, rb);
+      stage(smem, ra, rb, true);
       __syncthreads();
       for (int t = 0; t < nt; ++t) {
         const char* cur = smem + (t & 1) * STAGE;
@@ -743,7 +802,7 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
           lb.load(sb, kt0 + t + 1, tid, rb);
         }
         mfma_tile(cur, cur + A_BYTES);
-        if (more) stage(smem + ((t + 1) & 1) * STAGE, ra, rb);
+        if (more) stage(smem + ((t + 1) & 1) * STAGE, ra, rb, true);
         __syncthreads();
       }
     } else {
@@ -753,27 +812,28 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
       lb.load(sb, kt0, tid, b0);
       la.load(sa, min(kt0 + 1, last), tid, a1);
       lb.load(sb, min(kt0 + 1, last), tid, b1);
-      stage(smem, a0, b0);
+      stage(smem, a0, b0, true);
       __syncthreads();
       for (int t = 0;; t += 2) {
         // compute t from buffer 0; set 1 (tile t+1) in flight; set 0 free
         la.load(sa, min(kt0 + t + 2, last), tid, a0);
         lb.load(sb, min(kt0 + t + 2, last), tid, b0);
         mfma_tile(smem, smem + A_BYTES);
-        stage(smem + STAGE, a1, b1);
+        stage(smem + STAGE, a1, b1, t + 1 < nt);
         __syncthreads();
         if (t + 1 >= nt) break;
         // compute t+1 from buffer 1; set 0 (tile t+2) in flight; set 1 free
         la.load(sa, min(kt0 + t + 3, last), tid, a1);
         lb.load(sb, min(kt0 + t + 3, last), tid, b1);
         mfma_tile(smem + STAGE, smem + STAGE + A_BYTES);
-        stage(smem, a0, b0);
+        stage(smem, a0, b0, t + 2 < nt);
         __syncthreads();
         if (t + 2 >= nt) break;
       }
     }
   }
-  epi.template apply<BM, BN>(acc, smem, m0, n0, M, N, wm, wn, lane, tid);
+  if constexpr (HasSum<LA>::value) la.finish(sa, tn == 0, tid);
+  epi.template apply<BM, BN, MI, NI>(acc, smem, m0, n0, M, N, wm, wn, lane, tid);
 }
 
 // K-tile prefetch depth of the main loop (1 = next tile, 2 = two tiles ahead, used for the
@@ -809,17 +869,28 @@ static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int 
   return hipGetLastError();
 }
 
-// tile shape: 0 = 128x128, 1 = 256x64 (narrow N), 2 = 64x256 (narrow M)
+// tile shape: 0 = 128x128, 1 = 256x64 (narrow N), 2 = 64x256 (narrow M), 3 = 256x128,
+// 4 = 128x256 (wide-wave tiles, used when they still give every CU a block)
+static int g_big_tiles = 0;
+static int g_big_min_blocks = 240;
+static inline int tile_bm(int tile) { return tile == 1 || tile == 3 ? 256 : tile == 2 ? 64 : 128; }
+static inline int tile_bn(int tile) { return tile == 1 ? 64 : tile == 2 || tile == 4 ? 256 : 128; }
 static int pick_tile(int M, int N) {
   if (N <= 64 && M > 64) return 1;
   if (M <= 64 && N > 64) return 2;
+  if (g_big_tiles) {
+    const long t3 = (long)((M + 255) / 256) * ((N + 127) / 128);
+    const long t4 = (long)((M + 127) / 128) * ((N + 255) / 256);
+    if (M >= N && t3 >= g_big_min_blocks) return 3;
+    if (N > M && t4 >= g_big_min_blocks) return 4;
+  }
   return 0;
 }
 
 // pick a split-K factor so a small-output / long-K GEMM still fills 256 CUs
 static int auto_splits(int M, int N, int K, int tile, int target = g_split_target) {
-  const int BMv = tile == 1 ? 256 : tile == 2 ? 64 : 128;
-  const int BNv = tile == 1 ? 64 : tile == 2 ? 256 : 128;
+  const int BMv = tile_bm(tile);
+  const int BNv = tile_bn(tile);
   const int tiles = ((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
   const int ktiles = (K + BK - 1) / BK;
   int s = 1;
@@ -876,6 +947,8 @@ static DgradClass mkclass(int S, int ph, int pw, int H, int W, int Ho, int Wo, i
   do {                                                                                         \
     if ((TILE) == 1) return launch<256, 64>(MKA(256), MKB(64), EPI, M, N, K, SPLITS, ST);      \
     if ((TILE) == 2) return launch<64, 256>(MKA(64), MKB(256), EPI, M, N, K, SPLITS, ST);      \
+    if ((TILE) == 3) return launch<256, 128>(MKA(256), MKB(128), EPI, M, N, K, SPLITS, ST);    \
+    if ((TILE) == 4) return launch<128, 256>(MKA(128), MKB(256), EPI, M, N, K, SPLITS, ST);    \
     return launch<128, 128>(MKA(128), MKB(128), EPI, M, N, K, SPLITS, ST);                     \
   } while (0)
 
@@ -892,10 +965,11 @@ MLC_EXPORT int mlc_gemm_config(int prefetch) {
 // value (-1: bad key)
 MLC_EXPORT int mlc_gemm_get_set(int key, int value) {
   int* k = key == 0 ? &igemm::g_prefetch : key == 1 ? &igemm::g_split_target
-          : key == 2 ? &igemm::g_split_target_mat : nullptr;
+          : key == 2 ? &igemm::g_split_target_mat : key == 3 ? &igemm::g_big_tiles
+          : key == 4 ? &igemm::g_big_min_blocks : nullptr;
   if (!k) return -1;
   const int old = *k;
-  if (value > 0) *k = value;
+  if (value >= 0 && (value > 0 || key == 3)) *k = value;
   return old;
 }
 
@@ -1096,6 +1170,37 @@ MLC_EXPORT int mlc_gemm_f32out(const bf16* A, const bf16* B, float* C, const flo
   MLC_TILE_DISPATCH(tile, M, N, K, 1, st, epi, GA_MC, GB_MC);
 }
 
+// Dense-layer weight + bias gradient in one GEMM: dW[M][N] += dY^T X (fp32 atomics,
+// split-K) and dbias[M] += column sums of dY, taken from dY's staged tiles.  dY [K][M]
+// (lda), X [K][N] (ldb), M % 8 == N % 8 == 0.
+// With a workspace (ws_floats >= splits*M*N, ldc == N) the split-K partial tiles go to fp32
+// slabs and one reduction pass adds their sum into dW; otherwise fp32 atomics into dW.
+MLC_EXPORT int mlc_linear_wgrad_bias(const bf16* A, const bf16* B, float* C, float* dbias, int M, int N, int K,
+                                     int lda, int ldb, int ldc, int splits, float* ws, long ws_floats,
+                                     hipStream_t st) {
+  if (K % 8 || lda % 8 || ldb % 8 || M % 8 || N % 8) return -1;
+  const int tile = pick_tile(M, N);
+  if (splits <= 0) splits = auto_splits(M, N, K, tile, g_split_target_mat);
+  const size_t slab = (size_t)M * N;
+#define GA_MCS(R) (MatMCSum<R>{A, lda, K, M, dbias})
+  if (ws && ldc == N && splits > 1 && (long)(splits * slab) <= ws_floats) {
+    const int ktiles = (K + BK - 1) / BK;
+    const int per = (ktiles + splits - 1) / splits;
+    splits = (ktiles + per - 1) / per;
+    EpiF32Slab epi{ws, N, slab};
+    const hipError_t e = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_MCS, GB_MC); }();
+    if (e != hipSuccess) return e;
+    const long n4 = (long)slab / 4;
+    long blocks = (n4 + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, C, n4, splits, n4, 1);
+    return hipGetLastError();
+  }
+  EpiF32Atomic epi{C, ldc};
+  MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_MCS, GB_MC);
+#undef GA_MCS
+}
+
 // bf16-output GEMM with a dense-layer epilogue: C = act(op(A) op(B) + bias) (pre-
 // activation to preact when given), or C = (op(A) op(B)) * act'(dact) (+ addend).
 
@@ -1105,6 +1210,8 @@ static hipError_t launch_tiles(int tile, int M, int N, int K, int splits, hipStr
                                FB fb) {
   if (tile == 1) return launch<256, 64>(fa.template make<256>(), fb.template make<64>(), epi, M, N, K, splits, st);
   if (tile == 2) return launch<64, 256>(fa.template make<64>(), fb.template make<256>(), epi, M, N, K, splits, st);
+  if (tile == 3) return launch<256, 128>(fa.template make<256>(), fb.template make<128>(), epi, M, N, K, splits, st);
+  if (tile == 4) return launch<128, 256>(fa.template make<128>(), fb.template make<256>(), epi, M, N, K, splits, st);
   return launch<128, 128>(fa.template make<128>(), fb.template make<128>(), epi, M, N, K, splits, st);
 }
 struct MkMatKC { const bf16* p; int ld, rows, K; template <int R> MatKC<R> make() const { return MatKC<R>{p, ld, rows, K}; } };
@@ -1115,20 +1222,23 @@ struct MkMatMC { const bf16* p; int ld, K, cols; template <int R> MatMC<R> make(
 #define GB_MC_F (MkMatMC{B, ldb, K, N})
 
 namespace {
-// Split-K finish for the dense GEMM: ws [M][N] fp32 holds the split-K sums (zero on
-// entry; re-zeroed here so the next call can reuse it), C = epilogue(ws) in bf16.
+// Split-K finish for the dense GEMM: ws holds `splits` fp32 slabs [splits][M][N] of
+// partial sums (written with plain stores by EpiF32Slab); C = epilogue(sum of slabs).
 __global__ void __launch_bounds__(256)
-dense_finalize_kernel(float* __restrict__ ws, bf16* __restrict__ C, int ldc, const float* __restrict__ bias,
-                      int act, bf16* __restrict__ preact, const bf16* __restrict__ addend,
-                      const bf16* __restrict__ dact, int M, int N) {
+dense_finalize_kernel(const float* __restrict__ ws, int splits, bf16* __restrict__ C, int ldc,
+                      const float* __restrict__ bias, int act, bf16* __restrict__ preact,
+                      const bf16* __restrict__ addend, const bf16* __restrict__ dact, int M, int N) {
   const long n8 = (long)M * (N / 8);
+  const size_t slab = (size_t)M * N;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
     const int m = (int)(i / (N / 8)), c = (int)(i % (N / 8)) * 8;
-    float4* w4 = reinterpret_cast<float4*>(ws + (size_t)m * N + c);
-    const float4 p = w4[0], q = w4[1];
-    w4[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-    w4[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-    float a[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < splits; ++k) {
+      const float4* w4 = reinterpret_cast<const float4*>(ws + k * slab + (size_t)m * N + c);
+      const float4 p = w4[0], q = w4[1];
+      a[0] += p.x; a[1] += p.y; a[2] += p.z; a[3] += p.w;
+      a[4] += q.x; a[5] += q.y; a[6] += q.z; a[7] += q.w;
+    }
     const size_t o = (size_t)m * ldc + c;
     if (bias) {
 #pragma unroll
@@ -1161,21 +1271,29 @@ dense_finalize_kernel(float* __restrict__ ws, bf16* __restrict__ C, int ldc, con
 
 // bf16-output GEMM with a dense-layer epilogue: C = act(op(A) op(B) + bias) (pre-
 // activation to preact when given), or C = (op(A) op(B)) * act'(dact) (+ addend).
-// ws (optional, M*N fp32, zero on entry and on exit): when the output has too few tiles
-// to fill the chip, the K reduction is split across workgroups into ws with fp32 atomics
-// and the epilogue runs in a finishing pass.
+// ws (optional, ws_floats fp32, any contents): when the output has too few tiles to fill
+// the chip, the K reduction is split across workgroups into per-split fp32 slabs of ws
+// (plain stores: ~4x cheaper than fp32 atomics into one buffer) and the epilogue runs in a
+// finishing pass that sums the slabs.
 MLC_EXPORT int mlc_gemm_bf16_ex(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int lda, int ldb,
                                 int ldc, int ta, int tb, const float* bias, int act, bf16* preact,
-                                const bf16* addend, const bf16* dact, float* ws, hipStream_t st) {
+                                const bf16* addend, const bf16* dact, float* ws, long ws_floats,
+                                hipStream_t st) {
   if (K % 8 || N % 8 || ldc % 8 || lda % 8 || ldb % 8 || (ta && M % 8)) return -1;
   const int tile = pick_tile(M, N);
-  const int BMv = tile == 1 ? 256 : tile == 2 ? 64 : 128, BNv = tile == 1 ? 64 : tile == 2 ? 256 : 128;
+  const int BMv = tile_bm(tile), BNv = tile_bn(tile);
   const int tiles = ((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
   const int ktiles = (K + BK - 1) / BK;
   int splits = 1;
-  if (ws) while (tiles * splits < 384 && ktiles / (splits * 2) >= 4) splits *= 2;
+  const long slab = (long)M * N;
+  if (ws)
+    while (tiles * splits < 384 && ktiles / (splits * 2) >= 4 && slab * splits * 2 <= ws_floats) splits *= 2;
   if (splits > 1) {
-    EpiF32Atomic epi{ws, N};
+    {  // the launch rounds splits so that no split is empty: finish exactly those slabs
+      const int per = (ktiles + splits - 1) / splits;
+      splits = (ktiles + per - 1) / per;
+    }
+    EpiF32Slab epi{ws, N, (size_t)slab};
     hipError_t e;
     if (!ta && tb) e = launch_tiles(tile, M, N, K, splits, st, epi, GA_KC_F, GB_KC_F);
     else if (!ta && !tb) e = launch_tiles(tile, M, N, K, splits, st, epi, GA_KC_F, GB_MC_F);
@@ -1184,8 +1302,8 @@ MLC_EXPORT int mlc_gemm_bf16_ex(const bf16* A, const bf16* B, bf16* C, int M, in
     if (e != hipSuccess) return e;
     long blocks = ((long)M * (N / 8) + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(dense_finalize_kernel, dim3(blocks), dim3(256), 0, st, ws, C, ldc, bias, act, preact,
-                       addend, dact, M, N);
+    hipLaunchKernelGGL(dense_finalize_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, C, ldc, bias, act,
+                       preact, addend, dact, M, N);
     return hipGetLastError();
   }
   EpiBF16<IdentityRows, true> epi{C, ldc, nullptr, nullptr, IdentityRows{}, addend};

@@ -50,8 +50,11 @@ class _Dense:
     def bwd_params(self, dy, x):
         """dW += dy^T x, db += colsum(dy) (straight into the grad arena)."""
         a = self.ctx.arena
-        Fn.linear_wgrad(dy, x, out=self.w.grad, accumulate=True)
-        Tx.colsum_acc(dy, self.b.grad)
+        if dy.shape[0] % 8 == 0 and dy.shape[1] % 8 == 0 and x.shape[1] % 8 == 0:
+            Fn.linear_wgrad_bias(dy, x, self.w.grad, self.b.grad)
+        else:
+            Fn.linear_wgrad(dy, x, out=self.w.grad, accumulate=True)
+            Tx.colsum_acc(dy, self.b.grad)
         a.mark_ready(self.w)
         a.mark_ready(self.b)
 

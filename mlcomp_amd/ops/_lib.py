@@ -24,11 +24,12 @@ _SIGS = {
     'mlc_conv_wgrad': [vp, vp, vp] + [i32] * 14 + [vp, i64, vp],
     'mlc_gemm_f32out': [vp, vp, vp, vp] + [i32] * 11 + [vp],
     'mlc_gemm_bf16out': [vp, vp, vp] + [i32] * 8 + [vp],
-    'mlc_gemm_bf16_ex': [vp, vp, vp] + [i32] * 8 + [vp, i32, vp, vp, vp, vp, vp],
+    'mlc_gemm_bf16_ex': [vp, vp, vp] + [i32] * 8 + [vp, i32, vp, vp, vp, vp, i64, vp],
     'mlc_ln_fwd': [vp] * 8 + [i32, i32, f32, f32, f32, vp, u32, u32, vp],
     'mlc_ln_bwd': [vp] * 10 + [i32, i32, f32, f32, vp, u32, u32, vp],
     'mlc_softmax_fwd': [vp] * 4 + [i64, i32, i32, f32, f32, vp, u32, vp],
     'mlc_softmax_bwd': [vp] * 3 + [i64, i32, f32, f32, vp, u32, vp],
+    'mlc_linear_wgrad_bias': [vp] * 4 + [i32] * 7 + [vp, i64, vp],
     'mlc_attn_fwd': [vp] * 4 + [i32, i32, i32, f32, f32, vp, u32, vp],
     'mlc_attn_bwd': [vp] * 5 + [i32, i32, i32, f32, f32, vp, u32, vp],
     'mlc_colsum_acc': [vp, vp, vp, i32, i32, vp],
@@ -88,6 +89,10 @@ def load():
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, C.c_int)
+        # A/B knobs of the GEMM engine (tile policy / min blocks for the wide-wave tiles)
+        for key, env in ((3, 'MLC_GEMM_BIG'), (4, 'MLC_GEMM_BIG_MIN')):
+            if os.environ.get(env):
+                lib.mlc_gemm_get_set(key, int(os.environ[env]))
         _LIB = lib
     return _LIB
 

@@ -405,6 +405,24 @@ def linear_wgrad(dout, x, out=None, accumulate=False):
     return g
 
 
+def linear_wgrad_bias(dout, x, dw, db):
+    """dW [O, I] += dout^T x and db [O] += colsum(dout) in ONE GEMM: the bias gradient is
+    summed from dout's tiles as the wgrad kernel stages them (``mlc_linear_wgrad_bias``)."""
+    B, O = dout.shape
+    I = x.shape[1]
+    if _cuda(dout):
+        assert dout.is_contiguous() and x.is_contiguous() and x.shape[0] == B
+        assert tuple(dw.shape) == (O, I) and dw.is_contiguous() and db.numel() == O
+        from .transformer import gemm_workspace
+        ws = gemm_workspace(dout.device, 8 * O * I)   # split-K slabs (<= 8 splits)
+        _lib.call('mlc_linear_wgrad_bias', _lib.ptr(dout), _lib.ptr(x), _lib.ptr(dw), _lib.ptr(db), O, I, B, O, I, I,
+                  0, _lib.ptr(ws), ws.numel(), _lib.stream())
+        return dw, db
+    dw.add_(dout.float().t() @ x.float())
+    db.add_(dout.float().sum(0))
+    return dw, db
+
+
 def colsum(g, out):
     R, Cc = g.shape
     if _cuda(g):

@@ -217,8 +217,9 @@ _WS_OLD = []   # superseded buffers stay alive: a captured graph may still point
 
 
 def gemm_workspace(device, n: int) -> torch.Tensor:
-    """Zeroed fp32 split-K workspace per device (the finishing kernel re-zeroes what it
-    used), grown on demand - first during eager warm-up, so graph capture reuses it."""
+    """fp32 split-K slab workspace per device (``splits`` x M x N partial sums, fully
+    overwritten by each split-K GEMM), grown on demand - first during eager warm-up, so
+    graph capture reuses it."""
     key = str(device)
     buf = _WS.get(key)
     if buf is None or buf.numel() < n:
@@ -246,8 +247,8 @@ def dense_fwd(x, w, bias=None, act: int = 0, want_preact: bool = False):
         y = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
         u = torch.empty_like(y) if want_preact else None
         _lib.call('mlc_gemm_bf16_ex', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), M, N, K, K, K, N, 0, 1,
-                  _lib.ptr(bias), act, _lib.ptr(u), None, None, _lib.ptr(gemm_workspace(x.device, M * N)),
-                  _lib.stream())
+                  _lib.ptr(bias), act, _lib.ptr(u), None, None, _lib.ptr(gemm_workspace(x.device, 4 * M * N)),
+                  4 * M * N, _lib.stream())
         return y, u
     z = x.float() @ w.float().t()
     if bias is not None:
@@ -265,8 +266,8 @@ def dense_dgrad(dy, w, dact_u=None, addend=None):
     if _cuda(dy):
         dx = torch.empty(M, K, device=dy.device, dtype=torch.bfloat16)
         _lib.call('mlc_gemm_bf16_ex', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(dx), M, K, N, N, K, K, 0, 0, None, 0,
-                  None, _lib.ptr(addend), _lib.ptr(dact_u), _lib.ptr(gemm_workspace(dy.device, M * K)),
-                  _lib.stream())
+                  None, _lib.ptr(addend), _lib.ptr(dact_u), _lib.ptr(gemm_workspace(dy.device, 4 * M * K)),
+                  4 * M * K, _lib.stream())
         return dx
     z = dy.float() @ w.float()
     z = z.to(torch.bfloat16).float()

@@ -40,12 +40,13 @@ def main():
         dy = torch.randn(M, N, device='cuda').to(torch.bfloat16)
         t_dgl = timeit(lambda: torch.matmul(dy, w))
         res = []
-        for pf in (1, 2):
-            _lib.load().mlc_gemm_config(pf)
+        lib = _lib.load()
+        for big in (0, 1):
+            old = lib.mlc_gemm_get_set(3, big)
             t_nat = timeit(lambda: Tx.dense_fwd(x, w, b))
             t_dg = timeit(lambda: Tx.dense_dgrad(dy, w))
-            res.append(f'pf{pf} fwd {fl / t_nat / 1e12:6.1f} dgrad {fl / t_dg / 1e12:6.1f}')
-        _lib.load().mlc_gemm_config(1)
+            lib.mlc_gemm_get_set(3, old)
+            res.append(f'big{big} fwd {fl / t_nat / 1e12:6.1f} dgrad {fl / t_dg / 1e12:6.1f}')
         print(f'{name:20s} M={M:7d} N={N:5d} K={K:5d} | lib fwd {fl / t_lib / 1e12:6.1f} dgrad '
               f'{fl / t_dgl / 1e12:6.1f} | ' + ' | '.join(res) + '  TF/s', flush=True)
 

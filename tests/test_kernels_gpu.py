@@ -14,6 +14,22 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 
 
+@pytest.fixture(params=[0, 1], ids=['tiles-std', 'tiles-wide'], autouse=True)
+def gemm_tiles(request):
+    """Run every GEMM-backed test with the standard 64x64-per-wave tiles and again with the
+    wide-wave 256x128 / 128x256 tiles forced on (min blocks 1)."""
+    from mlcomp_amd.ops import _lib
+    if not torch.cuda.is_available():
+        yield
+        return
+    lib = _lib.load()
+    old_big = lib.mlc_gemm_get_set(3, request.param)
+    old_min = lib.mlc_gemm_get_set(4, 1 if request.param else 240)
+    yield
+    lib.mlc_gemm_get_set(3, old_big)
+    lib.mlc_gemm_get_set(4, old_min)
+
+
 def rel_err(a, b):
     a = a.float().cpu()
     b = b.float().cpu()

@@ -10,6 +10,22 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 
 
+@pytest.fixture(params=[0, 1], ids=['tiles-std', 'tiles-wide'], autouse=True)
+def gemm_tiles(request):
+    """Run every GEMM-backed test with the standard 64x64-per-wave tiles and again with the
+    wide-wave 256x128 / 128x256 tiles forced on (min blocks 1)."""
+    from mlcomp_amd.ops import _lib
+    if not torch.cuda.is_available():
+        yield
+        return
+    lib = _lib.load()
+    old_big = lib.mlc_gemm_get_set(3, request.param)
+    old_min = lib.mlc_gemm_get_set(4, 1 if request.param else 240)
+    yield
+    lib.mlc_gemm_get_set(3, old_big)
+    lib.mlc_gemm_get_set(4, old_min)
+
+
 def rel(a, b):
     a, b = a.float().cpu(), b.float().cpu()
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
@@ -111,6 +127,20 @@ def test_fused_attention_fwd_bwd(B, S, H, p, masked):
     for part in range(3):   # dQ, dK, dV separately
         sl = slice(part * E, (part + 1) * E)
         assert rel(dq_g[:, sl], dq_r[:, sl]) < 2e-2, part
+
+
+@pytest.mark.parametrize('T,O,I', [(4096, 768, 2304), (4096, 3072, 768), (336, 64, 512), (1000, 512, 64),
+                                   (96, 8, 16)])
+def test_linear_wgrad_bias_fused(T, O, I):
+    from mlcomp_amd.ops import functional as Fn
+    dy, x = _bf(T, O, seed=8), _bf(T, I, seed=9)
+    dw0, db0 = torch.randn(O, I), torch.randn(O)
+    dw_g, db_g = dw0.to(DEV), db0.to(DEV)
+    Fn.linear_wgrad_bias(dy.to(DEV), x.to(DEV), dw_g, db_g)
+    torch.cuda.synchronize()
+    dw_r = dw0 + dy.float().t() @ x.float()
+    db_r = db0 + dy.float().sum(0)
+    assert rel(dw_g, dw_r) < 1e-3 and rel(db_g, db_r) < 1e-4
 
 
 def test_dropout_kernel_matches_hash():
