@@ -66,9 +66,18 @@ def main():
         dist.init_process_group('nccl', device_id=device)
 
     is_bert = args.model.startswith('bert')
+    is_unet = args.model.startswith('unet')
     if args.batch is None:
-        args.batch = 32 if is_bert else 256
-    if is_bert:
+        args.batch = 32 if (is_bert or is_unet) else 256
+    if is_unet:
+        # U-Net (BASELINE config 3): --model unet[-<encoder>], 256x256 unless --image-size
+        from mlcomp_amd.train.segment import build_seg_step
+        if args.image_size == 224:
+            args.image_size = 256
+        enc = args.model.split('-', 1)[1] if '-' in args.model else 'resnet34'
+        step = build_seg_step(enc, batch=args.batch, impl=args.impl, image_size=args.image_size, device=device,
+                              world_size=world, use_graph=(args.graph if args.graph >= 0 else None))
+    elif is_bert:
         from mlcomp_amd.train.bert import build_bert_step
         step = build_bert_step(args.model, batch=args.batch, seq_len=args.seq_len, impl=args.impl,
                                device=device, world_size=world,
@@ -114,6 +123,18 @@ def main():
             'config': {'model': args.model, 'global_batch': args.batch * world, 'per_gpu_batch': args.batch,
                        'seq_len': args.seq_len, 'parallelism': f'dp{world}', 'impl': args.impl,
                        'optimizer': 'AdamW lr 2e-5 wd 0.01, fp32 master weights', 'dropout': 0.1,
+                       'final_loss': loss}}
+        print(json.dumps(out), flush=True)
+    elif rank == 0 and is_unet:
+        out = {
+            'metric': 'images/sec (whole node) U-Net segmentation DAG train task',
+            'value': round(value, 2), 'unit': 'images/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'bf16',
+            'data': f'synthetic ({args.image_size}x{args.image_size}x3 images, blob masks, 1 class, random-init weights)',
+            'config': {'model': args.model, 'global_batch': args.batch * world, 'per_gpu_batch': args.batch,
+                       'image_size': args.image_size, 'parallelism': f'dp{world}', 'impl': args.impl,
+                       'optimizer': 'Adam lr 3e-4, fp32 master weights', 'loss': 'BCE + Dice',
                        'final_loss': loss}}
         print(json.dumps(out), flush=True)
     elif rank == 0:

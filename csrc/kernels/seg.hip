@@ -1,0 +1,248 @@
+// Segmentation-model kernels (U-Net decoder and head) for gfx950, NHWC bf16.
+//
+// * upcat: x2 nearest upsample of the decoder input fused with the channel concat of the
+//   encoder skip: out[n,y,x,:C1] = lo[n,y/2,x/2,:], out[n,y,x,C1:] = skip[n,y,x,:].  One
+//   16-byte chunk per thread, both sources and the destination read/written once.
+//   Backward: dlo = 2x2 sum-pool of dout[..., :C1] (fp32 accumulate), dskip = dout[..., C1:].
+// * seg head + BCE-with-logits + soft-Dice loss, classes = 1: the 1x1
+//   output conv (Cin -> 1, + bias) is a per-pixel dot product, so it is fused with the
+//   loss.  Forward: logit, sigmoid, and the four global sums the loss needs (BCE sum,
+//   sum s*t, sum s, sum t) reduced per block then one atomic each.  Backward (the Dice
+//   gradient needs the global sums, hence a second pass): dlogit, dx = dlogit * w, and
+//   dw / db block-reduced into the grad arena.
+//   loss = bce_w * mean(BCE) + dice_w * (1 - (2*I + eps) / (U + eps)),  I = sum s*t,
+//   U = sum s + sum t  (contrib/criterion.BCEDiceLoss).
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+__global__ void __launch_bounds__(NT)
+upcat_fwd_kernel(const bf16* __restrict__ lo, const bf16* __restrict__ skip, bf16* __restrict__ out, int N, int h,
+                 int w, int C1, int C2) {
+  const int H = 2 * h, W = 2 * w, C = C1 + C2, cpr = C / 8;
+  const long total = (long)N * H * W * cpr;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cpr);
+    const long p = i / cpr;                  // output pixel (n, y, x)
+    const int x = (int)(p % W);
+    const long t = p / W;
+    const int y = (int)(t % H);
+    const long n = t / H;
+    uint4 v;
+    if (c8 * 8 < C1) {
+      v = *reinterpret_cast<const uint4*>(lo + ((n * h + (y >> 1)) * w + (x >> 1)) * C1 + c8 * 8);
+    } else {
+      v = *reinterpret_cast<const uint4*>(skip + p * C2 + (c8 * 8 - C1));
+    }
+    *reinterpret_cast<uint4*>(out + p * C + c8 * 8) = v;
+  }
+}
+
+__global__ void __launch_bounds__(NT)
+upcat_bwd_lo_kernel(const bf16* __restrict__ dout, bf16* __restrict__ dlo, int N, int h, int w, int C1, int C) {
+  const int W = 2 * w, cpr = C1 / 8;
+  const long total = (long)N * h * w * cpr;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cpr);
+    const long q = i / cpr;                  // low-res pixel (n, yy, xx)
+    const int xx = (int)(q % w);
+    const long t = q / w;
+    const int yy = (int)(t % h);
+    const long n = t / h;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const long p = (n * 2 * h + 2 * yy + a) * W + 2 * xx + b;
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(dout + p * C + c8 * 8), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += f[e];
+      }
+    *reinterpret_cast<uint4*>(dlo + q * C1 + c8 * 8) = pack8(acc);
+  }
+}
+
+__global__ void __launch_bounds__(NT)
+upcat_bwd_skip_kernel(const bf16* __restrict__ dout, bf16* __restrict__ dskip, long P, int C1, int C2) {
+  const int C = C1 + C2, cpr = C2 / 8;
+  const long total = P * cpr;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cpr);
+    const long p = i / cpr;
+    *reinterpret_cast<uint4*>(dskip + p * C2 + c8 * 8) =
+        *reinterpret_cast<const uint4*>(dout + p * C + C1 + c8 * 8);
+  }
+}
+
+// block-wide sum of NV floats per thread; result valid in thread 0
+template <int NV>
+__device__ __forceinline__ void block_sum(float (&v)[NV], float* red) {
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) red[wave * NV + k] = v[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      float s = 0.f;
+      for (int q = 0; q < NT / 64; ++q) s += red[q * NV + k];
+      v[k] = s;
+    }
+  }
+}
+
+__device__ __forceinline__ float pixel_logit(const bf16* xp, const float* w, float b, int C) {
+  float z = b;
+  for (int c = 0; c < C; c += 8) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(xp + c), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) z += f[e] * w[c + e];
+  }
+  return z;
+}
+
+// sums[0..3] += (BCE sum, sum s*t, sum s, sum t)
+__global__ void __launch_bounds__(NT)
+seg_head_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+                    const float* __restrict__ target, float* __restrict__ logits, float* __restrict__ sums, long P,
+                    int C) {
+  __shared__ float red[NT / 64 * 4];
+  __shared__ float ws[256];
+  for (int c = threadIdx.x; c < C; c += NT) ws[c] = w[c];
+  __syncthreads();
+  const float b = bias[0];
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (long p = (long)blockIdx.x * NT + threadIdx.x; p < P; p += (long)gridDim.x * NT) {
+    const float z = pixel_logit(x + p * C, ws, b, C);
+    const float t = target[p];
+    const float s = 1.f / (1.f + __expf(-z));
+    if (logits) logits[p] = z;
+    acc[0] += fmaxf(z, 0.f) - z * t + log1pf(__expf(-fabsf(z)));
+    acc[1] += s * t;
+    acc[2] += s;
+    acc[3] += t;
+  }
+  block_sum<4>(acc, red);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) atomicAdd(sums + k, acc[k]);
+  }
+}
+
+// dx[p] = dz_p * w;  dw[c] += sum_p dz_p x[p,c];  db += sum_p dz_p
+__global__ void __launch_bounds__(NT)
+seg_head_bwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+                    const float* __restrict__ target, const float* __restrict__ sums, bf16* __restrict__ dx,
+                    float* __restrict__ dw, float* __restrict__ db, long P, int C, float bce_w, float dice_w,
+                    float eps) {
+  __shared__ float red[NT / 64 * 4];
+  __shared__ float ws[256];
+  __shared__ float dws[NT / 64][256];
+  for (int c = threadIdx.x; c < C; c += NT) ws[c] = w[c];
+  for (int c = threadIdx.x; c < NT / 64 * 256; c += NT) (&dws[0][0])[c] = 0.f;
+  __syncthreads();
+  const float b = bias[0];
+  const float I = sums[1], U = sums[2] + sums[3];
+  const float inv_n = 1.f / (float)P;
+  const float den = U + eps, num = 2.f * I + eps;
+  // d(1 - dice)/ds = -(2 t den - num) / den^2
+  const float ka = -2.f / den, kb = num / (den * den);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float dbias = 0.f;
+  // per-wave channel partials of dw in LDS (C <= 256), summed over waves at the end
+  for (long p0 = (long)blockIdx.x * NT; p0 < P; p0 += (long)gridDim.x * NT) {
+    const long p = p0 + threadIdx.x;
+    const bool ok = p < P;                    // every lane runs the wave reductions
+    float dz = 0.f;
+    if (ok) {
+      const float z = pixel_logit(x + p * C, ws, b, C);
+      const float t = target[p];
+      const float s = 1.f / (1.f + __expf(-z));
+      dz = bce_w * (s - t) * inv_n + dice_w * (ka * t + kb) * s * (1.f - s);
+    }
+    for (int c = 0; c < C; c += 8) {
+      float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, g[8];
+      if (ok) unpack8(*reinterpret_cast<const uint4*>(x + p * C + c), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        g[e] = dz * ws[c + e];
+        f[e] *= dz;
+      }
+      if (ok) *reinterpret_cast<uint4*>(dx + p * C + c) = pack8(g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float r = wave_sum(f[e]);
+        if (lane == 0) dws[wave][c + e] += r;
+      }
+    }
+    dbias += dz;
+  }
+  float v[1] = {dbias};
+  block_sum<1>(v, red);
+  if (threadIdx.x == 0) atomicAdd(db, v[0]);
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += NT) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < NT / 64; ++q) s += dws[q][c];
+    atomicAdd(dw + c, s);
+  }
+}
+
+inline int grid_for(long work) {
+  long b = (work + NT - 1) / NT;
+  return (int)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
+}
+
+}  // namespace
+
+// out [N,2h,2w,C1+C2] = concat(upsample2x(lo [N,h,w,C1]), skip [N,2h,2w,C2]); C2 may be 0
+MLC_EXPORT int mlc_upcat_fwd(const bf16* lo, const bf16* skip, bf16* out, int N, int h, int w, int C1, int C2,
+                             hipStream_t st) {
+  if (C1 % 8 || C2 % 8 || (C2 && !skip)) return -1;
+  const long work = (long)N * 4 * h * w * ((C1 + C2) / 8);
+  hipLaunchKernelGGL(upcat_fwd_kernel, dim3(grid_for(work)), dim3(NT), 0, st, lo, skip, out, N, h, w, C1, C2);
+  return hipGetLastError();
+}
+
+MLC_EXPORT int mlc_upcat_bwd(const bf16* dout, bf16* dlo, bf16* dskip, int N, int h, int w, int C1, int C2,
+                             hipStream_t st) {
+  if (C1 % 8 || C2 % 8) return -1;
+  hipLaunchKernelGGL(upcat_bwd_lo_kernel, dim3(grid_for((long)N * h * w * (C1 / 8))), dim3(NT), 0, st, dout, dlo, N,
+                     h, w, C1, C1 + C2);
+  if (C2 && dskip) {
+    const long P = (long)N * 4 * h * w;
+    hipLaunchKernelGGL(upcat_bwd_skip_kernel, dim3(grid_for(P * (C2 / 8))), dim3(NT), 0, st, dout, dskip, P, C1, C2);
+  }
+  return hipGetLastError();
+}
+
+// x [P][C] bf16 (C % 8 == 0, C <= 256), w [C], bias [1], target [P] fp32 in {0,1} (soft ok);
+// logits [P] fp32 (optional); sums [4] fp32 zeroed by the caller
+MLC_EXPORT int mlc_seg_head_fwd(const bf16* x, const float* w, const float* bias, const float* target, float* logits,
+                                float* sums, long P, int C, hipStream_t st) {
+  if (C % 8 || C > 256) return -1;
+  hipLaunchKernelGGL(seg_head_fwd_kernel, dim3(grid_for(P) < 2048 ? grid_for(P) : 2048), dim3(NT), 0, st, x, w, bias,
+                     target, logits, sums, P, C);
+  return hipGetLastError();
+}
+
+// dx [P][C] bf16 written; dw [C] / db [1] accumulated (+=)
+MLC_EXPORT int mlc_seg_head_bwd(const bf16* x, const float* w, const float* bias, const float* target,
+                                const float* sums, bf16* dx, float* dw, float* db, long P, int C, float bce_w,
+                                float dice_w, float eps, hipStream_t st) {
+  if (C % 8 || C > 256) return -1;
+  hipLaunchKernelGGL(seg_head_bwd_kernel, dim3(grid_for(P) < 2048 ? grid_for(P) : 2048), dim3(NT), 0, st, x, w, bias,
+                     target, sums, dx, dw, db, P, C, bce_w, dice_w, eps);
+  return hipGetLastError();
+}

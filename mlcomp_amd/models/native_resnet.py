@@ -21,36 +21,46 @@ from .resnet import BasicBlock, Bottleneck, ResNet
 STEM_CIN = 8
 
 
+def lower_resnet_body(ctx: NativeContext, model: ResNet, prefix: str = ''):
+    """Lower the stem and the four residual stages of ``model`` onto native layers.
+    Returns (stem ConvBN, MaxPool, [ResidualBlock], index of the last block of each stage).
+    Consecutive blocks are linked (``prev``) so a block's first dgrad pre-reduces the
+    previous block's output BN."""
+    if model.groups != 1:
+        raise NotImplementedError('native ResNet path supports groups=1 (use impl=torch)')
+    stem_m = model.stem
+    stem = ConvBN(ctx, f'{prefix}stem', stem_m.conv, stem_m.bn, act=True, cin_pad=STEM_CIN)
+    pool = MaxPool(3, 2, 1)
+    blocks, ends = [], []
+    for li in range(1, 5):
+        for bi, blk in enumerate(getattr(model, f'layer{li}')):
+            pre = f'{prefix}layer{li}.{bi}'
+            units = []
+            if isinstance(blk, Bottleneck):
+                names = ('cb1', 'cb2', 'cb3')
+            elif isinstance(blk, BasicBlock):
+                names = ('cb1', 'cb2')
+            else:
+                raise TypeError(type(blk))
+            for nm in names:
+                cb = getattr(blk, nm)
+                units.append(ConvBN(ctx, f'{pre}.{nm}', cb.conv, cb.bn, act=cb.act))
+            down = None
+            if blk.downsample is not None:
+                d = blk.downsample.cb
+                down = ConvBN(ctx, f'{pre}.downsample.cb', d.conv, d.bn, act=False)
+            rb = ResidualBlock(units, down)
+            rb.prev = blocks[-1] if blocks else None
+            blocks.append(rb)
+        ends.append(len(blocks) - 1)
+    return stem, pool, blocks, ends
+
+
 class NativeResNet:
     def __init__(self, model: ResNet, device, smoothing: float = 0.0):
-        if model.groups != 1:
-            raise NotImplementedError('native ResNet path supports groups=1 (use impl=torch)')
         self.torch_model = model
         ctx = self.ctx = NativeContext()
-        stem = model.stem
-        self.stem = ConvBN(ctx, 'stem', stem.conv, stem.bn, act=True, cin_pad=STEM_CIN)
-        self.pool = MaxPool(3, 2, 1)
-        self.blocks = []
-        for li in range(1, 5):
-            for bi, blk in enumerate(getattr(model, f'layer{li}')):
-                pre = f'layer{li}.{bi}'
-                units = []
-                if isinstance(blk, Bottleneck):
-                    names = ('cb1', 'cb2', 'cb3')
-                elif isinstance(blk, BasicBlock):
-                    names = ('cb1', 'cb2')
-                else:
-                    raise TypeError(type(blk))
-                for nm in names:
-                    cb = getattr(blk, nm)
-                    units.append(ConvBN(ctx, f'{pre}.{nm}', cb.conv, cb.bn, act=cb.act))
-                down = None
-                if blk.downsample is not None:
-                    d = blk.downsample.cb
-                    down = ConvBN(ctx, f'{pre}.downsample.cb', d.conv, d.bn, act=False)
-                rb = ResidualBlock(units, down)
-                rb.prev = self.blocks[-1] if self.blocks else None
-                self.blocks.append(rb)
+        self.stem, self.pool, self.blocks, _ = lower_resnet_body(ctx, model)
         self.head = ClassifierHead(ctx, 'fc', model.fc, smoothing)
         ctx.finalize(device)
         for u in self._units():

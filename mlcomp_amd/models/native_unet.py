@@ -1,0 +1,177 @@
+"""Native (HIP-kernel) execution of the U-Net segmentation model
+(:class:`mlcomp_amd.contrib.segmentation.models.Unet`, the reference's
+`mlcomp/contrib/segmentation/unet/model.py:6-57`) with a ResNet encoder.
+
+* encoder: the ResNet stem + four stages lowered exactly like the classifier
+  (:func:`~mlcomp_amd.models.native_resnet.lower_resnet_body`): fused conv+BN(+residual)
+  (+ReLU) nodes, BN statistics out of the conv epilogues, BN-backward reductions fused into
+  the dgrad epilogues.  The outputs of stages 1-3 and of the stem also feed decoder skips,
+  so their gradient is only complete after the skip gradient is added: the block after
+  each of them is unlinked (``prev = None``) and reduces its own BN from the full sum.
+* decoder block: one fused kernel for the x2 nearest upsample + skip concat
+  (``ops.seg.upcat_*``), then two fused conv3x3+BN+ReLU nodes.
+* head: the 1x1 output conv (16 -> 1 class, + bias) is a per-pixel dot product fused with
+  BCE-with-logits + soft-Dice (``ops.seg.seg_head_*``).
+
+Activations are NHWC bf16 end to end; parameters live in the flat arenas (fused Adam,
+bucketed RCCL all-reduce).  ``export_to_torch()`` writes the weights back.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from mlcomp_amd.ops import seg
+from mlcomp_amd.ops.layers import ConvBN, NativeContext
+from .native_resnet import lower_resnet_body
+
+
+class _UpCatFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, lo, skip, anchor):
+        ctx.c1 = lo.shape[3]
+        ctx.has_skip = skip is not None
+        return seg.upcat_fwd(lo, skip)
+
+    @staticmethod
+    def backward(ctx, d):
+        dlo, dskip = seg.upcat_bwd(d, ctx.c1)
+        return dlo, (dskip if ctx.has_skip else None), None
+
+
+class SegHead:
+    """1x1 conv (C -> 1, bias) + BCE-with-logits + soft-Dice, one forward and one
+    backward kernel.  ``__call__`` returns the loss (device scalar); backward assumes
+    d(loss) = 1."""
+
+    def __init__(self, ctx: NativeContext, name: str, conv: nn.Conv2d, bce_w=1.0, dice_w=1.0, eps=1e-7):
+        assert conv.out_channels == 1 and conv.kernel_size == (1, 1), 'native SegHead: 1 class, 1x1 conv'
+        self.ctx = ctx
+        self.conv = conv
+        self.C = conv.in_channels
+        self.w = ctx.arena.weight(f'{name}.weight', (self.C,))
+        self.b = ctx.arena.vector(f'{name}.bias', (1,))
+        self.bce_w, self.dice_w, self.eps = bce_w, dice_w, eps
+        self.k_sums = ctx.ws.request(f'{name}.sums', 4)
+        self.logits = None      # optional fp32 [P] buffer the forward fills (metrics/inference)
+
+    def load_from_torch(self):
+        dev = self.ctx.device
+        self.w.master.copy_(self.conv.weight.detach().float().reshape(-1).to(dev))
+        b = self.conv.bias.detach().float() if self.conv.bias is not None else torch.zeros(1)
+        self.b.master.copy_(b.to(dev))
+
+    def export_to_torch(self):
+        self.conv.weight.data.copy_(self.w.master.reshape(self.conv.weight.shape).to(self.conv.weight.device))
+        if self.conv.bias is not None:
+            self.conv.bias.data.copy_(self.b.master.to(self.conv.bias.device))
+
+    def sums(self):
+        return self.ctx.ws[self.k_sums]
+
+    def __call__(self, x, target):
+        return _SegHeadFn.apply(x, target, self.ctx.anchor, self)
+
+
+class _SegHeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, target, anchor, h: SegHead):
+        xf = x.reshape(-1, h.C)
+        sums = h.sums()
+        seg.seg_head_fwd(xf, h.w.master, h.b.master, target, sums, logits=h.logits)
+        ctx.h = h
+        ctx.save_for_backward(x, target)
+        return seg.seg_loss(sums, xf.shape[0], h.bce_w, h.dice_w, h.eps)
+
+    @staticmethod
+    def backward(ctx, dloss):
+        x, target = ctx.saved_tensors
+        h: SegHead = ctx.h
+        dx = seg.seg_head_bwd(x.reshape(-1, h.C), h.w.master, h.b.master, target, h.sums(), h.w.grad, h.b.grad,
+                              h.bce_w, h.dice_w, h.eps)
+        h.ctx.arena.mark_ready(h.w)
+        h.ctx.arena.mark_ready(h.b)
+        return dx.view(x.shape), None, None, None
+
+
+class NativeUnet:
+    def __init__(self, model, device, bce_w=1.0, dice_w=1.0, eps=1e-7):
+        from mlcomp_amd.contrib.segmentation.encoders import ResNetEncoder
+        enc, dec = model.encoder, model.decoder
+        if not isinstance(enc, ResNetEncoder):
+            raise NotImplementedError('native U-Net: ResNet encoders (use engine=torch for others)')
+        if not isinstance(dec.center, nn.Identity):
+            raise NotImplementedError('native U-Net: center block not supported')
+        self.torch_model = model
+        ctx = self.ctx = NativeContext()
+        self.stem, self.pool, self.blocks, self.ends = lower_resnet_body(ctx, enc.body, prefix='encoder.body.')
+        for e in self.ends[:3]:          # stage outputs 1-3 feed skips (see module doc)
+            self.blocks[e + 1].prev = None
+        self.dec = []
+        for i, blk in enumerate(dec.blocks):
+            if not (isinstance(blk.att_in, nn.Identity) and isinstance(blk.att_out, nn.Identity)):
+                raise NotImplementedError('native U-Net: scSE attention not supported')
+            c1, c2 = blk.convs[0], blk.convs[1]
+            if not (isinstance(c1[1], nn.BatchNorm2d) and isinstance(c2[1], nn.BatchNorm2d)):
+                raise NotImplementedError('native U-Net: decoder_use_batchnorm=True required')
+            pre = f'decoder.blocks.{i}.convs'
+            self.dec.append((ConvBN(ctx, f'{pre}.0', c1[0], c1[1], act=True),
+                             ConvBN(ctx, f'{pre}.1', c2[0], c2[1], act=True)))
+        self.head = SegHead(ctx, 'decoder.final_conv', dec.final_conv, bce_w, dice_w, eps)
+        ctx.finalize(device)
+        for u in self._units():
+            u.load_from_torch()
+        self.head.load_from_torch()
+        ctx.arena.decay.refresh_mirror()
+
+    def _units(self):
+        yield self.stem
+        for blk in self.blocks:
+            yield from blk.units
+            if blk.down is not None:
+                yield blk.down
+        for c1, c2 in self.dec:
+            yield c1
+            yield c2
+
+    # ------------------------------------------------------------------ execution
+    def features(self, x):
+        """x: NHWC bf16 image (channels padded to 8) -> decoder output [N, H, W, 16]."""
+        anchor = self.ctx.anchor
+        x0 = self.stem(x)
+        y = self.pool(x0, anchor)
+        feats = []
+        for i, blk in enumerate(self.blocks):
+            y = blk(y)
+            if i in self.ends:
+                feats.append(y)
+        x1, x2, x3, x4 = feats
+        d = x4
+        for (c1, c2), skip in zip(self.dec, [x3, x2, x1, x0, None]):
+            d = _UpCatFn.apply(d, skip, anchor)
+            d = c2(c1(d))
+        return d
+
+    def loss(self, x, target):
+        """BCE + Dice loss (device scalar); ``target`` fp32 [N*H*W] in pixel order."""
+        return self.head(self.features(x), target)
+
+    def train(self, mode=True):
+        self.ctx.training = mode
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    @property
+    def arena(self):
+        return self.ctx.arena
+
+    def export_to_torch(self):
+        for u in self._units():
+            u.export_to_torch()
+        self.head.export_to_torch()
+        return self.torch_model
+
+    def num_params(self):
+        return self.ctx.arena.num_params()

@@ -1,0 +1,112 @@
+"""The native training step for U-Net segmentation (BASELINE config 3).
+
+forward (fused conv+BN+ReLU nodes, fused upsample+concat) -> fused 1x1 head + BCE + Dice
+-> backward (wgrad straight into the flat grad arena, bucketed RCCL all-reduce on a side
+stream as buckets fill) -> one fused Adam launch per arena.  Captured into one HIP graph
+after ``warmup_eager`` eager steps, exactly like :class:`NativeClassifierStep`.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+from mlcomp_amd.models.native_resnet import STEM_CIN
+from mlcomp_amd.models.native_unet import NativeUnet
+from mlcomp_amd.ops import functional as Fn
+from mlcomp_amd.parallel.comm import make_comm
+from mlcomp_amd.parallel.ddp import GradBucketer
+from mlcomp_amd.train.optim import FusedAdam, FusedSGD
+
+
+def synthetic_masks(batch, size, device, generator):
+    """Blob-shaped binary masks: a smoothed random field thresholded at its median-ish."""
+    low = torch.randn(batch, 1, size // 16, size // 16, device=device, generator=generator)
+    m = torch.nn.functional.interpolate(low, size=(size, size), mode='bilinear', align_corners=False)
+    return (m > 0.3).float()
+
+
+class NativeSegmentationStep:
+    def __init__(self, encoder='resnet34', batch=32, image_size=256, device=None, world_size=1, use_graph=True,
+                 lr=3e-4, weight_decay=0.0, optimizer='Adam', momentum=0.9, betas=(0.9, 0.999), eps=1e-8,
+                 seed=0, warmup_eager=2, torch_model=None, comm=None):
+        from mlcomp_amd.contrib.segmentation.models import Unet
+        self.device = torch.device(device or 'cuda')
+        torch.manual_seed(seed)
+        tm = torch_model if torch_model is not None else Unet(encoder_name=encoder, classes=1)
+        self.net = NativeUnet(tm, self.device)
+        self.net.ctx.grad_prezeroed = True
+        self.world = world_size
+        self.comm = comm if comm is not None else (make_comm(self.device) if world_size > 1 else None)
+        self.bucketer = GradBucketer(self.net.arena, self.comm)
+        self.bucketer.broadcast_params()
+        if optimizer in ('Adam', 'AdamW'):
+            self.opt = FusedAdam(self.net.arena, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                                 decoupled=optimizer == 'AdamW', grad_scale=1.0 / world_size)
+        else:
+            self.opt = FusedSGD(self.net.arena, lr=lr, momentum=momentum, weight_decay=weight_decay,
+                                grad_scale=1.0 / world_size)
+        self.batch = batch
+        rank = int(os.environ.get('RANK', '0'))
+        g = torch.Generator(device=self.device)
+        g.manual_seed(4321 + rank)
+        img = torch.randn(batch, image_size, image_size, 3, device=self.device, generator=g)
+        self.x = torch.nn.functional.pad(img, (0, STEM_CIN - 3)).to(torch.bfloat16).contiguous()
+        self.t = synthetic_masks(batch, image_size, self.device, g).reshape(-1).contiguous()
+        self.use_graph = use_graph and self.device.type == 'cuda'
+        self.warmup_eager = warmup_eager
+        self.graph = None
+        self.calls = 0
+        self._loss = None
+
+    def load_batch(self, images: torch.Tensor, masks: torch.Tensor):
+        """Copy a batch into the static buffers: images NCHW float (or NHWC bf16 padded),
+        masks [N, 1, H, W] / [N, H, W] in {0, 1}."""
+        x = images
+        if x.dim() == 4 and x.shape[1] in (1, 3) and x.dtype != torch.bfloat16:
+            x = Fn.nchw_to_nhwc(x.to(self.device, non_blocking=True).float(), pad_to=STEM_CIN)
+        self.x.copy_(x)
+        self.t.copy_(masks.to(self.device, non_blocking=True).float().reshape(-1))
+
+    def _body(self):
+        self.net.ctx.ws.zero()
+        self.net.arena.zero_grad()
+        self.bucketer.begin()
+        loss = self.net.loss(self.x, self.t)
+        loss.backward()
+        self.bucketer.finish()
+        self.opt.step()
+        self._loss = loss.detach()
+
+    def __call__(self):
+        self.calls += 1
+        if hasattr(self.opt, 'prepare'):
+            self.opt.prepare()
+        if not self.use_graph:
+            self._body()
+            return
+        if self.graph is None:
+            if self.calls <= self.warmup_eager:
+                s = torch.cuda.Stream(self.device)
+                s.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(s):
+                    self._body()
+                torch.cuda.current_stream(self.device).wait_stream(s)
+                return
+            torch.cuda.synchronize(self.device)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._body()
+        self.graph.replay()
+
+    def set_lr(self, lr):
+        self.opt.set_lr(lr)
+
+    def last_loss(self) -> Optional[float]:
+        return None if self._loss is None else float(self._loss.item())
+
+    def dice(self) -> float:
+        """Soft Dice of the last forward (from the head's loss sums)."""
+        s = self.net.head.sums()
+        return float(((2 * s[1] + 1e-7) / (s[2] + s[3] + 1e-7)).item())
