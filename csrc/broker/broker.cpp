@@ -66,6 +66,11 @@ struct Conn {
 class Broker {
  public:
   explicit Broker(int listen_fd) : lfd_(listen_fd) {}
+  ~Broker() {
+    for (auto& kv : conns_) close(kv.first);
+    if (ep_ >= 0) close(ep_);
+    close(lfd_);
+  }
   void run();
 
  private:
@@ -338,6 +343,11 @@ void Broker::on_read(Conn* c) {
   flush(c);
 }
 
+// SIGTERM / SIGINT end the event loop so the broker exits through its destructors (a
+// clean shutdown is what lets the ASan/LSan build report real leaks, not killed state)
+volatile sig_atomic_t g_stop = 0;
+void on_stop_signal(int) { g_stop = 1; }
+
 void Broker::run() {
   ep_ = epoll_create1(0);
   epoll_event ev{};
@@ -345,9 +355,10 @@ void Broker::run() {
   ev.data.fd = lfd_;
   epoll_ctl(ep_, EPOLL_CTL_ADD, lfd_, &ev);
   std::vector<epoll_event> events(256);
-  for (;;) {
+  while (!g_stop) {
     int n = epoll_wait(ep_, events.data(), (int)events.size(), next_timeout_ms());
     if (n < 0 && errno != EINTR) { perror("epoll_wait"); return; }
+    if (g_stop) break;
     for (int i = 0; i < n; ++i) {
       int fd = events[i].data.fd;
       if (fd == lfd_) { accept_all(); continue; }
@@ -382,6 +393,12 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--port")) port = atoi(argv[i + 1]);
   }
   signal(SIGPIPE, SIG_IGN);
+  struct sigaction sa{};
+  sa.sa_handler = on_stop_signal;
+  sigemptyset(&sa.sa_mask);
+  sa.sa_flags = 0;                    // no SA_RESTART: epoll_wait returns EINTR
+  sigaction(SIGTERM, &sa, nullptr);
+  sigaction(SIGINT, &sa, nullptr);
   int lfd = socket(AF_INET, SOCK_STREAM, 0);
   int one = 1;
   setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));

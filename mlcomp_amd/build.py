@@ -71,18 +71,27 @@ def build_kernels(verbose=False, jobs=None):
     return KERNEL_LIB
 
 
-def build_broker(verbose=False):
+SANITIZERS = {'asan': ['-fsanitize=address,undefined', '-fno-omit-frame-pointer', '-fno-sanitize-recover=all'],
+              'tsan': ['-fsanitize=thread']}
+
+
+def build_broker(verbose=False, sanitize=None):
+    """The C++ broker daemon; ``sanitize='asan'`` (AddressSanitizer + UBSan, any report
+    aborts) or ``'tsan'`` builds an instrumented twin ``mlcomp-broker-<san>`` for the
+    sanitizer tests; host code only."""
     os.makedirs(OUT, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(ROOT, 'csrc', 'broker', '*.cpp')))
     hdrs = glob.glob(os.path.join(ROOT, 'csrc', 'broker', '*.h'))
     if not srcs:
         return None
-    if _newer(BROKER_BIN, srcs + hdrs):
+    out = BROKER_BIN if not sanitize else f'{BROKER_BIN}-{sanitize}'
+    if _newer(out, srcs + hdrs):
         cxx = shutil.which('g++') or 'c++'
-        _run([cxx, '-O2', '-std=c++17', '-pthread', '-Wall', '-o', BROKER_BIN] + srcs)
+        flags = ['-O2'] if not sanitize else ['-O1', '-g'] + SANITIZERS[sanitize]
+        _run([cxx] + flags + ['-std=c++17', '-pthread', '-Wall', '-o', out] + srcs)
     if verbose:
-        print(f'[build] broker -> {BROKER_BIN}')
-    return BROKER_BIN
+        print(f'[build] broker -> {out}')
+    return out
 
 
 def build_runtime(verbose=False):

@@ -1,6 +1,7 @@
 """Transport: the native mlcomp-broker daemon (csrc/broker/broker.cpp) and the
 in-process broker obey the same contract (FIFO, blocking pop, lease/ack/requeue on
 disconnect, revoke, result store)."""
+import contextlib
 import os
 import socket
 import subprocess
@@ -20,25 +21,42 @@ def _free_port():
     return p
 
 
-@pytest.fixture
-def daemon():
+@contextlib.contextmanager
+def _broker_daemon(sanitize, tmp_path):
+    """Run the broker daemon; with ``sanitize='asan'`` the AddressSanitizer + UBSan build:
+    the test's traffic runs against it, then it is stopped with SIGTERM (clean shutdown
+    through its destructors, so LeakSanitizer runs) and must exit 0 with no report."""
     from mlcomp_amd.build import build_broker
-    binary = build_broker()
+    binary = build_broker(sanitize=sanitize)
     port = _free_port()
-    p = subprocess.Popen([binary, '--host', '127.0.0.1', '--port', str(port)], stdout=subprocess.PIPE)
+    err = open(tmp_path / f'broker-{sanitize or "plain"}.err', 'w+')
+    p = subprocess.Popen([binary, '--host', '127.0.0.1', '--port', str(port)], stdout=subprocess.PIPE, stderr=err)
     p.stdout.readline()
-    yield port
-    p.kill()
-    p.wait()
+    try:
+        yield port
+    finally:
+        p.terminate()
+        rc = p.wait(timeout=30)
+        err.seek(0)
+        log = err.read()
+        err.close()
+    assert rc == 0, (rc, log[-4000:])
+    assert 'Sanitizer' not in log and 'runtime error' not in log, log[-4000:]
 
 
-@pytest.fixture(params=['native', 'inproc'])
-def broker_factory(request):
+@pytest.fixture(params=['plain', 'asan'])
+def daemon(request, tmp_path):
+    with _broker_daemon(None if request.param == 'plain' else request.param, tmp_path) as port:
+        yield port
+
+
+@pytest.fixture(params=['native', 'native-asan', 'inproc'])
+def broker_factory(request, tmp_path):
     if request.param == 'inproc':
         b = InProcBroker()
         yield lambda: b
-    else:
-        port = request.getfixturevalue('daemon')
+        return
+    with _broker_daemon('asan' if request.param == 'native-asan' else None, tmp_path) as port:
         clients = []
 
         def make():
