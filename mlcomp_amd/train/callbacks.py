@@ -189,7 +189,10 @@ class CheckpointCallback(Callback):
 
     def on_stage_start(self, state):
         if self.resume and os.path.exists(self.resume):
-            ckpt = torch.load(self.resume, map_location='cpu', weights_only=True)
+            _, ckpt = load_checkpoint(self.resume)
+            if ckpt is None:
+                self.resume = None
+                return
             state.load_checkpoint(ckpt)
             self.best_score = ckpt.get('best_score')
             self.resume = None
@@ -207,11 +210,36 @@ class CheckpointCallback(Callback):
         if is_best:
             self.best_score = score
         ckpt['best_score'] = self.best_score
-        torch.save(ckpt, os.path.join(d, 'last_full.pth'))
-        torch.save({'model_state_dict': ckpt['model_state_dict']}, os.path.join(d, 'last.pth'))
+        save_checkpoint(ckpt, os.path.join(d, 'last_full.pth'))
+        save_checkpoint({'model_state_dict': ckpt['model_state_dict']}, os.path.join(d, 'last.pth'))
         if is_best:
-            torch.save(ckpt, os.path.join(d, 'best_full.pth'))
-            torch.save({'model_state_dict': ckpt['model_state_dict']}, os.path.join(d, 'best.pth'))
+            save_checkpoint(ckpt, os.path.join(d, 'best_full.pth'))
+            save_checkpoint({'model_state_dict': ckpt['model_state_dict']}, os.path.join(d, 'best.pth'))
+
+
+def save_checkpoint(obj, path: str):
+    """Write-then-rename, so a crash mid-write never leaves a torn checkpoint under the
+    final name (resume reads whatever file is there)."""
+    from mlcomp_amd.utils import faults
+    tmp = f'{path}.tmp{os.getpid()}'
+    torch.save(obj, tmp)
+    os.replace(tmp, path)
+    faults.after_checkpoint_write(path)
+
+
+def load_checkpoint(*paths):
+    """The first of ``paths`` that exists and loads (``weights_only``); returns
+    ``(path, ckpt)`` or ``(None, None)``.  A truncated / corrupt file is skipped with a
+    warning instead of failing the resume."""
+    import warnings
+    for path in paths:
+        if not path or not os.path.exists(path):
+            continue
+        try:
+            return path, torch.load(path, map_location='cpu', weights_only=True)
+        except Exception as e:   # truncated zip, bad pickle, ...
+            warnings.warn(f'unreadable checkpoint {path}: {type(e).__name__}: {e}')
+    return None, None
 
 
 @register_callback

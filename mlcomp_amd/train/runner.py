@@ -24,6 +24,8 @@ from typing import Dict, List, Optional
 import torch
 import torch.nn as nn
 
+from mlcomp_amd.utils import faults
+
 from .callbacks import Callback
 from .data import DeviceSyntheticLoader, make_loader
 from .experiment import ConfigExperiment
@@ -304,6 +306,9 @@ class Runner:
         self._fire('on_loader_start')
         for i, batch in enumerate(loader):
             st.loader_step = i + 1
+            if st.is_train:
+                self._train_batches = getattr(self, '_train_batches', 0) + 1
+                faults.maybe_kill_rank(self.rank, self._train_batches)
             st.batch_metrics = {}
             st.loss = None
             st.output = None

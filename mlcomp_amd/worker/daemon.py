@@ -208,6 +208,9 @@ class WorkerSupervisor:
                     kill_pid(t.pid)
 
     def heartbeat(self):
+        from mlcomp_amd.utils import faults
+        if faults.heartbeat_dropped():
+            return
         s = config.get()
         u = usage_snapshot(self.gpu)
         self._usage.append(u)

@@ -202,6 +202,9 @@ class Executor(ABC):
         self.step.enter()
         if not task.debug and config.get().FILE_SYNC_INTERVAL:
             self.wait_data_sync()
+        from mlcomp_amd.utils import faults
+        faults.arm_task_kill()
+        faults.maybe_crash_task()
         res = self.work()
         self.task_provider.commit()
         return res

@@ -197,10 +197,15 @@ class Train(Executor):
                     self.error(f'checkpoint copy failed: {e}')
         elif r.get('master_task_id') and r['master_task_id'] != self.task.id:
             path = join(s.TASK_FOLDER, str(r['master_task_id']), experiment.logdir, 'checkpoints', fname)
-        if not os.path.exists(path):
-            self.info(f'no checkpoint at {path}')
+        other = join(os.path.dirname(path), 'best_full.pth' if fname == 'last_full.pth' else 'last_full.pth')
+        from mlcomp_amd.train.callbacks import load_checkpoint
+        got, ckpt = load_checkpoint(path, other)
+        if ckpt is None:
+            self.info(f'no readable checkpoint at {path} (or {other}): starting fresh')
             return 0
-        ckpt = torch.load(path, map_location='cpu', weights_only=True)
+        if got != path:
+            self.error(f'checkpoint {path} unreadable: resuming from {got}')
+        path = got
         start = 0
         for k in list(experiment.stages_config):
             if k == ckpt['stage']:
@@ -248,8 +253,9 @@ class Train(Executor):
         device = torch.device('cuda', 0) if torch.cuda.is_available() else torch.device('cpu')
         runner = Runner(experiment, device=device, extra_callbacks=extra, rank=rank, world_size=world)
         if self.resume_path:
+            from mlcomp_amd.train.callbacks import load_checkpoint
             runner.model = experiment.get_model(stages[0])
-            ck = torch.load(self.resume_path, map_location='cpu', weights_only=True)
+            _, ck = load_checkpoint(self.resume_path)
             runner.model.load_state_dict(ck['model_state_dict'])
         runner.run_experiment(stages, start_epoch=start_epoch)
         if self.master and self.trace:
