@@ -28,20 +28,22 @@ static __device__ __forceinline__ void unpack8(const uint4& u, float* f) {
   }
 }
 
-// round-to-nearest-even float -> bf16 bits
+// float -> bf16 with the hardware converter (v_cvt_pk_bf16_f32: round-to-nearest-even,
+// NaN stays NaN); one instruction per PAIR of values, so pack two at a time
+static __device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
+  const bf16x2 r = {(bf16)a, (bf16)b};
+  return __builtin_bit_cast(uint32_t, r);
+}
 static __device__ __forceinline__ uint32_t f2bf_bits(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) return (u >> 16) | ((u & 0xffff) ? 0x40u : 0u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return u >> 16;
+  return (uint32_t)__builtin_bit_cast(unsigned short, (bf16)f);
 }
 
 static __device__ __forceinline__ uint4 pack8(const float* f) {
   uint4 r;
-  r.x = f2bf_bits(f[0]) | (f2bf_bits(f[1]) << 16);
-  r.y = f2bf_bits(f[2]) | (f2bf_bits(f[3]) << 16);
-  r.z = f2bf_bits(f[4]) | (f2bf_bits(f[5]) << 16);
-  r.w = f2bf_bits(f[6]) | (f2bf_bits(f[7]) << 16);
+  r.x = pack2_bf16(f[0], f[1]);
+  r.y = pack2_bf16(f[2], f[3]);
+  r.z = pack2_bf16(f[4], f[5]);
+  r.w = pack2_bf16(f[6], f[7]);
   return r;
 }
 

@@ -14,8 +14,8 @@ constexpr int NT = 256;
 
 __device__ __forceinline__ void store_bf16x4(bf16* dst, const float* f) {
   uint2 u;
-  u.x = f2bf_bits(f[0]) | (f2bf_bits(f[1]) << 16);
-  u.y = f2bf_bits(f[2]) | (f2bf_bits(f[3]) << 16);
+  u.x = pack2_bf16(f[0], f[1]);
+  u.y = pack2_bf16(f[2], f[3]);
   *reinterpret_cast<uint2*>(dst) = u;
 }
 }  // namespace

@@ -44,8 +44,8 @@ __device__ __forceinline__ void load4(const bf16* p, float* f) {
 }
 __device__ __forceinline__ void store4(bf16* p, const float* f) {
   uint2 u;
-  u.x = f2bf_bits(f[0]) | (f2bf_bits(f[1]) << 16);
-  u.y = f2bf_bits(f[2]) | (f2bf_bits(f[3]) << 16);
+  u.x = pack2_bf16(f[0], f[1]);
+  u.y = pack2_bf16(f[2], f[3]);
   *reinterpret_cast<uint2*>(p) = u;
 }
 
