@@ -732,7 +732,11 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int MI = TileCfg<BM, BN>::MI, NI = TileCfg<BM, BN>::NI;
   constexpr int WN = BN / (32 * NI);
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  // PF = 0: one LDS stage (single-K-tile GEMMs: 1x1 convs over 64 channels), sized only
+  // for the tile and the epilogue's staging image, so 4 blocks fit a CU instead of 2
+  constexpr int EPI_BYTES = BM * (BN + 8) * 2;
+  constexpr int SMEM = PF == 0 ? (STAGE > EPI_BYTES ? STAGE : EPI_BYTES) : 2 * STAGE;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
 
@@ -788,7 +792,18 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
     }
   };
   if (nt > 0) {
-    if constexpr (PF == 1) {
+    if constexpr (PF == 0) {
+      for (int t = 0; t < nt; ++t) {
+        uint4 ra[BM / 32], rb[BN / 32];
+        la.load(sa, kt0 + t, tid, ra);
+        lb.load(sb, kt0 + t, tid, rb);
+        if (t > 0) __syncthreads();          // previous tile's fragment reads are done
+        stage(smem, ra, rb, true);
+        __syncthreads();
+        mfma_tile(smem, smem + A_BYTES);
+      }
+      __syncthreads();                       // the epilogue reuses the LDS
+    } else if constexpr (PF == 1) {
       uint4 ra[BM / 32], rb[BN / 32];
       la.load(sa, kt0, tid, ra);
       lb.load(sb, kt0, tid, rb);
@@ -846,6 +861,8 @@ static int g_prefetch = 2;
 // (measured on every ResNet-50 wgrad shape: 256 vs 768 blocks saves 10-30 %); gathered
 // operands (3x3 / 7x7 convs) want the occupancy.
 static int g_split_target = 768;
+// single-LDS-stage variant for single-K-tile splits (A/B knob 5)
+static int g_single_stage = 1;
 static int g_split_target_mat = 256;
 
 template <int BM, int BN, class LA, class LB, class EPI>
@@ -858,6 +875,10 @@ static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int 
   const int per = ktiles > 0 ? (ktiles + splits - 1) / splits : 0;
   splits = per > 0 ? (ktiles + per - 1) / per : 1;
   dim3 grid(tiles, 1, splits);
+  if (per <= 1 && g_single_stage) {
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, EPI, 0>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
+    return hipGetLastError();
+  }
   // the second register set only fits the square tile without spilling
   if constexpr (BM == BN) {
     if (g_prefetch >= 2 && per >= 4) {
@@ -966,10 +987,10 @@ MLC_EXPORT int mlc_gemm_config(int prefetch) {
 MLC_EXPORT int mlc_gemm_get_set(int key, int value) {
   int* k = key == 0 ? &igemm::g_prefetch : key == 1 ? &igemm::g_split_target
           : key == 2 ? &igemm::g_split_target_mat : key == 3 ? &igemm::g_big_tiles
-          : key == 4 ? &igemm::g_big_min_blocks : nullptr;
+          : key == 4 ? &igemm::g_big_min_blocks : key == 5 ? &igemm::g_single_stage : nullptr;
   if (!k) return -1;
   const int old = *k;
-  if (value >= 0 && (value > 0 || key == 3)) *k = value;
+  if (value >= 0 && (value > 0 || key == 3 || key == 5)) *k = value;
   return old;
 }
 

@@ -94,7 +94,7 @@ def load():
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, C.c_int)
         # A/B knobs of the GEMM engine (tile policy / min blocks for the wide-wave tiles)
-        for key, env in ((3, 'MLC_GEMM_BIG'), (4, 'MLC_GEMM_BIG_MIN')):
+        for key, env in ((3, 'MLC_GEMM_BIG'), (4, 'MLC_GEMM_BIG_MIN'), (5, 'MLC_GEMM_SINGLE_STAGE')):
             if os.environ.get(env):
                 lib.mlc_gemm_get_set(key, int(os.environ[env]))
         _LIB = lib
