@@ -513,7 +513,8 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
     // issued before the chunk's stores, so the loads overlap instead of serialising
     // behind stores the compiler must assume alias them (out may alias addend)
     constexpr int ITERS = BM / RPI;
-    constexpr int U = ITERS < 4 ? ITERS : 4;
+    constexpr int UMAX = kDense ? 4 : 8;   // conv epilogues: every row's loads in flight at once
+    constexpr int U = ITERS < UMAX ? ITERS : UMAX;
     const bool has_add = addend != nullptr, has_mask = red && bn.mask, has_y1 = red && bn.y1;
 #pragma unroll 1
     for (int it0 = 0; it0 < ITERS; it0 += U) {
