@@ -3,10 +3,16 @@
 
 ``NativeResNet(torch_model)`` lowers the module tree onto native layers
 (`mlcomp_amd.ops.layers`): every ConvBNAct becomes one fused conv+BN(+residual)(+ReLU)
-autograd node whose BN statistics come out of the conv epilogue, the stem takes the
-image as NHWC bf16 with channels padded 3 -> 8 (the MFMA loaders move 8 channels per
-16-byte chunk; the padded input channels are zero so their weights get zero gradient and
-stay zero), and the head fuses avg-pool, the FC layer and softmax cross-entropy.
+autograd node whose BN statistics come out of the conv epilogue, and the head fuses
+avg-pool, the FC layer and softmax cross-entropy.
+
+The stem takes the image as NHWC bf16 with channels padded 3 -> 8.  Its 7x7/2 conv runs as
+a 4x4/1 conv over the 2x2 space-to-depth image (``s2d_stem``, `ops.functional.stem_s2d`:
+K = 256 instead of 7x7x8 = 392 padded to 448), and BN + ReLU + 3x3/2 max-pool are one
+fused pass whose backward recomputes the pool scatter inside the BN-backward passes
+(``fuse_stem_pool``, `ops.layers.StemPool`, csrc/kernels/stem.hip).  Reference graph:
+torchvision-style ResNet as built by the reference's classify presets
+(`mlcomp/contrib/catalyst/configs/classify/resnet50.yml`).
 
 Weights are copied into the flat arenas once; ``export_to_torch()`` writes them back
 (for checkpoints in the standard PyTorch layout).
@@ -15,13 +21,13 @@ from __future__ import annotations
 
 import torch
 
-from mlcomp_amd.ops.layers import ClassifierHead, ConvBN, MaxPool, NativeContext, ResidualBlock
+from mlcomp_amd.ops.layers import ClassifierHead, ConvBN, MaxPool, NativeContext, ResidualBlock, StemPool
 from .resnet import BasicBlock, Bottleneck, ResNet
 
 STEM_CIN = 8
 
 
-def lower_resnet_body(ctx: NativeContext, model: ResNet, prefix: str = ''):
+def lower_resnet_body(ctx: NativeContext, model: ResNet, prefix: str = '', s2d_stem: bool = False):
     """Lower the stem and the four residual stages of ``model`` onto native layers.
     Returns (stem ConvBN, MaxPool, [ResidualBlock], index of the last block of each stage).
     Consecutive blocks are linked (``prev``) so a block's first dgrad pre-reduces the
@@ -29,7 +35,9 @@ def lower_resnet_body(ctx: NativeContext, model: ResNet, prefix: str = ''):
     if model.groups != 1:
         raise NotImplementedError('native ResNet path supports groups=1 (use impl=torch)')
     stem_m = model.stem
-    stem = ConvBN(ctx, f'{prefix}stem', stem_m.conv, stem_m.bn, act=True, cin_pad=STEM_CIN)
+    s2d = s2d_stem and tuple(stem_m.conv.weight.shape[1:]) == (3, 7, 7) and stem_m.conv.stride[0] == 2 \
+        and stem_m.conv.padding[0] == 3
+    stem = ConvBN(ctx, f'{prefix}stem', stem_m.conv, stem_m.bn, act=True, cin_pad=STEM_CIN, s2d=s2d)
     pool = MaxPool(3, 2, 1)
     blocks, ends = [], []
     for li in range(1, 5):
@@ -57,10 +65,13 @@ def lower_resnet_body(ctx: NativeContext, model: ResNet, prefix: str = ''):
 
 
 class NativeResNet:
-    def __init__(self, model: ResNet, device, smoothing: float = 0.0):
+    def __init__(self, model: ResNet, device, smoothing: float = 0.0, fuse_stem_pool: bool = True,
+                 s2d_stem: bool = True):
         self.torch_model = model
         ctx = self.ctx = NativeContext()
-        self.stem, self.pool, self.blocks, _ = lower_resnet_body(ctx, model)
+        self.stem, self.pool, self.blocks, _ = lower_resnet_body(ctx, model, s2d_stem=s2d_stem)
+        # the classifier never reads the un-pooled stem activation: fuse BN+ReLU+maxpool
+        self.stem_pool = StemPool(self.stem) if fuse_stem_pool else None
         self.head = ClassifierHead(ctx, 'fc', model.fc, smoothing)
         ctx.finalize(device)
         for u in self._units():
@@ -78,8 +89,11 @@ class NativeResNet:
     # ------------------------------------------------------------------ execution
     def features(self, x):
         anchor = self.ctx.anchor
-        x = self.stem(x)
-        x = self.pool(x, anchor)
+        if self.stem_pool is not None:
+            x = self.stem_pool(x)
+        else:
+            x = self.stem(x)
+            x = self.pool(x, anchor)
         for blk in self.blocks:
             x = blk(x)
         return x

@@ -336,6 +336,80 @@ def maxpool_bwd(dy, idx, x_shape, k=3, s=2, p=1):
     return dxf.reshape(N, C, H, W).permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
 
 
+def stem_s2d(x, pad=3):
+    """NHWC bf16 image (3 real channels, any channel stride) -> the 2x2 space-to-depth
+    image of its ``pad``-padded version, [N, (H+2p)/2, (W+2p)/2, 16] with channel
+    (dy*2+dx)*3+ci and channels 12..15 zero (csrc/kernels/stem.hip)."""
+    N, H, W, Cs = x.shape
+    Hb, Wb = (H + 2 * pad) // 2, (W + 2 * pad) // 2
+    if _cuda(x):
+        out = torch.empty(N, Hb, Wb, 16, device=x.device, dtype=torch.bfloat16)
+        _lib.call('mlc_stem_s2d', _lib.ptr(x.contiguous()), _lib.ptr(out), N, H, W, Cs, pad, _lib.stream())
+        return out
+    xp = F.pad(x[..., :3].float(), (0, 0, pad, pad, pad, pad))
+    xp = xp.reshape(N, Hb, 2, Wb, 2, 3).permute(0, 1, 3, 2, 4, 5).reshape(N, Hb, Wb, 12)
+    return F.pad(xp, (0, 4)).to(torch.bfloat16).contiguous()
+
+
+def stem_w_to_s2d(w):
+    """[Co, Ci<=3, 7, 7] filter -> [Co, 4, 4, 16] space-to-depth filter (see stem_s2d)."""
+    Co, Ci = w.shape[:2]
+    w8 = F.pad(w.float(), (0, 1, 0, 1))                          # 8x8, tap 7 = 0
+    w8 = F.pad(w8, (0, 0, 0, 0, 0, 3 - Ci)) if Ci < 3 else w8
+    w2 = w8.reshape(Co, 3, 4, 2, 4, 2).permute(0, 2, 4, 3, 5, 1).reshape(Co, 4, 4, 12)
+    return F.pad(w2, (0, 4))
+
+
+def stem_w_from_s2d(w2, Ci=3):
+    """Inverse of :func:`stem_w_to_s2d`: [Co, 4, 4, 16] -> [Co, Ci, 7, 7]."""
+    Co = w2.shape[0]
+    w8 = w2[..., :12].reshape(Co, 4, 4, 2, 2, 3).permute(0, 5, 1, 3, 2, 4).reshape(Co, 3, 8, 8)
+    return w8[:, :Ci, :7, :7].contiguous()
+
+
+def stem_pool_fwd(y, scale, shift):
+    """ResNet stem tail: pooled = maxpool3x3/2(relu(y*scale + shift)) without
+    materialising the activation (csrc/kernels/stem.hip).  Returns (pooled, idx); idx is
+    the window argmax (uint8, 255 = ReLU inactive) on the GPU, an encoded int64 index
+    (flat argmax * 2 + active) on the CPU."""
+    N, H, W, C = y.shape
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    if _cuda(y):
+        out = torch.empty(N, Ho, Wo, C, device=y.device, dtype=torch.bfloat16)
+        idx = torch.empty(N, Ho, Wo, C, device=y.device, dtype=torch.uint8)
+        _lib.call('mlc_stem_pool_fwd', _lib.ptr(y), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(out),
+                  _lib.ptr(idx), N, H, W, C, _lib.stream())
+        return out, idx
+    a = (y.float() * scale + shift).permute(0, 3, 1, 2)
+    m, ind = F.max_pool2d(a, 3, 2, 1, return_indices=True)
+    active = (m > 0).long()
+    out = m.clamp_min(0).permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+    return out, (ind * 2 + active).permute(0, 2, 3, 1).contiguous()
+
+
+def stem_pool_bwd(dp, idx, y, mean, invstd, gamma, dgamma, dbeta, sums, coef):
+    """Backward of :func:`stem_pool_fwd` through the BatchNorm: returns dy (bf16, the conv
+    output gradient) and writes dgamma/dbeta.  ``sums`` (NSTAT*2*C fp32) must be zero on
+    entry; ``coef`` is 3*C fp32 scratch."""
+    N, H, W, C = y.shape
+    rows = N * H * W
+    if _cuda(dp):
+        _lib.call('mlc_stem_pool_bwd_reduce', _lib.ptr(dp), _lib.ptr(idx), _lib.ptr(y), _lib.ptr(mean),
+                  _lib.ptr(sums), N, H, W, C, _lib.stream())
+        _lib.call('mlc_bn_bwd_finalize', _lib.ptr(sums), _lib.ptr(invstd), _lib.ptr(gamma), _lib.ptr(coef),
+                  _lib.ptr(dgamma), _lib.ptr(dbeta), rows, C, _lib.stream())
+        dy = torch.empty_like(y)
+        _lib.call('mlc_stem_pool_bwd_apply', _lib.ptr(dp), _lib.ptr(idx), _lib.ptr(y), _lib.ptr(mean),
+                  _lib.ptr(coef), _lib.ptr(dy), N, H, W, C, _lib.stream())
+        return dy
+    ind, active = idx.permute(0, 3, 1, 2) // 2, idx.permute(0, 3, 1, 2) % 2
+    g = dp.permute(0, 3, 1, 2).float() * active
+    du = torch.zeros(N, C, H * W).scatter_add_(2, ind.reshape(N, C, -1), g.reshape(N, C, -1))
+    du = du.reshape(N, C, H, W).permute(0, 2, 3, 1).contiguous()
+    dy, _ = bn_bwd(du, None, y, mean, invstd, gamma, dgamma=dgamma, dbeta=dbeta)
+    return dy
+
+
 def avgpool_fwd(x):
     N, H, W, C = x.shape
     if _cuda(x):

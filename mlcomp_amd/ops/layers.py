@@ -75,7 +75,7 @@ class ConvBN:
     """conv (no bias) -> BatchNorm (train-mode batch stats) -> [+residual] -> [ReLU]."""
 
     def __init__(self, ctx: NativeContext, name: str, conv: nn.Conv2d, bn: nn.BatchNorm2d,
-                 act: bool, cin_pad: Optional[int] = None):
+                 act: bool, cin_pad: Optional[int] = None, s2d: bool = False):
         assert conv.groups == 1, 'native ConvBN supports groups=1'
         self.ctx = ctx
         self.name = name
@@ -87,6 +87,14 @@ class ConvBN:
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
         self.dil = conv.dilation[0]
+        # s2d: a 7x7/2 pad-3 stem over <= 3 channels runs as a 4x4/1 conv over the 2x2
+        # space-to-depth input (Fn.stem_s2d): K = 256 instead of 392 padded to 448
+        self.s2d = s2d
+        if s2d:
+            assert (KH, KW, self.stride, self.pad, self.dil) == (7, 7, 2, 3, 1) and Ci <= 3, \
+                's2d stem needs a 7x7/2 pad-3 conv over <= 3 channels'
+            self.k, self.stride, self.pad, self.cin_p = (4, 4), 1, 0, 16
+            KH = KW = 4
         self.act = act
         self.eps = bn.eps
         self.momentum = bn.momentum if bn.momentum is not None else 0.1
@@ -101,9 +109,15 @@ class ConvBN:
     def load_from_torch(self):
         conv, bn = self._src
         dev = self.ctx.device
-        w = conv.weight.detach().permute(0, 2, 3, 1).float()
-        if self.cin_p != self.cin:
-            w = torch.nn.functional.pad(w, (0, self.cin_p - self.cin))
+        if self.s2d:
+            w = Fn.stem_w_to_s2d(conv.weight.detach().cpu())
+            # taps of the zero-extended 8x8 filter (row/col 7) and the 4 pad channels must
+            # stay zero: their gradients are masked after every wgrad
+            self._gmask = (Fn.stem_w_to_s2d(torch.ones(self.Co, self.cin, 7, 7)) != 0).float().to(dev)
+        else:
+            w = conv.weight.detach().permute(0, 2, 3, 1).float()
+            if self.cin_p != self.cin:
+                w = torch.nn.functional.pad(w, (0, self.cin_p - self.cin))
         self.w.master.copy_(w.to(dev))
         self.gamma.master.copy_(bn.weight.detach().to(dev))
         self.beta.master.copy_(bn.bias.detach().to(dev))
@@ -116,7 +130,10 @@ class ConvBN:
 
     def export_to_torch(self):
         conv, bn = self._src
-        w = self.w.master[..., :self.cin].permute(0, 3, 1, 2).contiguous()
+        if self.s2d:
+            w = Fn.stem_w_from_s2d(self.w.master.detach().float().cpu(), self.cin)
+        else:
+            w = self.w.master[..., :self.cin].permute(0, 3, 1, 2).contiguous()
         conv.weight.data.copy_(w.to(conv.weight.device))
         bn.weight.data.copy_(self.gamma.master.to(bn.weight.device))
         bn.bias.data.copy_(self.beta.master.to(bn.bias.device))
@@ -132,6 +149,8 @@ class ConvBN:
         ``(y, scale, shift)`` (applied in the same pass).  ``defer=True`` stops after the
         statistics: z is not materialised (returns None; scale/shift are ready)."""
         ws = self.ctx.ws
+        if self.s2d and x.shape[-1] != 16:
+            x = Fn.stem_s2d(x, 3)
         raff = None
         if isinstance(res, tuple):
             res, rs, rh = res
@@ -165,6 +184,14 @@ class ConvBN:
         x, y, z = rec
         return (y, self.save_mean, self.ctx.ws[self.k_bw])
 
+    def wgrad(self, dy, x):
+        """Weight gradient into the arena (masked for the s2d stem), then mark it ready."""
+        Fn.conv2d_wgrad(dy, x, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad,
+                        accumulate=self.ctx.grad_prezeroed)
+        if self.s2d:
+            self.w.grad.mul_(self._gmask)
+        self.ctx.arena.mark_ready(self.w)
+
     def bwd(self, dz, rec, want_dres=False, dx_addend=None, need_dx=True, dx_out=None,
             prereduced=False, dgrad_bn=None):
         x, y, z = rec
@@ -175,9 +202,7 @@ class ConvBN:
                              coef=self.coef, prereduced=prereduced)
         arena.mark_ready(self.gamma)
         arena.mark_ready(self.beta)
-        Fn.conv2d_wgrad(dy, x, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad,
-                        accumulate=self.ctx.grad_prezeroed)
-        arena.mark_ready(self.w)
+        self.wgrad(dy, x)
         dx = None
         if need_dx:
             dx = Fn.conv2d_dgrad(dy, self.w.bf16, x.shape, self.stride, self.pad, self.dil,
@@ -335,6 +360,49 @@ class _MaxPoolFn(torch.autograd.Function):
         (idx,) = ctx.saved_tensors
         m = ctx.m
         return Fn.maxpool_bwd(dy.contiguous(), idx, ctx.xshape, m.k, m.s, m.p), None, None
+
+
+class StemPool:
+    """The classifier stem: conv -> BN -> ReLU -> maxpool 3x3/2 with the ReLU output never
+    materialised.  The conv epilogue accumulates the BN statistics, one fused pass applies
+    BN + ReLU + max-pool (csrc/kernels/stem.hip), and the backward recomputes the pooled
+    gradient scatter inside the two BN-backward passes.  (U-Net keeps ``stem`` + ``MaxPool``:
+    its decoder reads the un-pooled stem activation as a skip connection.)"""
+
+    def __init__(self, stem: ConvBN):
+        assert stem.act, 'StemPool fuses the stem ReLU'
+        self.stem = stem
+        self.ctx = stem.ctx
+
+    def __call__(self, x):
+        return _StemPoolFn.apply(x, self.ctx.anchor, self)
+
+
+class _StemPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, m: StemPool):
+        st = m.stem
+        if not st.ctx.training:
+            z, _ = st.fwd(x)
+            out, _ = Fn.maxpool_fwd(z)
+            return out
+        _, (x_, y, _) = st.fwd(x, defer=True)
+        out, idx = Fn.stem_pool_fwd(y, st.scale, st.shift)
+        ctx.m = m
+        ctx.save_for_backward(x_, y, idx)
+        return out
+
+    @staticmethod
+    def backward(ctx, dp):
+        st: ConvBN = ctx.m.stem
+        x, y, idx = ctx.saved_tensors
+        arena = st.ctx.arena
+        dy = Fn.stem_pool_bwd(dp.contiguous(), idx, y, st.save_mean, st.save_invstd, st.gamma.master,
+                              st.gamma.grad, st.beta.grad, st.ctx.ws[st.k_bw], st.coef)
+        arena.mark_ready(st.gamma)
+        arena.mark_ready(st.beta)
+        st.wgrad(dy, x)
+        return None, None, None
 
 
 # ---------------------------------------------------------------------------- head

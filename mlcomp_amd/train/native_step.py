@@ -52,7 +52,7 @@ class NativeClassifierStep:
         g = torch.Generator(device=self.device)
         g.manual_seed(1234 + rank)
         img = torch.randn(batch, image_size, image_size, 3, device=self.device, generator=g)
-        self.x = torch.nn.functional.pad(img, (0, STEM_CIN - 3)).to(torch.bfloat16).contiguous()
+        self.x = self._prep(torch.nn.functional.pad(img, (0, STEM_CIN - 3)).to(torch.bfloat16).contiguous())
         self.y = torch.randint(0, num_classes, (batch,), device=self.device, generator=g)
         self.use_graph = use_graph and self.device.type == 'cuda'
         self.warmup_eager = warmup_eager
@@ -66,8 +66,15 @@ class NativeClassifierStep:
         x = images_nchw_or_nhwc
         if x.dim() == 4 and x.shape[1] in (1, 3) and x.dtype != torch.bfloat16:
             x = Fn.nchw_to_nhwc(x.to(self.device, non_blocking=True).float(), pad_to=STEM_CIN)
-        self.x.copy_(x)
+        self.x.copy_(self._prep(x.to(self.device, non_blocking=True)))
         self.y.copy_(labels.to(self.device, non_blocking=True))
+
+    def _prep(self, x_nhwc):
+        """Input-pipeline layout of the stem: the space-to-depth image when the stem runs as
+        a 4x4 conv over it (done here, once per batch, not inside the captured step)."""
+        if getattr(self.net.stem, 's2d', False) and x_nhwc.shape[-1] != 16:
+            return Fn.stem_s2d(x_nhwc, 3)
+        return x_nhwc
 
     # ------------------------------------------------------------------ step
     def _body(self):

@@ -319,3 +319,53 @@ def test_native_fused_bn_bwd_matches_unfused():
     assert ((ga - gb).norm() / gb.norm()).item() < 2e-2
     na, nb = a.net.arena.nodecay.grad, b.net.arena.nodecay.grad
     assert ((na - nb).norm() / nb.norm()).item() < 2e-2
+
+
+@pytest.mark.parametrize('shape', [(2, 12, 12, 64), (3, 11, 13, 64), (2, 10, 9, 32)])
+def test_stem_pool_fused(shape):
+    """Fused BN-apply + ReLU + maxpool 3x3/2 and its backward through the BN (stem.hip)
+    vs the fp32 reference path."""
+    C = shape[-1]
+    y = _bf(*shape, scale=2.0, seed=21)
+    g = torch.Generator().manual_seed(22)
+    scale = torch.rand(C, generator=g) * 2 - 0.5      # some negative gammas
+    shift = torch.randn(C, generator=g) * 0.5
+    mean = torch.randn(C, generator=g) * 0.1
+    invstd = torch.rand(C, generator=g) + 0.5
+    gamma = torch.rand(C, generator=g) + 0.5
+    Ho, Wo = (shape[1] - 1) // 2 + 1, (shape[2] - 1) // 2 + 1
+    dp = _bf(shape[0], Ho, Wo, C, seed=23)
+
+    def run(dev):
+        t = lambda v: v.to(dev)
+        out, idx = Fn.stem_pool_fwd(t(y), t(scale), t(shift))
+        dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        sums = torch.zeros(Fn.NSTAT * 2 * C, device=dev)
+        coef = torch.empty(3 * C, device=dev)
+        dy = Fn.stem_pool_bwd(t(dp), idx, t(y), t(mean), t(invstd), t(gamma), dg, db, sums, coef)
+        return out, dy, dg, db
+
+    ref = run('cpu')
+    res = run(DEV)
+    torch.cuda.synchronize()
+    assert rel_err(res[0], ref[0]) < 5e-3
+    for a, b in zip(res[1:], ref[1:]):
+        assert rel_err(a, b) < 1e-2
+
+
+def test_stem_s2d_conv():
+    """Space-to-depth stem: the HIP s2d transform matches the reference, and the 4x4/1 conv
+    over it with the regrouped filter equals the 7x7/2 pad-3 conv."""
+    x = _bf(2, 30, 26, 8, seed=31)
+    x[..., 3:] = 0
+    xs_ref = Fn.stem_s2d(x)
+    xs = Fn.stem_s2d(x.to(DEV))
+    torch.cuda.synchronize()
+    assert rel_err(xs, xs_ref) == 0.0
+    w = torch.randn(64, 3, 7, 7, generator=torch.Generator().manual_seed(32)) * 0.1
+    w2 = Fn.stem_w_to_s2d(w).to(torch.bfloat16)
+    y = Fn.conv2d_fwd(xs, w2.to(DEV), 1, 0, 1)
+    ref = torch.nn.functional.conv2d(x[..., :3].permute(0, 3, 1, 2).float(), w.to(torch.bfloat16).float(),
+                                     stride=2, padding=3).permute(0, 2, 3, 1)
+    torch.cuda.synchronize()
+    assert rel_err(y, ref) < 1e-2

@@ -3,6 +3,8 @@ against plain PyTorch autograd on the same model, on CPU (reference op paths).""
 import torch
 import torch.nn.functional as F
 
+from mlcomp_amd.ops import functional as Fn
+
 from mlcomp_amd.models import build_model
 from mlcomp_amd.models.native_resnet import STEM_CIN
 from mlcomp_amd.train.native_step import NativeClassifierStep
@@ -27,7 +29,10 @@ def test_native_step_matches_torch_autograd():
     step = NativeClassifierStep(torch_model=tm, batch=8, image_size=32, device='cpu',
                                 num_classes=16, lr=0.1, momentum=0.0, weight_decay=0.0,
                                 use_graph=False)
-    x_nhwc = step.x[..., :3].float()
+    # the step keeps its input as the stem's space-to-depth image: undo it (pad 3)
+    xs = step.x[..., :12].float()
+    N_, Hb, Wb, _ = xs.shape
+    x_nhwc = xs.reshape(N_, Hb, Wb, 2, 2, 3).permute(0, 1, 3, 2, 4, 5).reshape(N_, 2 * Hb, 2 * Wb, 3)[:, 3:-3, 3:-3]
     x = x_nhwc.permute(0, 3, 1, 2).contiguous()
     y = step.y
     ref.train()
@@ -41,14 +46,20 @@ def test_native_step_matches_torch_autograd():
     # bf16 activations through 18 BN layers over a tiny batch: a pure torch bf16 run of
     # this same model/batch reaches cosine ~0.87-0.96 vs fp32 (checked when writing this
     # test), so the bar is "at least as close as stock bf16"
-    g_stem = arena.by_name['stem.conv.weight'].grad[..., :3].permute(0, 3, 1, 2)
+    # the stem runs as a 4x4 conv over the space-to-depth image: map its gradient back
+    g2 = arena.by_name['stem.conv.weight'].grad
+    assert tuple(g2.shape) == (64, 4, 4, 16)
+    g_stem = Fn.stem_w_from_s2d(g2)
     assert _cos(g_stem, ref.stem.conv.weight.grad) > 0.85
     g = arena.by_name['layer2.0.cb1.conv.weight'].grad.permute(0, 3, 1, 2)
     assert _cos(g, ref.layer2[0].cb1.conv.weight.grad) > 0.85
     assert _cos(arena.by_name['fc.weight'].grad[:16], ref.fc.weight.grad) > 0.99
     assert _cos(arena.by_name['layer4.1.cb2.bn.weight'].grad, ref.layer4[1].cb2.bn.weight.grad) > 0.95
-    # padded stem input channels never receive gradient
-    assert arena.by_name['stem.conv.weight'].grad[..., 3:].abs().max() == 0
+    # the zero-extended taps (row/col 7 of the 8x8 filter) and pad channels never
+    # receive gradient, so the s2d filter stays an exact 7x7 filter
+    mask = Fn.stem_w_to_s2d(torch.ones(64, 3, 7, 7)) != 0
+    assert g2[~mask].abs().max() == 0
+    assert arena.by_name['stem.conv.weight'].master[~mask].abs().max() == 0
     # SGD applied: master = old - lr * grad
     new_fc = arena.by_name['fc.weight'].master[:16]
     exp = ref.fc.weight.detach() - 0.1 * arena.by_name['fc.weight'].grad[:16]

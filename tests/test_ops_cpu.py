@@ -52,3 +52,33 @@ def test_maxpool_reference_matches_autograd():
     xr = x.permute(0, 3, 1, 2).float().requires_grad_()
     F.max_pool2d(xr, 3, 2, 1).backward(dy.permute(0, 3, 1, 2).float())
     assert (dx.permute(0, 3, 1, 2).float() - xr.grad).abs().max() < 0.05
+
+
+def test_stem_pool_reference_matches_autograd():
+    """The fused stem tail's reference path (BN-apply + ReLU + maxpool, and its backward
+    through a training BatchNorm) against torch autograd of the unfused graph."""
+    import torch.nn.functional as F
+    from mlcomp_amd.ops import functional as Fn
+    torch.manual_seed(3)
+    N, H, W, C = 2, 12, 10, 16
+    y = torch.randn(N, H, W, C).to(torch.bfloat16)
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C) * 0.2
+    yf = y.float().requires_grad_(True)
+    g_ = gamma.clone().requires_grad_(True)
+    b_ = beta.clone().requires_grad_(True)
+    bn = F.batch_norm(yf.permute(0, 3, 1, 2), None, None, g_, b_, training=True, eps=1e-5)
+    ref = F.max_pool2d(F.relu(bn), 3, 2, 1)
+    dp = torch.randn_like(ref)
+    ref.backward(dp)
+    mean = y.float().mean((0, 1, 2))
+    var = y.float().var((0, 1, 2), unbiased=False)
+    invstd = torch.rsqrt(var + 1e-5)
+    scale, shift = gamma * invstd, beta - mean * gamma * invstd
+    out, idx = Fn.stem_pool_fwd(y, scale, shift)
+    assert torch.allclose(out.float(), ref.detach().permute(0, 2, 3, 1), atol=2e-2, rtol=2e-2)
+    dg, db = torch.empty(C), torch.empty(C)
+    dy = Fn.stem_pool_bwd(dp.permute(0, 2, 3, 1).to(torch.bfloat16), idx, y, mean, invstd, gamma, dg, db,
+                          None, None)
+    assert torch.allclose(dy.float(), yf.grad, atol=3e-2, rtol=3e-2)
+    assert torch.allclose(dg, g_.grad, atol=3e-2, rtol=3e-2)
+    assert torch.allclose(db, b_.grad, atol=3e-2, rtol=3e-2)
