@@ -47,6 +47,22 @@ static __device__ __forceinline__ uint4 pack8(const float* f) {
   return r;
 }
 
+// 16-byte global load through an ext-vector type.  Loading HIP's uint4 struct directly
+// lets hipcc split a conditional load into four branch-wrapped dword loads (seen in the
+// conv epilogues) or serialise a batch of loads with vmcnt(0) after each; the vector type
+// keeps one dwordx4 per chunk and lets the loads of a batch fly together.
+static __device__ __forceinline__ uint4 ldg16(const void* p) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = *reinterpret_cast<const u32x4*>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+// 8 consecutive floats (two 16-byte loads)
+static __device__ __forceinline__ void ldg8f(const float* p, float* f) {
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  const f32x4v a = *reinterpret_cast<const f32x4v*>(p), b = *reinterpret_cast<const f32x4v*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
 static __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

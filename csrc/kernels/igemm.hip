@@ -486,18 +486,24 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
     float mu0[8], mu1[8], s1[8], s2[8], t2[8], ma0[8], mb0[8], ma1[8], mb1[8];
     const bool aff = red && !bn.mask && bn.msc0, aff1 = aff && bn.msc1;
     if (red) {
+      // per-column constants: vector loads from a clamped (always valid) column, under
+      // wave-uniform pointer tests only; columns past N are never stored
+      const int ncl = nc < N ? nc : 0;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        mu0[e] = nc < N ? bn.mean0[nc + e] : 0.f;
-        mu1[e] = (bn.y1 && nc < N) ? bn.mean1[nc + e] : 0.f;
         s1[e] = 0.f; s2[e] = 0.f; t2[e] = 0.f;
-        ma0[e] = (aff && nc < N) ? bn.msc0[nc + e] : 0.f;
-        mb0[e] = (aff && nc < N) ? bn.msh0[nc + e] : 0.f;
-        ma1[e] = (aff1 && nc < N) ? bn.msc1[nc + e] : 0.f;
-        mb1[e] = (aff1 && nc < N) ? bn.msh1[nc + e] : 0.f;
+        mu1[e] = 0.f; ma0[e] = 0.f; mb0[e] = 0.f; ma1[e] = 0.f; mb1[e] = 0.f;
       }
+      ldg8f(bn.mean0 + ncl, mu0);
+      if (bn.y1) ldg8f(bn.mean1 + ncl, mu1);
+      if (aff) { ldg8f(bn.msc0 + ncl, ma0); ldg8f(bn.msh0 + ncl, mb0); }
+      if (aff1) { ldg8f(bn.msc1 + ncl, ma1); ldg8f(bn.msh1 + ncl, mb1); }
     }
     const bool dense = kDense && (bias || act || dact);
+    float bz[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bz[e] = 0.f;
+    if (kDense && bias) ldg8f(bias + (nc < N ? nc : 0), bz);
     if (!addend && !red && !dense) {  // plain store (forward convs / GEMMs)
 #pragma unroll
       for (int it = 0; it < BM / RPI; ++it) {
@@ -528,16 +534,17 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
         const int row = tid / CPR + RPI * (it0 + u);
         const int m = m0 + row;
         ok[u] = m < M && nc < N;
-        off[u] = ok[u] ? rowmap(m) * ld + nc : 0;
+        off[u] = ok[u] ? rowmap(m) * ld + nc : 0;   // rows/cols outside: element 0 (valid)
         vv[u] = *reinterpret_cast<const uint4*>(lds + row * RS + c * 16);
         const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
-        aa[u] = (ok[u] && has_add) ? *reinterpret_cast<const uint4*>(addend + off[u]) : zero;
+        // unconditional per lane (the store is what ok[u] guards), uniform per pointer
+        aa[u] = has_add ? ldg16(addend + off[u]) : zero;
         if constexpr (!kDense) {
-          zz[u] = (ok[u] && has_mask) ? *reinterpret_cast<const uint4*>(bn.mask + off[u]) : zero;
-          p0[u] = (ok[u] && red) ? *reinterpret_cast<const uint4*>(bn.y0 + off[u]) : zero;
-          p1[u] = (ok[u] && has_y1) ? *reinterpret_cast<const uint4*>(bn.y1 + off[u]) : zero;
+          zz[u] = has_mask ? ldg16(bn.mask + off[u]) : zero;
+          p0[u] = red ? ldg16(bn.y0 + off[u]) : zero;
+          p1[u] = has_y1 ? ldg16(bn.y1 + off[u]) : zero;
         }
-        if constexpr (kDense) du[u] = (ok[u] && dact) ? *reinterpret_cast<const uint4*>(dact + off[u]) : zero;
+        if constexpr (kDense) du[u] = dact ? ldg16(dact + off[u]) : zero;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -549,7 +556,7 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
           if constexpr (kDense) {
           if (bias) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) a[e] += bias[nc + e];
+            for (int e = 0; e < 8; ++e) a[e] += bz[e];
           }
           if (preact) *reinterpret_cast<uint4*>(preact + off[u]) = pack8(a);
           if (act == 1) {
