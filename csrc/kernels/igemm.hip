@@ -1088,22 +1088,22 @@ namespace {
 __global__ void __launch_bounds__(256)
 splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n4, int splits,
                      long slab4, int accumulate) {
-  const float4* w4 = reinterpret_cast<const float4*>(ws);
+  // ext-vector loads (HIP's float4 struct loads were not batched by hipcc)
+  typedef float v4 __attribute__((ext_vector_type(4)));
+  const v4* w4 = reinterpret_cast<const v4*>(ws);
+  v4* o4 = reinterpret_cast<v4*>(out);
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    float4 a = accumulate ? reinterpret_cast<const float4*>(out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+    v4 a = accumulate ? o4[i] : (v4){0.f, 0.f, 0.f, 0.f};
+    v4 b = {0.f, 0.f, 0.f, 0.f};
     int k = 0;
     for (; k + 4 <= splits; k += 4) {  // four independent loads in flight
-      const float4 u0 = w4[(k + 0) * slab4 + i], u1 = w4[(k + 1) * slab4 + i];
-      const float4 u2 = w4[(k + 2) * slab4 + i], u3 = w4[(k + 3) * slab4 + i];
-      a.x += u0.x + u1.x; a.y += u0.y + u1.y; a.z += u0.z + u1.z; a.w += u0.w + u1.w;
-      b.x += u2.x + u3.x; b.y += u2.y + u3.y; b.z += u2.z + u3.z; b.w += u2.w + u3.w;
+      const v4 u0 = w4[(k + 0) * slab4 + i], u1 = w4[(k + 1) * slab4 + i];
+      const v4 u2 = w4[(k + 2) * slab4 + i], u3 = w4[(k + 3) * slab4 + i];
+      a += u0 + u1;
+      b += u2 + u3;
     }
-    for (; k < splits; ++k) {
-      const float4 u = w4[k * slab4 + i];
-      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
-    }
-    reinterpret_cast<float4*>(out)[i] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    for (; k < splits; ++k) a += w4[k * slab4 + i];
+    o4[i] = a + b;
   }
 }
 }  // namespace
@@ -1257,21 +1257,34 @@ __global__ void __launch_bounds__(256)
 dense_finalize_kernel(const float* __restrict__ ws, int splits, bf16* __restrict__ C, int ldc,
                       const float* __restrict__ bias, int act, bf16* __restrict__ preact,
                       const bf16* __restrict__ addend, const bf16* __restrict__ dact, int M, int N) {
-  const long n8 = (long)M * (N / 8);
+  typedef float v4 __attribute__((ext_vector_type(4)));
+  const int G = N / 8;
+  const int n8 = M * G;                    // < 2^31 for every dense layer here
   const size_t slab = (size_t)M * N;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
-    const int m = (int)(i / (N / 8)), c = (int)(i % (N / 8)) * 8;
-    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < splits; ++k) {
-      const float4* w4 = reinterpret_cast<const float4*>(ws + k * slab + (size_t)m * N + c);
-      const float4 p = w4[0], q = w4[1];
-      a[0] += p.x; a[1] += p.y; a[2] += p.z; a[3] += p.w;
-      a[4] += q.x; a[5] += q.y; a[6] += q.z; a[7] += q.w;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n8; i += gridDim.x * 256) {
+    const int m = i / G, c = (i - m * G) * 8;
+    const float* base = ws + (size_t)m * N + c;
+    v4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
+    int k = 0;
+    for (; k + 2 <= splits; k += 2) {      // both slabs' loads in flight together
+      const v4 p0 = *reinterpret_cast<const v4*>(base + k * slab);
+      const v4 q0 = *reinterpret_cast<const v4*>(base + k * slab + 4);
+      const v4 p1 = *reinterpret_cast<const v4*>(base + (k + 1) * slab);
+      const v4 q1 = *reinterpret_cast<const v4*>(base + (k + 1) * slab + 4);
+      lo += p0 + p1;
+      hi += q0 + q1;
     }
+    if (k < splits) {
+      lo += *reinterpret_cast<const v4*>(base + k * slab);
+      hi += *reinterpret_cast<const v4*>(base + k * slab + 4);
+    }
+    float a[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     const size_t o = (size_t)m * ldc + c;
     if (bias) {
+      float bz[8];
+      ldg8f(bias + c, bz);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) a[e] += bias[c + e];
+      for (int e = 0; e < 8; ++e) a[e] += bz[e];
     }
     if (preact) *reinterpret_cast<uint4*>(preact + o) = pack8(a);
     if (act == 1) {
@@ -1280,7 +1293,7 @@ dense_finalize_kernel(const float* __restrict__ ws, int splits, bf16* __restrict
     }
     if (dact) {
       float z[8];
-      unpack8(*reinterpret_cast<const uint4*>(dact + o), z);
+      unpack8(ldg16(dact + o), z);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float cdf = 0.5f * (1.f + erff(z[e] * 0.70710678118654752f));
@@ -1289,7 +1302,7 @@ dense_finalize_kernel(const float* __restrict__ ws, int splits, bf16* __restrict
     }
     if (addend) {
       float b[8];
-      unpack8(*reinterpret_cast<const uint4*>(addend + o), b);
+      unpack8(ldg16(addend + o), b);
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[e] += b[e];
     }
