@@ -37,10 +37,18 @@ __host__ __device__ __forceinline__ uint32_t drop_threshold(float p) {
   return (uint32_t)(p * 16777216.0f);
 }
 
+// 8-byte loads through an ext-vector type (see ldg16 in common.h); callers issue them from
+// a clamped, always-valid column so no load sits under a per-lane branch
 __device__ __forceinline__ void load4(const bf16* p, float* f) {
-  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 u = *reinterpret_cast<const u32x2*>(p);
   f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
   f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+__device__ __forceinline__ void load4f(const float* p, float* f) {
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  const f32x4v v = *reinterpret_cast<const f32x4v*>(p);
+  f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
 }
 __device__ __forceinline__ void store4(bf16* p, const float* f) {
   uint2 u;
@@ -68,13 +76,16 @@ ln_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ r, bf16* __re
 #pragma unroll
   for (int k = 0; k < MAXC; ++k) {
     const int c = lane + 64 * k;
+    const size_t o = base + 4 * (c < nch ? c : 0);
+    float xv[4], rr[4];
+    load4(x + o, xv);
+    if (r) load4(r + o, rr);
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[k][e] = 0.f;
     if (c < nch) {
-      load4(x + base + 4 * c, v[k]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[k][e] = xv[e];
       if (r) {
-        float rr[4];
-        load4(r + base + 4 * c, rr);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float q = rr[e];
@@ -102,12 +113,15 @@ ln_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ r, bf16* __re
 #pragma unroll
   for (int k = 0; k < MAXC; ++k) {
     const int c = lane + 64 * k;
+    float ga[4], be[4];
+    load4f(gamma + 4 * (c < nch ? c : 0), ga);
+    load4f(beta + 4 * (c < nch ? c : 0), be);
     if (c < nch) {
       float o[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int col = 4 * c + e;
-        o[e] = (v[k][e] - mean) * rstd * gamma[col] + beta[col];
+        o[e] = (v[k][e] - mean) * rstd * ga[e] + be[e];
         if (thr_out)
           o[e] = keep(seed, salt_out, (uint32_t)(base + col), thr_out) ? o[e] * inv_keep_out : 0.f;
       }
@@ -135,21 +149,34 @@ ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ s, const flo
   for (int k = 0; k < MAXC; ++k)
 #pragma unroll
     for (int e = 0; e < 4; ++e) { dg[k][e] = 0.f; db[k][e] = 0.f; }
+  float gam[MAXC][4];   // this lane's gamma columns, loaded once
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int c = lane + 64 * k;
+    load4f(gamma + 4 * (c < nch ? c : 0), gam[k]);
+  }
   const int waves_total = gridDim.x * (NT / 64);
   for (int row = blockIdx.x * (NT / 64) + wave; row < T; row += waves_total) {
     const size_t base = (size_t)row * H;
     const float mean = mean_in[row], rstd = rstd_in[row];
     float g[MAXC][4], xh[MAXC][4];
     float a = 0.f, b = 0.f;
+    float dv[MAXC][4], svv[MAXC][4];
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {   // every row load in flight before any math
+      const int c = lane + 64 * k;
+      const size_t o = base + 4 * (c < nch ? c : 0);
+      load4(dy + o, dv[k]);
+      load4(s + o, svv[k]);
+    }
 #pragma unroll
     for (int k = 0; k < MAXC; ++k) {
       const int c = lane + 64 * k;
 #pragma unroll
       for (int e = 0; e < 4; ++e) { g[k][e] = 0.f; xh[k][e] = 0.f; }
       if (c < nch) {
-        float d[4], sv[4];
-        load4(dy + base + 4 * c, d);
-        load4(s + base + 4 * c, sv);
+        float* d = dv[k];
+        const float* sv = svv[k];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int col = 4 * c + e;
@@ -157,7 +184,7 @@ ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ s, const flo
           xh[k][e] = (sv[e] - mean) * rstd;
           db[k][e] += d[e];
           dg[k][e] += d[e] * xh[k][e];
-          g[k][e] = d[e] * gamma[col];
+          g[k][e] = d[e] * gam[k][e];
           a += g[k][e];
           b += g[k][e] * xh[k][e];
         }

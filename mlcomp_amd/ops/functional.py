@@ -351,6 +351,13 @@ def stem_s2d(x, pad=3):
     return F.pad(xp, (0, 4)).to(torch.bfloat16).contiguous()
 
 
+def stem_s2d_to_nhwc(xs, pad=3):
+    """Inverse of :func:`stem_s2d`: [N, Hb, Wb, 16] -> the [N, H, W, 3] image (float)."""
+    N, Hb, Wb, _ = xs.shape
+    x = xs[..., :12].float().reshape(N, Hb, Wb, 2, 2, 3).permute(0, 1, 3, 2, 4, 5)
+    return x.reshape(N, 2 * Hb, 2 * Wb, 3)[:, pad:2 * Hb - pad, pad:2 * Wb - pad]
+
+
 def stem_w_to_s2d(w):
     """[Co, Ci<=3, 7, 7] filter -> [Co, 4, 4, 16] space-to-depth filter (see stem_s2d)."""
     Co, Ci = w.shape[:2]

@@ -52,7 +52,7 @@ class NativeSegmentationStep:
         g = torch.Generator(device=self.device)
         g.manual_seed(4321 + rank)
         img = torch.randn(batch, image_size, image_size, 3, device=self.device, generator=g)
-        self.x = torch.nn.functional.pad(img, (0, STEM_CIN - 3)).to(torch.bfloat16).contiguous()
+        self.x = self._prep(torch.nn.functional.pad(img, (0, STEM_CIN - 3)).to(torch.bfloat16).contiguous())
         self.t = synthetic_masks(batch, image_size, self.device, g).reshape(-1).contiguous()
         self.use_graph = use_graph and self.device.type == 'cuda'
         self.warmup_eager = warmup_eager
@@ -60,13 +60,19 @@ class NativeSegmentationStep:
         self.calls = 0
         self._loss = None
 
+    def _prep(self, x_nhwc):
+        """The stem's space-to-depth input layout (see NativeClassifierStep._prep)."""
+        if getattr(self.net.stem, 's2d', False) and x_nhwc.shape[-1] != 16:
+            return Fn.stem_s2d(x_nhwc, 3)
+        return x_nhwc
+
     def load_batch(self, images: torch.Tensor, masks: torch.Tensor):
         """Copy a batch into the static buffers: images NCHW float (or NHWC bf16 padded),
         masks [N, 1, H, W] / [N, H, W] in {0, 1}."""
         x = images
         if x.dim() == 4 and x.shape[1] in (1, 3) and x.dtype != torch.bfloat16:
             x = Fn.nchw_to_nhwc(x.to(self.device, non_blocking=True).float(), pad_to=STEM_CIN)
-        self.x.copy_(x)
+        self.x.copy_(self._prep(x.to(self.device, non_blocking=True)))
         self.t.copy_(masks.to(self.device, non_blocking=True).float().reshape(-1))
 
     def _body(self):

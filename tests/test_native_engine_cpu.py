@@ -30,9 +30,7 @@ def test_native_step_matches_torch_autograd():
                                 num_classes=16, lr=0.1, momentum=0.0, weight_decay=0.0,
                                 use_graph=False)
     # the step keeps its input as the stem's space-to-depth image: undo it (pad 3)
-    xs = step.x[..., :12].float()
-    N_, Hb, Wb, _ = xs.shape
-    x_nhwc = xs.reshape(N_, Hb, Wb, 2, 2, 3).permute(0, 1, 3, 2, 4, 5).reshape(N_, 2 * Hb, 2 * Wb, 3)[:, 3:-3, 3:-3]
+    x_nhwc = Fn.stem_s2d_to_nhwc(step.x)
     x = x_nhwc.permute(0, 3, 1, 2).contiguous()
     y = step.y
     ref.train()

@@ -4,6 +4,7 @@ import torch
 
 from mlcomp_amd.contrib.criterion import BCEDiceLoss
 from mlcomp_amd.contrib.segmentation.models import Unet
+from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops import seg
 from mlcomp_amd.train.native_seg_step import NativeSegmentationStep
 
@@ -54,7 +55,7 @@ def test_native_unet_matches_torch_autograd():
                 m.weight.uniform_(0.5, 1.5)
     ref.load_state_dict(tm.state_dict())
     step = NativeSegmentationStep(torch_model=tm, batch=2, image_size=64, device='cpu', lr=1e-3, use_graph=False)
-    x = step.x[..., :3].float().permute(0, 3, 1, 2).contiguous()
+    x = Fn.stem_s2d_to_nhwc(step.x).permute(0, 3, 1, 2).contiguous()   # the step holds the s2d image
     t = step.t.view(2, 1, 64, 64)
     ref.train()
     loss = BCEDiceLoss()(ref(x), t)
@@ -77,7 +78,7 @@ def test_native_unet_matches_torch_autograd():
     assert _cos(g, ref.decoder.blocks[0].convs[0][0].weight.grad) > 0.8
     g = a['encoder.body.layer2.0.cb1.conv.weight'].grad.permute(0, 3, 1, 2)
     assert _cos(g, ref.encoder.body.layer2[0].cb1.conv.weight.grad) > 0.8
-    g = a['encoder.body.stem.conv.weight'].grad[..., :3].permute(0, 3, 1, 2)
+    g = Fn.stem_w_from_s2d(a['encoder.body.stem.conv.weight'].grad)
     assert _cos(g, ref.encoder.body.stem.conv.weight.grad) > 0.8
     # a full step trains
     losses = []
