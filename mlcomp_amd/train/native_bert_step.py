@@ -9,6 +9,7 @@ advanced inside the graph.
 from __future__ import annotations
 
 import os
+import warnings
 from typing import Optional
 
 import torch
@@ -95,9 +96,18 @@ class NativeBertStep:
                 torch.cuda.current_stream(self.device).wait_stream(s)
                 return
             torch.cuda.synchronize(self.device)
-            self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            graph = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(graph):
+                    self._body()
+            except RuntimeError as e:   # capture refused (e.g. a collective the runtime
+                # cannot capture): keep training eagerly instead of failing the task
+                warnings.warn(f'HIP graph capture failed, running the step eagerly: {e}')
+                torch.cuda.synchronize(self.device)
+                self.use_graph = False
                 self._body()
+                return
+            self.graph = graph
         self.graph.replay()
 
     def set_lr(self, lr):
