@@ -174,7 +174,7 @@ def test_cli_commands(mlc_root, monkeypatch, tmp_path):
     d.mkdir()
     (d / 'config.yml').write_text(yaml.safe_dump(
         {'info': {'name': 'cli', 'project': 'pcli'},
-         'executors': {'a': {'type': 'bash', 'command': 'echo $msg > out.txt', 'msg': 'hi'}}}))
+         'executors': {'a': {'type': 'bash', 'command': f'echo $msg > {d / "out.txt"}', 'msg': 'hi'}}}))
     res = r.invoke(main, ['dag', str(d / 'config.yml'), '--params', 'executors/a/msg:yo'])
     assert res.exit_code == 0, res.output
     res = r.invoke(main, ['execute', str(d / 'config.yml')])
