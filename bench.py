@@ -33,8 +33,8 @@ BASELINE_VALUE = None
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
-    p.add_argument('--steps', type=int, default=20)
-    p.add_argument('--warmup', type=int, default=5)
+    p.add_argument('--steps', type=int, default=50)
+    p.add_argument('--warmup', type=int, default=10)
     p.add_argument('--batch', type=int, default=None, help='per-GPU batch (256 images / 32 sequences)')
     p.add_argument('--seq-len', type=int, default=128, help='BERT sequence length')
     p.add_argument('--model', default='resnet50')
