@@ -12,7 +12,9 @@
 //   PING                           -> PONG
 //   STATS                          -> OK {"queues":..,"leased":..,"results":..,"clients":..}
 // A leased message whose consumer disconnects before ACK is re-queued at the head of
-// its queue, so a crashed worker never loses a task.  Waiters are served FIFO.
+// its queue (and handed to a blocked POP waiter right away), so a crashed worker never
+// loses a task.  Waiters are served FIFO.  Requests a client sent before half-closing
+// its socket are still executed and answered.
 //
 // usage: mlcomp-broker [--host 127.0.0.1] [--port 6380]
 #include <arpa/inet.h>
@@ -81,6 +83,7 @@ class Broker {
   std::unordered_map<std::string, std::string> results_;
   std::unordered_map<int, std::unique_ptr<Conn>> conns_;
   std::list<Waiter> waiters_;
+  bool need_wake_ = false;  // set by close_conn (re-queued leases); drained by run()
 
   void accept_all();
   void on_read(Conn* c);
@@ -148,7 +151,10 @@ void Broker::close_conn(Conn* c) {
     if (l == leased_.end()) continue;
     queues_[l->second.queue].push_front(l->second);
     leased_.erase(l);
+    need_wake_ = true;
   }
+  // waiters are woken from run(), not here: close_conn can be reached from flush()
+  // inside wake(), whose iterator a nested wake() would invalidate
   epoll_ctl(ep_, EPOLL_CTL_DEL, c->fd, nullptr);
   close(c->fd);
 }
@@ -323,10 +329,11 @@ void Broker::handle(Conn* c, const std::string& line) {
 
 void Broker::on_read(Conn* c) {
   char buf[65536];
+  bool eof = false;
   for (;;) {
     ssize_t n = recv(c->fd, buf, sizeof(buf), 0);
     if (n > 0) { c->in.append(buf, (size_t)n); continue; }
-    if (n == 0) { close_conn(c); return; }
+    if (n == 0) { eof = true; break; }  // peer half-closed: serve what it sent first
     if (errno == EAGAIN || errno == EWOULDBLOCK) break;
     close_conn(c);
     return;
@@ -341,6 +348,7 @@ void Broker::on_read(Conn* c) {
   }
   if (c->in.size() > (64u << 20)) { close_conn(c); return; }
   flush(c);
+  if (eof) close_conn(c);
 }
 
 // SIGTERM / SIGINT end the event loop so the broker exits through its destructors (a
@@ -365,13 +373,13 @@ void Broker::run() {
       auto it = conns_.find(fd);
       if (it == conns_.end()) continue;
       Conn* c = it->second.get();
-      if (events[i].events & (EPOLLERR | EPOLLHUP)) { close_conn(c); }
-      else {
-        if (events[i].events & EPOLLIN) on_read(c);
-        if (!c->closed && (events[i].events & EPOLLOUT)) flush(c);
-        if (!c->closed && (events[i].events & EPOLLRDHUP)) close_conn(c);
-      }
+      if (events[i].events & EPOLLERR) { close_conn(c); continue; }
+      // EPOLLIN / EPOLLRDHUP / EPOLLHUP: read to EOF (on_read parses and answers the
+      // complete requests still buffered, then closes)
+      if (events[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP)) on_read(c);
+      if (!c->closed && (events[i].events & EPOLLOUT)) flush(c);
     }
+    while (need_wake_) { need_wake_ = false; wake(); }
     expire();
     // a waiter that got its answer may have more pipelined requests queued
     for (auto it = conns_.begin(); it != conns_.end();) {

@@ -172,28 +172,38 @@ class BrokerClient(Broker):
 
     def close(self):
         with self._lock:
-            if self._sock:
-                try:
-                    self._sock.close()
-                except OSError:
-                    pass
-            self._sock = self._rf = None
+            self._drop()
+
+    # safe to re-send after a lost reply: a POP lease dies with the old connection (the
+    # broker re-queues it), the others do not change state twice.  PUSH / SET / NACK /
+    # REVOKE are retried only when the request never reached the socket.
+    IDEMPOTENT = frozenset(('PING', 'POP', 'LEN', 'ACK', 'STATS'))
+
+    def _drop(self):
+        if self._sock is not None:
+            try:
+                self._sock.close()
+            except OSError:
+                pass
+        self._sock = self._rf = None
 
     def _cmd(self, *parts: str) -> str:
         line = (' '.join(parts) + '\n').encode()
         with self._lock:
             for attempt in (0, 1):
+                sent = False
                 try:
                     if self._sock is None:
                         self._connect()
                     self._sock.sendall(line)
+                    sent = True
                     resp = self._rf.readline()
                     if not resp:
                         raise ConnectionError('broker closed the connection')
                     break
                 except (OSError, ConnectionError):
-                    self._sock = self._rf = None
-                    if attempt:
+                    self._drop()
+                    if attempt or (sent and parts[0] not in self.IDEMPOTENT):
                         raise
         resp = resp.decode().rstrip('\n')
         if resp.startswith('ERR'):

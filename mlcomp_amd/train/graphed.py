@@ -1,0 +1,82 @@
+"""Shared driver of the native training steps: eager warmup -> one HIP-graph capture ->
+replay, with a collective fallback to eager execution.
+
+The three native steps (:class:`~mlcomp_amd.train.native_step.NativeClassifierStep`,
+:class:`~mlcomp_amd.train.native_bert_step.NativeBertStep`,
+:class:`~mlcomp_amd.train.native_seg_step.NativeSegmentationStep`) implement ``_body()``
+(zero grads, forward, backward with bucketed all-reduce, fused optimizer) and inherit the
+step protocol from :class:`GraphedStep`:
+
+* every call first runs the optimizer's host-side ``prepare()`` (step counter, Adam bias
+  corrections written into device memory), so graph replays see a fresh step each time;
+* ``warmup_eager`` calls run ``_body()`` eagerly on a side stream (allocator warmup, lazy
+  kernel-library init), then the next call captures ``_body()`` into one graph;
+* if capture fails on ANY rank, every rank discards its graph and runs eagerly from then
+  on.  Capture records work without executing it, so no device state (and no collective)
+  has moved when the failure is seen; the ranks agree with one all-reduce of a flag before
+  anything runs, which keeps the collective sequence identical on every rank.  Host state
+  that ``_body()`` touched (bucket counters) is reset by ``_body()`` itself on the retry.
+"""
+from __future__ import annotations
+
+import warnings
+
+import torch
+
+
+class GraphedStep:
+    use_graph: bool
+    warmup_eager: int
+    graph = None
+    calls: int = 0
+    comm = None
+    capture_error = None
+
+    def _body(self):  # pragma: no cover - implemented by the concrete steps
+        raise NotImplementedError
+
+    def _agree(self, ok: bool) -> bool:
+        """True only when every rank reports ``ok`` (one MIN all-reduce of a flag)."""
+        if self.comm is None or getattr(self.comm, 'world', 1) <= 1:
+            return ok
+        flag = torch.tensor([1.0 if ok else 0.0], device=self.device)
+        self.comm.all_reduce(flag, 'min')
+        return bool(flag.item() > 0.5)
+
+    def _capture(self):
+        torch.cuda.synchronize(self.device)
+        graph = torch.cuda.CUDAGraph()
+        err = None
+        try:
+            with torch.cuda.graph(graph):
+                self._body()
+        except Exception as e:   # capture refused (a collective or op the runtime cannot
+            err = e              # capture): decided collectively below
+        torch.cuda.synchronize(self.device)
+        if self._agree(err is None):
+            return graph
+        self.capture_error = err if err is not None else RuntimeError('capture failed on a peer rank')
+        warnings.warn(f'HIP graph capture failed, running the step eagerly: {self.capture_error}')
+        del graph
+        return None
+
+    def __call__(self):
+        self.calls += 1
+        self.opt.prepare()
+        if not self.use_graph:
+            self._body()
+            return
+        if self.graph is None:
+            if self.calls <= self.warmup_eager:
+                s = torch.cuda.Stream(self.device)
+                s.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(s):
+                    self._body()
+                torch.cuda.current_stream(self.device).wait_stream(s)
+                return
+            self.graph = self._capture()
+            if self.graph is None:
+                self.use_graph = False
+                self._body()
+                return
+        self.graph.replay()

@@ -9,7 +9,6 @@ advanced inside the graph.
 from __future__ import annotations
 
 import os
-import warnings
 from typing import Optional
 
 import torch
@@ -18,10 +17,11 @@ from mlcomp_amd.models import build_model
 from mlcomp_amd.models.native_bert import NativeBert
 from mlcomp_amd.parallel.comm import make_comm
 from mlcomp_amd.parallel.ddp import GradBucketer
+from mlcomp_amd.train.graphed import GraphedStep
 from mlcomp_amd.train.optim import FusedAdam
 
 
-class NativeBertStep:
+class NativeBertStep(GraphedStep):
     def __init__(self, model_name='bert-base', batch=32, seq_len=128, device=None, world_size=1, use_graph=True,
                  num_labels=2, lr=2e-5, weight_decay=0.01, betas=(0.9, 0.999), eps=1e-6, seed=0, warmup_eager=2,
                  torch_model=None, dropout: Optional[float] = None, comm=None):
@@ -80,35 +80,6 @@ class NativeBertStep:
         loss.backward()
         self.bucketer.finish()
         self.opt.step()
-
-    def __call__(self):
-        self.calls += 1
-        self.opt.prepare()
-        if not self.use_graph:
-            self._body()
-            return
-        if self.graph is None:
-            if self.calls <= self.warmup_eager:
-                s = torch.cuda.Stream(self.device)
-                s.wait_stream(torch.cuda.current_stream(self.device))
-                with torch.cuda.stream(s):
-                    self._body()
-                torch.cuda.current_stream(self.device).wait_stream(s)
-                return
-            torch.cuda.synchronize(self.device)
-            graph = torch.cuda.CUDAGraph()
-            try:
-                with torch.cuda.graph(graph):
-                    self._body()
-            except RuntimeError as e:   # capture refused (e.g. a collective the runtime
-                # cannot capture): keep training eagerly instead of failing the task
-                warnings.warn(f'HIP graph capture failed, running the step eagerly: {e}')
-                torch.cuda.synchronize(self.device)
-                self.use_graph = False
-                self._body()
-                return
-            self.graph = graph
-        self.graph.replay()
 
     def set_lr(self, lr):
         self.opt.set_lr(lr)

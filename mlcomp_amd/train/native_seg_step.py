@@ -8,7 +8,6 @@ after ``warmup_eager`` eager steps, exactly like :class:`NativeClassifierStep`.
 from __future__ import annotations
 
 import os
-import warnings
 from typing import Optional
 
 import torch
@@ -18,6 +17,7 @@ from mlcomp_amd.models.native_unet import NativeUnet
 from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.parallel.comm import make_comm
 from mlcomp_amd.parallel.ddp import GradBucketer
+from mlcomp_amd.train.graphed import GraphedStep
 from mlcomp_amd.train.optim import FusedAdam, FusedSGD
 
 
@@ -28,7 +28,7 @@ def synthetic_masks(batch, size, device, generator):
     return (m > 0.3).float()
 
 
-class NativeSegmentationStep:
+class NativeSegmentationStep(GraphedStep):
     def __init__(self, encoder='resnet34', batch=32, image_size=256, device=None, world_size=1, use_graph=True,
                  lr=3e-4, weight_decay=0.0, optimizer='Adam', momentum=0.9, betas=(0.9, 0.999), eps=1e-8,
                  seed=0, warmup_eager=2, torch_model=None, comm=None):
@@ -85,36 +85,6 @@ class NativeSegmentationStep:
         self.bucketer.finish()
         self.opt.step()
         self._loss = loss.detach()
-
-    def __call__(self):
-        self.calls += 1
-        if hasattr(self.opt, 'prepare'):
-            self.opt.prepare()
-        if not self.use_graph:
-            self._body()
-            return
-        if self.graph is None:
-            if self.calls <= self.warmup_eager:
-                s = torch.cuda.Stream(self.device)
-                s.wait_stream(torch.cuda.current_stream(self.device))
-                with torch.cuda.stream(s):
-                    self._body()
-                torch.cuda.current_stream(self.device).wait_stream(s)
-                return
-            torch.cuda.synchronize(self.device)
-            graph = torch.cuda.CUDAGraph()
-            try:
-                with torch.cuda.graph(graph):
-                    self._body()
-            except RuntimeError as e:   # capture refused (e.g. a collective the runtime
-                # cannot capture): keep training eagerly instead of failing the task
-                warnings.warn(f'HIP graph capture failed, running the step eagerly: {e}')
-                torch.cuda.synchronize(self.device)
-                self.use_graph = False
-                self._body()
-                return
-            self.graph = graph
-        self.graph.replay()
 
     def set_lr(self, lr):
         self.opt.set_lr(lr)

@@ -12,7 +12,6 @@ new batch into them (outside the graph) for real-data training.
 from __future__ import annotations
 
 import os
-import warnings
 from typing import Optional
 
 import torch
@@ -22,10 +21,11 @@ from mlcomp_amd.models.native_resnet import STEM_CIN, NativeResNet
 from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.parallel.comm import make_comm
 from mlcomp_amd.parallel.ddp import GradBucketer
+from mlcomp_amd.train.graphed import GraphedStep
 from mlcomp_amd.train.optim import FusedAdam, FusedSGD
 
 
-class NativeClassifierStep:
+class NativeClassifierStep(GraphedStep):
     def __init__(self, model_name='resnet50', batch=256, image_size=224, device=None,
                  world_size=1, use_graph=True, num_classes=1000, lr=0.1, momentum=0.9,
                  weight_decay=5e-5, nesterov=False, smoothing=0.0, seed=0, warmup_eager=2,
@@ -87,36 +87,6 @@ class NativeClassifierStep:
         self.bucketer.finish()
         self.opt.step()
         self._loss = self.net.head.loss_sum()
-
-    def __call__(self):
-        self.calls += 1
-        if hasattr(self.opt, 'prepare'):
-            self.opt.prepare()  # Adam bias corrections live in device memory (graph-safe)
-        if not self.use_graph:
-            self._body()
-            return
-        if self.graph is None:
-            if self.calls <= self.warmup_eager:
-                s = torch.cuda.Stream(self.device)
-                s.wait_stream(torch.cuda.current_stream(self.device))
-                with torch.cuda.stream(s):
-                    self._body()
-                torch.cuda.current_stream(self.device).wait_stream(s)
-                return
-            torch.cuda.synchronize(self.device)
-            graph = torch.cuda.CUDAGraph()
-            try:
-                with torch.cuda.graph(graph):
-                    self._body()
-            except RuntimeError as e:   # capture refused (e.g. a collective the runtime
-                # cannot capture): keep training eagerly instead of failing the task
-                warnings.warn(f'HIP graph capture failed, running the step eagerly: {e}')
-                torch.cuda.synchronize(self.device)
-                self.use_graph = False
-                self._body()
-                return
-            self.graph = graph
-        self.graph.replay()
 
     def set_lr(self, lr):
         self.opt.set_lr(lr)

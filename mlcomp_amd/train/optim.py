@@ -4,6 +4,11 @@ One kernel launch per arena per step (`csrc/kernels/optim.hip`).  The learning r
 gradient scale live in a small device tensor (``hyper``) so a HIP-graph-captured step
 picks up LR-schedule changes without re-capture: ``set_lr`` is a tiny H2D copy outside
 the graph.
+
+Step counting is host work: ``prepare()`` runs once per training step on the host
+(outside any captured graph) and advances ``steps``; ``step()`` only enqueues the update
+kernels, so a graph that captured ``step()`` once and is replayed N times still sees N
+distinct bias corrections.
 """
 from __future__ import annotations
 
@@ -13,7 +18,24 @@ from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops.arena import ParamArena
 
 
-class FusedSGD:
+class _ArenaStateMixin:
+    """Checkpointable optimizer state: the step counter and every arena state buffer
+    (momentum / Adam moments) as CPU tensors, keyed ``<arena>.<buffer>``."""
+
+    def state_dict(self) -> dict:
+        bufs = {f'{a.name}.{k}': v.detach().cpu() for a in self.arena.arenas() for k, v in a.state.items()}
+        return {'steps': int(self.steps), 'buffers': bufs}
+
+    def load_state_dict(self, d: dict):
+        self.steps = int(d.get('steps', 0))
+        for a in self.arena.arenas():
+            for k, v in a.state.items():
+                src = d.get('buffers', {}).get(f'{a.name}.{k}')
+                if src is not None and src.numel() == v.numel():
+                    v.copy_(src.to(v.device))
+
+
+class FusedSGD(_ArenaStateMixin):
     def __init__(self, arena: ParamArena, lr=0.1, momentum=0.9, weight_decay=0.0,
                  nesterov=False, dampening=0.0, grad_scale=1.0):
         self.arena = arena
@@ -35,6 +57,10 @@ class FusedSGD:
     def set_grad_scale(self, s):
         self.hyper[1].fill_(s)
 
+    def prepare(self):
+        """Host side of one step (call once per step, outside any graph)."""
+        self.steps += 1
+
     def step(self):
         # the first step seeds momentum = grad (torch.optim.SGD semantics); with zeroed
         # buffers "mu*0 + (1-dampening)*g" equals that when dampening == 0, which keeps
@@ -43,10 +69,9 @@ class FusedSGD:
             Fn.sgd_step(a.master, a.grad, a.state['momentum'], a.mirror, self.hyper,
                         a.numel if a.decay else 0, a.numel if a.mirror is not None else 0,
                         self.momentum, self.dampening, self.wd, self.nesterov, False)
-        self.steps += 1
 
 
-class FusedAdam:
+class FusedAdam(_ArenaStateMixin):
     def __init__(self, arena: ParamArena, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
                  weight_decay=0.0, decoupled=True, grad_scale=1.0):
         self.arena = arena
@@ -70,8 +95,10 @@ class FusedAdam:
         self.hyper[1].fill_(s)
 
     def prepare(self):
-        """Update the bias corrections for the coming step (outside any graph)."""
-        t = self.steps + 1
+        """Advance the step counter and write the bias corrections of the coming step
+        into ``hyper`` (a host->device fill, outside any graph)."""
+        self.steps += 1
+        t = self.steps
         self.hyper[2].fill_(1 - self.b1 ** t)
         self.hyper[3].fill_(1 - self.b2 ** t)
 
@@ -81,4 +108,3 @@ class FusedAdam:
                          self.hyper, a.numel if a.decay else 0,
                          a.numel if a.mirror is not None else 0, self.b1, self.b2, self.eps,
                          self.wd, self.decoupled)
-        self.steps += 1

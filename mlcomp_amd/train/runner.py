@@ -134,6 +134,8 @@ class Runner:
         self.state.rank, self.state.world_size = rank, world_size
         self.state.logdir = experiment.logdir
         self.exception = None
+        self._resume_ckpt: Optional[dict] = None   # applied at the start of the first stage
+        self._native_opt_state: Optional[dict] = None  # applied when the native step is built
 
     # ------------------------------------------------------------------ setup
     def _build_model(self, stage):
@@ -167,9 +169,7 @@ class Runner:
                 world_size=self.world_size, num_labels=self.model.config.num_labels, lr=spec.get('lr', 2e-5),
                 weight_decay=spec.get('weight_decay', 0.01), betas=tuple(spec.get('betas', (0.9, 0.999))),
                 eps=spec.get('eps', 1e-6), use_graph=self.experiment.args.get('graph', True))
-            dummy = torch.zeros(1, requires_grad=True)
-            self.optimizer = torch.optim.SGD([dummy], lr=spec.get('lr', 2e-5))
-            self.scheduler = self.experiment.get_scheduler(stage, self.optimizer)
+            self._apply_native_opt_state()
             return
         if self.native_kind == 'unet':
             from .native_seg_step import NativeSegmentationStep
@@ -182,9 +182,7 @@ class Runner:
                 momentum=spec.get('momentum', 0.9), weight_decay=spec.get('weight_decay', 0.0),
                 betas=tuple(spec.get('betas', (0.9, 0.999))), eps=spec.get('eps', 1e-8),
                 use_graph=self.experiment.args.get('graph', True))
-            dummy = torch.zeros(1, requires_grad=True)
-            self.optimizer = torch.optim.SGD([dummy], lr=spec.get('lr', 3e-4))
-            self.scheduler = self.experiment.get_scheduler(stage, self.optimizer)
+            self._apply_native_opt_state()
             return
         from .native_step import NativeClassifierStep
         name = spec.get('optimizer', 'SGD')
@@ -197,10 +195,21 @@ class Runner:
             weight_decay=spec.get('weight_decay', 0.0), nesterov=spec.get('nesterov', False),
             use_graph=self.experiment.args.get('graph', True), optimizer=name,
             betas=tuple(spec.get('betas', (0.9, 0.999))), eps=spec.get('eps', 1e-8))
-        # a torch optimizer over one dummy tensor drives torch LR schedulers
+        self._apply_native_opt_state()
+
+    def _native_sched(self, stage):
+        """Native engines: a torch optimizer over one dummy tensor carries the LR and drives
+        the torch LR schedulers (built with the stage, before the first batch, so a resumed
+        scheduler/LR state can be loaded into it)."""
+        lr = self.experiment.optimizer_spec(stage).get('lr', 0.1)
         dummy = torch.zeros(1, requires_grad=True)
-        self.optimizer = torch.optim.SGD([dummy], lr=spec.get('lr', 0.1))
+        self.optimizer = torch.optim.SGD([dummy], lr=lr)
         self.scheduler = self.experiment.get_scheduler(stage, self.optimizer)
+
+    def _apply_native_opt_state(self):
+        if self._native_opt_state is not None and self.native_step is not None:
+            self.native_step.opt.load_state_dict(self._native_opt_state)
+            self._native_opt_state = None
 
     def sync_lr(self):
         if self.native_step is not None:
@@ -250,20 +259,40 @@ class Runner:
                 'model_state_dict': {k: v.detach().cpu() for k, v in self.model.state_dict().items()},
                 'optimizer_state_dict': self.optimizer.state_dict() if self.optimizer else None,
                 'scheduler_state_dict': self.scheduler.state_dict() if self.scheduler else None,
+                'native_optimizer': self.native_step.opt.state_dict() if self.native_step is not None else None,
                 'checkpoint_data': dict(self.state.checkpoint_data, epoch=self.state.epoch),
                 'epoch_metrics': dict(self.state.epoch_metrics),
                 'valid_metrics': dict(self.state.valid_metrics)}
 
+    def resume(self, ckpt_or_path):
+        """Resume mid-stage (`catalyst_.py:341-345` hands the checkpoint to Catalyst's
+        CheckpointCallback): weights, optimizer moments (torch or native arenas), LR
+        scheduler position and the best score are restored when the first stage starts,
+        on every rank."""
+        if isinstance(ckpt_or_path, str):
+            from .callbacks import load_checkpoint
+            _, ckpt_or_path = load_checkpoint(ckpt_or_path)
+        self._resume_ckpt = ckpt_or_path
+
     def load_checkpoint(self, ckpt: dict):
+        """Full state restore into the built stage (model, optimizer, scheduler)."""
         self.model.load_state_dict(ckpt['model_state_dict'])
-        if self.native_step is not None:
-            self.native_step = None  # rebuilt from the loaded weights on the next batch
-        if ckpt.get('optimizer_state_dict') and self.optimizer is not None and self.native_step is None \
-                and not self.state.native:
+        if self.state.native:
+            # the native step is (re)built from the loaded weights on the next batch; its
+            # arena optimizer state is applied right after it is built
+            self.native_step = None
+            self._native_opt_state = ckpt.get('native_optimizer')
+        if ckpt.get('optimizer_state_dict') and self.optimizer is not None:
             try:
                 self.optimizer.load_state_dict(ckpt['optimizer_state_dict'])
-            except ValueError:
+            except (ValueError, KeyError):
                 pass
+        if ckpt.get('scheduler_state_dict') and self.scheduler is not None:
+            self.scheduler.load_state_dict(ckpt['scheduler_state_dict'])
+        from .callbacks import CheckpointCallback
+        for c in getattr(self, 'callbacks', []):
+            if isinstance(c, CheckpointCallback):
+                c.best_score = ckpt.get('best_score')
 
     # ------------------------------------------------------------------ loops
     def _run_batch_torch(self, batch):
@@ -417,9 +446,16 @@ class Runner:
             self.scheduler = self.experiment.get_scheduler(stage, self.optimizer)
         else:
             self.native_step = None
+            self._native_sched(stage)
         self.loaders = self._loaders(stage)
         st.loaders = self.loaders
         self.callbacks = self._callbacks(stage)
+        if self._resume_ckpt is not None:
+            ck, self._resume_ckpt = self._resume_ckpt, None
+            if ck.get('stage') in (None, stage):
+                self.load_checkpoint(ck)
+            else:   # the checkpointed stage had finished: carry the weights only
+                self.model.load_state_dict(ck['model_state_dict'])
         self._fire('on_stage_start')
         for epoch in range(start_epoch, st.num_epochs):
             st.epoch = epoch

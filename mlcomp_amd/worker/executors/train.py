@@ -253,10 +253,9 @@ class Train(Executor):
         device = torch.device('cuda', 0) if torch.cuda.is_available() else torch.device('cpu')
         runner = Runner(experiment, device=device, extra_callbacks=extra, rank=rank, world_size=world)
         if self.resume_path:
-            from mlcomp_amd.train.callbacks import load_checkpoint
-            runner.model = experiment.get_model(stages[0])
-            _, ck = load_checkpoint(self.resume_path)
-            runner.model.load_state_dict(ck['model_state_dict'])
+            # full state (weights, optimizer, LR schedule, best score), applied when the
+            # first remaining stage starts
+            runner.resume(self.resume_path)
         runner.run_experiment(stages, start_epoch=start_epoch)
         if self.master and self.trace:
             model = runner.model.eval().cpu().float()

@@ -128,3 +128,56 @@ def test_lease_requeued_when_consumer_dies(daemon):
         time.sleep(0.02)
     q, m2 = a.pop(['jobs'], 1.0)
     assert m2['args'] == [7]
+
+
+def test_dead_consumer_lease_goes_to_blocked_waiter(daemon):
+    """A consumer dies holding a lease while another is blocked in POP: the re-queued
+    message must reach the waiter immediately, not at the next PUSH or its timeout."""
+    a = BrokerClient('127.0.0.1', daemon)
+    a.push('jobs2', {'task': 'execute', 'args': [9]})
+    dying = BrokerClient('127.0.0.1', daemon)
+    assert dying.pop(['jobs2'], 1.0)[1]['args'] == [9]
+    waiter = BrokerClient('127.0.0.1', daemon)
+    got = []
+    t0 = time.time()
+    t = threading.Thread(target=lambda: got.append(waiter.pop(['jobs2'], 8.0)))
+    t.start()
+    time.sleep(0.3)
+    dying.close()
+    t.join(10)
+    assert got and got[0] is not None and got[0][1]['args'] == [9]
+    assert time.time() - t0 < 4.0
+
+
+def test_request_before_half_close_is_served(daemon):
+    s = socket.create_connection(('127.0.0.1', daemon))
+    s.sendall(b'PUSH half {"task":"x"}\n')
+    s.shutdown(socket.SHUT_WR)
+    reply = s.makefile('rb').readline()
+    s.close()
+    assert reply.startswith(b'OK ')
+    assert BrokerClient('127.0.0.1', daemon).queue_len('half') == 1
+
+
+def test_client_does_not_resend_non_idempotent_push(daemon):
+    c = BrokerClient('127.0.0.1', daemon)
+    c.ping()
+
+    class LostReply:
+        """The request reaches the broker, the reply is lost."""
+        def __init__(self, sock):
+            self.sock = sock
+
+        def sendall(self, data):
+            self.sock.sendall(data)
+
+        def close(self):
+            self.sock.close()
+
+    real = c._sock
+    c._sock = LostReply(real)
+    c._rf = type('R', (), {'readline': lambda self: b''})()
+    with pytest.raises((ConnectionError, OSError)):
+        c.push('once', {'task': 'y'})
+    time.sleep(0.1)
+    assert BrokerClient('127.0.0.1', daemon).queue_len('once') == 1

@@ -222,3 +222,46 @@ def test_native_engines_data_parallel_two_ranks(tmp_path, kind):
     b = torch.load(tmp_path / f'{kind}1.pt', weights_only=True)
     assert torch.isfinite(a['w']).all() and a['g'].abs().sum() > 0
     assert torch.allclose(a['g'], b['g']) and torch.allclose(a['w'], b['w'])
+
+
+def test_resume_mid_stage_restores_optimizer_schedule_and_best(tmp_path):
+    """Resuming at epoch k restores the optimizer moments, the LR-schedule position and the
+    best score (`catalyst_.py:341-345`), so a worse first resumed epoch does not overwrite
+    best_full.pth."""
+    sched = {'scheduler': 'StepLR', 'step_size': 1, 'gamma': 0.5}
+    torch.manual_seed(0)
+    r = Runner(ConfigExperiment(_cfg(tmp_path, epochs=2, sched=sched)), device='cpu')
+    r.run_experiment()
+    ck = tmp_path / 'checkpoints'
+    d = torch.load(ck / 'last_full.pth', map_location='cpu', weights_only=True)
+    assert d['checkpoint_data']['epoch'] == 1 and d['best_score'] is not None
+    # pretend the best score so far was unbeatable: a resumed epoch must not replace it
+    d['best_score'] = 2.0
+    torch.save(d, ck / 'last_full.pth')
+    best_before = (ck / 'best_full.pth').read_bytes()
+    r2 = Runner(ConfigExperiment(_cfg(tmp_path, epochs=3, sched=sched)), device='cpu')
+    r2.resume(str(ck / 'last_full.pth'))
+    seen = {}
+
+    class Probe:
+        order = 1
+        master_only = False
+
+        def __getattr__(self, name):
+            return lambda state: None
+
+        def on_epoch_start(self, state):
+            seen.setdefault('lr', state.current_lr())
+            seen.setdefault('exp_avg', [v['exp_avg'].clone() for v in state.optimizer.state.values()])
+
+    r2.extra_callbacks['probe'] = Probe()
+    st = r2.run_experiment(start_epoch=2)
+    assert st.epoch == 2
+    assert abs(seen['lr'] - 0.01 * 0.5 ** 2) < 1e-9          # StepLR position carried over
+    opt_state = d['optimizer_state_dict']['state']
+    assert len(seen['exp_avg']) == len(opt_state) > 0
+    for got, ref in zip(seen['exp_avg'], [v['exp_avg'] for v in opt_state.values()]):
+        assert torch.equal(got, ref)                             # Adam moments restored
+    saver = [c for c in r2.callbacks if type(c).__name__ == 'CheckpointCallback'][0]
+    assert saver.best_score == 2.0
+    assert (ck / 'best_full.pth').read_bytes() == best_before
