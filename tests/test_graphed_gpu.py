@@ -31,9 +31,14 @@ def _rel(a, b):
     return ((pa - pb).norm() / pa.norm()).item()
 
 
+def _moved(st, p0):
+    return (st.net.arena.decay.master - p0).norm().item()
+
+
 @pytest.mark.parametrize('optimizer', ['Adam', 'AdamW'])
 def test_graph_adam_steps_advance_every_replay(optimizer):
     a, b = _pair(optimizer)
+    p0 = a.net.arena.decay.master.clone()
     for _ in range(ITERS):
         a()
         b()
@@ -42,10 +47,13 @@ def test_graph_adam_steps_advance_every_replay(optimizer):
     assert a.opt.steps == b.opt.steps == ITERS == b.calls
     bc1, bc2 = b.opt.hyper[2].item(), b.opt.hyper[3].item()
     assert abs(bc1 - (1 - 0.9 ** ITERS)) < 1e-6 and abs(bc2 - (1 - 0.999 ** ITERS)) < 1e-6
-    # fp32-atomic split-K / BN reductions differ in the last bits between runs; with the
-    # bias corrections right, graph and eager weights stay within ~1e-4 of each other
-    assert _rel(a, b) < 2e-3, _rel(a, b)
-    assert abs(a.last_loss() - b.last_loss()) < 1e-2 * abs(a.last_loss()) + 1e-3
+    # Adam's update is ~lr*sign(g) for tiny gradients, so the last-bit differences of the
+    # fp32-atomic split-K / BN reductions flip some of them: graph and eager weights drift
+    # apart by ~1-2 %.  A frozen bias correction instead scales every update by ~0.2, which
+    # the distance travelled from the initial weights exposes directly.
+    ma, mb = _moved(a, p0), _moved(b, p0)
+    assert 0.95 < mb / ma < 1.05, (ma, mb)
+    assert _rel(a, b) < 5e-2, _rel(a, b)
 
 
 def test_refused_capture_falls_back_to_matching_eager_steps(monkeypatch):
@@ -62,6 +70,7 @@ def test_refused_capture_falls_back_to_matching_eager_steps(monkeypatch):
 
     monkeypatch.setattr(graphed.torch.cuda, 'graph', refusing)
     a, b = _pair('Adam')
+    p0 = a.net.arena.decay.master.clone()
     with pytest.warns(UserWarning, match='capture failed'):
         for _ in range(ITERS):
             a()
@@ -69,4 +78,6 @@ def test_refused_capture_falls_back_to_matching_eager_steps(monkeypatch):
     torch.cuda.synchronize()
     assert b.graph is None and not b.use_graph and b.capture_error is not None
     assert a.opt.steps == b.opt.steps == ITERS
-    assert _rel(a, b) < 2e-3, _rel(a, b)
+    ma, mb = _moved(a, p0), _moved(b, p0)
+    assert 0.95 < mb / ma < 1.05, (ma, mb)
+    assert _rel(a, b) < 5e-2, _rel(a, b)
