@@ -26,26 +26,12 @@
 // sum / sum-of-squares, spread over NSTAT copies to avoid same-address atomic
 // contention), fp32 atomic add (split-K weight gradients), fp32 store (+bias).
 #include "common.h"
+#include "convgeom.h"
 
 namespace igemm {
 
 constexpr int BK = 64, NTHR = 256;
-constexpr int NSTAT = 32;                          // BN-stat partial copies
 
-// ------------------------------------------------------------------ fast division
-struct FastDiv {
-  unsigned d, mul, sh;
-  __host__ __device__ FastDiv() : d(1), mul(0), sh(0) {}
-  __host__ explicit FastDiv(unsigned dd) : d(dd) {
-    sh = 0;
-    while ((1u << sh) < d) ++sh;
-    mul = (unsigned)((((unsigned long long)1 << 32) * ((1ull << sh) - d)) / d + 1);
-  }
-  __device__ __forceinline__ unsigned div(unsigned n) const { return (__umulhi(n, mul) + n) >> sh; }
-  __device__ __forceinline__ void divmod(unsigned n, unsigned& q, unsigned& r) const {
-    q = div(n); r = n - q * d;
-  }
-};
 
 // ---------------------------------------------------------------- LDS images
 // KC image: [rows][64 k] bf16, 128 B rows, 16 B chunk c of row r stored at
@@ -103,13 +89,6 @@ __device__ __forceinline__ uint4 bload(Rsrc r, unsigned voff) {
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
 }
 
-// ---------------------------------------------------------------- geometry
-struct ConvGeom {
-  int N, H, W, C;      // input NHWC
-  int Ho, Wo, Co;      // output
-  int KH, KW, stride, pad, dil;
-  FastDiv fWo, fHo, fW, fH, fC, fCo, fKW;
-};
 
 // ---------------------------------------------------------------- loaders
 // Thread -> 16 B chunk mapping (chunk i of R/32 per thread), unless a loader overrides
@@ -204,11 +183,6 @@ struct MatMCSum {
 template <class L, class = void> struct HasSum { static constexpr bool value = false; };
 template <class L> struct HasSum<L, decltype((void)L::SUM)> { static constexpr bool value = L::SUM; };
 
-// Per-row tap mask: bit r (r < 15) = filter row r lands inside the input, bit 16+s =
-// filter column s does; a K chunk of tap (r, s) is loaded iff (mask & P) == P with
-// P = 1<<r | 1<<(16+s).  P = 1<<15 (never set) marks a chunk past K.
-__device__ __forceinline__ unsigned tap_pat(int r, int s) { return (1u << r) | (1u << (16 + s)); }
-constexpr unsigned NO_TAP = 1u << 15;
 
 // conv fwd A operand: rows = output pixels (n, ho, wo), k = (r, s, ci), ci fastest.
 // Row offsets are relative to the block's first row; the tap offset is per chunk.
@@ -259,31 +233,6 @@ struct ConvFwdA {
   }
 };
 
-// Transposed-conv (dgrad) geometry of ONE stride-parity class: output rows are the input
-// pixels (n, hi = i*S+ph, wi = j*S+pw), i < Hc, j < Wc.  Only filter taps r = r0 +
-// rstep*a (a < nr), s = s0 + sstep*b (b < ns) reach the class; for them the dy pixel is
-// (i + dh0 - a*dhs, j + dw0 - b*dws).  The K loop runs over (a, b, 64-channel block of
-// Co): K = nr*ns*ncb*64, channels past Co read as zero.
-struct DgradClass {
-  int S, ph, pw, Hc, Wc;
-  FastDiv fWc, fHc;
-  int r0, s0, rstep, sstep, nr, ns, ncb;
-  FastDiv fns, fncb;
-  int dh0, dhs, dw0, dws;
-  long long tmin;      // smallest tap offset (elements), folded into the base
-  __device__ __forceinline__ void decode(int m, int& n, int& i, int& j) const {
-    unsigned t, q, rr;
-    fWc.divmod((unsigned)m, t, rr); j = (int)rr;
-    fHc.divmod(t, q, rr); i = (int)rr; n = (int)q;
-  }
-  // K-tile -> (a, b, first channel)
-  __device__ __forceinline__ void tap(int kt, int& a, int& b, int& co0) const {
-    unsigned t, cb, aa, bb;
-    fncb.divmod((unsigned)kt, t, cb);
-    fns.divmod(t, aa, bb);
-    a = (int)aa; b = (int)bb; co0 = (int)cb * BK;
-  }
-};
 
 template <int R>
 struct ConvDgradA {  // rows = class pixels, k = (a, b, co)
@@ -930,46 +879,10 @@ static int auto_splits(int M, int N, int K, int tile, int target = g_split_targe
 }  // namespace igemm
 
 using namespace igemm;
+using namespace igemm_host;
 
-static ConvGeom mkgeom(int N, int H, int W, int C, int Co, int KH, int KW, int stride, int pad,
-                       int dil, int Ho, int Wo) {
-  ConvGeom g;
-  g.N = N; g.H = H; g.W = W; g.C = C; g.Co = Co; g.KH = KH; g.KW = KW;
-  g.stride = stride; g.pad = pad; g.dil = dil; g.Ho = Ho; g.Wo = Wo;
-  g.fWo = FastDiv(Wo); g.fHo = FastDiv(Ho); g.fW = FastDiv(W); g.fH = FastDiv(H);
-  g.fC = FastDiv(C); g.fCo = FastDiv(Co); g.fKW = FastDiv(KW);
-  return g;
-}
 
-static int gcd_i(int a, int b) { while (b) { const int t = a % b; a = b; b = t; } return a; }
 
-// The stride-parity class (ph, pw) of a dgrad output: the filter taps that reach it form
-// arithmetic progressions r = r0 + rstep*a, s = s0 + sstep*b.  A class no tap reaches has
-// nr*ns == 0 and is still launched (K = 0) so its rows get the epilogue (0 + addend, BN).
-static DgradClass mkclass(int S, int ph, int pw, int H, int W, int Ho, int Wo, int Co, int KH, int KW,
-                          int pad, int dil) {
-  DgradClass c;
-  c.S = S; c.ph = ph; c.pw = pw;
-  c.Hc = (H - ph + S - 1) / S; c.Wc = (W - pw + S - 1) / S;
-  c.fWc = FastDiv(c.Wc > 0 ? c.Wc : 1); c.fHc = FastDiv(c.Hc > 0 ? c.Hc : 1);
-  auto axis = [&](int p, int KK, int& r0, int& step, int& n, int& d0, int& ds) {
-    r0 = -1; n = 0;
-    for (int r = 0; r < KK; ++r)
-      if ((((p + pad - r * dil) % S) + S) % S == 0) { if (r0 < 0) r0 = r; ++n; }
-    step = S / gcd_i(S, dil);
-    if (n == 0) { r0 = 0; d0 = 0; ds = 0; return; }
-    d0 = (p + pad - r0 * dil) / S;
-    ds = step * dil / S;
-  };
-  axis(ph, KH, c.r0, c.rstep, c.nr, c.dh0, c.dhs);
-  axis(pw, KW, c.s0, c.sstep, c.ns, c.dw0, c.dws);
-  c.ncb = (Co + BK - 1) / BK;
-  c.fns = FastDiv(c.ns > 0 ? c.ns : 1); c.fncb = FastDiv(c.ncb);
-  c.tmin = (c.nr > 0 && c.ns > 0)
-               ? ((long long)(c.dh0 - (c.nr - 1) * c.dhs) * Wo + (c.dw0 - (c.ns - 1) * c.dws)) * Co : 0;
-  (void)Ho;
-  return c;
-}
 
 // dispatch one GEMM over the three tile shapes; MK(R) builds the loaders for R rows
 #define MLC_TILE_DISPATCH(TILE, M, N, K, SPLITS, ST, EPI, MKA, MKB)                              \

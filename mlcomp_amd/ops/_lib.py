@@ -24,6 +24,9 @@ _SIGS = {
     'mlc_conv_wgrad': [vp, vp, vp] + [i32] * 14 + [vp, i64, vp],
     'mlc_gemm_f32out': [vp, vp, vp, vp] + [i32] * 11 + [vp],
     'mlc_gemm_bf16out': [vp, vp, vp] + [i32] * 8 + [vp],
+    'mlc_gemm256_nt': [vp, vp, vp, vp] + [i32] * 6 + [vp, i32, vp, vp, i32, i32, vp],
+    'mlc_gemm256_tn': [vp, vp, vp] + [i32] * 8 + [vp],
+    'mlc_conv256_fwd': [vp] * 5 + [i32] * 13 + [vp],
     'mlc_gemm_bf16_ex': [vp, vp, vp] + [i32] * 8 + [vp, i32, vp, vp, vp, vp, i64, vp],
     'mlc_ln_fwd': [vp] * 8 + [i32, i32, f32, f32, f32, vp, u32, u32, vp],
     'mlc_ln_bwd': [vp] * 10 + [i32, i32, f32, f32, vp, u32, u32, vp],
