@@ -43,6 +43,11 @@ def parse():
     p.add_argument('--graph', type=int, default=-1,
                    help='capture the step in a HIP graph (default: on for native)')
     p.add_argument('--json-out', default=None)
+    p.add_argument('--data', default='synthetic', choices=['synthetic', 'records'],
+                   help='records: feed the ResNet step from a record file through the native input '
+                        'pipeline (C++ gather threads + GPU augment kernel) instead of a resident batch')
+    p.add_argument('--records', default=None, help='record file for --data records (default: a generated one)')
+    p.add_argument('--loader-threads', type=int, default=12)
     return p.parse_args()
 
 
@@ -89,6 +94,20 @@ def main():
                                 world_size=world,
                                 use_graph=(args.graph if args.graph >= 0 else None))
 
+    feed = None
+    if args.data == 'records':
+        if is_bert or is_unet:
+            print('--data records feeds the image classifiers only', file=sys.stderr)
+            sys.exit(2)
+        feed = _record_feed(args, rank, world, device, dist)
+        inner = step
+
+        def step():
+            b = next(feed)
+            inner.load_batch(b['features'], b['targets'])
+            inner()
+        step.last_loss = inner.last_loss
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -113,7 +132,19 @@ def main():
     images = args.batch * world * args.steps
     value = images / elapsed
     loss = step.last_loss()
-    if rank == 0 and is_bert:
+    if rank == 0 and feed is not None:
+        out = {
+            'metric': 'images/sec (whole node) ResNet-50 DAG train task, record-file input pipeline',
+            'value': round(value, 2), 'unit': 'images/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'bf16',
+            'data': 'synthetic uint8 256x256x3 images in an mlrec file (RandomResizedCrop 224 + flip on the GPU), '
+                    'random-init weights',
+            'config': {'model': args.model, 'global_batch': args.batch * world, 'per_gpu_batch': args.batch,
+                       'image_size': args.image_size, 'parallelism': f'dp{world}', 'impl': args.impl,
+                       'loader_threads': args.loader_threads, 'final_loss': loss}}
+        print(json.dumps(out), flush=True)
+    elif rank == 0 and is_bert:
         out = {
             'metric': 'sequences/sec (whole node) BERT fine-tune DAG train task',
             'value': round(value, 2), 'unit': 'sequences/s', 'n_gpus': world, 'steps': args.steps,
@@ -170,6 +201,32 @@ def main():
                 f.write(line + '\n')
     if world > 1:
         dist.destroy_process_group()
+
+
+def _record_feed(args, rank, world, device, dist):
+    """An endless batch iterator over a record file through the native input pipeline
+    (mlcomp_amd.train.records): C++ threads gather uint8 records into pinned slots, the
+    augment kernel writes the stem's space-to-depth input."""
+    import numpy as np
+    from mlcomp_amd.train.records import RecordLoader, write_records
+    path = args.records
+    if path is None:
+        path = os.path.join(os.environ.get('TMPDIR', '/tmp'), f'mlc_bench_{os.getpid() if world == 1 else "dp"}.mlrec')
+        if rank == 0:
+            n = max(2560, 4 * args.batch * world)
+            rng = np.random.default_rng(0)
+            chunks = (rng.integers(0, 256, (256, 256, 256, 3), dtype=np.uint8) for _ in range((n + 255) // 256))
+            imgs = (im for c in chunks for im in c)
+            write_records(path, imgs, (int(v) for v in rng.integers(0, 1000, n)), shape=(256, 256, 3))
+        if world > 1:
+            dist.barrier()
+    loader = RecordLoader(path, args.batch, out_size=args.image_size, train=True, rank=rank, world_size=world,
+                          threads=args.loader_threads, depth=4, layout='s2d', device=device)
+
+    def gen():
+        while True:
+            yield from loader
+    return gen()
 
 
 if __name__ == '__main__':

@@ -5,8 +5,10 @@
 * ``mlcomp-broker`` - the C++17 epoll task-queue daemon (``csrc/broker``), the native
   replacement for the reference's vendored redis-server (`mlcomp/bin/redis-server`,
   launched at `mlcomp/server/__main__.py:66-79`).
-* ``libmlcomp_runtime.so`` - host-side C++ runtime helpers (``csrc/runtime``): the
-  threaded batch loader / collate used by the data pipeline.
+* ``libmlcomp_runtime.so`` - host-side C++ runtime (``csrc/runtime``): the memory-mapped
+  record files and the threaded batch gatherer of the native input pipeline
+  (:mod:`mlcomp_amd.train.records`); ``mlcomp-records-selftest-<san>`` is its
+  ThreadSanitizer / AddressSanitizer self-test.
 
 Outputs live under ``mlcomp_amd/_native/`` so they travel with the repo snapshot.
 Compilation is incremental (mtime based) and parallel.
@@ -94,9 +96,14 @@ def build_broker(verbose=False, sanitize=None):
     return out
 
 
+def _runtime_srcs():
+    return sorted(s for s in glob.glob(os.path.join(ROOT, 'csrc', 'runtime', '*.cpp'))
+                  if not s.endswith('_selftest.cpp'))
+
+
 def build_runtime(verbose=False):
     os.makedirs(OUT, exist_ok=True)
-    srcs = sorted(glob.glob(os.path.join(ROOT, 'csrc', 'runtime', '*.cpp')))
+    srcs = _runtime_srcs()
     hdrs = glob.glob(os.path.join(ROOT, 'csrc', 'runtime', '*.h'))
     if not srcs:
         return None
@@ -107,6 +114,21 @@ def build_runtime(verbose=False):
     if verbose:
         print(f'[build] runtime -> {RUNTIME_LIB}')
     return RUNTIME_LIB
+
+
+def build_runtime_selftest(sanitize='tsan', verbose=False):
+    """The record loader's self-test driver linked with an instrumented copy of the
+    runtime sources (``tsan``: ThreadSanitizer, ``asan``: AddressSanitizer + UBSan)."""
+    os.makedirs(OUT, exist_ok=True)
+    main = os.path.join(ROOT, 'csrc', 'runtime', 'records_selftest.cpp')
+    srcs = _runtime_srcs() + [main]
+    out = os.path.join(OUT, f'mlcomp-records-selftest-{sanitize}')
+    if _newer(out, srcs + glob.glob(os.path.join(ROOT, 'csrc', 'runtime', '*.h'))):
+        cxx = shutil.which('g++') or 'c++'
+        _run([cxx, '-O1', '-g', '-std=c++17', '-pthread', '-Wall'] + SANITIZERS[sanitize] + ['-o', out] + srcs)
+    if verbose:
+        print(f'[build] runtime selftest -> {out}')
+    return out
 
 
 def build_all(verbose=True):

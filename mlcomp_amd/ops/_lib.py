@@ -27,6 +27,7 @@ _SIGS = {
     'mlc_gemm256_nt': [vp, vp, vp, vp] + [i32] * 6 + [vp, i32, vp, vp, i32, i32, vp],
     'mlc_gemm256_tn': [vp, vp, vp] + [i32] * 8 + [vp],
     'mlc_conv256_fwd': [vp] * 5 + [i32] * 13 + [vp],
+    'mlc_augment': [vp, vp, vp, vp] + [i32] * 7 + [vp],
     'mlc_gemm_bf16_ex': [vp, vp, vp] + [i32] * 8 + [vp, i32, vp, vp, vp, vp, i64, vp],
     'mlc_ln_fwd': [vp] * 8 + [i32, i32, f32, f32, f32, vp, u32, u32, vp],
     'mlc_ln_bwd': [vp] * 10 + [i32, i32, f32, f32, vp, u32, u32, vp],
