@@ -70,5 +70,34 @@ def split_test_img(img_path):
         join(os.getcwd(), 'fold_test.csv'), index=False)
 
 
+@main.command('pack-records')
+@click.argument('img_path')
+@click.argument('out')
+@click.option('--size', type=int, default=256, help='stored square size (shorter side resized, centre crop)')
+@click.option('--fold-csv', default=None, help='fold.csv (image,label,fold): pack the rows of --fold only')
+@click.option('--fold', type=int, default=None)
+@click.option('--exclude-fold', is_flag=True, help='pack every fold except --fold (the training split)')
+def pack_records(img_path, out, size, fold_csv, fold, exclude_fold):
+    """Pack a class-per-folder image tree (or the rows of a fold.csv) into an .mlrec record
+    file for the native input pipeline (mlcomp_amd.train.records)."""
+    from mlcomp_amd.train.records import pack_images
+    if fold_csv:
+        import pandas as pd
+        df = pd.read_csv(fold_csv)
+        if fold is not None:
+            df = df[(df['fold'] != fold) if exclude_fold else (df['fold'] == fold)]
+        names = sorted(df['label'].astype(str).unique())
+        paths = [join(img_path, p) for p in df['image']]
+        labels = [names.index(str(v)) for v in df['label']]
+    else:
+        names = sorted(d for d in os.listdir(img_path) if os.path.isdir(join(img_path, d)))
+        pairs = [(join(img_path, d, f), i) for i, d in enumerate(names) for f in sorted(os.listdir(join(img_path, d)))]
+        paths, labels = [p for p, _ in pairs], [lab for _, lab in pairs]
+    n = pack_images(paths, labels, out, size=size)
+    with open(out + '.classes', 'w') as f:
+        f.write('\n'.join(names) + '\n')
+    click.echo(f'{n} images, {len(names)} classes -> {out}')
+
+
 if __name__ == '__main__':
     main()

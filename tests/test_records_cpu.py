@@ -131,3 +131,21 @@ def test_runner_trains_from_record_files(tmp_path):
     st = Runner(ConfigExperiment(cfg), device='cpu').run_experiment()
     m = st.epoch_metrics
     assert m['train_loss'] == m['train_loss'] and 'valid_accuracy01' in m
+
+
+def test_contrib_pack_records_cli(tmp_path):
+    from click.testing import CliRunner
+    from PIL import Image
+    from mlcomp_amd.contrib.__main__ import main
+    rng = np.random.default_rng(3)
+    for cls in ('cat', 'dog'):
+        (tmp_path / 'img' / cls).mkdir(parents=True)
+        for i in range(3):
+            Image.fromarray(rng.integers(0, 256, (30 + i, 40, 3), dtype=np.uint8)).save(tmp_path / 'img' / cls / f'{i}.png')
+    out = str(tmp_path / 'x.mlrec')
+    r = CliRunner().invoke(main, ['pack-records', str(tmp_path / 'img'), out, '--size', '24'])
+    assert r.exit_code == 0, r.output
+    f = RecordFile(out)
+    assert len(f) == 6 and f.shape == (24, 24, 3)
+    assert [f.label(i) for i in range(6)] == [0, 0, 0, 1, 1, 1]
+    assert open(out + '.classes').read().split() == ['cat', 'dog']
