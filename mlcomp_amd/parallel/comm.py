@@ -120,14 +120,24 @@ class TorchComm:
         pass
 
 
+_COMMS_MADE = 0
+
+
 def make_comm(device: Optional[torch.device] = None):
-    """Communicator for the current process group (None when world size is 1)."""
+    """Communicator for the current process group (None when world size is 1).
+
+    Every rank creates its communicators in the same order (one per native step, e.g. one
+    per training stage), so the n-th one of each rank publishes / reads the unique id under
+    its own store key ``mlc<n>/rccl_uid``: a later communicator can never pick up the id
+    of an earlier one that is still in the store."""
+    global _COMMS_MADE
     if not dist.is_available() or not dist.is_initialized():
         return None
     world = dist.get_world_size()
     if world == 1:
         return None
     rank = dist.get_rank()
+    _COMMS_MADE += 1
     if device is not None and torch.device(device).type == 'cuda':
-        return RcclComm(rank, world, device)
+        return RcclComm(rank, world, device, tag=f'mlc{_COMMS_MADE}')
     return TorchComm(rank, world)
