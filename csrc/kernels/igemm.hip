@@ -308,7 +308,7 @@ struct ConvWgradB {
   static constexpr bool KC = false;
   static constexpr int NC = R / 64;
   const bf16* x; ConvGeom g; int P, KK;
-  struct St { unsigned coff[NC]; int rd[NC], sd[NC]; };
+  struct St { unsigned coff[NC]; int rd[NC], sd[NC]; unsigned ci[NC]; };
   __device__ static int lds_off(int i, int tid) {
     return mc_off<R>((tid >> 3) + 32 * (i & 1), (tid & 7) + 8 * (i >> 1));
   }
@@ -319,6 +319,7 @@ struct ConvWgradB {
       unsigned rs_, ci, r, s;
       g.fC.divmod((unsigned)(kk < KK ? kk : 0), rs_, ci);
       g.fKW.divmod(rs_, r, s);
+      st.ci[c] = ci;
       st.coff[c] = (unsigned)(((int)r * g.dil * g.W + (int)s * g.dil) * g.C + (int)ci) * 2u;
       st.rd[c] = kk < KK ? (int)r * g.dil : (1 << 28);   // an invalid column never passes the bounds test
       st.sd[c] = (int)s * g.dil;
@@ -345,6 +346,121 @@ struct ConvWgradB {
       for (int c = 0; c < NC; ++c) {
         const bool ok = (unsigned)(hb + st.rd[c]) < (unsigned)g.H && (unsigned)(wb + st.sd[c]) < (unsigned)g.W;
         v[2 * c + j] = bload(rsr, ok ? rel + st.coff[c] : OOB);
+      }
+    }
+  }
+};
+
+// ---------------------------------------------------------------- BN-apply operand transform
+// A conv whose input is the output z = relu(y*sc + sh) of a BatchNorm can read the pre-BN
+// tensor y instead: the transform is applied per channel while the staged registers go to
+// LDS (after the loads landed), and chunks that stand for padding taps / rows past M /
+// k past K stay zero (the transform of a zero is not zero).  Forward: units 2 and 3 of a
+// bottleneck read y1 / y2, so z1 / z2 are never written; backward: the weight gradients
+// of those convs re-apply it to their activation operand.
+struct BnIn { const float* sc; const float* sh; };
+template <class L, class = void> struct HasXform { static constexpr bool value = false; };
+template <class L> struct HasXform<L, decltype((void)L::XF)> { static constexpr bool value = L::XF; };
+
+__device__ __forceinline__ uint4 bn_relu8(uint4 v, const float* a, const float* b, bool ok) {
+  float f[8];
+  unpack8(v, f);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e] * a[e] + b[e], 0.f);
+  const uint4 r = pack8(f);
+  return ok ? r : make_uint4(0u, 0u, 0u, 0u);
+}
+
+// plain [rows][K] activation (1x1 conv A operand): channel = k
+template <int R>
+struct MatKCBn : MatKC<R> {
+  static constexpr bool XF = true;
+  BnIn bn;
+  __device__ void xform(const typename MatKC<R>::St& st, int kt, int tid, uint4 (&v)[R / 32]) const {
+    const int c0 = kt * BK + (tid & 7) * 8;
+    const bool kv = c0 < this->K;
+    float a[8], b[8];
+    ldg8f(bn.sc + (kv ? c0 : 0), a);
+    ldg8f(bn.sh + (kv ? c0 : 0), b);
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) v[i] = bn_relu8(v[i], a, b, kv && st.off[i] != OOB);
+  }
+};
+
+// implicit-GEMM conv forward A operand: channel = ci of the chunk's tap
+template <int R>
+struct ConvFwdABn : ConvFwdA<R> {
+  static constexpr bool XF = true;
+  BnIn bn;
+  __device__ void xform(const typename ConvFwdA<R>::St& st, int kt, int tid, uint4 (&v)[R / 32]) const {
+    const ConvGeom& g = this->g;
+    const int k0 = kt * BK, k = k0 + (tid & 7) * 8;
+    unsigned rs_, cc, rr, ss;
+    if (g.C % BK == 0) {
+      g.fC.divmod((unsigned)k0, rs_, cc);
+      cc += (unsigned)(k - k0);
+    } else {
+      g.fC.divmod((unsigned)k, rs_, cc);
+    }
+    g.fKW.divmod(rs_, rr, ss);
+    const bool kv = k < this->K;
+    const unsigned P = kv ? tap_pat((int)rr, (int)ss) : NO_TAP;
+    float a[8], b[8];
+    ldg8f(bn.sc + (kv ? cc : 0), a);
+    ldg8f(bn.sh + (kv ? cc : 0), b);
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) v[i] = bn_relu8(v[i], a, b, (st.msk[i] & P) == P);
+  }
+};
+
+// 1x1 weight-gradient B operand x [P][C] (k = pixel rows, columns = channels)
+template <int R>
+struct MatMCBn : MatMC<R> {
+  static constexpr bool XF = true;
+  BnIn bn;
+  __device__ void xform(const typename MatMC<R>::St& st, int kt, int tid, uint4 (&v)[R / 32]) const {
+    const int c0 = st.n0 + (tid % (R / 8)) * 8;
+    const bool cv = c0 < this->cols;
+    float a[8], b[8];
+    ldg8f(bn.sc + (cv ? c0 : 0), a);
+    ldg8f(bn.sh + (cv ? c0 : 0), b);
+    const int left = this->K - kt * BK;
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) v[i] = bn_relu8(v[i], a, b, cv && MatMC<R>::kr(i, tid) < left);
+  }
+};
+
+// gathered weight-gradient B operand (3x3 ...): same bounds test as ConvWgradB::load
+template <int R>
+struct ConvWgradBBn : ConvWgradB<R> {
+  static constexpr bool XF = true;
+  BnIn bn;
+  __device__ void xform(const typename ConvWgradB<R>::St& st, int kt, int tid, uint4 (&v)[R / 32]) const {
+    constexpr int NC = ConvWgradB<R>::NC;
+    const ConvGeom& g = this->g;
+    const int p0 = kt * BK;
+    unsigned t, w0, n0, h0;
+    g.fWo.divmod((unsigned)p0, t, w0);
+    g.fHo.divmod(t, n0, h0);
+    int hb[2], wb[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kr = (tid >> 3) + 32 * j;
+      unsigned cw, wo, ch, ho;
+      g.fWo.divmod(w0 + (unsigned)kr, cw, wo);
+      g.fHo.divmod(h0 + cw, ch, ho);
+      hb[j] = p0 + kr < this->P ? (int)ho * g.stride - g.pad : -(1 << 29);
+      wb[j] = (int)wo * g.stride - g.pad;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float a[8], b[8];
+      ldg8f(bn.sc + st.ci[c], a);
+      ldg8f(bn.sh + st.ci[c], b);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bool ok = (unsigned)(hb[j] + st.rd[c]) < (unsigned)g.H && (unsigned)(wb[j] + st.sd[c]) < (unsigned)g.W;
+        v[2 * c + j] = bn_relu8(v[2 * c + j], a, b, ok);
       }
     }
   }
@@ -740,8 +856,11 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
   };
-  // real: the tile is inside this split (PF=2 re-stages the clamped last tile)
-  auto stage = [&](char* buf, const uint4 (&ra)[BM / 32], const uint4 (&rb)[BN / 32], bool real) {
+  // real: the tile is inside this split (PF=2 re-stages the clamped last tile); kt: the
+  // K-tile the registers hold (for operand transforms)
+  auto stage = [&](char* buf, uint4 (&ra)[BM / 32], uint4 (&rb)[BN / 32], int kt, bool real) {
+    if constexpr (HasXform<LA>::value) la.xform(sa, kt, tid, ra);
+    if constexpr (HasXform<LB>::value) lb.xform(sb, kt, tid, rb);
     store_stage<LA, BM>(buf, tid, ra);
     store_stage<LB, BN>(buf + A_BYTES, tid, rb);
     if constexpr (HasSum<LA>::value) {
@@ -755,7 +874,7 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
         la.load(sa, kt0 + t, tid, ra);
         lb.load(sb, kt0 + t, tid, rb);
         if (t > 0) __syncthreads();          // previous tile's fragment reads are done
-        stage(smem, ra, rb, true);
+        stage(smem, ra, rb, kt0 + t, true);
         __syncthreads();
         mfma_tile(smem, smem + A_BYTES);
       }
@@ -764,7 +883,7 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
       uint4 ra[BM / 32], rb[BN / 32];
       la.load(sa, kt0, tid, ra);
       lb.load(sb, kt0, tid, rb);
-      stage(smem, ra, rb, true);
+      stage(smem, ra, rb, kt0, true);
       __syncthreads();
       for (int t = 0; t < nt; ++t) {
         const char* cur = smem + (t & 1) * STAGE;
@@ -774,7 +893,7 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
           lb.load(sb, kt0 + t + 1, tid, rb);
         }
         mfma_tile(cur, cur + A_BYTES);
-        if (more) stage(smem + ((t + 1) & 1) * STAGE, ra, rb, true);
+        if (more) stage(smem + ((t + 1) & 1) * STAGE, ra, rb, kt0 + t + 1, true);
         __syncthreads();
       }
     } else {
@@ -784,21 +903,21 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
       lb.load(sb, kt0, tid, b0);
       la.load(sa, min(kt0 + 1, last), tid, a1);
       lb.load(sb, min(kt0 + 1, last), tid, b1);
-      stage(smem, a0, b0, true);
+      stage(smem, a0, b0, kt0, true);
       __syncthreads();
       for (int t = 0;; t += 2) {
         // compute t from buffer 0; set 1 (tile t+1) in flight; set 0 free
         la.load(sa, min(kt0 + t + 2, last), tid, a0);
         lb.load(sb, min(kt0 + t + 2, last), tid, b0);
         mfma_tile(smem, smem + A_BYTES);
-        stage(smem + STAGE, a1, b1, t + 1 < nt);
+        stage(smem + STAGE, a1, b1, min(kt0 + t + 1, last), t + 1 < nt);
         __syncthreads();
         if (t + 1 >= nt) break;
         // compute t+1 from buffer 1; set 0 (tile t+2) in flight; set 1 free
         la.load(sa, min(kt0 + t + 3, last), tid, a1);
         lb.load(sb, min(kt0 + t + 3, last), tid, b1);
         mfma_tile(smem + STAGE, smem + STAGE + A_BYTES);
-        stage(smem, a0, b0, t + 2 < nt);
+        stage(smem, a0, b0, min(kt0 + t + 2, last), t + 2 < nt);
         __syncthreads();
         if (t + 2 >= nt) break;
       }
@@ -919,20 +1038,35 @@ MLC_EXPORT int mlc_gemm_get_set(int key, int value) {
 // hold NSTAT*Co fp32 (zeroed by the caller); per-channel partial sums of y and y^2 are
 // accumulated into them (reduce over the NSTAT copies to get the BN statistics).
 // Requires C % 8 == 0 and Co % 8 == 0.
+// in_sc/in_sh (optional, [C] fp32): x is the PRE-BatchNorm tensor of a ReLU BN and the
+// conv reads relu(x * in_sc + in_sh) (BnIn transform in the A loader; zero padding stays
+// zero), so the BN output never has to be written.
 MLC_EXPORT int mlc_conv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, float* sumsq,
                             int N, int H, int W, int C, int Co, int KH, int KW, int stride,
-                            int pad, int dil, int Ho, int Wo, hipStream_t st) {
-  if (C % 8 || Co % 8 || KH > 15 || KW > 16) return -1;
+                            int pad, int dil, int Ho, int Wo, const float* in_sc, const float* in_sh,
+                            hipStream_t st) {
+  if (C % 8 || Co % 8 || KH > 15 || KW > 16 || ((in_sc == nullptr) != (in_sh == nullptr))) return -1;
   const int M = N * Ho * Wo, K = KH * KW * C;
   const int tile = pick_tile(M, Co);
   EpiBF16<> epi{y, Co, sum, sumsq, IdentityRows{}};
+  const BnIn bn{in_sc, in_sh};
 #define MKB(R) (MatKC<R>{w, K, Co, K})
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
+    if (in_sc) {
+#define MKA(R) (MatKCBn<R>{{x, C, M, K}, bn})
+      MLC_TILE_DISPATCH(tile, M, Co, K, 1, st, epi, MKA, MKB);
+#undef MKA
+    }
 #define MKA(R) (MatKC<R>{x, C, M, K})
     MLC_TILE_DISPATCH(tile, M, Co, K, 1, st, epi, MKA, MKB);
 #undef MKA
   }
   const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
+  if (in_sc) {
+#define MKA(R) (ConvFwdABn<R>{{x, g, M, K}, bn})
+    MLC_TILE_DISPATCH(tile, M, Co, K, 1, st, epi, MKA, MKB);
+#undef MKA
+  }
 #define MKA(R) (ConvFwdA<R>{x, g, M, K})
   MLC_TILE_DISPATCH(tile, M, Co, K, 1, st, epi, MKA, MKB);
 #undef MKA
@@ -1026,11 +1160,13 @@ splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long
 // workspace (ws_floats >= splits*Co*KK) the split-K partial tiles go to fp32 slabs with
 // plain stores and one reduction pass sums them into dw; without, they are added into dw
 // with fp32 atomics (memory-side, ~1.3 TB/s: the slab round trip is ~4x cheaper).
+// in_sc/in_sh: as in mlc_conv_fwd - x is pre-BN and the conv's input is relu(x*sc + sh).
 MLC_EXPORT int mlc_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, int H, int W,
                               int C, int Co, int KH, int KW, int stride, int pad, int dil,
                               int Ho, int Wo, int splits, int accumulate, float* ws, long ws_floats,
-                              hipStream_t st) {
-  if (C % 8 || Co % 8) return -1;
+                              const float* in_sc, const float* in_sh, hipStream_t st) {
+  if (C % 8 || Co % 8 || ((in_sc == nullptr) != (in_sh == nullptr))) return -1;
+  const BnIn bn{in_sc, in_sh};
   const int P = N * Ho * Wo, KK = KH * KW * C;
   const int tile = pick_tile(Co, KK);
   const bool plain = KH == 1 && KW == 1 && stride == 1 && pad == 0;
@@ -1055,12 +1191,21 @@ MLC_EXPORT int mlc_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, i
     }
     EpiF32Slab epi{ws, KK, slab};
     hipError_t e;
+    if (in_sc) {
+#define MKB(R) (MatMCBn<R>{{x, C, P, C}, bn})
+      if (plain) e = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB); }();
+#undef MKB
+#define MKB(R) (ConvWgradBBn<R>{{x, g, P, KK}, bn})
+      else e = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB); }();
+#undef MKB
+    } else {
 #define MKB(R) (MatMC<R>{x, C, P, C})
-    if (plain) e = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB); }();
+      if (plain) e = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB); }();
 #undef MKB
 #define MKB(R) (ConvWgradB<R>{x, g, P, KK})
-    else e = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB); }();
+      else e = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB); }();
 #undef MKB
+    }
     if (e != hipSuccess) return e;
     const long n4 = (long)slab / 4;
     long blocks = (n4 + 255) / 256;
@@ -1071,6 +1216,16 @@ MLC_EXPORT int mlc_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, i
   }
   if (!accumulate) (void)hipMemsetAsync(dw, 0, slab * sizeof(float), st);
   EpiF32Atomic epi{dw, KK};
+  if (in_sc) {
+    if (plain) {
+#define MKB(R) (MatMCBn<R>{{x, C, P, C}, bn})
+      MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
+#undef MKB
+    }
+#define MKB(R) (ConvWgradBBn<R>{{x, g, P, KK}, bn})
+    MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
+#undef MKB
+  }
   if (plain) {
 #define MKB(R) (MatMC<R>{x, C, P, C})
     MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);

@@ -19,9 +19,9 @@ _LOCK = threading.Lock()
 vp, i32, i64, f32, u32 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_uint
 
 _SIGS = {
-    'mlc_conv_fwd': [vp, vp, vp, vp, vp] + [i32] * 12 + [vp],
+    'mlc_conv_fwd': [vp, vp, vp, vp, vp] + [i32] * 12 + [vp, vp, vp],
     'mlc_conv_dgrad': [vp] * 4 + [i32] * 12 + [vp] * 11 + [vp],
-    'mlc_conv_wgrad': [vp, vp, vp] + [i32] * 14 + [vp, i64, vp],
+    'mlc_conv_wgrad': [vp, vp, vp] + [i32] * 14 + [vp, i64, vp, vp, vp],
     'mlc_gemm_f32out': [vp, vp, vp, vp] + [i32] * 11 + [vp],
     'mlc_gemm_bf16out': [vp, vp, vp] + [i32] * 8 + [vp],
     'mlc_gemm256_nt': [vp, vp, vp, vp] + [i32] * 6 + [vp, i32, vp, vp, i32, i32, vp],

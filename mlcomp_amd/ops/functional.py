@@ -33,12 +33,20 @@ def conv_out_hw(H, W, KH, KW, stride, pad, dil):
 
 
 # ---------------------------------------------------------------- conv
+def bn_relu_input(x: torch.Tensor, in_affine) -> torch.Tensor:
+    """relu(x * sc + sh) per channel (NHWC) - the conv input an ``in_affine`` stands for."""
+    sc, sh = in_affine
+    return torch.relu(x.float() * sc + sh).to(torch.bfloat16)
+
+
 def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, stride=1, pad=0, dil=1,
                stats: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+               out: Optional[torch.Tensor] = None, in_affine=None) -> torch.Tensor:
     """y = conv(x, w) in NHWC; if ``stats`` given (see :func:`stat_buffers`: two
     [NSTAT*Co] fp32 buffers), accumulates per-channel partial sums of y and y^2 into
-    them (the BN forward statistics, reduced over the NSTAT copies by bn_fwd_apply)."""
+    them (the BN forward statistics, reduced over the NSTAT copies by bn_fwd_apply).
+    ``in_affine = (sc, sh)``: ``x`` is the pre-BN tensor of a ReLU BatchNorm and the conv
+    input is relu(x*sc + sh), applied inside the kernel's operand loader."""
     N, H, W, C = x.shape
     Co, KH, KW, Ci = w.shape
     assert Ci == C, (w.shape, x.shape)
@@ -46,9 +54,12 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, stride=1, pad=0, dil=1,
     if _cuda(x):
         y = out if out is not None else torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.bfloat16)
         s1, s2 = (stats if stats is not None else (None, None))
+        sc, sh = in_affine if in_affine is not None else (None, None)
         _lib.call('mlc_conv_fwd', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(s1), _lib.ptr(s2),
-                  N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo, _lib.stream())
+                  N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo, _lib.ptr(sc), _lib.ptr(sh), _lib.stream())
         return y
+    if in_affine is not None:
+        x = bn_relu_input(x, in_affine)
     yf = F.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), None, stride, pad, dil)
     if stats is not None:
         stats[0][:Co].add_(yf.sum(dim=(0, 2, 3)))
@@ -139,19 +150,23 @@ def slab_workspace(device, n: int) -> torch.Tensor:
 
 
 def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride=1, pad=0, dil=1,
-                 out: Optional[torch.Tensor] = None, accumulate=False) -> torch.Tensor:
+                 out: Optional[torch.Tensor] = None, accumulate=False, in_affine=None) -> torch.Tensor:
     """fp32 weight gradient in [Co, KH, KW, Ci] order (written into ``out`` if given).
-    Split-K partial sums go through a slab workspace and one reduction pass."""
+    Split-K partial sums go through a slab workspace and one reduction pass.
+    ``in_affine``: as in :func:`conv2d_fwd` (x is pre-BN, the input is relu(x*sc + sh))."""
     Co, KH, KW, Ci = w_shape
     N, H, W, C = x.shape
     _, Ho, Wo, _ = dy.shape
     if _cuda(dy):
         dw = out if out is not None else torch.empty(Co, KH, KW, Ci, device=dy.device, dtype=torch.float32)
         ws = slab_workspace(dy.device, min(32 * Co * KH * KW * Ci, 64 << 20)) if _USE_SLAB else None
+        sc, sh = in_affine if in_affine is not None else (None, None)
         _lib.call('mlc_conv_wgrad', _lib.ptr(dy), _lib.ptr(x), _lib.ptr(dw), N, H, W, C, Co, KH, KW,
                   stride, pad, dil, Ho, Wo, 0, int(accumulate), _lib.ptr(ws),
-                  ws.numel() if ws is not None else 0, _lib.stream())
+                  ws.numel() if ws is not None else 0, _lib.ptr(sc), _lib.ptr(sh), _lib.stream())
         return dw
+    if in_affine is not None:
+        x = bn_relu_input(x, in_affine)
     dwf = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).float(), (Co, Ci, KH, KW),
                                       dy.permute(0, 3, 1, 2).float(), stride, pad, dil)
     dwf = dwf.permute(0, 2, 3, 1)

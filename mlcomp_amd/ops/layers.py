@@ -14,6 +14,7 @@ memset at the start of the step.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -144,10 +145,12 @@ class ConvBN:
         return _ConvBNFn.apply(x, res, self.ctx.anchor, self)
 
     # raw (autograd-free) halves, composed by the block-level Functions
-    def fwd(self, x, res=None, defer=False):
+    def fwd(self, x, res=None, defer=False, in_affine=None):
         """z = act(BN(conv(x)) [+ res]); ``res`` is a tensor or a deferred BN output
         ``(y, scale, shift)`` (applied in the same pass).  ``defer=True`` stops after the
-        statistics: z is not materialised (returns None; scale/shift are ready)."""
+        statistics: z is not materialised (returns None; scale/shift are ready).
+        ``in_affine = (sc, sh)``: ``x`` is the pre-BN output of the previous (ReLU) unit,
+        whose BN + ReLU the conv applies while loading its operand."""
         ws = self.ctx.ws
         if self.s2d and x.shape[-1] != 16:
             x = Fn.stem_s2d(x, 3)
@@ -156,7 +159,7 @@ class ConvBN:
             res, rs, rh = res
             raff = (rs, rh)
         if not self.ctx.training:  # inference BN: running statistics, no stat epilogue
-            y = Fn.conv2d_fwd(x, self.w.bf16, self.stride, self.pad, self.dil)
+            y = Fn.conv2d_fwd(x, self.w.bf16, self.stride, self.pad, self.dil, in_affine=in_affine)
             torch.rsqrt(self.run_var + self.eps, out=self.scale).mul_(self.gamma.master)
             torch.sub(self.beta.master, self.run_mean * self.scale, out=self.shift)
             if defer:
@@ -164,7 +167,7 @@ class ConvBN:
             z = Fn.bn_apply(y, res, self.scale, self.shift, self.act, res_affine=raff)
             return z, (x, y, z)
         s1, s2 = ws[self.k_s1], ws[self.k_s2]
-        y = Fn.conv2d_fwd(x, self.w.bf16, self.stride, self.pad, self.dil, stats=(s1, s2))
+        y = Fn.conv2d_fwd(x, self.w.bf16, self.stride, self.pad, self.dil, stats=(s1, s2), in_affine=in_affine)
         training = self.ctx.training
         z = Fn.bn_fwd_apply(y, res, s1, s2, self.gamma.master, self.beta.master, self.save_mean,
                             self.save_invstd, self.run_mean if training else None,
@@ -184,16 +187,16 @@ class ConvBN:
         x, y, z = rec
         return (y, self.save_mean, self.ctx.ws[self.k_bw])
 
-    def wgrad(self, dy, x):
+    def wgrad(self, dy, x, in_affine=None):
         """Weight gradient into the arena (masked for the s2d stem), then mark it ready."""
         Fn.conv2d_wgrad(dy, x, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad,
-                        accumulate=self.ctx.grad_prezeroed)
+                        accumulate=self.ctx.grad_prezeroed, in_affine=in_affine)
         if self.s2d:
             self.w.grad.mul_(self._gmask)
         self.ctx.arena.mark_ready(self.w)
 
     def bwd(self, dz, rec, want_dres=False, dx_addend=None, need_dx=True, dx_out=None,
-            prereduced=False, dgrad_bn=None):
+            prereduced=False, dgrad_bn=None, in_affine=None):
         x, y, z = rec
         arena = self.ctx.arena
         dy, dres = Fn.bn_bwd(dz, z if self.act else None, y, self.save_mean, self.save_invstd,
@@ -202,7 +205,7 @@ class ConvBN:
                              coef=self.coef, prereduced=prereduced)
         arena.mark_ready(self.gamma)
         arena.mark_ready(self.beta)
-        self.wgrad(dy, x)
+        self.wgrad(dy, x, in_affine)
         dx = None
         if need_dx:
             dx = Fn.conv2d_dgrad(dy, self.w.bf16, x.shape, self.stride, self.pad, self.dil,
@@ -244,8 +247,30 @@ class ResidualBlock:
         self.ctx = units[0].ctx
         self.prev: Optional['ResidualBlock'] = None
         self.fuse_bn_bwd = True
+        # BN-apply fusion (MLC_FUSE_BN_FWD: 0 off, 1 into 1x1 consumers, 2 into every
+        # consumer): an inner unit's output z_i = relu(BN(y_i)) is not written; unit i+1
+        # reads y_i and applies BN+ReLU in its conv and weight-gradient operand loaders.
+        # Measured on MI355X (docs/kernels.md): the loader transform costs the 3x3 convs
+        # more than the saved pass, so the default is off.
+        mode = int(os.environ.get('MLC_FUSE_BN_FWD', '0'))
+        self.fuse_into = [False] + [
+            mode >= 1 and prev.act and (mode >= 2 or (u.k == (1, 1) and u.stride == 1 and u.pad == 0))
+            for prev, u in zip(units[:-1], units[1:])]
         self.dout_prereduced = False
         self._last = None   # (rec of the last unit, rec of down) of the latest forward
+
+    @property
+    def fuse_bn_fwd(self) -> bool:
+        return any(self.fuse_into)
+
+    @fuse_bn_fwd.setter
+    def fuse_bn_fwd(self, on: bool):
+        self.fuse_into = [False] + [bool(on) and p.act for p in self.units[:-1]]
+
+    def in_affines(self):
+        """Input transform of each unit: (scale, shift) of the previous unit's BN where the
+        BN-apply is fused into this unit's loaders, else None."""
+        return [None] + [(p.scale, p.shift) if f else None for p, f in zip(self.units[:-1], self.fuse_into[1:])]
 
     def __call__(self, x):
         return _ResidualBlockFn.apply(x, self.ctx.anchor, self)
@@ -277,10 +302,15 @@ class _ResidualBlockFn(torch.autograd.Function):
         else:
             identity, rd = x, None
         y = x
-        for u in blk.units[:-1]:
-            y, r = u.fwd(y)
+        affs = blk.in_affines()
+        for i, u in enumerate(blk.units[:-1]):
+            if blk.fuse_into[i + 1]:
+                _, r = u.fwd(y, defer=True, in_affine=affs[i])
+                y = r[1]           # pre-BN output; the next conv applies BN + ReLU
+            else:
+                y, r = u.fwd(y, in_affine=affs[i])
             recs.append(r)
-        out, r = blk.units[-1].fwd(y, identity)
+        out, r = blk.units[-1].fwd(y, identity, in_affine=affs[-1])
         recs.append(r)
         blk._last = (r, rd)
         ctx.blk = blk
@@ -303,6 +333,9 @@ class _ResidualBlockFn(torch.autograd.Function):
         blk.dout_prereduced = False
         units = blk.units
         fuse = blk.fuse_bn_bwd
+        affs = blk.in_affines()
+        if blk.fuse_bn_fwd:
+            assert fuse, 'the BN-apply fusion needs the fused BN-backward reductions (z is not stored)'
 
         def spec_for(i):  # fused reduction of unit i's BN in unit i+1's dgrad
             u = units[i]
@@ -314,11 +347,12 @@ class _ResidualBlockFn(torch.autograd.Function):
 
         # last unit: its dres is the shortcut-branch gradient
         sp = spec_for(len(units) - 2) if len(units) > 1 else None
-        d, dres = units[-1].bwd(dout, recs[-1], want_dres=True, prereduced=pre, dgrad_bn=sp)
+        d, dres = units[-1].bwd(dout, recs[-1], want_dres=True, prereduced=pre, dgrad_bn=sp,
+                                in_affine=affs[-1])
         fused = sp is not None
         for i in range(len(units) - 2, 0, -1):
             sp = spec_for(i - 1)
-            d, _ = units[i].bwd(d, recs[i], prereduced=fused, dgrad_bn=sp)
+            d, _ = units[i].bwd(d, recs[i], prereduced=fused, dgrad_bn=sp, in_affine=affs[i])
             fused = sp is not None
         if blk.down is not None:
             # shortcut conv first; its dx becomes the addend of the first unit's dgrad

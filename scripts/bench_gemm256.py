@@ -54,7 +54,7 @@ def conv_old(x, w, y, stride, pad, stats=None):
     Co, KH, KW, _ = w.shape
     Ho, Wo = y.shape[1], y.shape[2]
     s1, s2 = stats if stats is not None else (None, None)
-    _lib.call('mlc_conv_fwd', P(x), P(w), P(y), P(s1), P(s2), N, H, W, C, Co, KH, KW, stride, pad, 1, Ho, Wo, S())
+    _lib.call('mlc_conv_fwd', P(x), P(w), P(y), P(s1), P(s2), N, H, W, C, Co, KH, KW, stride, pad, 1, Ho, Wo, None, None, S())
 
 
 def rel(a, b):

@@ -119,10 +119,47 @@ def test_conv_wgrad_accumulate_slab_and_atomic(case):
     out2 = torch.ones(Co, K, K, C, device=DEV)
     xd, dyd = x.to(DEV), dy.to(DEV)
     _lib.call('mlc_conv_wgrad', _lib.ptr(dyd), _lib.ptr(xd), _lib.ptr(out2), N, H, W, C, Co, K, K, s, p, 1,
-              Ho, Wo, 0, 1, None, 0, _lib.stream())
+              Ho, Wo, 0, 1, None, 0, None, None, _lib.stream())
     torch.cuda.synchronize()
     assert rel_err(out, ref) < 5e-3
     assert rel_err(out2, ref) < 5e-3
+
+
+AFF_CASES = [c for c in CONV_CASES if c[3] >= 32]
+
+
+def _affine(C, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(C, generator=g) * 0.8, torch.randn(C, generator=g) * 0.5
+
+
+@pytest.mark.parametrize('case', AFF_CASES)
+def test_conv_fwd_bn_input_transform(case):
+    """conv(relu(y*sc + sh)) with the transform inside the A loader == conv of the
+    materialised input (padding taps stay zero)."""
+    N, H, W, C, Co, K, s, p = case
+    y = _bf(N, H, W, C, seed=31)
+    w = _bf(Co, K, K, C, scale=(1.0 / (K * K * C)) ** 0.5, seed=32)
+    sc, sh = _affine(C, 33)
+    ref = Fn.conv2d_fwd(Fn.bn_relu_input(y, (sc, sh)), w, s, p)
+    s1, s2 = Fn.stat_buffers(Co, DEV)
+    out = Fn.conv2d_fwd(y.to(DEV), w.to(DEV), s, p, stats=(s1, s2), in_affine=(sc.to(DEV), sh.to(DEV)))
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 1e-2
+    assert rel_err(s1.reshape(Fn.NSTAT, Co).sum(0), ref.float().reshape(-1, Co).sum(0)) < 2e-2
+
+
+@pytest.mark.parametrize('case', AFF_CASES)
+def test_conv_wgrad_bn_input_transform(case):
+    N, H, W, C, Co, K, s, p = case
+    Ho, Wo = Fn.conv_out_hw(H, W, K, K, s, p, 1)
+    y = _bf(N, H, W, C, seed=34)
+    dy = _bf(N, Ho, Wo, Co, seed=35)
+    sc, sh = _affine(C, 36)
+    ref = Fn.conv2d_wgrad(dy, Fn.bn_relu_input(y, (sc, sh)), (Co, K, K, C), s, p)
+    out = Fn.conv2d_wgrad(dy.to(DEV), y.to(DEV), (Co, K, K, C), s, p, in_affine=(sc.to(DEV), sh.to(DEV)))
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 5e-3
 
 
 def test_bn_apply_residual_affine():
@@ -297,8 +334,9 @@ def test_conv_dgrad_bn_epilogue(case, two, aff):
 
 
 def test_native_fused_bn_bwd_matches_unfused():
-    """Engine-level: gradients with the BN-backward reduction fused into dgrad epilogues
-    equal (up to float-atomic order) the ones from the separate reduction kernel."""
+    """Engine-level: gradients with the BN-backward reduction fused into dgrad epilogues and
+    the inner BN+ReLU applied inside the next conv's loaders equal (up to float-atomic
+    order) the ones from the separate reduction / apply kernels."""
     torch.manual_seed(5)
     from mlcomp_amd.models import build_model
     from mlcomp_amd.train.native_step import NativeClassifierStep
@@ -309,8 +347,11 @@ def test_native_fused_bn_bwd_matches_unfused():
                              use_graph=False, lr=0.0, momentum=0.0)
     b = NativeClassifierStep(torch_model=tm2, batch=8, image_size=64, device=DEV, num_classes=16,
                              use_graph=False, lr=0.0, momentum=0.0)
+    for blk in a.net.blocks:
+        blk.fuse_bn_fwd = True     # every inner BN+ReLU applied in the next conv's loaders
     for blk in b.net.blocks:
         blk.fuse_bn_bwd = False
+        blk.fuse_bn_fwd = False
     b.load_batch(a.x, a.y)
     a()
     b()
