@@ -13,8 +13,10 @@ MI355X:
   stream (event fence from the compute stream), overlapping the rest of backward.
 * Bucket size: an 8-GPU ring all-reduce moves 2*(7/8)*S per GPU over point-to-point
   xGMI (7 links x ~153 GB/s); with RCCL using several channels the per-peer chunk
-  (S/8) should stay >= ~1-4 MB to amortise latency, hence 32 MB buckets, and a smaller
-  first bucket (8 MB) so communication starts early in backward.
+  (S/8) should stay >= ~1-4 MB to amortise latency, hence 32 MB buckets, a smaller
+  first bucket (8 MB) so communication starts early in backward, and a final bucket
+  capped at 4 MB (``MLC_LAST_BUCKET_MB``): it holds the first layers' gradients, which
+  are ready only when backward ends, so its all-reduce is the exposed tail of the step.
 * The collectives are stream work of the framework's own RCCL communicator, so the
   whole step (forward, backward, all-reduces, optimizer) is captured in one HIP graph.
 * Bucket assignment is a pure function of the arena layout, hence identical on every
@@ -47,18 +49,35 @@ class Bucket:
         return (self.end - self.start) * 4
 
 
-def plan_buckets(arena: Arena, bucket_bytes: int, first_bucket_bytes: int) -> List[Bucket]:
+def plan_buckets(arena: Arena, bucket_bytes: int, first_bucket_bytes: int,
+                 last_bucket_bytes: Optional[int] = None) -> List[Bucket]:
+    """Contiguous arena slices in backward order: a small first bucket (communication
+    starts early in backward), ``bucket_bytes`` buckets, and - when ``last_bucket_bytes``
+    is given - a final bucket of at most that size.  The final bucket is the only one whose
+    all-reduce cannot overlap backward (its last gradient is the network's first layer), so
+    keeping it small keeps the exposed tail short."""
+    slots = arena.slots_in_backward_order()
+    if not slots:
+        return []
+    ends = [slots[i + 1].offset if i + 1 < len(slots) else arena.numel for i in range(len(slots))]
+    tail_from = len(slots)   # index of the first slot of the capped final bucket
+    if last_bucket_bytes:
+        j = len(slots) - 1
+        while j > 0 and (arena.numel - slots[j - 1].offset) * 4 <= last_bucket_bytes:
+            j -= 1
+        tail_from = j if j > 0 else len(slots)
     buckets = []
     cur: List[Slot] = []
     start = 0
     limit = first_bucket_bytes
-    slots = arena.slots_in_backward_order()
-    for i, s in enumerate(slots):
+    for i, s in enumerate(slots[:tail_from]):
         cur.append(s)
-        end = slots[i + 1].offset if i + 1 < len(slots) else arena.numel
-        if (end - start) * 4 >= limit or i + 1 == len(slots):
+        end = ends[i]
+        if (end - start) * 4 >= limit or i + 1 == tail_from:
             buckets.append(Bucket(arena, start, end, cur))
             cur, start, limit = [], end, bucket_bytes
+    if tail_from < len(slots):
+        buckets.append(Bucket(arena, slots[tail_from].offset, arena.numel, slots[tail_from:]))
     return buckets
 
 
@@ -69,8 +88,9 @@ class GradBucketer:
         self.comm = comm
         bmb = bucket_mb or float(os.environ.get('MLC_BUCKET_MB', 32))
         fmb = first_bucket_mb or float(os.environ.get('MLC_FIRST_BUCKET_MB', 8))
+        lmb = float(os.environ.get('MLC_LAST_BUCKET_MB', 4))
         self.buckets: List[Bucket] = plan_buckets(params.decay, int(bmb * 2 ** 20),
-                                                  int(fmb * 2 ** 20))
+                                                  int(fmb * 2 ** 20), int(lmb * 2 ** 20) if lmb > 0 else None)
         # BN affine + biases: small, reduced as one trailing bucket
         self.buckets += plan_buckets(params.nodecay, 1 << 62, 1 << 62)
         self.slot_bucket: Dict[int, Bucket] = {}

@@ -265,3 +265,23 @@ def test_resume_mid_stage_restores_optimizer_schedule_and_best(tmp_path):
     saver = [c for c in r2.callbacks if type(c).__name__ == 'CheckpointCallback'][0]
     assert saver.best_score == 2.0
     assert (ck / 'best_full.pth').read_bytes() == best_before
+
+
+def test_bucket_plan_caps_the_exposed_last_bucket():
+    """Buckets tile the arena contiguously in backward order; the first is small and the
+    final one (first layers, ready only at the end of backward) is capped."""
+    from mlcomp_amd.models import build_model
+    from mlcomp_amd.models.native_resnet import NativeResNet
+    from mlcomp_amd.parallel.ddp import plan_buckets
+    net = NativeResNet(build_model('resnet50', num_classes=1000), 'cpu')
+    a = net.arena.decay
+    mb = 2 ** 20
+    for last in (None, 4 * mb, 1 * mb):
+        bs = plan_buckets(a, 32 * mb, 8 * mb, last)
+        assert bs[0].start == 0 and bs[-1].end == a.numel
+        assert all(x.end == y.start for x, y in zip(bs, bs[1:]))
+        assert sum(len(b.slots) for b in bs) == len(a.slots)
+        assert bs[0].nbytes >= 8 * mb
+        if last:
+            assert bs[-1].nbytes <= last and len(bs[-1].slots) >= 1
+    assert plan_buckets(a, 32 * mb, 8 * mb, 4 * mb)[-1].nbytes < plan_buckets(a, 32 * mb, 8 * mb)[-1].nbytes
