@@ -48,15 +48,17 @@ class _Dense:
         return Tx.dense_fwd(x, self.w.bf16, self.b.master, act, want_preact)
 
     def bwd_params(self, dy, x):
-        """dW += dy^T x, db += colsum(dy) (straight into the grad arena)."""
-        a = self.ctx.arena
+        """dW += dy^T x, db += colsum(dy) (straight into the grad arena); the caller calls
+        :meth:`mark` after the layer's dgrad, the last backward reader of W."""
         if dy.shape[0] % 8 == 0 and dy.shape[1] % 8 == 0 and x.shape[1] % 8 == 0:
             Fn.linear_wgrad_bias(dy, x, self.w.grad, self.b.grad)
         else:
             Fn.linear_wgrad(dy, x, out=self.w.grad, accumulate=True)
             Tx.colsum_acc(dy, self.b.grad)
-        a.mark_ready(self.w)
-        a.mark_ready(self.b)
+
+    def mark(self):
+        self.ctx.arena.mark_ready(self.w)
+        self.ctx.arena.mark_ready(self.b)
 
 
 class _LN:
@@ -140,13 +142,16 @@ class NativeBertLayer:
         self.ln2.mark()
         self.ffn2.bwd_params(df, g)
         du = Tx.dense_dgrad(df, self.ffn2.w.bf16, dact_u=u)          # grad of the GELU input
+        self.ffn2.mark()
         self.ffn1.bwd_params(du, h1)
         dh1 = Tx.dense_dgrad(du, self.ffn1.w.bf16, addend=ds2)       # + residual branch
+        self.ffn1.mark()
         ds1, dao = Tx.ln_bwd(dh1, s1, m1, r1, self.ln1.g.master, self.ln1.g.grad, self.ln1.b.grad,
                              ws[self.ln1.k_sums], p_in=ph, seed=net.seed, salt_in=self.salt + 1, want_dr=True)
         self.ln1.mark()
         self.out.bwd_params(dao, ctx2)
         dctx2 = Tx.dense_dgrad(dao, self.out.w.bf16)
+        self.out.mark()
         if fused:
             qkv, lse = att
             dqkv = Tx.attn_bwd(qkv, key_bias, dctx2, lse, B, S, nh, 1.0 / math.sqrt(dh), pa, net.seed, self.salt)
@@ -160,7 +165,9 @@ class NativeBertLayer:
             dk = torch.bmm(dS.transpose(1, 2), q)
             dqkv = torch.stack([dq, dk, dv]).view(3, B, nh, S, dh).permute(1, 3, 0, 2, 4).reshape(B * S, 3 * nh * dh)
         self.qkv.bwd_params(dqkv, x)
-        return Tx.dense_dgrad(dqkv, self.qkv.w.bf16, addend=ds1)
+        dx = Tx.dense_dgrad(dqkv, self.qkv.w.bf16, addend=ds1)
+        self.qkv.mark()
+        return dx
 
 
 class _BertLayerFn(torch.autograd.Function):
@@ -231,13 +238,14 @@ class _HeadFn(torch.autograd.Function):
         a = net.ctx.arena
         Fn.linear_wgrad(dl, pd, out=net.cls_w.grad, accumulate=True)
         Tx.colsum_acc(dl, net.cls_b.grad) if dl.shape[1] % 8 == 0 else net.cls_b.grad.add_(dl.float().sum(0))
+        dpd = Fn.linear_dgrad(dl, net.cls_w.bf16)
         a.mark_ready(net.cls_w)
         a.mark_ready(net.cls_b)
-        dpd = Fn.linear_dgrad(dl, net.cls_w.bf16)
         dpooled = Tx.dropout(dpd, net.p_hidden, net.seed, 2)   # same mask, same scale
         dz = (dpooled.float() * (1 - pooled.float() ** 2)).to(torch.bfloat16)
         net.pooler.bwd_params(dz, cls)
         dcls = Tx.dense_dgrad(dz, net.pooler.w.bf16)
+        net.pooler.mark()
         dh = torch.zeros(net.B, net.S, dcls.shape[1], device=dcls.device, dtype=torch.bfloat16)
         dh[:, 0] = dcls
         return dh.view(net.B * net.S, -1), None, None, None

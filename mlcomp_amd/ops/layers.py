@@ -4,7 +4,8 @@ A native layer is a small Python object (not an ``nn.Module``) whose parameters 
 slots of a :class:`~mlcomp_amd.ops.arena.ParamArena`.  Its autograd Function writes
 parameter gradients *directly* into the arena's grad buffer (wgrad epilogues, BN
 dgamma/dbeta) and notifies the arena (``mark_ready``) so the gradient bucketer can
-launch the all-reduce of a completed bucket while backward continues.  Autograd only
+launch the all-reduce (and the optimizer update) of a completed bucket while backward
+continues; a slot is marked only after the last backward kernel that reads its weight.  Autograd only
 carries activation gradients; every Function takes the model's ``anchor`` tensor
 (requires_grad=True) so the graph is built even though the input image needs no grad.
 
@@ -188,12 +189,13 @@ class ConvBN:
         return (y, self.save_mean, self.ctx.ws[self.k_bw])
 
     def wgrad(self, dy, x, in_affine=None):
-        """Weight gradient into the arena (masked for the s2d stem), then mark it ready."""
+        """Weight gradient into the arena (masked for the s2d stem).  The caller marks the
+        slot ready once nothing later in backward reads the weight (its dgrad): a marked
+        bucket may be updated by the optimizer right away (GradBucketer)."""
         Fn.conv2d_wgrad(dy, x, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad,
                         accumulate=self.ctx.grad_prezeroed, in_affine=in_affine)
         if self.s2d:
             self.w.grad.mul_(self._gmask)
-        self.ctx.arena.mark_ready(self.w)
 
     def bwd(self, dz, rec, want_dres=False, dx_addend=None, need_dx=True, dx_out=None,
             prereduced=False, dgrad_bn=None, in_affine=None):
@@ -210,6 +212,7 @@ class ConvBN:
         if need_dx:
             dx = Fn.conv2d_dgrad(dy, self.w.bf16, x.shape, self.stride, self.pad, self.dil,
                                  addend=dx_addend, out=dx_out, bn=dgrad_bn)
+        arena.mark_ready(self.w)   # after the dgrad: the last reader of w in backward
         return dx, dres
 
 
@@ -436,6 +439,7 @@ class _StemPoolFn(torch.autograd.Function):
         arena.mark_ready(st.gamma)
         arena.mark_ready(st.beta)
         st.wgrad(dy, x)
+        arena.mark_ready(st.w)
         return None, None, None
 
 
@@ -502,9 +506,9 @@ class _HeadFn(torch.autograd.Function):
         h: ClassifierHead = ctx.h
         arena = h.ctx.arena
         Fn.linear_wgrad(dl, pooled, out=h.w.grad)
-        arena.mark_ready(h.w)
         Fn.colsum(dl, h.b.grad)
-        arena.mark_ready(h.b)
         dpooled = Fn.linear_dgrad(dl, h.w.bf16)
+        arena.mark_ready(h.w)      # after the dgrad (the last reader of w)
+        arena.mark_ready(h.b)
         dx = Fn.avgpool_bwd(dpooled, ctx.xshape)
         return dx, None, None, None

@@ -8,9 +8,12 @@ MI355X:
 * Gradients already live in one flat fp32 arena, laid out in backward order
   (`mlcomp_amd.ops.arena`).  A bucket is a contiguous slice of it, so an all-reduce is
   issued on the slice itself - no flatten/unflatten copies.
-* Native layers call ``arena.mark_ready(slot)`` right after writing a gradient; when
-  the last slot of a bucket is ready the bucket is all-reduced on a dedicated side
-  stream (event fence from the compute stream), overlapping the rest of backward.
+* Native layers call ``arena.mark_ready(slot)`` once a gradient is written and nothing
+  later in backward reads the weight; when the last slot of a bucket is ready the bucket
+  is all-reduced on a dedicated side stream (event fence from the compute stream),
+  overlapping the rest of backward, and (``attach_optimizer``) its fused optimizer
+  update follows on the same stream - so on one GPU too the optimizer pass overlaps
+  backward instead of running after it.
 * Bucket size: an 8-GPU ring all-reduce moves 2*(7/8)*S per GPU over point-to-point
   xGMI (7 links x ~153 GB/s); with RCCL using several channels the per-peer chunk
   (S/8) should stay >= ~1-4 MB to amortise latency, hence 32 MB buckets, a smaller
@@ -99,24 +102,42 @@ class GradBucketer:
                 self.slot_bucket[id(s)] = b
         self.is_cuda = params.device.type == 'cuda'
         self.side = torch.cuda.Stream(params.device) if self.is_cuda else None
+        self.opt = None
+        # debug / test mode: run each bucket's work on the compute stream at the moment the
+        # bucket completes, so a weight read after its slot was marked ready shows up as a
+        # numeric difference instead of a timing-dependent race
+        self.sync = os.environ.get('MLC_BUCKET_SYNC', '0') == '1'
         params.ready_hook = self._ready
+
+    def attach_optimizer(self, opt):
+        """Optimizer-in-backward: each bucket's fused update (``opt.step_slice``) follows
+        its all-reduce on the side stream, overlapping the rest of backward; the step then
+        needs no optimizer launch of its own (``opt.step()`` must not be called)."""
+        self.opt = opt
 
     def begin(self):
         for b in self.buckets:
             b.pending = len(b.slots)
             b.launched = False
 
+    def _work(self, b: Bucket, stream=None):
+        if self.comm is not None:
+            self.comm.all_reduce(b.view, 'sum', stream=stream)
+        if self.opt is not None:
+            self.opt.step_slice(b.arena, b.start, b.end)
+
     def _launch(self, b: Bucket):
         b.launched = True
-        if self.comm is None:
+        if self.comm is None and self.opt is None:
             return
-        if self.is_cuda:
+        if self.is_cuda and not self.sync:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.params.device))
             self.side.wait_event(ev)
-            self.comm.all_reduce(b.view, 'sum', stream=self.side)
+            with torch.cuda.stream(self.side):
+                self._work(b, self.side)
         else:
-            self.comm.all_reduce(b.view, 'sum')
+            self._work(b)
 
     def _ready(self, slot: Slot):
         b = self.slot_bucket.get(id(slot))
@@ -132,7 +153,7 @@ class GradBucketer:
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)
-        if self.is_cuda and self.comm is not None:
+        if self.is_cuda and (self.comm is not None or self.opt is not None) and not self.sync:
             ev = torch.cuda.Event()
             ev.record(self.side)
             torch.cuda.current_stream(self.params.device).wait_event(ev)

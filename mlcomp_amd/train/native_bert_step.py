@@ -39,6 +39,13 @@ class NativeBertStep(GraphedStep):
         self.bucketer.broadcast_params()
         self.opt = FusedAdam(self.net.arena, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, decoupled=True,
                              grad_scale=1.0 / world_size)
+        # optimizer-in-backward (MLC_OPT_IN_BWD=1): each gradient bucket is updated on the side
+        # stream as soon as it is complete (and all-reduced).  Measured slower on MI355X
+        # (profiles/round2_ab): the memory-bound update competes with the memory-bound
+        # backward passes, so the default is one update launch per arena after backward.
+        self.opt_in_bwd = os.environ.get('MLC_OPT_IN_BWD', '0') == '1'
+        if self.opt_in_bwd:
+            self.bucketer.attach_optimizer(self.opt)
         self.batch, self.seq_len = batch, seq_len
         rank = int(os.environ.get('RANK', '0'))
         g = torch.Generator(device=self.device)
@@ -79,7 +86,8 @@ class NativeBertStep(GraphedStep):
         loss = net.loss(self.ids, self.tt, self.key_bias, self.y)
         loss.backward()
         self.bucketer.finish()
-        self.opt.step()
+        if not self.opt_in_bwd:
+            self.opt.step()
 
     def set_lr(self, lr):
         self.opt.set_lr(lr)

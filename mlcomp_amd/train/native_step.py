@@ -48,6 +48,13 @@ class NativeClassifierStep(GraphedStep):
         else:
             self.opt = FusedSGD(self.net.arena, lr=lr, momentum=momentum, weight_decay=weight_decay,
                                 nesterov=nesterov, grad_scale=1.0 / world_size)
+        # optimizer-in-backward (MLC_OPT_IN_BWD=1): each gradient bucket is updated on the side
+        # stream as soon as it is complete (and all-reduced).  Measured slower on MI355X
+        # (profiles/round2_ab): the memory-bound update competes with the memory-bound
+        # backward passes, so the default is one update launch per arena after backward.
+        self.opt_in_bwd = os.environ.get('MLC_OPT_IN_BWD', '0') == '1'
+        if self.opt_in_bwd:
+            self.bucketer.attach_optimizer(self.opt)
         self.batch = batch
         rank = int(os.environ.get('RANK', '0'))
         g = torch.Generator(device=self.device)
@@ -85,7 +92,8 @@ class NativeClassifierStep(GraphedStep):
         loss = self.net.loss(self.x, self.y)
         loss.backward()
         self.bucketer.finish()
-        self.opt.step()
+        if not self.opt_in_bwd:
+            self.opt.step()
         self._loss = self.net.head.loss_sum()
 
     def set_lr(self, lr):

@@ -19,6 +19,12 @@ from mlcomp_amd.ops.arena import ParamArena
 
 
 class _ArenaStateMixin:
+    def _slice(self, a, start, end):
+        """views of one contiguous slice of an arena: (master, grad, mirror, n, ndecay, nbf)"""
+        n = end - start
+        mirror = a.mirror[start:end] if a.mirror is not None else None
+        return a.master[start:end], a.grad[start:end], mirror, n, n if a.decay else 0, n if mirror is not None else 0
+
     """Checkpointable optimizer state: the step counter and every arena state buffer
     (momentum / Adam moments) as CPU tensors, keyed ``<arena>.<buffer>``."""
 
@@ -70,6 +76,12 @@ class FusedSGD(_ArenaStateMixin):
                         a.numel if a.decay else 0, a.numel if a.mirror is not None else 0,
                         self.momentum, self.dampening, self.wd, self.nesterov, False)
 
+    def step_slice(self, a, start, end):
+        """The update of elements [start, end) of arena ``a`` (one gradient bucket)."""
+        p, g, bf, n, nd, nb = self._slice(a, start, end)
+        Fn.sgd_step(p, g, a.state['momentum'][start:end], bf, self.hyper, nd, nb, self.momentum, self.dampening,
+                    self.wd, self.nesterov, False)
+
 
 class FusedAdam(_ArenaStateMixin):
     def __init__(self, arena: ParamArena, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
@@ -108,3 +120,9 @@ class FusedAdam(_ArenaStateMixin):
                          self.hyper, a.numel if a.decay else 0,
                          a.numel if a.mirror is not None else 0, self.b1, self.b2, self.eps,
                          self.wd, self.decoupled)
+
+    def step_slice(self, a, start, end):
+        """The update of elements [start, end) of arena ``a`` (one gradient bucket)."""
+        p, g, bf, n, nd, nb = self._slice(a, start, end)
+        Fn.adam_step(p, g, a.state['exp_avg'][start:end], a.state['exp_avg_sq'][start:end], bf, self.hyper, nd, nb,
+                     self.b1, self.b2, self.eps, self.wd, self.decoupled)

@@ -285,3 +285,35 @@ def test_bucket_plan_caps_the_exposed_last_bucket():
         if last:
             assert bs[-1].nbytes <= last and len(bs[-1].slots) >= 1
     assert plan_buckets(a, 32 * mb, 8 * mb, 4 * mb)[-1].nbytes < plan_buckets(a, 32 * mb, 8 * mb)[-1].nbytes
+
+
+@pytest.mark.parametrize('kind', ['resnet', 'unet', 'bert'])
+def test_optimizer_in_backward_matches_step_at_end(kind, monkeypatch):
+    """Each gradient bucket is updated as soon as its last gradient is marked ready.  On the
+    CPU that update runs immediately, so a weight read in backward after its slot was marked
+    (a dgrad after its wgrad) would change the result: both modes must agree exactly."""
+    # one bucket per parameter: every slot is updated the moment it is marked
+    monkeypatch.setenv('MLC_BUCKET_MB', '0.0001')
+    monkeypatch.setenv('MLC_FIRST_BUCKET_MB', '0.0001')
+    monkeypatch.setenv('MLC_LAST_BUCKET_MB', '0')
+
+    def run(flag):
+        monkeypatch.setenv('MLC_OPT_IN_BWD', flag)
+        torch.manual_seed(0)
+        if kind == 'resnet':
+            from mlcomp_amd.train.native_step import NativeClassifierStep
+            st = NativeClassifierStep('resnet18', batch=4, image_size=32, device='cpu', num_classes=10,
+                                      use_graph=False, lr=0.1)
+        elif kind == 'unet':
+            from mlcomp_amd.train.native_seg_step import NativeSegmentationStep
+            st = NativeSegmentationStep('resnet18', batch=2, image_size=64, device='cpu', use_graph=False, lr=1e-2)
+        else:
+            from mlcomp_amd.train.native_bert_step import NativeBertStep
+            st = NativeBertStep('bert-tiny', batch=4, seq_len=16, device='cpu', use_graph=False, lr=1e-2)
+        assert st.opt_in_bwd == (flag == '1')
+        for _ in range(2):
+            st()
+        return torch.cat([a.master.flatten() for a in st.net.arena.arenas()])
+    a, b = run('1'), run('0')
+    assert torch.isfinite(a).all()
+    assert torch.allclose(a, b, atol=1e-6, rtol=1e-5), (a - b).abs().max()
