@@ -4,9 +4,9 @@
 //   encoder skip: out[n,y,x,:C1] = lo[n,y/2,x/2,:], out[n,y,x,C1:] = skip[n,y,x,:].  One
 //   16-byte chunk per thread, both sources and the destination read/written once.
 //   Backward: dlo = 2x2 sum-pool of dout[..., :C1] (fp32 accumulate), dskip = dout[..., C1:].
-// * seg head + BCE-with-logits + soft-Dice loss, classes = 1: the 1x1
-//   output conv (Cin -> 1, + bias) is a per-pixel dot product, so it is fused with the
-//   loss.  Forward: logit, sigmoid, and the four global sums the loss needs (BCE sum,
+// * seg head + BCE-with-logits + soft-Dice loss, K <= 4 classes (one
+//   sigmoid per class, the Severstal-style multi-label masks): the 1x1 output conv
+//   (Cin -> K, + bias) is K per-pixel dot products, so it is fused with the loss.  Forward: logit, sigmoid, and the four global sums the loss needs (BCE sum,
 //   sum s*t, sum s, sum t) reduced per block then one atomic each.  Backward (the Dice
 //   gradient needs the global sums, hence a second pass): dlogit, dx = dlogit * w, and
 //   dw / db block-reduced into the grad arena.
@@ -100,37 +100,47 @@ __device__ __forceinline__ void block_sum(float (&v)[NV], float* red) {
   }
 }
 
-__device__ __forceinline__ float pixel_logit(const bf16* xp, const float* w, float b, int C) {
-  float z = b;
+// K (<= 8) per-pixel logits z_k = b_k + x[p] . w_k, weights [K][C] staged in LDS
+template <int K>
+__device__ __forceinline__ void pixel_logits(const bf16* xp, const float* w, const float* b, int C, float (&z)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) z[k] = b[k];
   for (int c = 0; c < C; c += 8) {
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(xp + c), f);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) z += f[e] * w[c + e];
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[k] += f[e] * w[k * C + c + e];
   }
-  return z;
 }
 
-// sums[0..3] += (BCE sum, sum s*t, sum s, sum t)
+// sums[0..3] += (BCE sum, sum s*t, sum s, sum t) over pixels and classes; target [P][K]
+template <int K>
 __global__ void __launch_bounds__(NT)
 seg_head_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
                     const float* __restrict__ target, float* __restrict__ logits, float* __restrict__ sums, long P,
                     int C) {
   __shared__ float red[NT / 64 * 4];
-  __shared__ float ws[256];
-  for (int c = threadIdx.x; c < C; c += NT) ws[c] = w[c];
+  __shared__ float ws[K * 256];
+  __shared__ float bs[K];
+  for (int c = threadIdx.x; c < K * C; c += NT) ws[c] = w[c];
+  if (threadIdx.x < K) bs[threadIdx.x] = bias[threadIdx.x];
   __syncthreads();
-  const float b = bias[0];
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   for (long p = (long)blockIdx.x * NT + threadIdx.x; p < P; p += (long)gridDim.x * NT) {
-    const float z = pixel_logit(x + p * C, ws, b, C);
-    const float t = target[p];
-    const float s = 1.f / (1.f + __expf(-z));
-    if (logits) logits[p] = z;
-    acc[0] += fmaxf(z, 0.f) - z * t + log1pf(__expf(-fabsf(z)));
-    acc[1] += s * t;
-    acc[2] += s;
-    acc[3] += t;
+    float z[K];
+    pixel_logits<K>(x + p * C, ws, bs, C, z);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const float t = target[p * K + k];
+      const float sg = 1.f / (1.f + __expf(-z[k]));
+      if (logits) logits[p * K + k] = z[k];
+      acc[0] += fmaxf(z[k], 0.f) - z[k] * t + log1pf(__expf(-fabsf(z[k])));
+      acc[1] += sg * t;
+      acc[2] += sg;
+      acc[3] += t;
+    }
   }
   block_sum<4>(acc, red);
   if (threadIdx.x == 0) {
@@ -139,59 +149,75 @@ seg_head_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w, con
   }
 }
 
-// dx[p] = dz_p * w;  dw[c] += sum_p dz_p x[p,c];  db += sum_p dz_p
+// dx[p] = sum_k dz_pk w_k;  dw[k][c] += sum_p dz_pk x[p,c];  db[k] += sum_p dz_pk
+template <int K>
 __global__ void __launch_bounds__(NT)
 seg_head_bwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
                     const float* __restrict__ target, const float* __restrict__ sums, bf16* __restrict__ dx,
                     float* __restrict__ dw, float* __restrict__ db, long P, int C, float bce_w, float dice_w,
                     float eps) {
-  __shared__ float red[NT / 64 * 4];
-  __shared__ float ws[256];
-  __shared__ float dws[NT / 64][256];
-  for (int c = threadIdx.x; c < C; c += NT) ws[c] = w[c];
-  for (int c = threadIdx.x; c < NT / 64 * 256; c += NT) (&dws[0][0])[c] = 0.f;
+  __shared__ float red[NT / 64 * K];
+  __shared__ float ws[K * 256];
+  __shared__ float bs[K];
+  __shared__ float dws[NT / 64][K * 256];
+  for (int c = threadIdx.x; c < K * C; c += NT) ws[c] = w[c];
+  if (threadIdx.x < K) bs[threadIdx.x] = bias[threadIdx.x];
+  for (int c = threadIdx.x; c < NT / 64 * K * 256; c += NT) (&dws[0][0])[c] = 0.f;
   __syncthreads();
-  const float b = bias[0];
   const float I = sums[1], U = sums[2] + sums[3];
-  const float inv_n = 1.f / (float)P;
+  const float inv_n = 1.f / ((float)P * K);
   const float den = U + eps, num = 2.f * I + eps;
   // d(1 - dice)/ds = -(2 t den - num) / den^2
   const float ka = -2.f / den, kb = num / (den * den);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float dbias = 0.f;
-  // per-wave channel partials of dw in LDS (C <= 256), summed over waves at the end
+  float dbias[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) dbias[k] = 0.f;
+  // per-wave partials of dw in LDS (K*C <= 1024), summed over waves at the end
   for (long p0 = (long)blockIdx.x * NT; p0 < P; p0 += (long)gridDim.x * NT) {
     const long p = p0 + threadIdx.x;
     const bool ok = p < P;                    // every lane runs the wave reductions
-    float dz = 0.f;
+    float dz[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) dz[k] = 0.f;
     if (ok) {
-      const float z = pixel_logit(x + p * C, ws, b, C);
-      const float t = target[p];
-      const float s = 1.f / (1.f + __expf(-z));
-      dz = bce_w * (s - t) * inv_n + dice_w * (ka * t + kb) * s * (1.f - s);
+      float z[K];
+      pixel_logits<K>(x + p * C, ws, bs, C, z);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const float t = target[p * K + k];
+        const float sg = 1.f / (1.f + __expf(-z[k]));
+        dz[k] = bce_w * (sg - t) * inv_n + dice_w * (ka * t + kb) * sg * (1.f - sg);
+      }
     }
     for (int c = 0; c < C; c += 8) {
       float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, g[8];
       if (ok) unpack8(*reinterpret_cast<const uint4*>(x + p * C + c), f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        g[e] = dz * ws[c + e];
-        f[e] *= dz;
+        g[e] = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) g[e] += dz[k] * ws[k * C + c + e];
       }
       if (ok) *reinterpret_cast<uint4*>(dx + p * C + c) = pack8(g);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float r = wave_sum(f[e]);
-        if (lane == 0) dws[wave][c + e] += r;
-      }
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float r = wave_sum(f[e] * dz[k]);
+          if (lane == 0) dws[wave][k * C + c + e] += r;
+        }
     }
-    dbias += dz;
+#pragma unroll
+    for (int k = 0; k < K; ++k) dbias[k] += dz[k];
   }
-  float v[1] = {dbias};
-  block_sum<1>(v, red);
-  if (threadIdx.x == 0) atomicAdd(db, v[0]);
+  block_sum<K>(dbias, red);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) atomicAdd(db + k, dbias[k]);
+  }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += NT) {
+  for (int c = threadIdx.x; c < K * C; c += NT) {
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < NT / 64; ++q) s += dws[q][c];
@@ -227,22 +253,31 @@ MLC_EXPORT int mlc_upcat_bwd(const bf16* dout, bf16* dlo, bf16* dskip, int N, in
   return hipGetLastError();
 }
 
-// x [P][C] bf16 (C % 8 == 0, C <= 256), w [C], bias [1], target [P] fp32 in {0,1} (soft ok);
-// logits [P] fp32 (optional); sums [4] fp32 zeroed by the caller
+// x [P][C] bf16 (C % 8 == 0, C <= 256), w [K][C], bias [K], target [P][K] fp32 in {0,1}
+// (soft ok); logits [P][K] fp32 (optional); sums [4] fp32 zeroed by the caller.  K <= 4.
+#define SEG_K_DISPATCH(KERNEL, ...)                                                                       \
+  switch (K) {                                                                                          \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                                          \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;                                          \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break;                                          \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                                          \
+    default: return -1;                                                                                 \
+  }
 MLC_EXPORT int mlc_seg_head_fwd(const bf16* x, const float* w, const float* bias, const float* target, float* logits,
-                                float* sums, long P, int C, hipStream_t st) {
-  if (C % 8 || C > 256) return -1;
-  hipLaunchKernelGGL(seg_head_fwd_kernel, dim3(grid_for(P) < 2048 ? grid_for(P) : 2048), dim3(NT), 0, st, x, w, bias,
-                     target, logits, sums, P, C);
+                                float* sums, long P, int C, int K, hipStream_t st) {
+  if (C % 8 || C > 256 || K < 1 || K > 4) return -1;
+  const int grid = grid_for(P) < 2048 ? grid_for(P) : 2048;
+  SEG_K_DISPATCH(seg_head_fwd_kernel, dim3(grid), dim3(NT), 0, st, x, w, bias, target, logits, sums, P, C);
   return hipGetLastError();
 }
 
-// dx [P][C] bf16 written; dw [C] / db [1] accumulated (+=)
+// dx [P][C] bf16 written; dw [K][C] / db [K] accumulated (+=)
 MLC_EXPORT int mlc_seg_head_bwd(const bf16* x, const float* w, const float* bias, const float* target,
-                                const float* sums, bf16* dx, float* dw, float* db, long P, int C, float bce_w,
+                                const float* sums, bf16* dx, float* dw, float* db, long P, int C, int K, float bce_w,
                                 float dice_w, float eps, hipStream_t st) {
-  if (C % 8 || C > 256) return -1;
-  hipLaunchKernelGGL(seg_head_bwd_kernel, dim3(grid_for(P) < 2048 ? grid_for(P) : 2048), dim3(NT), 0, st, x, w, bias,
-                     target, sums, dx, dw, db, P, C, bce_w, dice_w, eps);
+  if (C % 8 || C > 256 || K < 1 || K > 4) return -1;
+  const int grid = grid_for(P) < 2048 ? grid_for(P) : 2048;
+  SEG_K_DISPATCH(seg_head_bwd_kernel, dim3(grid), dim3(NT), 0, st, x, w, bias, target, sums, dx, dw, db, P, C, bce_w,
+                 dice_w, eps);
   return hipGetLastError();
 }

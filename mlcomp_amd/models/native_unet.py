@@ -10,7 +10,7 @@
   each of them is unlinked (``prev = None``) and reduces its own BN from the full sum.
 * decoder block: one fused kernel for the x2 nearest upsample + skip concat
   (``ops.seg.upcat_*``), then two fused conv3x3+BN+ReLU nodes.
-* head: the 1x1 output conv (16 -> 1 class, + bias) is a per-pixel dot product fused with
+* head: the 1x1 output conv (16 -> K <= 4 classes, + bias) is K per-pixel dot products fused with
   BCE-with-logits + soft-Dice (``ops.seg.seg_head_*``).
 
 Activations are NHWC bf16 end to end; parameters live in the flat arenas (fused Adam,
@@ -40,25 +40,27 @@ class _UpCatFn(torch.autograd.Function):
 
 
 class SegHead:
-    """1x1 conv (C -> 1, bias) + BCE-with-logits + soft-Dice, one forward and one
-    backward kernel.  ``__call__`` returns the loss (device scalar); backward assumes
+    """1x1 conv (C -> K <= 4 classes, bias) + per-class sigmoid BCE-with-logits + soft Dice
+    over all classes (contrib.criterion.BCEDiceLoss), one forward and one backward kernel.
+    Targets are [P, K] in pixel order (NHWC masks).  ``__call__`` returns the loss (device scalar); backward assumes
     d(loss) = 1."""
 
     def __init__(self, ctx: NativeContext, name: str, conv: nn.Conv2d, bce_w=1.0, dice_w=1.0, eps=1e-7):
-        assert conv.out_channels == 1 and conv.kernel_size == (1, 1), 'native SegHead: 1 class, 1x1 conv'
+        assert conv.out_channels <= 4 and conv.kernel_size == (1, 1), 'native SegHead: <= 4 classes, 1x1 conv'
         self.ctx = ctx
         self.conv = conv
         self.C = conv.in_channels
-        self.w = ctx.arena.weight(f'{name}.weight', (self.C,))
-        self.b = ctx.arena.vector(f'{name}.bias', (1,))
+        self.K = conv.out_channels
+        self.w = ctx.arena.weight(f'{name}.weight', (self.K, self.C))
+        self.b = ctx.arena.vector(f'{name}.bias', (self.K,))
         self.bce_w, self.dice_w, self.eps = bce_w, dice_w, eps
         self.k_sums = ctx.ws.request(f'{name}.sums', 4)
         self.logits = None      # optional fp32 [P] buffer the forward fills (metrics/inference)
 
     def load_from_torch(self):
         dev = self.ctx.device
-        self.w.master.copy_(self.conv.weight.detach().float().reshape(-1).to(dev))
-        b = self.conv.bias.detach().float() if self.conv.bias is not None else torch.zeros(1)
+        self.w.master.copy_(self.conv.weight.detach().float().reshape(self.K, self.C).to(dev))
+        b = self.conv.bias.detach().float() if self.conv.bias is not None else torch.zeros(self.K)
         self.b.master.copy_(b.to(dev))
 
     def export_to_torch(self):
@@ -81,7 +83,7 @@ class _SegHeadFn(torch.autograd.Function):
         seg.seg_head_fwd(xf, h.w.master, h.b.master, target, sums, logits=h.logits)
         ctx.h = h
         ctx.save_for_backward(x, target)
-        return seg.seg_loss(sums, xf.shape[0], h.bce_w, h.dice_w, h.eps)
+        return seg.seg_loss(sums, xf.shape[0] * h.K, h.bce_w, h.dice_w, h.eps)
 
     @staticmethod
     def backward(ctx, dloss):
@@ -154,7 +156,7 @@ class NativeUnet:
         return d
 
     def loss(self, x, target):
-        """BCE + Dice loss (device scalar); ``target`` fp32 [N*H*W] in pixel order."""
+        """BCE + Dice loss (device scalar); ``target`` fp32 [N*H*W*K] in pixel order."""
         return self.head(self.features(x), target)
 
     def train(self, mode=True):

@@ -36,8 +36,8 @@ _SIGS = {
     'mlc_linear_wgrad_bias': [vp] * 4 + [i32] * 7 + [vp, i64, vp],
     'mlc_upcat_fwd': [vp, vp, vp] + [i32] * 5 + [vp],
     'mlc_upcat_bwd': [vp, vp, vp] + [i32] * 5 + [vp],
-    'mlc_seg_head_fwd': [vp] * 6 + [i64, i32, vp],
-    'mlc_seg_head_bwd': [vp] * 8 + [i64, i32, f32, f32, f32, vp],
+    'mlc_seg_head_fwd': [vp] * 6 + [i64, i32, i32, vp],
+    'mlc_seg_head_bwd': [vp] * 8 + [i64, i32, i32, f32, f32, f32, vp],
     'mlc_attn_fwd': [vp] * 4 + [i32, i32, i32, f32, f32, vp, u32, vp],
     'mlc_attn_bwd': [vp] * 5 + [i32, i32, i32, f32, f32, vp, u32, vp],
     'mlc_colsum_acc': [vp, vp, vp, i32, i32, vp],

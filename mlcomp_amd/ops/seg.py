@@ -40,47 +40,52 @@ def upcat_bwd(dout, C1):
 
 
 def seg_head_fwd(x, w, b, target, sums, logits=None):
-    """x [P, C] bf16, w [C] / b [1] fp32, target [P] fp32.  Accumulates the loss sums
-    (BCE sum, sum s*t, sum s, sum t) into ``sums`` [4]; writes logits [P] if given."""
+    """x [P, C] bf16, w [K, C] (or [C] for one class) / b [K] fp32, target [P, K] (or [P])
+    fp32.  Accumulates the loss sums over pixels and classes (BCE sum, sum s*t, sum s,
+    sum t) into ``sums`` [4]; writes logits [P, K] if given."""
     P, C = x.shape
+    K = w.numel() // C
     if _cuda(x):
         _lib.call('mlc_seg_head_fwd', _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(target), _lib.ptr(logits),
-                  _lib.ptr(sums), P, C, _lib.stream())
+                  _lib.ptr(sums), P, C, K, _lib.stream())
         return sums
-    z = x.float() @ w.float() + b.float()
-    t = target.float()
+    z = x.float() @ w.float().reshape(K, C).t() + b.float().reshape(1, K)
+    t = target.float().reshape(P, K)
     s = torch.sigmoid(z)
     if logits is not None:
-        logits.copy_(z)
+        logits.copy_(z.reshape(logits.shape))
     bce = torch.nn.functional.binary_cross_entropy_with_logits(z, t, reduction='sum')
     sums.add_(torch.stack([bce, (s * t).sum(), s.sum(), t.sum()]))
     return sums
 
 
 def seg_loss(sums, n, bce_w=1.0, dice_w=1.0, eps=1e-7):
-    """Loss value from the forward sums (a device scalar, no host sync)."""
+    """Loss value from the forward sums (a device scalar, no host sync); ``n`` = pixels x
+    classes (the BCE mean's denominator)."""
     dice = (2 * sums[1] + eps) / (sums[2] + sums[3] + eps)
     return bce_w * sums[0] / n + dice_w * (1 - dice)
 
 
 def seg_head_bwd(x, w, b, target, sums, dw, db, bce_w=1.0, dice_w=1.0, eps=1e-7):
-    """Returns dx [P, C] bf16; dw [C] / db [1] are ACCUMULATED (+=)."""
+    """Returns dx [P, C] bf16; dw [K, C] / db [K] are ACCUMULATED (+=)."""
     P, C = x.shape
+    K = w.numel() // C
     if _cuda(x):
         dx = torch.empty_like(x)
         _lib.call('mlc_seg_head_bwd', _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(target), _lib.ptr(sums),
-                  _lib.ptr(dx), _lib.ptr(dw), _lib.ptr(db), P, C, float(bce_w), float(dice_w), float(eps),
+                  _lib.ptr(dx), _lib.ptr(dw), _lib.ptr(db), P, C, K, float(bce_w), float(dice_w), float(eps),
                   _lib.stream())
         return dx
-    z = x.float() @ w.float() + b.float()
-    t = target.float()
+    wk = w.float().reshape(K, C)
+    z = x.float() @ wk.t() + b.float().reshape(1, K)
+    t = target.float().reshape(P, K)
     s = torch.sigmoid(z)
     den = sums[2] + sums[3] + eps
     num = 2 * sums[1] + eps
-    dz = bce_w * (s - t) / P + dice_w * (-2 * t / den + num / den ** 2) * s * (1 - s)
-    dw.add_(x.float().t() @ dz)
-    db.add_(dz.sum().reshape(1))
-    return (dz[:, None] * w.float()[None]).to(torch.bfloat16)
+    dz = bce_w * (s - t) / (P * K) + dice_w * (-2 * t / den + num / den ** 2) * s * (1 - s)
+    dw.add_((dz.t() @ x.float()).reshape(dw.shape))
+    db.add_(dz.sum(0).reshape(db.shape))
+    return (dz @ wk).to(torch.bfloat16)
 
 
 __all__ = ['upcat_fwd', 'upcat_bwd', 'seg_head_fwd', 'seg_head_bwd', 'seg_loss']

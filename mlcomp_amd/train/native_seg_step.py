@@ -21,9 +21,10 @@ from mlcomp_amd.train.graphed import GraphedStep
 from mlcomp_amd.train.optim import FusedAdam, FusedSGD
 
 
-def synthetic_masks(batch, size, device, generator):
-    """Blob-shaped binary masks: a smoothed random field thresholded at its median-ish."""
-    low = torch.randn(batch, 1, size // 16, size // 16, device=device, generator=generator)
+def synthetic_masks(batch, size, device, generator, classes=1):
+    """Blob-shaped binary masks [batch, classes, size, size]: a smoothed random field
+    thresholded at its median-ish, one independent field per class."""
+    low = torch.randn(batch, classes, size // 16, size // 16, device=device, generator=generator)
     m = torch.nn.functional.interpolate(low, size=(size, size), mode='bilinear', align_corners=False)
     return (m > 0.3).float()
 
@@ -31,11 +32,11 @@ def synthetic_masks(batch, size, device, generator):
 class NativeSegmentationStep(GraphedStep):
     def __init__(self, encoder='resnet34', batch=32, image_size=256, device=None, world_size=1, use_graph=True,
                  lr=3e-4, weight_decay=0.0, optimizer='Adam', momentum=0.9, betas=(0.9, 0.999), eps=1e-8,
-                 seed=0, warmup_eager=2, torch_model=None, comm=None):
+                 seed=0, warmup_eager=2, torch_model=None, comm=None, classes=1):
         from mlcomp_amd.contrib.segmentation.models import Unet
         self.device = torch.device(device or 'cuda')
         torch.manual_seed(seed)
-        tm = torch_model if torch_model is not None else Unet(encoder_name=encoder, classes=1)
+        tm = torch_model if torch_model is not None else Unet(encoder_name=encoder, classes=classes)
         self.net = NativeUnet(tm, self.device)
         self.net.ctx.grad_prezeroed = True
         self.world = world_size
@@ -61,7 +62,10 @@ class NativeSegmentationStep(GraphedStep):
         g.manual_seed(4321 + rank)
         img = torch.randn(batch, image_size, image_size, 3, device=self.device, generator=g)
         self.x = self._prep(torch.nn.functional.pad(img, (0, STEM_CIN - 3)).to(torch.bfloat16).contiguous())
-        self.t = synthetic_masks(batch, image_size, self.device, g).reshape(-1).contiguous()
+        self.classes = self.net.head.K
+        # targets in pixel order [N, H, W, K] (the head's NHWC layout)
+        self.t = synthetic_masks(batch, image_size, self.device, g, self.classes).permute(0, 2, 3, 1).reshape(-1) \
+            .contiguous()
         self.use_graph = use_graph and self.device.type == 'cuda'
         self.warmup_eager = warmup_eager
         self.graph = None
@@ -76,12 +80,15 @@ class NativeSegmentationStep(GraphedStep):
 
     def load_batch(self, images: torch.Tensor, masks: torch.Tensor):
         """Copy a batch into the static buffers: images NCHW float (or NHWC bf16 padded),
-        masks [N, 1, H, W] / [N, H, W] in {0, 1}."""
+        masks [N, K, H, W] / [N, H, W] in {0, 1}."""
         x = images
         if x.dim() == 4 and x.shape[1] in (1, 3) and x.dtype != torch.bfloat16:
             x = Fn.nchw_to_nhwc(x.to(self.device, non_blocking=True).float(), pad_to=STEM_CIN)
         self.x.copy_(self._prep(x.to(self.device, non_blocking=True)))
-        self.t.copy_(masks.to(self.device, non_blocking=True).float().reshape(-1))
+        m = masks.to(self.device, non_blocking=True).float()
+        if m.dim() == 4:               # [N, K, H, W] -> pixel order [N, H, W, K]
+            m = m.permute(0, 2, 3, 1)
+        self.t.copy_(m.reshape(-1))
 
     def _body(self):
         self.net.ctx.ws.zero()

@@ -1,5 +1,6 @@
 """Native U-Net (encoder blocks, fused upsample+concat, fused head + BCE/Dice) against
 plain PyTorch autograd of the same model, on CPU (reference op paths)."""
+import pytest
 import torch
 
 from mlcomp_amd.contrib.criterion import BCEDiceLoss
@@ -87,3 +88,52 @@ def test_native_unet_matches_torch_autograd():
         losses.append(step.last_loss())
     assert losses[-1] < losses[0]
     net.export_to_torch()
+
+
+@pytest.mark.parametrize('K', [2, 4])
+def test_multiclass_seg_head_matches_bce_dice_autograd(K):
+    """K sigmoid classes (Severstal-style multi-label masks): BCE mean over pixels x classes
+    plus one soft Dice over everything, as contrib.criterion.BCEDiceLoss computes it."""
+    P, C = 300, 16
+    torch.manual_seed(K)
+    x = torch.randn(P, C).to(torch.bfloat16)
+    w, b = torch.randn(K, C) * 0.3, torch.randn(K) * 0.1
+    t = (torch.rand(P, K) > 0.6).float()
+    sums = torch.zeros(4)
+    seg.seg_head_fwd(x, w, b, t, sums)
+    xf, wf, bf = x.float().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    ref = BCEDiceLoss()(xf @ wf.t() + bf, t)
+    ref.backward()
+    assert abs(seg.seg_loss(sums, P * K).item() - ref.item()) < 1e-5
+    dw, db = torch.zeros(K, C), torch.zeros(K)
+    dx = seg.seg_head_bwd(x, w, b, t, sums, dw, db)
+    assert torch.allclose(dw, wf.grad, atol=1e-5) and torch.allclose(db, bf.grad, atol=1e-6)
+    assert _cos(dx, xf.grad) > 0.9999
+
+
+def test_native_unet_four_classes_matches_torch():
+    torch.manual_seed(1)
+    tm = Unet(encoder_name='resnet18', classes=4)
+    ref = Unet(encoder_name='resnet18', classes=4)
+    ref.load_state_dict(tm.state_dict())
+    step = NativeSegmentationStep(torch_model=tm, batch=2, image_size=64, device='cpu', lr=1e-3, use_graph=False)
+    assert step.classes == 4 and step.t.numel() == 2 * 64 * 64 * 4
+    x = Fn.stem_s2d_to_nhwc(step.x).permute(0, 3, 1, 2).contiguous()
+    t = step.t.view(2, 64, 64, 4).permute(0, 3, 1, 2)
+    ref.train()
+    loss = BCEDiceLoss()(ref(x), t)
+    loss.backward()
+    net = step.net
+    net.ctx.ws.zero()
+    net.arena.zero_grad()
+    l_nat = net.loss(step.x, step.t)
+    l_nat.backward()
+    assert abs(l_nat.item() - loss.item()) / loss.item() < 0.03
+    g = net.arena.by_name['decoder.final_conv.weight'].grad
+    assert _cos(g, ref.decoder.final_conv.weight.grad.reshape(4, -1)) > 0.95
+    step.load_batch(torch.randn(2, 3, 64, 64), (torch.rand(2, 4, 64, 64) > 0.5).float())
+    losses = []
+    for _ in range(3):
+        step()
+        losses.append(step.last_loss())
+    assert all(v == v for v in losses)
