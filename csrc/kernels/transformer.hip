@@ -15,27 +15,13 @@
 // stored, backward regenerates the mask, and the seed lives in device memory so a
 // captured HIP graph advances it on every replay.
 #include "common.h"
+#include "dropout.h"
 #include <type_traits>
 
 namespace {
 
 constexpr int NT = 256;
 constexpr int NSTAT = 32;
-
-__device__ __forceinline__ uint32_t hash_u32(uint32_t seed, uint32_t salt, uint32_t i) {
-  uint32_t x = i * 0x9E3779B9u ^ (seed * 0x85EBCA6Bu + salt * 0xC2B2AE35u);
-  x ^= x >> 16; x *= 0x7FEB352Du;
-  x ^= x >> 15; x *= 0x846CA68Bu;
-  x ^= x >> 16;
-  return x;
-}
-// keep with probability 1-p: compare the top 24 bits against the threshold
-__device__ __forceinline__ bool keep(uint32_t seed, uint32_t salt, uint32_t i, uint32_t thr) {
-  return (hash_u32(seed, salt, i) >> 8) >= thr;
-}
-__host__ __device__ __forceinline__ uint32_t drop_threshold(float p) {
-  return (uint32_t)(p * 16777216.0f);
-}
 
 // 8-byte loads through an ext-vector type (see ldg16 in common.h); callers issue them from
 // a clamped, always-valid column so no load sits under a per-lane branch

@@ -4,8 +4,10 @@ the residual-gradient sum are fused into the dgrad epilogues, LayerNorm is one k
 fused with the residual add and hidden dropout, and attention (QK^T, scale + key mask,
 softmax, attention dropout, PV; backward recomputing P from the saved log-sum-exp) is one
 MFMA kernel per direction that reads Q/K/V in place from the QKV projection and writes
-dQ/dK/dV straight into its gradient (``Tx.attn_fwd`` / ``Tx.attn_bwd``, head dim 64,
-S in {64, 128}); other shapes fall back to library batched GEMMs around the softmax kernel.
+dQ/dK/dV straight into its gradient (``Tx.attn_fwd`` / ``Tx.attn_bwd``: whole-tile kernels
+for head dim 64 with S in {64, 128}, streaming flash kernels for head dim 64 / 128 and any
+S that is a multiple of 64); other shapes fall back to library batched GEMMs around the
+softmax kernel.
 
 Parameters live in the flat arenas (``ops.arena``): matmul weights and embedding tables
 in the decay arena (bf16 mirror for the kernels), biases and LayerNorm affine in the
@@ -109,7 +111,8 @@ class NativeBertLayer:
         qkv, _ = self.qkv.fwd(x)
         if Tx.attn_supported(S, dh):
             # fused attention: reads q/k/v in place, writes the merged-head context
-            ctx2, lse = Tx.attn_fwd(qkv, key_bias, B, S, nh, 1.0 / math.sqrt(dh), pa, net.seed, self.salt)
+            ctx2, lse = Tx.attn_fwd(qkv, key_bias, B, S, nh, 1.0 / math.sqrt(dh), pa, net.seed, self.salt,
+                                    head_dim=dh)
             att = (qkv, lse)
         else:
             q, k, v = qkv.view(B, S, 3, nh, dh).permute(2, 0, 3, 1, 4).reshape(3, B * nh, S, dh).unbind(0)
@@ -154,7 +157,8 @@ class NativeBertLayer:
         self.out.mark()
         if fused:
             qkv, lse = att
-            dqkv = Tx.attn_bwd(qkv, key_bias, dctx2, lse, B, S, nh, 1.0 / math.sqrt(dh), pa, net.seed, self.salt)
+            dqkv = Tx.attn_bwd(qkv, key_bias, dctx2, lse, B, S, nh, 1.0 / math.sqrt(dh), pa, net.seed, self.salt,
+                               head_dim=dh, ctx=ctx2)
         else:
             q, k, v, P, Pd = att
             dctx = dctx2.view(B, S, nh, dh).transpose(1, 2).reshape(B * nh, S, dh)

@@ -5,6 +5,7 @@ CPU path reproduces bit-exactly, so masks agree between the two."""
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -146,14 +147,29 @@ def softmax_bwd(P, dPd, scale, p=0.0, seed=None, salt=0):
 
 
 # ---------------------------------------------------------------------------- fused attention
+# The streaming kernels measured faster than the whole-tile ones on every shape both take
+# (profiles/flash_attn/); MLC_ATTN_KERNEL=tile routes head dim 64, S in {64, 128} back to them.
+_FLASH_ONLY = os.environ.get('MLC_ATTN_KERNEL', 'flash') != 'tile'
+
+
+def _attn_small(S: int, head_dim: int) -> bool:
+    """Shapes of the whole-tile kernels ``mlc_attn_fwd`` / ``mlc_attn_bwd`` (transformer.hip)."""
+    return head_dim == 64 and S in (64, 128) and not _FLASH_ONLY
+
+
+def _attn_flash(S: int, head_dim: int) -> bool:
+    """Shapes of the streaming kernels ``mlc_flash_fwd`` / ``mlc_flash_bwd`` (flash_attn.hip)."""
+    return head_dim in (64, 128) and S >= 64 and S % 64 == 0
+
+
 def attn_supported(S: int, head_dim: int) -> bool:
-    """Shapes the fused attention kernels take (``mlc_attn_fwd`` / ``mlc_attn_bwd``)."""
-    return head_dim == 64 and S in (64, 128)
+    """Shapes the fused attention path takes (either kernel family)."""
+    return _attn_small(S, head_dim) or _attn_flash(S, head_dim)
 
 
-def _attn_ref_probs(qkv, key_bias, B, S, H, scale):
-    E = H * 64
-    q, k, v = qkv.float().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4).unbind(0)   # [B, H, S, 64]
+def _attn_ref_probs(qkv, key_bias, B, S, H, scale, D=64):
+    E = H * D
+    q, k, v = qkv.float().view(B, S, 3, H, D).permute(2, 0, 3, 1, 4).unbind(0)   # [B, H, S, D]
     x = torch.matmul(q, k.transpose(-1, -2)) * scale
     if key_bias is not None:
         x = x + key_bias.float()[:, None, None, :]
@@ -161,20 +177,25 @@ def _attn_ref_probs(qkv, key_bias, B, S, H, scale):
     return q, k, v, P, E
 
 
-def attn_fwd(qkv, key_bias, B, S, H, scale, p=0.0, seed=None, salt=0):
-    """Fused multi-head attention over the QKV projection output ``qkv`` [B*S, 3*H*64]
-    (columns q | k | v, head h at h*64).  Returns (ctx [B*S, H*64] bf16, lse [B*H*S] fp32).
+def attn_fwd(qkv, key_bias, B, S, H, scale, p=0.0, seed=None, salt=0, head_dim: int = 64):
+    """Fused multi-head attention over the QKV projection output ``qkv`` [B*S, 3*H*D]
+    (columns q | k | v, head h at h*D).  Returns (ctx [B*S, H*D] bf16, lse [B*H*S] fp32).
     Attention-probability dropout uses the softmax kernel's mask indexing
-    (((b*H + h)*S + q)*S + key), so both paths drop the same elements."""
+    (((b*H + h)*S + q)*S + key), so every path drops the same elements."""
+    D = head_dim
     if _cuda(qkv):
-        assert attn_supported(S, 64) and qkv.is_contiguous() and tuple(qkv.shape) == (B * S, 3 * H * 64)
+        assert attn_supported(S, D) and qkv.is_contiguous() and tuple(qkv.shape) == (B * S, 3 * H * D)
         assert key_bias is None or (key_bias.is_contiguous() and tuple(key_bias.shape) == (B, S))
-        ctx = torch.empty(B * S, H * 64, device=qkv.device, dtype=torch.bfloat16)
+        ctx = torch.empty(B * S, H * D, device=qkv.device, dtype=torch.bfloat16)
         lse = torch.empty(B * H * S, device=qkv.device, dtype=torch.float32)
-        _lib.call('mlc_attn_fwd', _lib.ptr(qkv), _lib.ptr(key_bias), _lib.ptr(ctx), _lib.ptr(lse), B, S, H,
-                  float(scale), float(p), _lib.ptr(seed), salt, _lib.stream())
+        if _attn_small(S, D):
+            _lib.call('mlc_attn_fwd', _lib.ptr(qkv), _lib.ptr(key_bias), _lib.ptr(ctx), _lib.ptr(lse), B, S, H,
+                      float(scale), float(p), _lib.ptr(seed), salt, _lib.stream())
+        else:
+            _lib.call('mlc_flash_fwd', _lib.ptr(qkv), _lib.ptr(key_bias), _lib.ptr(ctx), _lib.ptr(lse), B, S, H, D,
+                      float(scale), float(p), _lib.ptr(seed), salt, _lib.stream())
         return ctx, lse
-    q, k, v, P, E = _attn_ref_probs(qkv, key_bias, B, S, H, scale)
+    q, k, v, P, E = _attn_ref_probs(qkv, key_bias, B, S, H, scale, D)
     Pd = P
     if p > 0:
         m = keep_mask((B, H, S, S), p, _seed_val(seed), salt)
@@ -187,18 +208,27 @@ def attn_fwd(qkv, key_bias, B, S, H, scale, p=0.0, seed=None, salt=0):
     return ctx.to(torch.bfloat16), lse
 
 
-def attn_bwd(qkv, key_bias, dctx, lse, B, S, H, scale, p=0.0, seed=None, salt=0):
-    """Gradient of :func:`attn_fwd` wrt ``qkv``: returns dqkv [B*S, 3*H*64] bf16."""
+def attn_bwd(qkv, key_bias, dctx, lse, B, S, H, scale, p=0.0, seed=None, salt=0, head_dim: int = 64, ctx=None):
+    """Gradient of :func:`attn_fwd` wrt ``qkv``: returns dqkv [B*S, 3*H*D] bf16.  ``ctx``
+    (the forward output) is needed by the streaming kernels (rowsum(dO * O))."""
+    D = head_dim
     if _cuda(qkv):
-        assert attn_supported(S, 64) and qkv.is_contiguous() and tuple(qkv.shape) == (B * S, 3 * H * 64)
-        assert dctx.is_contiguous() and tuple(dctx.shape) == (B * S, H * 64) and lse.numel() == B * H * S
+        assert attn_supported(S, D) and qkv.is_contiguous() and tuple(qkv.shape) == (B * S, 3 * H * D)
+        assert dctx.is_contiguous() and tuple(dctx.shape) == (B * S, H * D) and lse.numel() == B * H * S
         assert key_bias is None or (key_bias.is_contiguous() and tuple(key_bias.shape) == (B, S))
         dqkv = torch.empty_like(qkv)
-        _lib.call('mlc_attn_bwd', _lib.ptr(qkv), _lib.ptr(key_bias), _lib.ptr(dctx), _lib.ptr(lse), _lib.ptr(dqkv),
-                  B, S, H, float(scale), float(p), _lib.ptr(seed), salt, _lib.stream())
+        if _attn_small(S, D):
+            _lib.call('mlc_attn_bwd', _lib.ptr(qkv), _lib.ptr(key_bias), _lib.ptr(dctx), _lib.ptr(lse),
+                      _lib.ptr(dqkv), B, S, H, float(scale), float(p), _lib.ptr(seed), salt, _lib.stream())
+        else:
+            assert ctx is not None and ctx.is_contiguous() and ctx.shape == dctx.shape
+            dot = torch.empty(B * H * S, device=qkv.device, dtype=torch.float32)
+            _lib.call('mlc_flash_bwd', _lib.ptr(qkv), _lib.ptr(key_bias), _lib.ptr(ctx), _lib.ptr(dctx),
+                      _lib.ptr(lse), _lib.ptr(dot), _lib.ptr(dqkv), B, S, H, D, float(scale), float(p),
+                      _lib.ptr(seed), salt, _lib.stream())
         return dqkv
-    q, k, v, P, E = _attn_ref_probs(qkv, key_bias, B, S, H, scale)
-    do = dctx.float().view(B, S, H, 64).permute(0, 2, 1, 3)
+    q, k, v, P, E = _attn_ref_probs(qkv, key_bias, B, S, H, scale, D)
+    do = dctx.float().view(B, S, H, D).permute(0, 2, 1, 3)
     m = keep_mask((B, H, S, S), p, _seed_val(seed), salt) if p > 0 else None
     Pd = torch.where(m, P / (1 - p), torch.zeros_like(P)) if m is not None else P
     dv = torch.matmul(Pd.transpose(-1, -2), do)

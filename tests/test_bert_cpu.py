@@ -15,11 +15,13 @@ def _cos(a, b):
     return (a @ b / (a.norm() * b.norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize('S', [16, 64])     # 64: fused-attention path (head dim 64)
-def test_native_bert_matches_torch_autograd(S):
+# S=64: whole-tile fused-attention path (head dim 64); (128, 256): head dim 128, flash path
+@pytest.mark.parametrize('S,hidden', [(16, 128), (64, 128), (128, 256)])
+def test_native_bert_matches_torch_autograd(S, hidden):
     torch.manual_seed(0)
-    tm = build_model('bert-tiny', num_classes=3, hidden_dropout=0.0, attention_dropout=0.0)
-    ref = build_model('bert-tiny', num_classes=3, hidden_dropout=0.0, attention_dropout=0.0)
+    kw = dict(num_classes=3, hidden_dropout=0.0, attention_dropout=0.0, hidden=hidden)
+    tm = build_model('bert-tiny', **kw)
+    ref = build_model('bert-tiny', **kw)
     ref.load_state_dict(tm.state_dict())
     B = 4
     net = NativeBert(tm, 'cpu', B, S)

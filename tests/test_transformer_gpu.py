@@ -105,8 +105,10 @@ def test_dense_epilogues(M, N, K):
 
 @pytest.mark.parametrize('B,S,H,p,masked', [(2, 128, 3, 0.0, False), (3, 128, 12, 0.1, True),
                                              (2, 64, 4, 0.1, True), (1, 64, 2, 0.0, False)])
-def test_fused_attention_fwd_bwd(B, S, H, p, masked):
+def test_fused_attention_fwd_bwd(B, S, H, p, masked, monkeypatch):
+    """Whole-tile kernels (head dim 64, S in {64, 128}) vs the fp32 reference."""
     import math
+    monkeypatch.setattr(Tx, '_FLASH_ONLY', False)
     qkv = _bf(B * S, 3 * H * 64, seed=6, scale=0.7)
     dctx = _bf(B * S, H * 64, seed=7)
     kb = None
@@ -127,6 +129,95 @@ def test_fused_attention_fwd_bwd(B, S, H, p, masked):
     for part in range(3):   # dQ, dK, dV separately
         sl = slice(part * E, (part + 1) * E)
         assert rel(dq_g[:, sl], dq_r[:, sl]) < 2e-2, part
+
+
+@pytest.mark.parametrize('B,S,H,D,p,masked', [(2, 64, 2, 64, 0.0, False), (2, 192, 3, 64, 0.1, True),
+                                               (1, 512, 2, 64, 0.1, True), (2, 128, 2, 128, 0.0, True),
+                                               (1, 320, 2, 128, 0.1, False), (3, 128, 4, 64, 0.1, True)])
+def test_flash_attention_fwd_bwd(B, S, H, D, p, masked, monkeypatch):
+    """Streaming (flash) kernels vs the fp32 reference: S multiple of 64 incl. S % 128 != 0
+    (a block's last waves idle), head dims 64 / 128, key masks and attention dropout; the
+    (3, 128, 4, 64) case forces the flash path on a shape the whole-tile kernel also takes."""
+    import math
+    monkeypatch.setattr(Tx, '_FLASH_ONLY', True)
+    qkv = _bf(B * S, 3 * H * D, seed=16, scale=0.7)
+    dctx = _bf(B * S, H * D, seed=17)
+    kb = None
+    if masked:
+        kb = torch.zeros(B, S)
+        kb[0, S - 37:] = float('-inf')
+        kb[-1, :5] = -2.5                 # a finite bias too
+    seed = torch.tensor([29], dtype=torch.int32)
+    scale = 1.0 / math.sqrt(D)
+    ctx_r, lse_r = Tx.attn_fwd(qkv, kb, B, S, H, scale, p, seed, 33, head_dim=D)
+    dq_r = Tx.attn_bwd(qkv, kb, dctx, lse_r, B, S, H, scale, p, seed, 33, head_dim=D, ctx=ctx_r)
+    kbg = kb.to(DEV) if kb is not None else None
+    ctx_g, lse_g = Tx.attn_fwd(qkv.to(DEV), kbg, B, S, H, scale, p, seed.to(DEV), 33, head_dim=D)
+    dq_g = Tx.attn_bwd(qkv.to(DEV), kbg, dctx.to(DEV), lse_g, B, S, H, scale, p, seed.to(DEV), 33, head_dim=D,
+                       ctx=ctx_g)
+    torch.cuda.synchronize()
+    assert rel(ctx_g, ctx_r) < 1e-2
+    assert rel(lse_g, lse_r) < 1e-4
+    E = H * D
+    for part in range(3):   # dQ, dK, dV separately
+        sl = slice(part * E, (part + 1) * E)
+        assert rel(dq_g[:, sl], dq_r[:, sl]) < 2e-2, part
+
+
+def test_flash_attention_fully_masked_sequence(monkeypatch):
+    """A sequence whose keys are all masked: zero context, lse = +inf, zero gradients (the
+    reference softmax is NaN there and is zeroed the same way)."""
+    import math
+    monkeypatch.setattr(Tx, '_FLASH_ONLY', True)
+    B, S, H, D = 2, 128, 2, 64
+    qkv = _bf(B * S, 3 * H * D, seed=18).to(DEV)
+    dctx = _bf(B * S, H * D, seed=19).to(DEV)
+    kb = torch.zeros(B, S, device=DEV)
+    kb[1] = float('-inf')
+    ctx, lse = Tx.attn_fwd(qkv, kb, B, S, H, 1 / math.sqrt(D), head_dim=D)
+    dqkv = Tx.attn_bwd(qkv, kb, dctx, lse, B, S, H, 1 / math.sqrt(D), head_dim=D, ctx=ctx)
+    torch.cuda.synchronize()
+    assert torch.isinf(lse.view(B, H, S)[1]).all() and torch.isfinite(lse.view(B, H, S)[0]).all()
+    assert ctx[S:].abs().max().item() == 0 and dqkv[S:].abs().max().item() == 0
+    assert ctx[:S].abs().max().item() > 0
+
+
+@pytest.mark.parametrize('S,hidden,heads', [(256, 128, 2), (192, 256, 2)])
+def test_native_bert_flash_matches_torch_autograd(S, hidden, heads):
+    """Native BERT on the GPU with the flash attention path (S > 128, head dim 64 / 128)
+    against fp32 autograd of the plain PyTorch model on the same weights."""
+    from mlcomp_amd.models import build_model
+    from mlcomp_amd.models.native_bert import NativeBert
+    torch.manual_seed(0)
+    kw = dict(num_classes=3, hidden_dropout=0.0, attention_dropout=0.0, hidden=hidden, heads=heads,
+              max_position=512)
+    tm = build_model('bert-tiny', **kw)
+    ref = build_model('bert-tiny', **kw)
+    ref.load_state_dict(tm.state_dict())
+    B = 8                                   # the classifier wgrad needs B % 8 == 0
+    net = NativeBert(tm.to(DEV), DEV, B, S)
+    ids = torch.randint(0, 1024, (B, S))
+    tt = torch.zeros(B, S, dtype=torch.long)
+    tt[:, S // 2:] = 1
+    y = torch.randint(0, 3, (B,))
+    am = torch.ones(B, S, dtype=torch.long)
+    am[0, S - 40:] = 0
+    net.ctx.ws.zero()
+    net.arena.zero_grad()
+    loss = net.loss(ids.to(DEV), tt.to(DEV), ref.key_bias(am).to(DEV), y.to(DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    lr = torch.nn.functional.cross_entropy(ref(ids, tt, am), y)
+    lr.backward()
+    assert abs(loss.item() - lr.item()) < 2e-2
+    a = net.arena.by_name
+
+    def cos(u, v):
+        u, v = u.flatten().float().cpu(), v.flatten().float()
+        return (u @ v / (u.norm() * v.norm() + 1e-12)).item()
+    for name, prm in [('layers.0.qkv.weight', ref.layers[0].qkv.weight), ('layers.1.qkv.bias', ref.layers[1].qkv.bias),
+                      ('layers.0.ffn1.weight', ref.layers[0].ffn1.weight), ('word', ref.word.weight)]:
+        assert cos(a[name].grad, prm.grad) > 0.99, name
 
 
 @pytest.mark.parametrize('T,O,I', [(4096, 768, 2304), (4096, 3072, 768), (336, 64, 512), (1000, 512, 64),
