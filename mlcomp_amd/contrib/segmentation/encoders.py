@@ -296,6 +296,9 @@ for _n, _a in {'dpn68': (True, 10, 128, 32, (3, 4, 12, 3), (16, 32, 32, 64)),
                'dpn107': (False, 128, 200, 50, (4, 8, 20, 3), (20, 64, 64, 128)),
                'dpn131': (False, 128, 160, 40, (4, 8, 28, 3), (16, 32, 32, 128))}.items():
     register_encoder(_n)((lambda a: (lambda: DPNEncoder(*a)))(_a))
+# dpn68b (pretrainedmodels' ``b=True``) splits the last 1x1 convolution of every block
+# into its residual and dense outputs: the same function and parameter count as dpn68
+register_encoder('dpn68b')(lambda: DPNEncoder(True, 10, 128, 32, (3, 4, 12, 3), (16, 32, 32, 64)))
 
 
 # ---------------------------------------------------------------------------- mobilenet v2
