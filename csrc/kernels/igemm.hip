@@ -738,6 +738,136 @@ struct EpiF32Slab {  // split-K partial tile -> slab blockIdx.z of ws ([splits][
   }
 };
 
+
+// Dense-layer finish of 8 consecutive columns from split-K slabs (shared by the fused
+// epilogue below and dense_finalize_kernel): sum `splits` fp32 slabs at element offset
+// `src`, then bias / GELU (pre-activation to preact) / GELU' (from dact) / + addend.
+struct DenseFinish {
+  bf16* C; int ldc; const float* bias; int act; bf16* preact; const bf16* addend; const bf16* dact;
+  __device__ __forceinline__ void run(const float* ws, size_t slab, int splits, size_t src, int m, int c) const {
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    const float* base = ws + src;
+    v4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
+    int k = 0;
+    for (; k + 2 <= splits; k += 2) {      // both slabs' loads in flight together
+      const v4 p0 = *reinterpret_cast<const v4*>(base + k * slab);
+      const v4 q0 = *reinterpret_cast<const v4*>(base + k * slab + 4);
+      const v4 p1 = *reinterpret_cast<const v4*>(base + (k + 1) * slab);
+      const v4 q1 = *reinterpret_cast<const v4*>(base + (k + 1) * slab + 4);
+      lo += p0 + p1;
+      hi += q0 + q1;
+    }
+    if (k < splits) {
+      lo += *reinterpret_cast<const v4*>(base + k * slab);
+      hi += *reinterpret_cast<const v4*>(base + k * slab + 4);
+    }
+    float a[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const size_t o = (size_t)m * ldc + c;
+    if (bias) {
+      float bz[8];
+      ldg8f(bias + c, bz);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += bz[e];
+    }
+    if (preact) *reinterpret_cast<uint4*>(preact + o) = pack8(a);
+    if (act == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = 0.5f * a[e] * (1.f + erff(a[e] * 0.70710678118654752f));
+    }
+    if (dact) {
+      float z[8];
+      unpack8(ldg16(dact + o), z);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float cdf = 0.5f * (1.f + erff(z[e] * 0.70710678118654752f));
+        a[e] *= cdf + z[e] * 0.3989422804014327f * __expf(-0.5f * z[e] * z[e]);
+      }
+    }
+    if (addend) {
+      float b[8];
+      unpack8(ldg16(addend + o), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += b[e];
+    }
+    *reinterpret_cast<uint4*>(C + o) = pack8(a);
+  }
+};
+
+// Split-K with the reduction inside the launch (cdna_hip_programming.md, projection GEMM
+// item 2): every split writes its fp32 partial tile to slab blockIdx.z of ws with plain
+// stores, publishes it (vmcnt drain, agent-scope release, drain again) and takes a ticket
+// from the tile's counter; the split that draws the last ticket acquires, resets the
+// counter and sums all slabs of the tile into the final output - fp32 (+= when
+// accumulating; weight gradients) or the dense bf16 epilogue.  Correct for any placement
+// of a tile's splits over XCDs; saves the separate reduce/finalize launch and its boundary.
+// cnt: one zeroed counter per tile (grid.x), left zeroed; launches sharing it must be
+// stream-ordered.
+struct EpiSlabFused {
+  float* ws; int ld; size_t slab; unsigned* cnt;
+  int dense;                 // 0: fp32 out[M][ld] (+)= sum; 1: DenseFinish (ld == N)
+  float* outf; int accumulate;
+  DenseFinish fin;
+  template <int BM, int BN, int MI, int NI>
+  __device__ void apply(f32x16 (&acc)[MI][NI], char* lds, int m0, int n0, int M, int N,
+                        int wm, int wn, int lane, int tid) const {
+    float* part = ws + (size_t)blockIdx.z * slab;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int n = n0 + wn * 32 * NI + 32 * j + (lane & 31);
+        if (n >= N) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * 32 * MI + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (m < M) part[(size_t)m * ld + n] = acc[i][j][r];
+        }
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(lds);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == gridDim.z - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    const int splits = gridDim.z;
+    if (dense) {
+      constexpr int G = BN / 8;
+      for (int q = tid; q < BM * G; q += NTHR) {
+        const int m = m0 + q / G, c = n0 + (q % G) * 8;
+        if (m < M && c < N) fin.run(ws, slab, splits, (size_t)m * ld + c, m, c);
+      }
+    } else {
+      typedef float v4 __attribute__((ext_vector_type(4)));
+      constexpr int G = BN / 4;
+      for (int q = tid; q < BM * G; q += NTHR) {
+        const int m = m0 + q / G, c = n0 + (q % G) * 4;
+        if (m >= M || c >= N) continue;
+        const size_t o = (size_t)m * ld + c;
+        v4 a = accumulate ? *reinterpret_cast<const v4*>(outf + o) : (v4){0.f, 0.f, 0.f, 0.f};
+        v4 b = {0.f, 0.f, 0.f, 0.f};
+        int k = 0;
+        for (; k + 2 <= splits; k += 2) {
+          a += *reinterpret_cast<const v4*>(ws + k * slab + o);
+          b += *reinterpret_cast<const v4*>(ws + (k + 1) * slab + o);
+        }
+        if (k < splits) a += *reinterpret_cast<const v4*>(ws + k * slab + o);
+        *reinterpret_cast<v4*>(outf + o) = a + b;
+      }
+    }
+  }
+};
+
 struct EpiF32Atomic {  // fp32 [M][ld] += (split-K partial sums)
   float* out; int ld;
   template <int BM, int BN, int MI, int NI>
@@ -970,6 +1100,32 @@ static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int 
 // 4 = 128x256 (wide-wave tiles, used when they still give every CU a block)
 static int g_big_tiles = 0;
 static int g_big_min_blocks = 240;
+// split-K reduction inside the GEMM launch (EpiSlabFused) instead of a separate
+// reduce / finalize kernel, for GEMMs whose slabs of one tile (splits x BM x BN fp32) the
+// reducing block can read in at most this many KB (A/B knob 6; 0 = never).  The reducer
+// reads them alone, so many splits (weight gradients, up to 16+) stay on the separate pass.
+static int g_splitk_fused = 0;
+constexpr int kSplitCounters = 1 << 16;
+// per-device tile counters for EpiSlabFused, allocated (zeroed) on first use outside stream
+// capture; nullptr -> the caller falls back to the separate reduction kernel
+static unsigned* split_counters(hipStream_t st, long tiles, int splits, int bm, int bn) {
+  static unsigned* buf[16] = {};
+  if (tiles > kSplitCounters || (long)splits * bm * bn * 4 > (long)g_splitk_fused * 1024) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  if (!buf[dev]) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    unsigned* p = nullptr;
+    if (hipMalloc(&p, kSplitCounters * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, kSplitCounters * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(p);
+      return nullptr;
+    }
+    buf[dev] = p;
+  }
+  return buf[dev];
+}
 static inline int tile_bm(int tile) { return tile == 1 || tile == 3 ? 256 : tile == 2 ? 64 : 128; }
 static inline int tile_bn(int tile) { return tile == 1 ? 64 : tile == 2 || tile == 4 ? 256 : 128; }
 static int pick_tile(int M, int N) {
@@ -1027,10 +1183,11 @@ MLC_EXPORT int mlc_gemm_config(int prefetch) {
 MLC_EXPORT int mlc_gemm_get_set(int key, int value) {
   int* k = key == 0 ? &igemm::g_prefetch : key == 1 ? &igemm::g_split_target
           : key == 2 ? &igemm::g_split_target_mat : key == 3 ? &igemm::g_big_tiles
-          : key == 4 ? &igemm::g_big_min_blocks : key == 5 ? &igemm::g_single_stage : nullptr;
+          : key == 4 ? &igemm::g_big_min_blocks : key == 5 ? &igemm::g_single_stage
+          : key == 6 ? &igemm::g_splitk_fused : nullptr;
   if (!k) return -1;
   const int old = *k;
-  if (value >= 0 && (value > 0 || key == 3 || key == 5)) *k = value;
+  if (value >= 0 && (value > 0 || key == 3 || key == 5 || key == 6)) *k = value;
   return old;
 }
 
@@ -1189,6 +1346,24 @@ MLC_EXPORT int mlc_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, i
       const int per = (ktiles + splits - 1) / splits;
       splits = (ktiles + per - 1) / per;
     }
+    const int BMv = tile_bm(tile), BNv = tile_bn(tile);
+    if (unsigned* cnt = split_counters(st, (long)((Co + BMv - 1) / BMv) * ((KK + BNv - 1) / BNv), splits, BMv, BNv)) {
+      EpiSlabFused epi{ws, KK, slab, cnt, 0, dw, accumulate, {}};
+      if (in_sc) {
+#define MKB(R) (MatMCBn<R>{{x, C, P, C}, bn})
+        if (plain) MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
+#undef MKB
+#define MKB(R) (ConvWgradBBn<R>{{x, g, P, KK}, bn})
+        MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
+#undef MKB
+      }
+#define MKB(R) (MatMC<R>{x, C, P, C})
+      if (plain) MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
+#undef MKB
+#define MKB(R) (ConvWgradB<R>{x, g, P, KK})
+      MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
+#undef MKB
+    }
     EpiF32Slab epi{ws, KK, slab};
     hipError_t e;
     if (in_sc) {
@@ -1284,6 +1459,11 @@ MLC_EXPORT int mlc_linear_wgrad_bias(const bf16* A, const bf16* B, float* C, flo
     const int ktiles = (K + BK - 1) / BK;
     const int per = (ktiles + splits - 1) / splits;
     splits = (ktiles + per - 1) / per;
+    const int BMv = tile_bm(tile), BNv = tile_bn(tile);
+    if (unsigned* cnt = split_counters(st, (long)((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv), splits, BMv, BNv)) {
+      EpiSlabFused epi{ws, N, slab, cnt, 0, C, 1, {}};
+      MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_MCS, GB_MC);
+    }
     EpiF32Slab epi{ws, N, slab};
     const hipError_t e = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_MCS, GB_MC); }();
     if (e != hipSuccess) return e;
@@ -1322,59 +1502,13 @@ namespace {
 // Split-K finish for the dense GEMM: ws holds `splits` fp32 slabs [splits][M][N] of
 // partial sums (written with plain stores by EpiF32Slab); C = epilogue(sum of slabs).
 __global__ void __launch_bounds__(256)
-dense_finalize_kernel(const float* __restrict__ ws, int splits, bf16* __restrict__ C, int ldc,
-                      const float* __restrict__ bias, int act, bf16* __restrict__ preact,
-                      const bf16* __restrict__ addend, const bf16* __restrict__ dact, int M, int N) {
-  typedef float v4 __attribute__((ext_vector_type(4)));
+dense_finalize_kernel(const float* __restrict__ ws, int splits, DenseFinish fin, int M, int N) {
   const int G = N / 8;
   const int n8 = M * G;                    // < 2^31 for every dense layer here
   const size_t slab = (size_t)M * N;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n8; i += gridDim.x * 256) {
     const int m = i / G, c = (i - m * G) * 8;
-    const float* base = ws + (size_t)m * N + c;
-    v4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
-    int k = 0;
-    for (; k + 2 <= splits; k += 2) {      // both slabs' loads in flight together
-      const v4 p0 = *reinterpret_cast<const v4*>(base + k * slab);
-      const v4 q0 = *reinterpret_cast<const v4*>(base + k * slab + 4);
-      const v4 p1 = *reinterpret_cast<const v4*>(base + (k + 1) * slab);
-      const v4 q1 = *reinterpret_cast<const v4*>(base + (k + 1) * slab + 4);
-      lo += p0 + p1;
-      hi += q0 + q1;
-    }
-    if (k < splits) {
-      lo += *reinterpret_cast<const v4*>(base + k * slab);
-      hi += *reinterpret_cast<const v4*>(base + k * slab + 4);
-    }
-    float a[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    const size_t o = (size_t)m * ldc + c;
-    if (bias) {
-      float bz[8];
-      ldg8f(bias + c, bz);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) a[e] += bz[e];
-    }
-    if (preact) *reinterpret_cast<uint4*>(preact + o) = pack8(a);
-    if (act == 1) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) a[e] = 0.5f * a[e] * (1.f + erff(a[e] * 0.70710678118654752f));
-    }
-    if (dact) {
-      float z[8];
-      unpack8(ldg16(dact + o), z);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float cdf = 0.5f * (1.f + erff(z[e] * 0.70710678118654752f));
-        a[e] *= cdf + z[e] * 0.3989422804014327f * __expf(-0.5f * z[e] * z[e]);
-      }
-    }
-    if (addend) {
-      float b[8];
-      unpack8(ldg16(addend + o), b);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) a[e] += b[e];
-    }
-    *reinterpret_cast<uint4*>(C + o) = pack8(a);
+    fin.run(ws, slab, splits, (size_t)m * N + c, m, c);
   }
 }
 }  // namespace
@@ -1403,6 +1537,14 @@ MLC_EXPORT int mlc_gemm_bf16_ex(const bf16* A, const bf16* B, bf16* C, int M, in
       const int per = (ktiles + splits - 1) / splits;
       splits = (ktiles + per - 1) / per;
     }
+    const DenseFinish fin{C, ldc, bias, act, preact, addend, dact};
+    if (unsigned* cnt = split_counters(st, tiles, splits, BMv, BNv)) {
+      EpiSlabFused epi{ws, N, (size_t)slab, cnt, 1, nullptr, 0, fin};
+      if (!ta && tb) return launch_tiles(tile, M, N, K, splits, st, epi, GA_KC_F, GB_KC_F);
+      if (!ta && !tb) return launch_tiles(tile, M, N, K, splits, st, epi, GA_KC_F, GB_MC_F);
+      if (ta && tb) return launch_tiles(tile, M, N, K, splits, st, epi, GA_MC_F, GB_KC_F);
+      return launch_tiles(tile, M, N, K, splits, st, epi, GA_MC_F, GB_MC_F);
+    }
     EpiF32Slab epi{ws, N, (size_t)slab};
     hipError_t e;
     if (!ta && tb) e = launch_tiles(tile, M, N, K, splits, st, epi, GA_KC_F, GB_KC_F);
@@ -1412,8 +1554,7 @@ MLC_EXPORT int mlc_gemm_bf16_ex(const bf16* A, const bf16* B, bf16* C, int M, in
     if (e != hipSuccess) return e;
     long blocks = ((long)M * (N / 8) + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(dense_finalize_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, C, ldc, bias, act,
-                       preact, addend, dact, M, N);
+    hipLaunchKernelGGL(dense_finalize_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, fin, M, N);
     return hipGetLastError();
   }
   EpiBF16<IdentityRows, true> epi{C, ldc, nullptr, nullptr, IdentityRows{}, addend};

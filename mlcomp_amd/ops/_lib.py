@@ -82,8 +82,9 @@ _RESTYPE = {'mlc_comm_init': vp}
 
 
 def lib_path():
+    """The in-tree kernel library (``MLC_KERNEL_LIB`` points at another build, for A/B runs)."""
     from mlcomp_amd.build import KERNEL_LIB
-    return KERNEL_LIB
+    return os.environ.get('MLC_KERNEL_LIB') or KERNEL_LIB
 
 
 def load():
@@ -104,7 +105,8 @@ def load():
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, C.c_int)
         # A/B knobs of the GEMM engine (tile policy / min blocks for the wide-wave tiles)
-        for key, env in ((3, 'MLC_GEMM_BIG'), (4, 'MLC_GEMM_BIG_MIN'), (5, 'MLC_GEMM_SINGLE_STAGE')):
+        for key, env in ((3, 'MLC_GEMM_BIG'), (4, 'MLC_GEMM_BIG_MIN'), (5, 'MLC_GEMM_SINGLE_STAGE'),
+                         (6, 'MLC_SPLITK_FUSED')):
             if os.environ.get(env):
                 lib.mlc_gemm_get_set(key, int(os.environ[env]))
         _LIB = lib

@@ -14,8 +14,8 @@ fi
 for model in ${AB_MODELS:-resnet50 bert-base unet}; do
   for i in 1 2; do
     for v in $AB_VALUES; do
-      env $AB_VAR=$v timeout -k 10 200 python bench.py --model $model --steps 30 --warmup 10 $AB_ARGS > $OUT/${model}_${v}_$i.log 2>&1; rc=$?
-      echo "$model $AB_VAR=$v run $i: $(tail -1 $OUT/${model}_${v}_$i.log | grep -o '"value": [0-9.]*, "unit": "[a-z/]*", "n_gpus": 1, "steps": 30, "warmup": 10, "ms_per_step": [0-9.]*')"; fatal $rc bench
+      env $AB_VAR=$v timeout -k 10 200 python bench.py --model $model --steps 30 --warmup 10 $AB_ARGS > $OUT/${model}_${v##*/}_$i.log 2>&1; rc=$?
+      echo "$model $AB_VAR=$v run $i: $(tail -1 $OUT/${model}_${v##*/}_$i.log | grep -o '"value": [0-9.]*, "unit": "[a-z/]*", "n_gpus": 1, "steps": 30, "warmup": 10, "ms_per_step": [0-9.]*')"; fatal $rc bench
     done
   done
 done

@@ -410,3 +410,55 @@ def test_stem_s2d_conv():
                                      stride=2, padding=3).permute(0, 2, 3, 1)
     torch.cuda.synchronize()
     assert rel_err(y, ref) < 1e-2
+
+
+def test_splitk_fused_reduction_matches_separate_pass():
+    """Split-K GEMMs reduce their slabs inside the launch (last-arriving split; knob 6 =
+    the per-tile slab KB it may read, here large enough for every split count) or in a
+    separate reduce / finalize kernel (knob 6 = 0): same results, and repeated launches
+    (tile counters reset by the reducer) stay identical."""
+    import math
+    from mlcomp_amd.ops import _lib
+    from mlcomp_amd.ops import transformer as Tx
+    lib = _lib.load()
+    N, H, W, C, Co = 16, 14, 14, 256, 256
+    x, dy = _bf(N, H, W, C, seed=31).to(DEV), _bf(N, H, W, Co, seed=32).to(DEV)
+    T, I, O = 4096, 768, 768
+    a, wt = _bf(T, I, seed=33).to(DEV), _bf(O, I, scale=I ** -0.5, seed=34).to(DEV)
+    bias = torch.randn(O, device=DEV)
+    u = _bf(T, I, seed=35).to(DEV)
+    add = _bf(T, I, seed=36).to(DEV)
+    g = _bf(T, O, seed=37).to(DEV)
+
+    def run():
+        outs = []
+        for _ in range(3):
+            wg = torch.full((Co, 3, 3, C), 0.5, device=DEV)
+            Fn.conv2d_wgrad(dy, x, (Co, 3, 3, C), 1, 1, out=wg, accumulate=True)
+            y, pre = Tx.dense_fwd(a, wt, bias, act=1, want_preact=True)
+            dx = Tx.dense_dgrad(g, wt, dact_u=u, addend=add)
+            dw, db = torch.zeros(O, I, device=DEV), torch.zeros(O, device=DEV)
+            Fn.linear_wgrad_bias(g, a, dw, db)
+            outs.append([wg, y, pre, dx, dw, db])
+        torch.cuda.synchronize()
+        names = ['conv wgrad', 'dense fwd', 'preact', 'dense dgrad', 'linear wgrad']
+        for o in outs[1:]:
+            for k, nm in enumerate(names):   # deterministic: the reducer sums slabs in split order
+                assert torch.equal(o[k], outs[0][k]), (nm, rel_err(o[k], outs[0][k]))
+            assert rel_err(o[5], outs[0][5]) < 1e-6   # bias gradient: column-sum atomics
+        return outs[0]
+
+    old = lib.mlc_gemm_get_set(6, 1 << 20)
+    try:
+        fused = run()
+        assert lib.mlc_gemm_get_set(6, 0) == 1 << 20 and lib.mlc_gemm_get_set(6, -1) == 0
+        sep = run()
+    finally:
+        lib.mlc_gemm_get_set(6, old)
+    for f, s_ in zip(fused, sep):
+        assert rel_err(f, s_) < 1e-5
+    ref = Fn.conv2d_wgrad(dy.cpu(), x.cpu(), (Co, 3, 3, C), 1, 1) + 0.5
+    assert rel_err(fused[0], ref) < 5e-3
+    z = a.float() @ wt.float().t() + bias
+    assert rel_err(fused[2], z) < 1e-2
+    assert rel_err(fused[1], 0.5 * z * (1 + torch.erf(z / math.sqrt(2)))) < 1e-2
