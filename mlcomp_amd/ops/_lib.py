@@ -47,6 +47,7 @@ _SIGS = {
     'mlc_bn_stat_copies': [],
     'mlc_gemm_config': [i32],
     'mlc_gemm_get_set': [i32, i32],
+    'mlc_bn_get_set': [i32, i32],
     'mlc_bn_finalize': [vp, vp, i32] + [vp] * 8 + [i64, i32, f32, f32, vp],
     'mlc_bn_fwd_apply': [vp] * 5 + [i64, i32, i32, vp],
     'mlc_bn_fwd_apply2': [vp] * 7 + [i64, i32, i32, vp],
@@ -109,6 +110,9 @@ def load():
                          (6, 'MLC_SPLITK_FUSED')):
             if os.environ.get(env):
                 lib.mlc_gemm_get_set(key, int(os.environ[env]))
+        for key, env in ((0, 'MLC_BN_UNROLL'), (1, 'MLC_BN_BLOCKS')):   # BN elementwise passes
+            if os.environ.get(env):
+                lib.mlc_bn_get_set(key, int(os.environ[env]))
         _LIB = lib
     return _LIB
 

@@ -175,10 +175,20 @@ def test_bn_apply_residual_affine():
     assert rel_err(out, ref) < 1e-2
 
 
+@pytest.fixture(params=[1, 4], ids=['bn-u1', 'bn-u4'])
+def bn_unroll(request):
+    """The BN elementwise passes with 1 and with 4 chunks per thread per iteration."""
+    from mlcomp_amd.ops import _lib
+    lib = _lib.load()
+    old = lib.mlc_bn_get_set(0, request.param)
+    yield request.param
+    lib.mlc_bn_get_set(0, old)
+
+
 @pytest.mark.parametrize('relu,res', [(True, True), (True, False), (False, False)])
-@pytest.mark.parametrize('C', [64, 256, 2048])
-def test_bn_fwd_bwd(relu, res, C):
-    rows_shape = (4, 5, 3, C)
+@pytest.mark.parametrize('C,shape', [(64, (4, 5, 3)), (256, (4, 5, 3)), (2048, (4, 5, 3)), (256, (4, 50, 31))])
+def test_bn_fwd_bwd(relu, res, C, shape, bn_unroll):
+    rows_shape = (*shape, C)
     y = _bf(*rows_shape, scale=2.0, seed=7) + 0.5
     r = _bf(*rows_shape, seed=8) if res else None
     gamma = torch.rand(C) + 0.5
