@@ -259,8 +259,8 @@ class Train(Executor):
         runner.run_experiment(stages, start_epoch=start_epoch)
         if self.master and self.trace:
             model = runner.model.eval().cpu().float()
-            size = experiment.stage_params(stages[-1], 'data_params').get('image_size', 224)
-            traced = torch.jit.trace(model, torch.randn(1, 3, size, size))
+            # one real input of the last stage (channels / size as the data has them)
+            traced = torch.jit.trace(model, experiment.get_native_batch(stages[-1]).cpu().float())
             torch.jit.save(traced, self.trace)
         if self.distr_info:
             import torch.distributed as dist

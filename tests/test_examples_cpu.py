@@ -37,7 +37,10 @@ def _ids(created):
 ALL_CONFIGS = ['bash/config.yml', 'bash/config_error.yml', 'bash/config_grid.yml', 'grid/dag.yml', 'grid/task.yml',
                'click/config.yml', 'hierarchical_logging/config.yml', 'progress_bar/config.yml',
                'mnist_lenet/config.yml', 'resnet50_ddp/config.yml', 'unet_segmentation/config.yml',
-               'bert_finetune/config.yml', 'multi_branch/config.yml']
+               'bert_finetune/config.yml', 'multi_branch/config.yml', 'cifar_simple/config.yml',
+               'digit-recognizer/all.yml', 'digit-recognizer/prepare.yml', 'digit-recognizer/train.yml',
+               'digit-recognizer/train-distr.yml', 'digit-recognizer/train-distr-stage.yml',
+               'digit-recognizer/grid.yml']
 
 
 def test_all_example_dags_build(cluster):
@@ -48,6 +51,15 @@ def test_all_example_dags_build(cluster):
     assert counts['grid/dag.yml'] == 6          # 3 DAGs x 2 tasks
     assert counts['unet_segmentation/config.yml'] == 2
     assert counts['multi_branch/config.yml'] == 3
+    assert counts['digit-recognizer/grid.yml'] == 6       # 3 batch sizes x 2 (workers, lr)
+    assert counts['digit-recognizer/all.yml'] == 5
+    # a pipe DAG holds executor templates only: tasks are created when a model starts on it
+    from mlcomp_amd.db.core import Session
+    from mlcomp_amd.db.enums import DagType
+    from mlcomp_amd.db.models import Dag
+    pipe = _run_example(cluster['tmp'], 'digit-recognizer/pipe.yml')
+    (dag_id,) = _ids(pipe)
+    assert Session.create_session(key='pp').get(Dag, dag_id).type == DagType.Pipe.value
 
 
 @pytest.mark.parametrize('cfg,expect', [('bash/config.yml', 'success'), ('bash/config_error.yml', 'failed'),
@@ -76,3 +88,38 @@ def test_mnist_lenet_dag_trains_on_cpu(cluster):
     assert t.score is not None
     names = {(r.part, r.name) for r in s.query(ReportSeries).filter(ReportSeries.task == t.id)}
     assert ('valid', 'accuracy01') in names and ('train', 'loss') in names
+
+
+CPU = {'executors/train/gpu': 0, 'executors/train/cpu': 1}
+
+
+def test_cifar_simple_user_experiment_trains_on_cpu(cluster):
+    """User experiment folder: experiment.py datasets + model.py registered model + .ignore."""
+    from mlcomp_amd.db.core import Session
+    from mlcomp_amd.db.enums import TaskStatus
+    from mlcomp_amd.db.models import Task
+    ids = _ids(_run_example(cluster['tmp'], 'cifar_simple/config.yml', params=CPU))
+    res = _wait(cluster['sup'], ids, timeout=300)
+    assert all(v == TaskStatus.Success for v in res.values()), res
+    t = Session.create_session(key='cf').get(Task, ids[0])
+    assert t.score is not None and t.score > 0.3      # 10 classes, learnable synthetic images
+
+
+def test_digit_recognizer_pipeline_on_cpu(cluster):
+    """The reference's end-to-end example: data -> split -> train (+ trace) -> valid -> infer
+    with a submission file, through scheduler, broker and worker processes."""
+    from mlcomp_amd import config
+    from mlcomp_amd.db.core import Session
+    from mlcomp_amd.db.enums import TaskStatus
+    from mlcomp_amd.db.models import Task
+    ids = _ids(_run_example(cluster['tmp'], 'digit-recognizer/all.yml', params=CPU))
+    res = _wait(cluster['sup'], ids, timeout=600)
+    assert all(v == TaskStatus.Success for v in res.values()), res
+    s = Session.create_session(key='dr')
+    tasks = {t.name: t for t in (s.get(Task, i) for i in ids)}
+    assert tasks['valid'].score > 0.5
+    data = os.path.join(config.get().DATA_FOLDER, 'examples')
+    import pandas as pd
+    sub = pd.read_csv(os.path.join(data, 'submissions', 'net_test.csv'))
+    assert list(sub.columns) == ['ImageId', 'Label'] and len(sub) == 300
+    assert os.path.exists(os.path.join(config.get().MODEL_FOLDER, 'examples', 'net.pth'))
