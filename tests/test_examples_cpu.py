@@ -93,13 +93,25 @@ def test_mnist_lenet_dag_trains_on_cpu(cluster):
 CPU = {'executors/train/gpu': 0, 'executors/train/cpu': 1}
 
 
+def _wait_live(cluster, ids, timeout):
+    """_wait for multi-minute pipelines: keep the worker's heartbeat fresh (the scheduler only
+    dispatches to workers seen within the last 15 s; the fixture beats once)."""
+    import time
+    deadline = time.time() + timeout
+    while True:
+        cluster['ws'].heartbeat()
+        res = _wait(cluster['sup'], ids, timeout=5)
+        if all(v.value >= 3 for v in res.values()) or time.time() > deadline:   # >= Failed
+            return res
+
+
 def test_cifar_simple_user_experiment_trains_on_cpu(cluster):
     """User experiment folder: experiment.py datasets + model.py registered model + .ignore."""
     from mlcomp_amd.db.core import Session
     from mlcomp_amd.db.enums import TaskStatus
     from mlcomp_amd.db.models import Task
     ids = _ids(_run_example(cluster['tmp'], 'cifar_simple/config.yml', params=CPU))
-    res = _wait(cluster['sup'], ids, timeout=300)
+    res = _wait_live(cluster, ids, timeout=300)
     assert all(v == TaskStatus.Success for v in res.values()), res
     t = Session.create_session(key='cf').get(Task, ids[0])
     assert t.score is not None and t.score > 0.3      # 10 classes, learnable synthetic images
@@ -113,7 +125,7 @@ def test_digit_recognizer_pipeline_on_cpu(cluster):
     from mlcomp_amd.db.enums import TaskStatus
     from mlcomp_amd.db.models import Task
     ids = _ids(_run_example(cluster['tmp'], 'digit-recognizer/all.yml', params=CPU))
-    res = _wait(cluster['sup'], ids, timeout=600)
+    res = _wait_live(cluster, ids, timeout=600)
     assert all(v == TaskStatus.Success for v in res.values()), res
     s = Session.create_session(key='dr')
     tasks = {t.name: t for t in (s.get(Task, i) for i in ids)}
