@@ -62,6 +62,19 @@ class _Dense:
         self.ctx.arena.mark_ready(self.w)
         self.ctx.arena.mark_ready(self.b)
 
+    def bwd_params_async(self, dy, x):
+        """:meth:`bwd_params` on the context's weight-gradient stream (when there is one);
+        returns a join callable for after the layer's dgrad."""
+        side = self.ctx.wgrad_stream
+        if side is None:
+            self.bwd_params(dy, x)
+            return lambda: None
+        main = torch.cuda.current_stream(self.ctx.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self.bwd_params(dy, x)
+        return lambda: main.wait_stream(side)
+
 
 class _LN:
     def __init__(self, ctx: NativeContext, name: str, ln: torch.nn.LayerNorm):
@@ -143,17 +156,20 @@ class NativeBertLayer:
         ds2, df = Tx.ln_bwd(dh2, s2, m2, r2, self.ln2.g.master, self.ln2.g.grad, self.ln2.b.grad,
                             ws[self.ln2.k_sums], p_in=ph, seed=net.seed, salt_in=self.salt + 2, want_dr=True)
         self.ln2.mark()
-        self.ffn2.bwd_params(df, g)
+        join = self.ffn2.bwd_params_async(df, g)
         du = Tx.dense_dgrad(df, self.ffn2.w.bf16, dact_u=u)          # grad of the GELU input
+        join()
         self.ffn2.mark()
-        self.ffn1.bwd_params(du, h1)
+        join = self.ffn1.bwd_params_async(du, h1)
         dh1 = Tx.dense_dgrad(du, self.ffn1.w.bf16, addend=ds2)       # + residual branch
+        join()
         self.ffn1.mark()
         ds1, dao = Tx.ln_bwd(dh1, s1, m1, r1, self.ln1.g.master, self.ln1.g.grad, self.ln1.b.grad,
                              ws[self.ln1.k_sums], p_in=ph, seed=net.seed, salt_in=self.salt + 1, want_dr=True)
         self.ln1.mark()
-        self.out.bwd_params(dao, ctx2)
+        join = self.out.bwd_params_async(dao, ctx2)
         dctx2 = Tx.dense_dgrad(dao, self.out.w.bf16)
+        join()
         self.out.mark()
         if fused:
             qkv, lse = att
@@ -168,8 +184,9 @@ class NativeBertLayer:
             dq = torch.bmm(dS, k)
             dk = torch.bmm(dS.transpose(1, 2), q)
             dqkv = torch.stack([dq, dk, dv]).view(3, B, nh, S, dh).permute(1, 3, 0, 2, 4).reshape(B * S, 3 * nh * dh)
-        self.qkv.bwd_params(dqkv, x)
+        join = self.qkv.bwd_params_async(dqkv, x)
         dx = Tx.dense_dgrad(dqkv, self.qkv.w.bf16, addend=ds1)
+        join()
         self.qkv.mark()
         return dx
 

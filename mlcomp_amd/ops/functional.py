@@ -136,10 +136,28 @@ _SLAB = {}
 _SLAB_OLD = []   # superseded buffers stay alive: a captured graph may still point at them
 
 
+_SIDE_STREAMS = set()
+
+
+def register_side_stream(stream) -> None:
+    """GEMMs issued on ``stream`` (e.g. the weight-gradient stream) get workspaces of their
+    own, so they can run concurrently with GEMMs on the main stream."""
+    _SIDE_STREAMS.add((stream.device.index, stream.stream_id))
+
+
+def workspace_key(device) -> str:
+    device = torch.device(device)
+    if device.type == 'cuda' and _SIDE_STREAMS:
+        cs = torch.cuda.current_stream(device)
+        if (cs.device.index, cs.stream_id) in _SIDE_STREAMS:
+            return f'{device}/side'
+    return str(device)
+
+
 def slab_workspace(device, n: int) -> torch.Tensor:
     """fp32 split-K slab workspace (no zeroing needed), grown on demand - first during
-    eager warm-up, so graph capture reuses it."""
-    key = str(device)
+    eager warm-up, so graph capture reuses it.  One per stream role (workspace_key)."""
+    key = workspace_key(device)
     buf = _SLAB.get(key)
     if buf is None or buf.numel() < n:
         if buf is not None:

@@ -250,7 +250,8 @@ def gemm_workspace(device, n: int) -> torch.Tensor:
     """fp32 split-K slab workspace per device (``splits`` x M x N partial sums, fully
     overwritten by each split-K GEMM), grown on demand - first during eager warm-up, so
     graph capture reuses it."""
-    key = str(device)
+    from .functional import workspace_key
+    key = workspace_key(device)
     buf = _WS.get(key)
     if buf is None or buf.numel() < n:
         if buf is not None:
