@@ -18,10 +18,13 @@ bucketed RCCL all-reduce).  ``export_to_torch()`` writes the weights back.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
 from mlcomp_amd.ops import seg
+from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops.layers import ConvBN, NativeContext
 from .native_resnet import lower_resnet_body
 
@@ -37,6 +40,30 @@ class _UpCatFn(torch.autograd.Function):
     def backward(ctx, d):
         dlo, dskip = seg.upcat_bwd(d, ctx.c1)
         return dlo, (dskip if ctx.has_skip else None), None
+
+
+class _DecoderPairFn(torch.autograd.Function):
+    """A decoder block's two conv+BN+ReLU units as one autograd node, so the second
+    unit's dgrad epilogue also masks the first unit's output gradient and accumulates the
+    first BN's backward sums (``Fn.BnBwdSpec``): no separate BN-backward reduction pass."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, c1: ConvBN, c2: ConvBN):
+        z1, r1 = c1.fwd(x)
+        z2, r2 = c2.fwd(z1)
+        ctx.units = (c1, c2)
+        ctx.save_for_backward(*r1, *r2)
+        return z2
+
+    @staticmethod
+    def backward(ctx, dz):
+        c1, c2 = ctx.units
+        s = ctx.saved_tensors
+        r1, r2 = s[:3], s[3:]
+        spec = Fn.BnBwdSpec(None, [c1.bn_target(r1)], affine=[(c1.scale, c1.shift)])   # z1 = relu(BN(y1))
+        d1, _ = c2.bwd(dz.contiguous(), r2, dgrad_bn=spec)
+        dx, _ = c1.bwd(d1, r1, prereduced=True, need_dx=ctx.needs_input_grad[0])
+        return dx, None, None, None
 
 
 class SegHead:
@@ -121,6 +148,9 @@ class NativeUnet:
             self.dec.append((ConvBN(ctx, f'{pre}.0', c1[0], c1[1], act=True),
                              ConvBN(ctx, f'{pre}.1', c2[0], c2[1], act=True)))
         self.head = SegHead(ctx, 'decoder.final_conv', dec.final_conv, bce_w, dice_w, eps)
+        # decoder blocks as one autograd node with the first BN's backward reduction fused
+        # into the second conv's dgrad (MLC_UNET_PAIR=0: two separate nodes)
+        self.fuse_pair = os.environ.get('MLC_UNET_PAIR', '1') == '1'
         ctx.finalize(device)
         for u in self._units():
             u.load_from_torch()
@@ -152,7 +182,10 @@ class NativeUnet:
         d = x4
         for (c1, c2), skip in zip(self.dec, [x3, x2, x1, x0, None]):
             d = _UpCatFn.apply(d, skip, anchor)
-            d = c2(c1(d))
+            if self.fuse_pair:
+                d = _DecoderPairFn.apply(d, anchor, c1, c2)
+            else:
+                d = c2(c1(d))
         return d
 
     def loss(self, x, target):
