@@ -137,6 +137,8 @@ class NativeUnet:
                                                                           s2d_stem=True)
         for e in self.ends[:3]:          # stage outputs 1-3 feed skips (see module doc)
             self.blocks[e + 1].prev = None
+        for blk in self.blocks:          # measured -0.9 % here (profiles/round2_ab): off unless asked
+            blk.down_stream = os.environ.get('MLC_DOWN_STREAM_UNET', '0') == '1'
         self.dec = []
         for i, blk in enumerate(dec.blocks):
             if not (isinstance(blk.att_in, nn.Identity) and isinstance(blk.att_out, nn.Identity)):
