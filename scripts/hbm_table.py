@@ -25,8 +25,8 @@ def load(folder):
 
 
 def family(name):
-    n = name.split('(')[0]
-    for a, b in (('void ', ''), ('igemm::', ''), ('(anonymous namespace)::', ''), ('_ZN12_GLOBAL__N_1', '')):
+    n = name.replace('(anonymous namespace)::', '').split('(')[0]
+    for a, b in (('void ', ''), ('igemm::', ''), ('_ZN12_GLOBAL__N_1', '')):
         n = n.replace(a, b)
     return n[:100]
 
