@@ -300,6 +300,36 @@ struct ConvDgradB {
   }
 };
 
+// conv dgrad B operand from the transposed, flipped filter wt[C][KH][KW][Co]
+// (wtrans.hip): rows = ci, k = (a, b, co) as in ConvDgradB, but K-contiguous - the tap
+// (r, s) of W is tap (KH-1-r, KW-1-s) of wt, and its Co channels are one contiguous run.
+template <int R>
+struct ConvDgradBT {
+  static constexpr bool KC = true;
+  const bf16* wt; ConvGeom g; DgradClass cl;
+  struct St { unsigned off[R / 32]; int n0; };
+  __device__ static int lds_off(int i, int tid) { return kc_off((tid >> 3) + 32 * i, tid & 7); }
+  __device__ void init(St& st, int n0, int tid) const {
+    st.n0 = n0;
+    const int rl = g.KH * g.KW * g.Co;
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      st.off[i] = n0 + r < g.C ? (unsigned)(r * rl + (tid & 7) * 8) * 2u : OOB;
+    }
+  }
+  __device__ void load(const St& st, int kt, int tid, uint4 (&v)[R / 32]) const {
+    int a, b, co0;
+    cl.tap(kt, a, b, co0);
+    const int r = cl.r0 + a * cl.rstep, s = cl.s0 + b * cl.sstep;
+    const int tf = (g.KH - 1 - r) * g.KW + (g.KW - 1 - s);
+    const Rsrc rs = rsrc(wt + (size_t)st.n0 * g.KH * g.KW * g.Co + (size_t)tf * g.Co + co0);
+    const bool kv = co0 + (tid & 7) * 8 < g.Co;
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) v[i] = bload(rs, kv ? st.off[i] : OOB);
+  }
+};
+
 // conv wgrad B operand: k = output pixel p rows, cols = kk = (r, s, ci).  Thread t loads
 // pixels (t>>3) and (t>>3)+32 of the K-tile and column chunks (t&7)+8c (c < R/64): two
 // pixel decompositions per thread and K-tile, shared by its column chunks.
@@ -1283,6 +1313,68 @@ MLC_EXPORT int mlc_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, const bf1
     }
   return err;
 #undef MKB
+}
+
+// dgrad from the transposed, flipped filter wt[C][KH][KW][Co] (wtrans.hip), same
+// arguments and epilogue (addend, fused BN-backward reduction) as mlc_conv_dgrad.  The
+// filter operand is then K-contiguous (ds_read_b128) instead of ConvDgradB's transposed
+// LDS reads.  A stride-1 conv's dgrad IS a forward conv of dy over wt with pad' =
+// dil*(K-1) - pad, so it runs on the forward loaders; strided convs keep the parity-class
+// GEMMs with the ConvDgradBT filter loader.
+MLC_EXPORT int mlc_conv_dgrad_t(const bf16* dy, const bf16* wt, bf16* dx, const bf16* addend, int N,
+                                int H, int W, int C, int Co, int KH, int KW, int stride, int pad,
+                                int dil, int Ho, int Wo, const bf16* bn_mask, const bf16* bn_y0,
+                                const float* bn_mean0, float* bn_sums0, const bf16* bn_y1,
+                                const float* bn_mean1, float* bn_sums1, const float* bn_msc0,
+                                const float* bn_msh0, const float* bn_msc1, const float* bn_msh1,
+                                hipStream_t st) {
+  if (C % 8 || Co % 8 || KH > 15 || KW > 16 || stride < 1) return -1;
+  if (bn_msc0 && (!bn_msh0 || !bn_y0 || (bn_msc1 && (!bn_msh1 || !bn_y1)))) return -1;
+  if (bn_y0 && (!bn_mean0 || !bn_sums0 || (bn_y1 && (!bn_mean1 || !bn_sums1)))) return -1;
+  BnBwdEpi bn{bn_mask, bn_y0, bn_mean0, bn_sums0, bn_y1, bn_mean1, bn_sums1,
+              bn_msc0, bn_msh0, bn_msc1, bn_msh1};
+  const int ph = dil * (KH - 1) - pad, pw = dil * (KW - 1) - pad;
+  if (stride == 1 && ph >= 0 && ph == pw) {
+    if (Ho != H + 2 * pad - dil * (KH - 1) || Wo != W + 2 * pad - dil * (KW - 1)) return -1;
+    const int M = N * H * W, K = KH * KW * Co;
+    const int tile = pick_tile(M, C);
+    EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}, addend, bn};
+#define MKB(R) (MatKC<R>{wt, K, C, K})
+    if (KH == 1 && KW == 1) {
+#define MKA(R) (MatKC<R>{dy, Co, M, Co})
+      MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB);
+#undef MKA
+    }
+    // geometry of the equivalent forward conv: input dy [N, Ho, Wo, Co], output [N, H, W, C]
+    const ConvGeom gf = mkgeom(N, Ho, Wo, Co, C, KH, KW, 1, ph, dil, H, W);
+#define MKA(R) (ConvFwdA<R>{dy, gf, M, K})
+    MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB);
+#undef MKA
+#undef MKB
+  }
+  const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
+  hipError_t err = hipSuccess;
+  for (int qh = 0; qh < stride && qh < H; ++qh)
+    for (int qw = 0; qw < stride && qw < W; ++qw) {
+      const DgradClass cl = mkclass(stride, qh, qw, H, W, Ho, Wo, Co, KH, KW, pad, dil);
+      if (cl.nr > 15 || cl.ns > 16) return -1;
+      const int M = N * cl.Hc * cl.Wc, K = cl.nr * cl.ns * cl.ncb * BK;
+      if (M <= 0) continue;
+      const int tile = pick_tile(M, C);
+#define MKA(R) (ConvDgradA<R>{dy, g, M, K, cl})
+#define MKB(R) (ConvDgradBT<R>{wt, g, cl})
+      if (stride == 1) {
+        EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}, addend, bn};
+        err = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB); }();
+      } else {
+        EpiBF16<ClassRows> epi{dx, C, nullptr, nullptr, ClassRows{cl, H, W}, addend, bn};
+        err = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB); }();
+      }
+#undef MKA
+#undef MKB
+      if (err != hipSuccess) return err;
+    }
+  return err;
 }
 
 // dw[Co, KH*KW*C] (fp32) = sum_p dy[p][co] * im2col(x)[p][kk]; zeroes dw first unless

@@ -96,6 +96,7 @@ class NativeResNet:
             x = self.pool(x, anchor)
         for blk in self.blocks:
             x = blk(x)
+        self.ctx.refresh_wt()    # transposed filters for the backward's dgrads
         return x
 
     def loss(self, x, labels):

@@ -188,6 +188,7 @@ class NativeUnet:
                 d = _DecoderPairFn.apply(d, anchor, c1, c2)
             else:
                 d = c2(c1(d))
+        self.ctx.refresh_wt()    # transposed filters for the backward's dgrads
         return d
 
     def loss(self, x, target):

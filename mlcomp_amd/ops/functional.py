@@ -87,12 +87,82 @@ class BnBwdSpec:
         self.affine = list(affine) if affine is not None else None
 
 
+def wt_flip_transpose(w: torch.Tensor) -> torch.Tensor:
+    """[Co, KH, KW, Ci] filter -> [Ci, KH, KW, Co] with the taps flipped: the filter of the
+    stride-1 forward conv that computes this conv's input gradient (csrc/kernels/wtrans.hip)."""
+    return w.flip(1, 2).permute(3, 1, 2, 0).contiguous()
+
+
+def dgrad_as_fwd_conv(KH, KW, stride, pad, dil) -> bool:
+    """Shapes whose input gradient is a stride-1 forward conv of dy over the transposed
+    filter (the others use the parity-class GEMMs, with the transposed filter as well)."""
+    return stride == 1 and pad <= dil * (KH - 1) and dil * (KH - 1) - pad == dil * (KW - 1) - pad
+
+
+class WtTable:
+    """The transposed, flipped bf16 copies ``wt`` of a model's stride-1 conv filters, one
+    buffer, refreshed from the bf16 weight mirrors by one batched kernel launch per step
+    (``refresh``, after the forward pass: the weights cannot change before backward).  The
+    dgrad GEMMs then read both operands K-contiguous (``mlc_conv_dgrad_t``)."""
+
+    def __init__(self):
+        self.slots = []      # arena slots of [Co, KH, KW, Ci] filters
+        self.views = []
+        self.buf = None
+        self.desc = None
+        self.blocks = 0
+        self._srcs = None
+
+    def add(self, slot) -> int:
+        self.slots.append(slot)
+        return len(self.slots) - 1
+
+    def __getitem__(self, i) -> torch.Tensor:
+        return self.views[i]
+
+    def finalize(self, device):
+        if not self.slots:
+            return
+        total = sum((s.numel + 63) // 64 * 64 for s in self.slots)
+        self.buf = torch.zeros(total, device=device, dtype=torch.bfloat16)
+        off = 0
+        for s in self.slots:
+            Co, KH, KW, Ci = s.shape
+            self.views.append(self.buf[off:off + s.numel].view(Ci, KH, KW, Co))
+            off += (s.numel + 63) // 64 * 64
+        if self.buf.is_cuda:
+            self._build()    # outside any stream capture (the table is an H2D copy)
+
+    def _build(self):
+        rows, blk = [], 0
+        for s, v in zip(self.slots, self.views):
+            Co, KH, KW, Ci = s.shape
+            rows.append([s.bf16.data_ptr(), v.data_ptr(), Co, KH * KW, Ci, blk])
+            blk += KH * KW * ((Co + 63) // 64) * ((Ci + 63) // 64)
+        self.desc = torch.tensor(rows, dtype=torch.int64).to(self.buf.device)
+        self.blocks = blk
+        self._srcs = [r[0] for r in rows]
+
+    def refresh(self):
+        if self.buf is None:
+            return
+        if not self.buf.is_cuda:
+            for s, v in zip(self.slots, self.views):
+                v.copy_(wt_flip_transpose(s.bf16))
+            return
+        if self._srcs != [s.bf16.data_ptr() for s in self.slots]:
+            self._build()    # first call, or a weight mirror was re-allocated
+        _lib.call('mlc_wt_transpose', _lib.ptr(self.desc), len(self.slots), self.blocks, _lib.stream())
+
+
 def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=1, pad=0, dil=1,
                  addend: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-                 bn: Optional[BnBwdSpec] = None) -> torch.Tensor:
+                 bn: Optional[BnBwdSpec] = None, wt: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dx = conv_transpose(dy, w) [+ addend] (the addend fuses the gradient sum of a
     residual branch point into the epilogue; ``out`` may alias ``addend``).  With ``bn``
-    the epilogue also masks dx by ``bn.mask > 0`` and accumulates the BN-backward sums."""
+    the epilogue also masks dx by ``bn.mask > 0`` and accumulates the BN-backward sums.
+    ``wt`` (= :func:`wt_flip_transpose` of ``w``): read the filter operand K-contiguous
+    from it (stride 1: the equivalent forward conv, :func:`dgrad_as_fwd_conv`)."""
     N, H, W, C = x_shape
     Co, KH, KW, Ci = w.shape
     _, Ho, Wo, _ = dy.shape
@@ -105,11 +175,22 @@ def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=1, pad=0, di
                 b[1 + 3 * k:4 + 3 * k] = [yk, mk, sk]
             for k, (ak, hk) in enumerate(bn.affine or []):
                 b[7 + 2 * k:9 + 2 * k] = [ak, hk]
+        if wt is not None:
+            assert tuple(wt.shape) == (Ci, KH, KW, Co), (wt.shape, w.shape)
+            _lib.call('mlc_conv_dgrad_t', _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(addend), N, H, W,
+                      C, Co, KH, KW, stride, pad, dil, Ho, Wo, *[_lib.ptr(t) for t in b], _lib.stream())
+            return dx
         _lib.call('mlc_conv_dgrad', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(dx), _lib.ptr(addend), N, H, W, C,
                   Co, KH, KW, stride, pad, dil, Ho, Wo, *[_lib.ptr(t) for t in b], _lib.stream())
         return dx
-    dxf = torch.nn.grad.conv2d_input((N, C, H, W), w.permute(0, 3, 1, 2).float(),
-                                     dy.permute(0, 3, 1, 2).float(), stride, pad, dil)
+    if wt is not None and dgrad_as_fwd_conv(KH, KW, stride, pad, dil):   # forward conv over wt
+        dxf = F.conv2d(dy.permute(0, 3, 1, 2).float(), wt.permute(0, 3, 1, 2).float(), None, 1,
+                       dil * (KH - 1) - pad, dil)
+    else:
+        if wt is not None:
+            w = wt_flip_transpose(wt)     # the flip-transpose is its own inverse
+        dxf = torch.nn.grad.conv2d_input((N, C, H, W), w.permute(0, 3, 1, 2).float(),
+                                         dy.permute(0, 3, 1, 2).float(), stride, pad, dil)
     dxf = dxf.permute(0, 2, 3, 1)
     if addend is not None:
         dxf = dxf + addend.float()

@@ -69,15 +69,30 @@ class NativeContext:
         # (so no tensor outlives its stream's use); both read the same output gradient.
         # Measured +3 % ResNet-50, +1 % U-Net (profiles/round2_ab); 0 turns it off
         self.wgrad_stream = None
+        # MLC_DGRAD_WT=1 (default): the convs keep a transposed, flipped filter copy
+        # (Fn.WtTable) so their input-gradient GEMMs read the filter K-contiguous (stride 1:
+        # on the forward conv's loaders); the model refreshes it once per step after the
+        # forward pass (refresh_wt)
+        self.wt = Fn.WtTable() if os.environ.get('MLC_DGRAD_WT', '1') == '1' else None
+        self.wt_stale = False
 
     def finalize(self, device):
         self.device = torch.device(device)
         self.arena.finalize(device)
         self.ws.finalize(device)
+        if self.wt is not None:
+            self.wt.finalize(self.device)
         self.anchor = torch.zeros(1, device=device, requires_grad=True)
         if self.device.type == 'cuda' and os.environ.get('MLC_WGRAD_STREAM', '1') in ('1', '2'):
             self.wgrad_stream = torch.cuda.Stream(self.device)
             Fn.register_side_stream(self.wgrad_stream)
+
+    def refresh_wt(self):
+        """Re-derive the transposed filters from the current weights (one launch, on the
+        current stream).  Called by the model at the end of its training forward pass."""
+        if self.wt is not None and self.training:
+            self.wt.refresh()
+        self.wt_stale = False
 
 
 # ---------------------------------------------------------------------------- conv+bn
@@ -109,6 +124,9 @@ class ConvBN:
         self.eps = bn.eps
         self.momentum = bn.momentum if bn.momentum is not None else 0.1
         self.w = ctx.arena.weight(f'{name}.conv.weight', (Co, KH, KW, self.cin_p))
+        self.wt_idx = None
+        if ctx.wt is not None and not s2d:
+            self.wt_idx = ctx.wt.add(self.w)
         self.gamma = ctx.arena.vector(f'{name}.bn.weight', (Co,))
         self.beta = ctx.arena.vector(f'{name}.bn.bias', (Co,))
         self._src = (conv, bn)
@@ -176,6 +194,7 @@ class ConvBN:
             z = Fn.bn_apply(y, res, self.scale, self.shift, self.act, res_affine=raff)
             return z, (x, y, z)
         s1, s2 = ws[self.k_s1], ws[self.k_s2]
+        self.ctx.wt_stale = True
         y = Fn.conv2d_fwd(x, self.w.bf16, self.stride, self.pad, self.dil, stats=(s1, s2), in_affine=in_affine)
         training = self.ctx.training
         z = Fn.bn_fwd_apply(y, res, s1, s2, self.gamma.master, self.beta.master, self.save_mean,
@@ -230,8 +249,14 @@ class ConvBN:
             self.wgrad(dy, x, in_affine)
         dx = None
         if need_dx:
+            wt = None
+            if self.wt_idx is not None:
+                if self.ctx.wt_stale:
+                    raise RuntimeError('transposed filters are stale: the model must call '
+                                       'ctx.refresh_wt() after its training forward pass')
+                wt = self.ctx.wt[self.wt_idx]
             dx = Fn.conv2d_dgrad(dy, self.w.bf16, x.shape, self.stride, self.pad, self.dil,
-                                 addend=dx_addend, out=dx_out, bn=dgrad_bn)
+                                 addend=dx_addend, out=dx_out, bn=dgrad_bn, wt=wt)
         if side is not None and defer is not None:
             defer.append((dy, x, self.w))
             return dx, dres

@@ -472,3 +472,77 @@ def test_splitk_fused_reduction_matches_separate_pass():
     z = a.float() @ wt.float().t() + bias
     assert rel_err(fused[2], z) < 1e-2
     assert rel_err(fused[1], 0.5 * z * (1 + torch.erf(z / math.sqrt(2)))) < 1e-2
+
+
+class _FakeSlot:
+    """Stand-in for an arena slot: a [Co, KH, KW, Ci] bf16 filter."""
+
+    def __init__(self, w):
+        self.shape, self.numel, self._w = tuple(w.shape), w.numel(), w
+
+    @property
+    def bf16(self):
+        return self._w
+
+
+def test_wt_table_transpose_batched():
+    """One launch transposes + flips every registered filter (odd channel counts, 1x1,
+    3x3, 5x3 taps, > 64 channels on both axes) exactly."""
+    ws = [_bf(64, 3, 3, 64, seed=40), _bf(200, 1, 1, 72, seed=41), _bf(40, 5, 3, 136, seed=42),
+          _bf(512, 3, 3, 256, seed=43)]
+    tab = Fn.WtTable()
+    for w in ws:
+        tab.add(_FakeSlot(w.to(DEV)))
+    tab.finalize(DEV)
+    tab.refresh()
+    torch.cuda.synchronize()
+    for i, w in enumerate(ws):
+        assert torch.equal(tab[i].cpu(), Fn.wt_flip_transpose(w)), i
+
+
+WT_CASES = [
+    # N, H, W, C, Co, K, stride, pad, dil
+    (2, 14, 14, 64, 64, 1, 1, 0, 1),
+    (2, 14, 14, 64, 128, 3, 1, 1, 1),
+    (3, 9, 7, 136, 40, 3, 1, 1, 1),
+    (1, 7, 7, 512, 2048, 1, 1, 0, 1),
+    (2, 12, 12, 64, 64, 3, 1, 2, 2),      # dilated
+    (2, 10, 10, 64, 96, 3, 1, 0, 1),      # 'valid' conv: dx padded by 2
+    (2, 56, 56, 64, 64, 3, 1, 1, 1),
+    (2, 16, 16, 64, 128, 3, 2, 1, 1),     # strided: parity classes + ConvDgradBT
+    (2, 15, 13, 128, 64, 3, 2, 1, 1),
+    (3, 15, 15, 64, 128, 1, 2, 0, 1),     # 1x1/2: three classes no tap reaches
+    (2, 13, 11, 64, 72, 3, 3, 1, 1),      # stride 3, Co % 64 != 0
+]
+
+
+@pytest.mark.parametrize('case', WT_CASES)
+def test_conv_dgrad_transposed_filter(case):
+    """dgrad over the flipped transposed filter (stride 1: as a forward conv; strided: the
+    parity-class GEMMs with the K-contiguous filter loader) matches the fp32 reference of
+    the plain dgrad, with the addend + fused BN-backward epilogue too."""
+    N, H, W, C, Co, K, st, p, d = case
+    Ho, Wo = Fn.conv_out_hw(H, W, K, K, st, p, d)
+    dy = _bf(N, Ho, Wo, Co, seed=44)
+    w = _bf(Co, K, K, C, scale=(1.0 / (K * K * C)) ** 0.5, seed=45)
+    wt = Fn.wt_flip_transpose(w)
+    ref = Fn.conv2d_dgrad(dy, w, (N, H, W, C), st, p, d)
+    out = Fn.conv2d_dgrad(dy.to(DEV), w.to(DEV), (N, H, W, C), st, p, d, wt=wt.to(DEV))
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 1e-2
+    add, z, y0 = _bf(N, H, W, C, seed=46), _bf(N, H, W, C, seed=47), _bf(N, H, W, C, seed=48)
+    m0 = torch.randn(C) * 0.1
+
+    def run(dev, use_wt):
+        t = lambda v: v.to(dev)  # noqa: E731
+        sums = torch.zeros(Fn.NSTAT * 2 * C, device=dev)
+        spec = Fn.BnBwdSpec(t(z), [(t(y0), t(m0), sums)])
+        dx = Fn.conv2d_dgrad(t(dy), t(w), (N, H, W, C), st, p, d, addend=t(add), bn=spec,
+                             wt=t(wt) if use_wt else None)
+        return dx, sums.view(Fn.NSTAT, 2, C).sum(0).cpu()
+
+    rdx, rs = run('cpu', False)
+    gdx, gs = run(DEV, True)
+    torch.cuda.synchronize()
+    assert rel_err(gdx, rdx) < 1e-2
+    assert rel_err(gs[0], rs[0]) < 2e-2 and rel_err(gs[1], rs[1]) < 2e-2

@@ -40,7 +40,9 @@ def test_graph_replay_matches_eager():
     torch.cuda.synchronize()
     assert b.graph is not None
     la, lb = a.last_loss(), b.last_loss()
-    assert abs(la - lb) <= 1e-3 * max(1.0, abs(la)), (la, lb)
+    # float-atomic accumulation order differs run to run; on this fast-overfitting batch
+    # two eager/graph pairs measured |la - lb| between 1e-4 and 1.3e-3 (scripts/graph_noise_probe.py)
+    assert abs(la - lb) <= 3e-3 * max(1.0, abs(la)), (la, lb)
     pa = a.net.arena.decay.master
     pb = b.net.arena.decay.master
     # split-K weight gradients and BN statistics are accumulated with float atomics, so

@@ -1,5 +1,6 @@
 """CPU checks of the native op reference paths against autograd of plain PyTorch
 modules (the GPU kernels are in turn checked against these references)."""
+import pytest
 import torch
 import torch.nn.functional as F
 
@@ -82,3 +83,20 @@ def test_stem_pool_reference_matches_autograd():
     assert torch.allclose(dy.float(), yf.grad, atol=3e-2, rtol=3e-2)
     assert torch.allclose(dg, g_.grad, atol=3e-2, rtol=3e-2)
     assert torch.allclose(db, b_.grad, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize('K,s,p,d', [(1, 1, 0, 1), (3, 1, 1, 1), (3, 1, 2, 2), (3, 1, 0, 1), (5, 1, 2, 1),
+                                     (3, 2, 1, 1), (1, 2, 0, 1), (3, 3, 1, 1)])
+def test_dgrad_transposed_filter_reference(K, s, p, d):
+    """The transposed-filter dgrad (stride 1: a forward conv of dy over the flipped,
+    channel-swapped filter with pad d*(K-1)-p) equals the plain input gradient."""
+    torch.manual_seed(0)
+    N, H, W, C, Co = 2, 9, 8, 16, 24
+    Ho, Wo = Fn.conv_out_hw(H, W, K, K, s, p, d)
+    dy = torch.randn(N, Ho, Wo, Co).to(torch.bfloat16)
+    w = torch.randn(Co, K, K, C).to(torch.bfloat16)
+    assert Fn.dgrad_as_fwd_conv(K, K, s, p, d) == (s == 1)
+    a = Fn.conv2d_dgrad(dy, w, (N, H, W, C), s, p, d)
+    b = Fn.conv2d_dgrad(dy, w, (N, H, W, C), s, p, d, wt=Fn.wt_flip_transpose(w))
+    assert (a.float() - b.float()).abs().max().item() <= 1e-2 * a.float().abs().max().item()
+    assert torch.equal(Fn.wt_flip_transpose(Fn.wt_flip_transpose(w)), w)
