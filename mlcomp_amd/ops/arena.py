@@ -101,6 +101,7 @@ class ParamArena:
         self.by_name: Dict[str, Slot] = {}
         self.device = None
         self.ready_hook = None  # callable(slot) set by the gradient bucketer
+        self.flush = None       # callable() joining gradient work still in flight (native layers)
 
     def weight(self, name, shape) -> Slot:
         s = self.decay.add(name, shape)

@@ -75,6 +75,11 @@ class NativeContext:
         # forward pass (refresh_wt)
         self.wt = Fn.WtTable() if os.environ.get('MLC_DGRAD_WT', '1') == '1' else None
         self.wt_stale = False
+        # MLC_WGRAD_LAG=1: a layer's side-stream weight gradient is joined at the end of the
+        # NEXT layer's backward (event per layer) instead of its own, so the main stream does
+        # not stall on a just-finished wgrad; flush_wgrad joins the last one
+        self.wgrad_lag = os.environ.get('MLC_WGRAD_LAG', '0') == '1'
+        self._pending_wgrad = None
 
     def finalize(self, device):
         self.device = torch.device(device)
@@ -83,9 +88,24 @@ class NativeContext:
         if self.wt is not None:
             self.wt.finalize(self.device)
         self.anchor = torch.zeros(1, device=device, requires_grad=True)
+        self.arena.flush = self.flush_wgrad
         if self.device.type == 'cuda' and os.environ.get('MLC_WGRAD_STREAM', '1') in ('1', '2'):
             self.wgrad_stream = torch.cuda.Stream(self.device)
             Fn.register_side_stream(self.wgrad_stream)
+
+    def flush_wgrad(self):
+        """Join the lagged weight gradient (if any) into the current stream and mark its
+        slot ready.  Must run before anything reads the gradient arena (the bucketer's
+        finish() calls it through ``arena.flush``)."""
+        p = self._pending_wgrad
+        if p is None:
+            return
+        self._pending_wgrad = None
+        ev, _dy, _x, w = p
+        cur = torch.cuda.current_stream(self.device)
+        if cur != self.wgrad_stream:
+            cur.wait_event(ev)
+        self.arena.mark_ready(w)
 
     def refresh_wt(self):
         """Re-derive the transposed filters from the current weights (one launch, on the
@@ -259,6 +279,12 @@ class ConvBN:
                                  addend=dx_addend, out=dx_out, bn=dgrad_bn, wt=wt)
         if side is not None and defer is not None:
             defer.append((dy, x, self.w))
+            return dx, dres
+        if side is not None and self.ctx.wgrad_lag:
+            ev = torch.cuda.Event()
+            ev.record(side)
+            self.ctx.flush_wgrad()                 # join the previous layer's wgrad
+            self.ctx._pending_wgrad = (ev, dy, x, self.w)   # keeps dy, x alive until joined
             return dx, dres
         if side is not None:
             main.wait_stream(side)                 # join: the weight gradient is complete

@@ -150,6 +150,8 @@ class GradBucketer:
     def finish(self):
         """Launch buckets whose params got no gradient this step, then make the compute
         stream wait for every all-reduce."""
+        if getattr(self.params, 'flush', None) is not None:
+            self.params.flush()      # lagged weight gradients (MLC_WGRAD_LAG) are complete
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)
