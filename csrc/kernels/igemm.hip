@@ -27,6 +27,7 @@
 // contention), fp32 atomic add (split-K weight gradients), fp32 store (+bias).
 #include "common.h"
 #include "convgeom.h"
+#include <stdlib.h>
 
 namespace igemm {
 
@@ -954,7 +955,9 @@ struct EpiF32 {  // fp32 [M][ld] = acc (+ bias[n]) (+= if accumulate)
 // block per CU (96 KB of double-buffered LDS).
 template <int BM, int BN> struct TileCfg {
   static constexpr bool BIG = BM * BN > 128 * 128;
-  static constexpr int MI = (BIG && BM > BN) ? 4 : 2, NI = (BIG && BN > BM) ? 4 : 2;
+  // 128x64 (dense GEMMs with a 768-wide output): 2x2 waves of 64x32 (MI = 2, NI = 1)
+  static constexpr bool NARROW = BM == 128 && BN == 64;
+  static constexpr int MI = (BIG && BM > BN) ? 4 : 2, NI = NARROW ? 1 : (BIG && BN > BM) ? 4 : 2;
   static constexpr int OCC = BIG ? 1 : 2;
 };
 
@@ -1115,8 +1118,8 @@ static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int 
     hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, EPI, 0>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
     return hipGetLastError();
   }
-  // the second register set only fits the square tile without spilling
-  if constexpr (BM == BN) {
+  // the second register set only fits the square (and the 128x64) tile without spilling
+  if constexpr (BM == BN || TileCfg<BM, BN>::NARROW) {
     if (g_prefetch >= 2 && per >= 4) {
       hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, EPI, 2>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
       return hipGetLastError();
@@ -1135,6 +1138,9 @@ static int g_big_min_blocks = 240;
 // reducing block can read in at most this many KB (A/B knob 6; 0 = never).  The reducer
 // reads them alone, so many splits (weight gradients, up to 16+) stay on the separate pass.
 static int g_splitk_fused = 0;
+// 128x64 tiles instead of split-K for narrow dense outputs (A/B knob 7); -1: read
+// MLC_DENSE_NARROW on first use (default 0: measured neutral on BERT-base)
+static int g_dense_narrow = -1;
 constexpr int kSplitCounters = 1 << 16;
 // per-device tile counters for EpiSlabFused, allocated (zeroed) on first use outside stream
 // capture; nullptr -> the caller falls back to the separate reduction kernel
@@ -1214,10 +1220,10 @@ MLC_EXPORT int mlc_gemm_get_set(int key, int value) {
   int* k = key == 0 ? &igemm::g_prefetch : key == 1 ? &igemm::g_split_target
           : key == 2 ? &igemm::g_split_target_mat : key == 3 ? &igemm::g_big_tiles
           : key == 4 ? &igemm::g_big_min_blocks : key == 5 ? &igemm::g_single_stage
-          : key == 6 ? &igemm::g_splitk_fused : nullptr;
+          : key == 6 ? &igemm::g_splitk_fused : key == 7 ? &igemm::g_dense_narrow : nullptr;
   if (!k) return -1;
   const int old = *k;
-  if (value >= 0 && (value > 0 || key == 3 || key == 5 || key == 6)) *k = value;
+  if (value >= 0 && (value > 0 || key == 3 || key == 5 || key == 6 || key == 7)) *k = value;
   return old;
 }
 
@@ -1622,6 +1628,19 @@ MLC_EXPORT int mlc_gemm_bf16_ex(const bf16* A, const bf16* B, bf16* C, int M, in
   const int ktiles = (K + BK - 1) / BK;
   int splits = 1;
   const long slab = (long)M * N;
+  // a narrow output (N <= 1024, e.g. BERT's 768-wide projections) on 128x64 tiles fills
+  // the chip without split-K: no fp32 slabs, no finalize pass (MLC_DENSE_NARROW=1; measured
+  // neutral on the BERT-base step against split-K 2 + finalize, so off by default)
+  if (g_dense_narrow < 0) {
+    const char* e = getenv("MLC_DENSE_NARROW");
+    g_dense_narrow = e ? atoi(e) : 0;
+  }
+  if (g_dense_narrow && tile == 0 && N <= 1024 && tiles < 256 && ((M + 127) / 128) * ((N + 63) / 64) >= 256) {
+    EpiBF16<IdentityRows, true> epi{C, ldc, nullptr, nullptr, IdentityRows{}, addend};
+    epi.bias = bias; epi.act = act; epi.preact = preact; epi.dact = dact;
+    if (!ta && tb) return launch<128, 64>(GA_KC(128), GB_KC(64), epi, M, N, K, 1, st);
+    if (!ta && !tb) return launch<128, 64>(GA_KC(128), GB_MC(64), epi, M, N, K, 1, st);
+  }
   if (ws)
     while (tiles * splits < 384 && ktiles / (splits * 2) >= 4 && slab * splits * 2 <= ws_floats) splits *= 2;
   if (splits > 1) {

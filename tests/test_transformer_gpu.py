@@ -79,8 +79,19 @@ def test_softmax_fwd_bwd(L, p, masked):
     assert rel(dS_g, dS_r) < 2e-2
 
 
-@pytest.mark.parametrize('M,N,K', [(512, 3072, 768), (300, 768, 3072), (4096, 2304, 768), (64, 8, 128)])
-def test_dense_epilogues(M, N, K):
+@pytest.fixture(params=[0, 1], ids=['splitk', 'narrow'])
+def dense_narrow(request):
+    """Dense GEMMs with a narrow output: split-K + finalize (default) and 128x64 tiles."""
+    from mlcomp_amd.ops import _lib
+    lib = _lib.load()
+    old = lib.mlc_gemm_get_set(7, request.param)
+    yield
+    lib.mlc_gemm_get_set(7, max(old, 0))
+
+
+@pytest.mark.parametrize('M,N,K', [(512, 3072, 768), (300, 768, 3072), (4096, 2304, 768), (64, 8, 128),
+                                   (4096, 768, 3072), (4096, 776, 256)])   # last two: 128x64 narrow tiles
+def test_dense_epilogues(M, N, K, dense_narrow):
     x, w = _bf(M, K, seed=6), _bf(N, K, seed=7, scale=K ** -0.5)
     bias = torch.randn(N) * 0.1
     y_r, u_r = Tx.dense_fwd(x, w, bias, act=1, want_preact=True)
