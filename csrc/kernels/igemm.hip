@@ -89,6 +89,21 @@ __device__ __forceinline__ Rsrc rsrc(const void* base) {
 __device__ __forceinline__ uint4 bload(Rsrc r, unsigned voff) {
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
 }
+// LDS-DMA (buffer_load ... lds): 16 B per lane straight into LDS, lane-linear from the
+// wave-uniform destination `dst` (no VGPR round trip and no ds_write); an OOB voffset
+// writes zeros.  The KC images below are filled this way by the DMA main loop (PF = 3):
+// lane l of wave w, copy i, lands in image row w*8 + (l>>3) + 32i at slot l&7, so the
+// XOR swizzle moves to the source side - the lane fetches logical chunk (l&7) ^ swz(row),
+// and swz(row) = (tid>>4)&7 for every copy i.
+__device__ __forceinline__ void dma16(Rsrc rs, char* dst, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, 0);
+}
+__device__ __forceinline__ int dma_chunk(int tid) { return (tid & 7) ^ ((tid >> 4) & 7); }
+__device__ __forceinline__ char* dma_dst(char* img, int tid) {
+  return img + __builtin_amdgcn_readfirstlane(tid >> 6) * 1024;
+}
+template <int N> __device__ __forceinline__ void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 
 // ---------------------------------------------------------------- loaders
@@ -118,6 +133,16 @@ struct MatKC {  // [rows][K] row-major, ld elements per row
 #pragma unroll
     for (int i = 0; i < R / 32; ++i) v[i] = bload(rs, kv ? st.off[i] : OOB);
   }
+  static constexpr bool DMA = true;
+  __device__ void dma(const St& st, int kt, int tid, char* img) const {
+    const int k0 = kt * BK, ch = dma_chunk(tid);
+    const Rsrc rs = rsrc(p + (size_t)st.m0 * ld + k0);
+    const bool kv = ch * 8 < K - k0;
+    const unsigned delta = (unsigned)((ch - (tid & 7)) * 16);
+    char* dst = dma_dst(img, tid);
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) dma16(rs, dst + i * 4096, kv && st.off[i] != OOB ? st.off[i] + delta : OOB);
+  }
 };
 
 template <int R>
@@ -139,6 +164,25 @@ struct MatMC {  // [K][cols] row-major, ld elements per row
     const int left = K - k0;
 #pragma unroll
     for (int i = 0; i < R / 32; ++i) v[i] = bload(rs, kr(i, tid) < left ? st.off[i] : OOB);
+  }
+  // LDS-DMA: copy i of wave w covers k-rows kr(i, tid) lane-linearly (1 KiB = 8 / 4 / 2
+  // k-rows of 64 / 128 / 256 columns), so lane l lands in slot tid % (R/8) of its k-row
+  // and fetches the logical chunk that mc_off puts there (the XOR is an involution).
+  // Correct (GPU tests) but measured slower than the register-staged copy on the weight
+  // gradients (ResNet-50 wgrads 5.25 -> 5.43 ms, BERT-base -3.5 %), so not enabled.
+  static constexpr bool DMA = false;
+  __device__ void dma(const St& st, int kt, int tid, char* img) const {
+    const int k0 = kt * BK, left = K - k0;
+    const int slot = tid % (R / 8), k = tid / (R / 8);
+    const int ch = R == 64 ? slot ^ (((k >> 1) & 1) << 2) : slot ^ ((k & 3) << 2);
+    const bool cv = st.n0 + ch * 8 < cols;
+    const Rsrc rs = rsrc(p + (size_t)k0 * ld + st.n0);
+    char* dst = dma_dst(img, tid);
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) {
+      const int r = kr(i, tid);
+      dma16(rs, dst + i * 4096, cv && r < left ? (unsigned)(r * ld + ch * 8) * 2u : OOB);
+    }
   }
 };
 
@@ -231,6 +275,24 @@ struct ConvFwdA {
     const Rsrc rsr = rsrc(x + st.b0);
 #pragma unroll
     for (int i = 0; i < R / 32; ++i) v[i] = bload(rsr, (st.msk[i] & P) == P ? st.off[i] + toff : OOB);
+  }
+  static constexpr bool DMA = true;
+  __device__ void dma(const St& st, int kt, int tid, char* img) const {
+    const int k0 = kt * BK, k = k0 + dma_chunk(tid) * 8;
+    unsigned rs_, cc, rr, ss;
+    if (g.C % BK == 0) {
+      g.fC.divmod((unsigned)k0, rs_, cc);
+      cc += (unsigned)(k - k0);
+    } else {
+      g.fC.divmod((unsigned)k, rs_, cc);
+    }
+    g.fKW.divmod(rs_, rr, ss);
+    const unsigned P = k < K ? tap_pat((int)rr, (int)ss) : NO_TAP;
+    const unsigned toff = (unsigned)(((int)rr * g.dil * g.W + (int)ss * g.dil) * g.C + (int)cc) * 2u;
+    const Rsrc rsr = rsrc(x + st.b0);
+    char* dst = dma_dst(img, tid);
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) dma16(rsr, dst + i * 4096, (st.msk[i] & P) == P ? st.off[i] + toff : OOB);
   }
 };
 
@@ -392,6 +454,11 @@ struct ConvWgradB {
 struct BnIn { const float* sc; const float* sh; };
 template <class L, class = void> struct HasXform { static constexpr bool value = false; };
 template <class L> struct HasXform<L, decltype((void)L::XF)> { static constexpr bool value = L::XF; };
+// loaders that can fill their KC image by LDS-DMA (no register transform)
+template <class L, class = void> struct HasDma { static constexpr bool value = false; };
+template <class L> struct HasDma<L, decltype((void)L::DMA)> {
+  static constexpr bool value = L::DMA && !HasXform<L>::value && !HasSum<L>::value;
+};
 
 __device__ __forceinline__ uint4 bn_relu8(uint4 v, const float* a, const float* b, bool ok) {
   float f[8];
@@ -1042,6 +1109,30 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
         mfma_tile(smem, smem + A_BYTES);
       }
       __syncthreads();                       // the epilogue reuses the LDS
+    } else if constexpr (PF == 3) {
+      // LDS-DMA double buffer: tile t+1 streams global -> LDS (no VGPRs, no ds_write)
+      // while tile t is multiplied; each thread issues NDMA copies per tile, so
+      // vmcnt(NDMA) after issuing t+1 means this wave's copies of t have landed
+      constexpr int NDMA = BM / 32 + BN / 32;
+      la.dma(sa, kt0, tid, smem);
+      lb.dma(sb, kt0, tid, smem + A_BYTES);
+      for (int t = 0; t < nt; ++t) {
+        char* cur = smem + (t & 1) * STAGE;
+        if (t + 1 < nt) {
+          char* nxt = smem + ((t + 1) & 1) * STAGE;
+          la.dma(sa, kt0 + t + 1, tid, nxt);
+          lb.dma(sb, kt0 + t + 1, tid, nxt + A_BYTES);
+          vmwait<NDMA>();
+        } else {
+          vmwait<0>();
+        }
+        // raw s_barrier, not __syncthreads(): its fence would wait for vmcnt(0), i.e. for
+        // tile t+1's copies too, and serialise the DMA with the MFMAs
+        lds_barrier();                       // every wave's copies of tile t landed
+        mfma_tile(cur, cur + A_BYTES);
+        lds_barrier();                       // tile t's buffer is free for tile t+2
+      }
+      __syncthreads();                       // the epilogue reuses the LDS
     } else if constexpr (PF == 1) {
       uint4 ra[BM / 32], rb[BN / 32];
       la.load(sa, kt0, tid, ra);
@@ -1103,6 +1194,11 @@ static int g_split_target = 768;
 // single-LDS-stage variant for single-K-tile splits (A/B knob 5)
 static int g_single_stage = 1;
 static int g_split_target_mat = 256;
+// LDS-DMA main loop (PF = 3) for GEMMs whose two operands both have an enabled DMA copy
+// (the K-contiguous MatKC / ConvFwdA: forward convs, stride-1 dgrads, dense forward):
+// A/B knob 8; -1: read MLC_GEMM_DMA on first use (default 1: ResNet-50 +1.2 %, U-Net
+// +3.2 %, BERT +0.8 %, profiles/round2_ab/gemm_dma)
+static int g_gemm_dma = -1;
 
 template <int BM, int BN, class LA, class LB, class EPI>
 static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K,
@@ -1117,6 +1213,16 @@ static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int 
   if (per <= 1 && g_single_stage) {
     hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, EPI, 0>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
     return hipGetLastError();
+  }
+  if constexpr (HasDma<LA>::value && HasDma<LB>::value) {
+    if (g_gemm_dma < 0) {
+      const char* e = getenv("MLC_GEMM_DMA");
+      g_gemm_dma = e ? atoi(e) : 1;
+    }
+    if (g_gemm_dma && per >= 2) {
+      hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, EPI, 3>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
+      return hipGetLastError();
+    }
   }
   // the second register set only fits the square (and the 128x64) tile without spilling
   if constexpr (BM == BN || TileCfg<BM, BN>::NARROW) {
@@ -1220,10 +1326,11 @@ MLC_EXPORT int mlc_gemm_get_set(int key, int value) {
   int* k = key == 0 ? &igemm::g_prefetch : key == 1 ? &igemm::g_split_target
           : key == 2 ? &igemm::g_split_target_mat : key == 3 ? &igemm::g_big_tiles
           : key == 4 ? &igemm::g_big_min_blocks : key == 5 ? &igemm::g_single_stage
-          : key == 6 ? &igemm::g_splitk_fused : key == 7 ? &igemm::g_dense_narrow : nullptr;
+          : key == 6 ? &igemm::g_splitk_fused : key == 7 ? &igemm::g_dense_narrow
+          : key == 8 ? &igemm::g_gemm_dma : nullptr;
   if (!k) return -1;
   const int old = *k;
-  if (value >= 0 && (value > 0 || key == 3 || key == 5 || key == 6 || key == 7)) *k = value;
+  if (value >= 0 && (value > 0 || key == 3 || key == 5 || key == 6 || key == 7 || key == 8)) *k = value;
   return old;
 }
 

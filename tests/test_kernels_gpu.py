@@ -546,3 +546,60 @@ def test_conv_dgrad_transposed_filter(case):
     torch.cuda.synchronize()
     assert rel_err(gdx, rdx) < 1e-2
     assert rel_err(gs[0], rs[0]) < 2e-2 and rel_err(gs[1], rs[1]) < 2e-2
+
+
+@pytest.fixture(params=[0, 1], ids=['regs', 'dma'])
+def gemm_dma(request):
+    """The register-staged and the LDS-DMA main loop (knob 8), restored after."""
+    from mlcomp_amd.ops import _lib
+    lib = _lib.load()
+    old = lib.mlc_gemm_get_set(8, request.param)
+    yield
+    lib.mlc_gemm_get_set(8, 1 if old < 0 else old)
+
+
+@pytest.mark.parametrize('case', [c for c in CONV_CASES if c[3] != 8] + [(2, 28, 28, 128, 128, 3, 1, 1)])
+def test_conv_fwd_dgrad_lds_dma(case, gemm_dma):
+    """Forward conv (+BN statistics), transposed-filter dgrad and weight gradient on both
+    main loops: register-staged, and LDS-DMA (operands copied global -> LDS by
+    buffer_load ... lds, the swizzle applied on the source side)."""
+    N, H, W, C, Co, K, s, p = case
+    x = _bf(N, H, W, C, seed=51)
+    w = _bf(Co, K, K, C, scale=(1.0 / (K * K * C)) ** 0.5, seed=52)
+    s1c, s2c = Fn.stat_buffers(Co, 'cpu')
+    ref = Fn.conv2d_fwd(x, w, s, p, stats=(s1c, s2c))
+    s1g, s2g = Fn.stat_buffers(Co, DEV)
+    out = Fn.conv2d_fwd(x.to(DEV), w.to(DEV), s, p, stats=(s1g, s2g))
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 1e-2
+    red = lambda t: t.reshape(Fn.NSTAT, Co).sum(0)  # noqa: E731
+    assert rel_err(red(s1g), red(s1c)) < 1e-2 and rel_err(red(s2g), red(s2c)) < 1e-2
+    Ho, Wo = Fn.conv_out_hw(H, W, K, K, s, p, 1)
+    dy = _bf(N, Ho, Wo, Co, seed=53)
+    rd = Fn.conv2d_dgrad(dy, w, (N, H, W, C), s, p)
+    gd = Fn.conv2d_dgrad(dy.to(DEV), w.to(DEV), (N, H, W, C), s, p, wt=Fn.wt_flip_transpose(w).to(DEV))
+    torch.cuda.synchronize()
+    assert rel_err(gd, rd) < 1e-2
+    # weight gradient (MN-contiguous operands: register-staged copy in both modes)
+    rw = Fn.conv2d_wgrad(dy, x, w.shape, s, p)
+    gw = Fn.conv2d_wgrad(dy.to(DEV), x.to(DEV), w.shape, s, p)
+    torch.cuda.synchronize()
+    assert rel_err(gw, rw) < 1e-2
+
+
+@pytest.mark.parametrize('B,I,O', [(4096, 768, 2304), (300, 3072, 768), (512, 136, 72)])
+def test_linear_lds_dma(B, I, O, gemm_dma):
+    """Plain-matrix GEMM (both operands K-contiguous) on the LDS-DMA main loop, including
+    row / column / K tails."""
+    from mlcomp_amd.ops import transformer as Tx
+    x, w = _bf(B, I, seed=54), _bf(O, I, seed=55, scale=I ** -0.5)
+    bias = torch.randn(O) * 0.1
+    yr, _ = Tx.dense_fwd(x, w, bias)
+    yg, _ = Tx.dense_fwd(x.to(DEV), w.to(DEV), bias.to(DEV))
+    torch.cuda.synchronize()
+    assert rel_err(yg, yr) < 1e-2
+    dy = _bf(B, O, seed=56)     # input gradient: the filter operand is MN-contiguous
+    dr = Tx.dense_dgrad(dy, w)
+    dg = Tx.dense_dgrad(dy.to(DEV), w.to(DEV))
+    torch.cuda.synchronize()
+    assert rel_err(dg, dr) < 1e-2
