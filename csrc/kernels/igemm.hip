@@ -335,6 +335,19 @@ struct ConvDgradA {  // rows = class pixels, k = (a, b, co)
 #pragma unroll
     for (int u = 0; u < R / 32; ++u) v[u] = bload(rsr, (st.msk[u] & P) == P ? st.off[u] + t2 : OOB);
   }
+  static constexpr bool DMA = true;
+  __device__ void dma(const St& st, int kt, int tid, char* img) const {
+    int a, b, co0;
+    cl.tap(kt, a, b, co0);
+    const int co = co0 + dma_chunk(tid) * 8;
+    const unsigned P = co < g.Co ? tap_pat(a, b) : NO_TAP;
+    const long long toff = ((long long)(cl.dh0 - a * cl.dhs) * g.Wo + (cl.dw0 - b * cl.dws)) * g.Co + co - cl.tmin;
+    const unsigned t2 = (unsigned)toff * 2u;
+    const Rsrc rsr = rsrc(dy + st.b0);
+    char* dst = dma_dst(img, tid);
+#pragma unroll
+    for (int u = 0; u < R / 32; ++u) dma16(rsr, dst + u * 4096, (st.msk[u] & P) == P ? st.off[u] + t2 : OOB);
+  }
 };
 
 // conv dgrad B operand: k = (a, b, co) rows, cols = ci; W stored [co][r][s][ci]
@@ -390,6 +403,20 @@ struct ConvDgradBT {
     const bool kv = co0 + (tid & 7) * 8 < g.Co;
 #pragma unroll
     for (int i = 0; i < R / 32; ++i) v[i] = bload(rs, kv ? st.off[i] : OOB);
+  }
+  static constexpr bool DMA = true;
+  __device__ void dma(const St& st, int kt, int tid, char* img) const {
+    int a, b, co0;
+    cl.tap(kt, a, b, co0);
+    const int r = cl.r0 + a * cl.rstep, s = cl.s0 + b * cl.sstep;
+    const int tf = (g.KH - 1 - r) * g.KW + (g.KW - 1 - s);
+    const Rsrc rs = rsrc(wt + (size_t)st.n0 * g.KH * g.KW * g.Co + (size_t)tf * g.Co + co0);
+    const int ch = dma_chunk(tid);
+    const bool kv = co0 + ch * 8 < g.Co;
+    const unsigned delta = (unsigned)((ch - (tid & 7)) * 16);
+    char* dst = dma_dst(img, tid);
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) dma16(rs, dst + i * 4096, kv && st.off[i] != OOB ? st.off[i] + delta : OOB);
   }
 };
 
