@@ -23,6 +23,8 @@ from __future__ import annotations
 import math
 from typing import List
 
+import os
+
 import torch
 
 from mlcomp_amd.ops import functional as Fn
@@ -37,6 +39,12 @@ class _Dense:
         self.lin = lin
         self.w = ctx.arena.weight(f'{name}.weight', tuple(lin.weight.shape))
         self.b = ctx.arena.vector(f'{name}.bias', tuple(lin.bias.shape))
+        # MLC_DENSE_WT=1: a transposed weight copy for the input-gradient GEMM, so it reads
+        # both operands K-contiguous (LDS-DMA loop); refreshed after the forward pass.
+        # Measured -0.8 % on BERT-base (profiles/round2_ab/README.md), so off by default
+        self.wt_idx = None
+        if ctx.wt is not None and os.environ.get('MLC_DENSE_WT', '0') == '1':
+            self.wt_idx = ctx.wt.add(self.w)
 
     def load(self):
         self.w.master.copy_(self.lin.weight.detach().float())
@@ -47,7 +55,17 @@ class _Dense:
         self.lin.bias.data.copy_(self.b.master.to(self.lin.bias.device))
 
     def fwd(self, x, act=0, want_preact=False):
+        self.ctx.wt_stale = True
         return Tx.dense_fwd(x, self.w.bf16, self.b.master, act, want_preact)
+
+    def dgrad(self, dy, dact_u=None, addend=None):
+        """dx = dy @ W [* gelu'(dact_u)] [+ addend]."""
+        wt = None
+        if self.wt_idx is not None:
+            if self.ctx.wt_stale:
+                raise RuntimeError('transposed weights are stale: refresh_wt() must follow the forward pass')
+            wt = self.ctx.wt[self.wt_idx]
+        return Tx.dense_dgrad(dy, self.w.bf16, dact_u=dact_u, addend=addend, wt=wt)
 
     def bwd_params(self, dy, x):
         """dW += dy^T x, db += colsum(dy) (straight into the grad arena); the caller calls
@@ -157,18 +175,18 @@ class NativeBertLayer:
                             ws[self.ln2.k_sums], p_in=ph, seed=net.seed, salt_in=self.salt + 2, want_dr=True)
         self.ln2.mark()
         join = self.ffn2.bwd_params_async(df, g)
-        du = Tx.dense_dgrad(df, self.ffn2.w.bf16, dact_u=u)          # grad of the GELU input
+        du = self.ffn2.dgrad(df, dact_u=u)          # grad of the GELU input
         join()
         self.ffn2.mark()
         join = self.ffn1.bwd_params_async(du, h1)
-        dh1 = Tx.dense_dgrad(du, self.ffn1.w.bf16, addend=ds2)       # + residual branch
+        dh1 = self.ffn1.dgrad(du, addend=ds2)       # + residual branch
         join()
         self.ffn1.mark()
         ds1, dao = Tx.ln_bwd(dh1, s1, m1, r1, self.ln1.g.master, self.ln1.g.grad, self.ln1.b.grad,
                              ws[self.ln1.k_sums], p_in=ph, seed=net.seed, salt_in=self.salt + 1, want_dr=True)
         self.ln1.mark()
         join = self.out.bwd_params_async(dao, ctx2)
-        dctx2 = Tx.dense_dgrad(dao, self.out.w.bf16)
+        dctx2 = self.out.dgrad(dao)
         join()
         self.out.mark()
         if fused:
@@ -185,7 +203,7 @@ class NativeBertLayer:
             dk = torch.bmm(dS.transpose(1, 2), q)
             dqkv = torch.stack([dq, dk, dv]).view(3, B, nh, S, dh).permute(1, 3, 0, 2, 4).reshape(B * S, 3 * nh * dh)
         join = self.qkv.bwd_params_async(dqkv, x)
-        dx = Tx.dense_dgrad(dqkv, self.qkv.w.bf16, addend=ds1)
+        dx = self.qkv.dgrad(dqkv, addend=ds1)
         join()
         self.qkv.mark()
         return dx
@@ -242,6 +260,7 @@ class _HeadFn(torch.autograd.Function):
         B, S = net.B, net.S
         cls = h.view(B, S, -1)[:, 0].contiguous()
         z, _ = net.pooler.fwd(cls)
+        net.ctx.refresh_wt()    # every dense layer has run its forward: transposed copies for backward
         pooled = torch.tanh(z.float()).to(torch.bfloat16)
         pd = Tx.dropout(pooled, net.p_hidden, net.seed, 2)
         logits = Fn.linear_fwd(pd, net.cls_w.bf16, net.cls_b.master)
@@ -265,7 +284,7 @@ class _HeadFn(torch.autograd.Function):
         dpooled = Tx.dropout(dpd, net.p_hidden, net.seed, 2)   # same mask, same scale
         dz = (dpooled.float() * (1 - pooled.float() ** 2)).to(torch.bfloat16)
         net.pooler.bwd_params(dz, cls)
-        dcls = Tx.dense_dgrad(dz, net.pooler.w.bf16)
+        dcls = net.pooler.dgrad(dz)
         net.pooler.mark()
         dh = torch.zeros(net.B, net.S, dcls.shape[1], device=dcls.device, dtype=torch.bfloat16)
         dh[:, 0] = dcls

@@ -120,6 +120,11 @@ class WtTable:
     def __getitem__(self, i) -> torch.Tensor:
         return self.views[i]
 
+    @staticmethod
+    def _dims(shape):
+        """(Co, KH, KW, Ci) of a conv filter, or of a [out, in] dense weight (1x1 taps)."""
+        return tuple(shape) if len(shape) == 4 else (shape[0], 1, 1, shape[1])
+
     def finalize(self, device):
         if not self.slots:
             return
@@ -127,8 +132,9 @@ class WtTable:
         self.buf = torch.zeros(total, device=device, dtype=torch.bfloat16)
         off = 0
         for s in self.slots:
-            Co, KH, KW, Ci = s.shape
-            self.views.append(self.buf[off:off + s.numel].view(Ci, KH, KW, Co))
+            Co, KH, KW, Ci = self._dims(s.shape)
+            v = self.buf[off:off + s.numel]
+            self.views.append(v.view(Ci, KH, KW, Co) if len(s.shape) == 4 else v.view(Ci, Co))
             off += (s.numel + 63) // 64 * 64
         if self.buf.is_cuda:
             self._build()    # outside any stream capture (the table is an H2D copy)
@@ -136,7 +142,7 @@ class WtTable:
     def _build(self):
         rows, blk = [], 0
         for s, v in zip(self.slots, self.views):
-            Co, KH, KW, Ci = s.shape
+            Co, KH, KW, Ci = self._dims(s.shape)
             rows.append([s.bf16.data_ptr(), v.data_ptr(), Co, KH * KW, Ci, blk])
             blk += KH * KW * ((Co + 63) // 64) * ((Ci + 63) // 64)
         self.desc = torch.tensor(rows, dtype=torch.int64).to(self.buf.device)
@@ -148,7 +154,7 @@ class WtTable:
             return
         if not self.buf.is_cuda:
             for s, v in zip(self.slots, self.views):
-                v.copy_(wt_flip_transpose(s.bf16))
+                v.copy_(wt_flip_transpose(s.bf16) if s.bf16.dim() == 4 else s.bf16.t())
             return
         if self._srcs != [s.bf16.data_ptr() for s in self.slots]:
             self._build()    # first call, or a weight mirror was re-allocated

@@ -290,16 +290,23 @@ def dense_fwd(x, w, bias=None, act: int = 0, want_preact: bool = False):
     return z.to(torch.bfloat16), u
 
 
-def dense_dgrad(dy, w, dact_u=None, addend=None):
-    """dx = (dy @ w) [* gelu'(dact_u)] [+ addend]: dy [M, N], w [N, K] -> [M, K] bf16."""
+def dense_dgrad(dy, w, dact_u=None, addend=None, wt=None):
+    """dx = (dy @ w) [* gelu'(dact_u)] [+ addend]: dy [M, N], w [N, K] -> [M, K] bf16.
+    ``wt`` = w^T ([K, N], e.g. a ``Fn.WtTable`` view): the GEMM reads both operands
+    K-contiguous (the LDS-DMA main loop) instead of w as an MN-contiguous tile."""
     M, N = dy.shape
     K = w.shape[1]
     if _cuda(dy):
         dx = torch.empty(M, K, device=dy.device, dtype=torch.bfloat16)
-        _lib.call('mlc_gemm_bf16_ex', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(dx), M, K, N, N, K, K, 0, 0, None, 0,
+        b, ldb, tb = (wt, N, 1) if wt is not None else (w, K, 0)
+        if wt is not None:
+            assert tuple(wt.shape) == (K, N), (wt.shape, w.shape)
+        _lib.call('mlc_gemm_bf16_ex', _lib.ptr(dy), _lib.ptr(b), _lib.ptr(dx), M, K, N, N, ldb, K, 0, tb, None, 0,
                   None, _lib.ptr(addend), _lib.ptr(dact_u), _lib.ptr(gemm_workspace(dy.device, 4 * M * K)),
                   4 * M * K, _lib.stream())
         return dx
+    if wt is not None:
+        w = wt.t()
     z = dy.float() @ w.float()
     z = z.to(torch.bfloat16).float()
     if dact_u is not None:

@@ -101,6 +101,9 @@ def test_dense_epilogues(M, N, K, dense_narrow):
     dx_r = Tx.dense_dgrad(dy, w, dact_u=None, addend=add)
     dx_g = Tx.dense_dgrad(dy.to(DEV), w.to(DEV), addend=add.to(DEV))
     assert rel(dx_g, dx_r) < 1e-2
+    # from the transposed weight copy (both operands K-contiguous)
+    dx_t = Tx.dense_dgrad(dy.to(DEV), w.to(DEV), addend=add.to(DEV), wt=w.t().contiguous().to(DEV))
+    assert rel(dx_t, dx_r) < 1e-2
     # GELU-derivative epilogue: (dy2 @ w2) * gelu'(u)
     w2 = _bf(K, N, seed=10, scale=N ** -0.5)
     dy2 = _bf(M, K, seed=11)
