@@ -1216,11 +1216,16 @@ static int g_prefetch = 2;
 // Plain-matrix operands (1x1 convs, dense layers) prefer fewer splits: their K loop is
 // cheap, so the fp32 atomic traffic of extra splits costs more than the lost occupancy
 // (measured on every ResNet-50 wgrad shape: 256 vs 768 blocks saves 10-30 %); gathered
-// operands (3x3 / 7x7 convs) want the occupancy.
-static int g_split_target = 768;
+// operands (3x3 / 7x7 convs) want more occupancy.  Re-tuned on the whole step once the
+// weight gradients ran beside the LDS-DMA forward / dgrad GEMMs: gathered 768 -> 384 and
+// plain (1x1 conv) 256 -> 128 gave ResNet-50 +1.5 %, U-Net +3.6 % (profiles/round2_ab/split_retune).
+static int g_split_target = 384;
 // single-LDS-stage variant for single-K-tile splits (A/B knob 5)
 static int g_single_stage = 1;
-static int g_split_target_mat = 256;
+static int g_split_target_mat = 128;
+// dense-layer weight gradients (mlc_linear_wgrad_bias, mlc_gemm_f32out) keep 256: at 128
+// the BERT-base step lost 3 % (A/B knob 9)
+static int g_split_target_dense = 256;
 // LDS-DMA main loop (PF = 3) for GEMMs whose two operands both have an enabled DMA copy
 // (the K-contiguous MatKC / ConvFwdA: forward convs, stride-1 dgrads, dense forward):
 // A/B knob 8; -1: read MLC_GEMM_DMA on first use (default 1: ResNet-50 +1.2 %, U-Net
@@ -1354,7 +1359,7 @@ MLC_EXPORT int mlc_gemm_get_set(int key, int value) {
           : key == 2 ? &igemm::g_split_target_mat : key == 3 ? &igemm::g_big_tiles
           : key == 4 ? &igemm::g_big_min_blocks : key == 5 ? &igemm::g_single_stage
           : key == 6 ? &igemm::g_splitk_fused : key == 7 ? &igemm::g_dense_narrow
-          : key == 8 ? &igemm::g_gemm_dma : nullptr;
+          : key == 8 ? &igemm::g_gemm_dma : key == 9 ? &igemm::g_split_target_dense : nullptr;
   if (!k) return -1;
   const int old = *k;
   if (value >= 0 && (value > 0 || key == 3 || key == 5 || key == 6 || key == 7 || key == 8)) *k = value;
@@ -1660,7 +1665,7 @@ MLC_EXPORT int mlc_gemm_f32out(const bf16* A, const bf16* B, float* C, const flo
   if (K % 8 || lda % 8 || ldb % 8 || (ta && M % 8) || (!tb && N % 8)) return -1;
   const int tile = pick_tile(M, N);
   if (out_mode == 1) {
-    if (splits <= 0) splits = auto_splits(M, N, K, tile, g_split_target_mat);
+    if (splits <= 0) splits = auto_splits(M, N, K, tile, g_split_target_dense);
     EpiF32Atomic epi{C, ldc};
     if (!ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_KC, GB_KC);
     if (!ta && !tb) MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_KC, GB_MC);
@@ -1684,7 +1689,7 @@ MLC_EXPORT int mlc_linear_wgrad_bias(const bf16* A, const bf16* B, float* C, flo
                                      hipStream_t st) {
   if (K % 8 || lda % 8 || ldb % 8 || M % 8 || N % 8) return -1;
   const int tile = pick_tile(M, N);
-  if (splits <= 0) splits = auto_splits(M, N, K, tile, g_split_target_mat);
+  if (splits <= 0) splits = auto_splits(M, N, K, tile, g_split_target_dense);
   const size_t slab = (size_t)M * N;
 #define GA_MCS(R) (MatMCSum<R>{A, lda, K, M, dbias})
   if (ws && ldc == N && splits > 1 && (long)(splits * slab) <= ws_floats) {

@@ -100,3 +100,25 @@ def test_dgrad_transposed_filter_reference(K, s, p, d):
     b = Fn.conv2d_dgrad(dy, w, (N, H, W, C), s, p, d, wt=Fn.wt_flip_transpose(w))
     assert (a.float() - b.float()).abs().max().item() <= 1e-2 * a.float().abs().max().item()
     assert torch.equal(Fn.wt_flip_transpose(Fn.wt_flip_transpose(w)), w)
+
+
+class _Slot:
+    def __init__(self, w):
+        self.shape, self.numel, self.bf16 = tuple(w.shape), w.numel(), w
+
+
+def test_wt_table_cpu_conv_and_dense():
+    """WtTable on CPU: conv filters get the flipped channel-swapped copy, [out, in] dense
+    weights the plain transpose; both refresh in place from the current weights."""
+    torch.manual_seed(1)
+    wc = torch.randn(24, 3, 3, 16).to(torch.bfloat16)
+    wd = torch.randn(40, 32).to(torch.bfloat16)
+    tab = Fn.WtTable()
+    ic, idd = tab.add(_Slot(wc)), tab.add(_Slot(wd))
+    tab.finalize('cpu')
+    assert tuple(tab[ic].shape) == (16, 3, 3, 24) and tuple(tab[idd].shape) == (32, 40)
+    tab.refresh()
+    assert torch.equal(tab[ic], Fn.wt_flip_transpose(wc)) and torch.equal(tab[idd], wd.t())
+    wd.mul_(2)                        # a weight update: the next refresh follows it
+    tab.refresh()
+    assert torch.equal(tab[idd], wd.t())
