@@ -4,8 +4,10 @@
 // Single-threaded epoll server speaking a line protocol (one request, one response):
 //   PUSH <queue> <json>            -> OK <id>
 //   POP <timeout_ms> <q1> [q2 ...] -> MSG <queue> <id> <json> | NIL      (blocking, leased)
-//   ACK <id> | NACK <id>           -> OK          (NACK: back to the head of its queue)
+//   ACK <id> | NACK <id>           -> OK 1 | OK 0 (1: the lease existed; NACK: back to the head
+//                                                   of its queue)
 //   REVOKE <id>                    -> OK 1 | OK 0 (drop a pending message)
+//   HAS <id>                       -> OK 1 | OK 0 (the message is queued or leased)
 //   SET <key> <json>               -> OK          (result store)
 //   GET <key> <timeout_ms>         -> VAL <json> | NIL (blocking, consumes the value)
 //   LEN <queue>                    -> OK <n>
@@ -14,9 +16,17 @@
 // A leased message whose consumer disconnects before ACK is re-queued at the head of
 // its queue (and handed to a blocked POP waiter right away), so a crashed worker never
 // loses a task.  Waiters are served FIFO.  Requests a client sent before half-closing
-// its socket are still executed and answered.
+// its socket are still executed and answered (the connection closes once its replies,
+// including a blocked POP/GET's, have been written).
 //
-// usage: mlcomp-broker [--host 127.0.0.1] [--port 6380]
+// --journal <file>: every PUSH / ACK / REVOKE is appended to the file before it is
+// answered, and a restarted broker replays it: messages pushed and not yet acked or
+// revoked (leased ones included) are queued again in id order, so a broker restart does
+// not orphan dispatched tasks.  The journal is rewritten to the live set at start-up and
+// whenever it grows past 4x that set.  It survives a crash of the broker process (the
+// writes are flushed to the kernel), not a power loss (no fsync).
+//
+// usage: mlcomp-broker [--host 127.0.0.1] [--port 6380] [--journal FILE]
 #include <arpa/inet.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -27,6 +37,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -37,6 +48,7 @@
 #include <memory>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 namespace {
@@ -63,6 +75,7 @@ struct Conn {
   std::list<Waiter>::iterator wit;
   std::vector<std::string> leased;  // message ids leased to this connection
   bool closed = false;
+  bool eof = false;                 // the peer half-closed: close once the replies are out
 };
 
 class Broker {
@@ -72,7 +85,9 @@ class Broker {
     for (auto& kv : conns_) close(kv.first);
     if (ep_ >= 0) close(ep_);
     close(lfd_);
+    if (jf_) fclose(jf_);
   }
+  bool open_journal(const std::string& path);
   void run();
 
  private:
@@ -83,7 +98,15 @@ class Broker {
   std::unordered_map<std::string, std::string> results_;
   std::unordered_map<int, std::unique_ptr<Conn>> conns_;
   std::list<Waiter> waiters_;
+  std::unordered_set<std::string> queued_ids_;   // ids in queues_ (HAS without a scan)
   bool need_wake_ = false;  // set by close_conn (re-queued leases); drained by run()
+  std::string jpath_;
+  FILE* jf_ = nullptr;
+  size_t jlines_ = 0;
+
+  void journal(const char* tag, const std::string& id, const Msg* m = nullptr);
+  void compact_journal();
+  void enqueue_front(const Msg& m) { queues_[m.queue].push_front(m); queued_ids_.insert(m.id); }
 
   void accept_all();
   void on_read(Conn* c);
@@ -119,7 +142,9 @@ void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOC
 
 void Broker::watch_write(Conn* c, bool on) {
   epoll_event ev{};
-  ev.events = EPOLLIN | EPOLLRDHUP | (on ? EPOLLOUT : 0);
+  // after EOF the read side stays readable forever: stop watching it (no busy loop while
+  // a half-closed client's POP/GET is still blocked)
+  ev.events = (c->eof ? 0u : (uint32_t)(EPOLLIN | EPOLLRDHUP)) | (on ? EPOLLOUT : 0u);
   ev.data.fd = c->fd;
   epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &ev);
 }
@@ -149,7 +174,7 @@ void Broker::close_conn(Conn* c) {
   for (auto it = c->leased.rbegin(); it != c->leased.rend(); ++it) {
     auto l = leased_.find(*it);
     if (l == leased_.end()) continue;
-    queues_[l->second.queue].push_front(l->second);
+    enqueue_front(l->second);
     leased_.erase(l);
     need_wake_ = true;
   }
@@ -170,6 +195,7 @@ void Broker::flush(Conn* c) {
     }
     c->out.erase(0, (size_t)n);
   }
+  if (c->eof && !c->waiting) { close_conn(c); return; }
   watch_write(c, false);
 }
 
@@ -179,6 +205,7 @@ bool Broker::try_pop(Conn* c, const std::vector<std::string>& qs) {
     if (it == queues_.end() || it->second.empty()) continue;
     Msg m = it->second.front();
     it->second.pop_front();
+    queued_ids_.erase(m.id);
     reply(c, "MSG " + q + " " + m.id + " " + m.payload);
     c->leased.push_back(m.id);
     leased_[m.id] = m;
@@ -245,7 +272,9 @@ void Broker::handle(Conn* c, const std::string& line) {
     auto a = split(rest, 2);
     if (a.size() < 2) { reply(c, "ERR usage: PUSH queue payload"); return; }
     Msg m{std::to_string(next_id_++), a[0], a[1]};
+    journal("P", m.id, &m);
     queues_[a[0]].push_back(m);
+    queued_ids_.insert(m.id);
     reply(c, "OK " + m.id);
     wake();
     return;
@@ -264,8 +293,10 @@ void Broker::handle(Conn* c, const std::string& line) {
   }
   if (cmd == "ACK" || cmd == "NACK") {
     auto l = leased_.find(rest);
-    if (l != leased_.end()) {
-      if (cmd == "NACK") queues_[l->second.queue].push_front(l->second);
+    const bool had = l != leased_.end();
+    if (had) {
+      if (cmd == "NACK") enqueue_front(l->second);
+      else journal("A", rest);
       leased_.erase(l);
       for (auto& kv : conns_) {
         auto& v = kv.second->leased;
@@ -273,17 +304,29 @@ void Broker::handle(Conn* c, const std::string& line) {
           if (*it == rest) { v.erase(it); break; }
       }
     }
-    reply(c, "OK");
+    reply(c, had ? "OK 1" : "OK 0");
     if (cmd == "NACK") wake();
     return;
   }
   if (cmd == "REVOKE") {
-    for (auto& kv : queues_) {
-      auto& dq = kv.second;
-      for (auto it = dq.begin(); it != dq.end(); ++it)
-        if (it->id == rest) { dq.erase(it); reply(c, "OK 1"); return; }
+    if (queued_ids_.count(rest)) {
+      for (auto& kv : queues_) {
+        auto& dq = kv.second;
+        for (auto it = dq.begin(); it != dq.end(); ++it)
+          if (it->id == rest) {
+            dq.erase(it);
+            queued_ids_.erase(rest);
+            journal("R", rest);
+            reply(c, "OK 1");
+            return;
+          }
+      }
     }
     reply(c, "OK 0");
+    return;
+  }
+  if (cmd == "HAS") {
+    reply(c, (queued_ids_.count(rest) || leased_.count(rest)) ? "OK 1" : "OK 0");
     return;
   }
   if (cmd == "SET") {
@@ -347,8 +390,75 @@ void Broker::on_read(Conn* c) {
     handle(c, line);
   }
   if (c->in.size() > (64u << 20)) { close_conn(c); return; }
-  flush(c);
-  if (eof) close_conn(c);
+  if (eof && !c->eof) {
+    c->eof = true;
+    // the requests still buffered behind a blocked one are dropped with the connection:
+    // a half-closed client has stopped sending, but is owed the replies already due
+    if (!c->waiting) c->in.clear();
+  }
+  flush(c);   // closes a half-closed connection once nothing is pending
+}
+
+void Broker::journal(const char* tag, const std::string& id, const Msg* m) {
+  if (!jf_) return;
+  if (m)
+    fprintf(jf_, "%s %s %s %s\n", tag, id.c_str(), m->queue.c_str(), m->payload.c_str());
+  else
+    fprintf(jf_, "%s %s\n", tag, id.c_str());
+  fflush(jf_);
+  if (++jlines_ > 10000 && jlines_ > 4 * (queued_ids_.size() + leased_.size())) compact_journal();
+}
+
+// rewrite the journal to the live set (queued + leased, in id order) via tmp + rename
+void Broker::compact_journal() {
+  std::vector<const Msg*> live;
+  for (auto& kv : queues_)
+    for (auto& m : kv.second) live.push_back(&m);
+  for (auto& kv : leased_) live.push_back(&kv.second);
+  std::sort(live.begin(), live.end(), [](const Msg* a, const Msg* b) {
+    return std::stoull(a->id) < std::stoull(b->id);
+  });
+  const std::string tmp = jpath_ + ".tmp";
+  FILE* f = fopen(tmp.c_str(), "w");
+  if (!f) { perror("journal compaction"); return; }
+  for (const Msg* m : live) fprintf(f, "P %s %s %s\n", m->id.c_str(), m->queue.c_str(), m->payload.c_str());
+  fclose(f);
+  if (rename(tmp.c_str(), jpath_.c_str()) != 0) { perror("journal rename"); return; }
+  if (jf_) fclose(jf_);
+  jf_ = fopen(jpath_.c_str(), "a");
+  jlines_ = live.size();
+}
+
+// replay: P adds, A / R remove; survivors are queued in id order
+bool Broker::open_journal(const std::string& path) {
+  jpath_ = path;
+  std::map<unsigned long long, Msg> live;
+  if (FILE* f = fopen(path.c_str(), "r")) {
+    std::string line;
+    int ch;
+    for (;;) {
+      line.clear();
+      while ((ch = fgetc(f)) != EOF && ch != '\n') line.push_back((char)ch);
+      if (line.empty() && ch == EOF) break;
+      auto a = split(line, 4);
+      if (a.size() >= 2) {
+        unsigned long long id = strtoull(a[1].c_str(), nullptr, 10);
+        if (a[0] == "P" && a.size() == 4) live[id] = Msg{a[1], a[2], a[3]};
+        else if (a[0] == "A" || a[0] == "R") live.erase(id);
+        if (id >= next_id_) next_id_ = id + 1;
+      }
+      if (ch == EOF) break;
+    }
+    fclose(f);
+  }
+  for (auto& kv : live) {
+    queues_[kv.second.queue].push_back(kv.second);
+    queued_ids_.insert(kv.second.id);
+  }
+  compact_journal();
+  if (!jf_) return false;
+  fprintf(stdout, "mlcomp-broker journal %s: %zu pending message(s) restored\n", path.c_str(), live.size());
+  return true;
 }
 
 // SIGTERM / SIGINT end the event loop so the broker exits through its destructors (a
@@ -374,6 +484,8 @@ void Broker::run() {
       if (it == conns_.end()) continue;
       Conn* c = it->second.get();
       if (events[i].events & EPOLLERR) { close_conn(c); continue; }
+      // both directions gone: nobody can read a reply any more
+      if (c->eof && (events[i].events & EPOLLHUP)) { close_conn(c); continue; }
       // EPOLLIN / EPOLLRDHUP / EPOLLHUP: read to EOF (on_read parses and answers the
       // complete requests still buffered, then closes)
       if (events[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP)) on_read(c);
@@ -385,7 +497,7 @@ void Broker::run() {
     for (auto it = conns_.begin(); it != conns_.end();) {
       Conn* c = it->second.get();
       if (c->closed) { it = conns_.erase(it); continue; }
-      if (!c->waiting && c->in.find('\n') != std::string::npos) on_read(c);
+      if (!c->waiting && !c->eof && c->in.find('\n') != std::string::npos) on_read(c);
       ++it;
     }
   }
@@ -394,11 +506,12 @@ void Broker::run() {
 }  // namespace
 
 int main(int argc, char** argv) {
-  std::string host = "127.0.0.1";
+  std::string host = "127.0.0.1", jpath;
   int port = 6380;
   for (int i = 1; i + 1 < argc; i += 2) {
     if (!strcmp(argv[i], "--host")) host = argv[i + 1];
     else if (!strcmp(argv[i], "--port")) port = atoi(argv[i + 1]);
+    else if (!strcmp(argv[i], "--journal")) jpath = argv[i + 1];
   }
   signal(SIGPIPE, SIG_IGN);
   struct sigaction sa{};
@@ -420,8 +533,13 @@ int main(int argc, char** argv) {
   if (bind(lfd, (sockaddr*)&addr, sizeof(addr)) < 0) { perror("bind"); return 1; }
   if (listen(lfd, 512) < 0) { perror("listen"); return 1; }
   set_nonblock(lfd);
+  Broker broker(lfd);
+  if (!jpath.empty() && !broker.open_journal(jpath)) {
+    fprintf(stderr, "cannot open journal %s\n", jpath.c_str());
+    return 1;
+  }
   fprintf(stdout, "mlcomp-broker listening on %s:%d\n", host.c_str(), port);
   fflush(stdout);
-  Broker(lfd).run();
+  broker.run();
   return 0;
 }

@@ -191,7 +191,8 @@ struct Loader {
     order.clear();
     for (uint64_t i = 0; i < per; ++i) order.push_back(all[(i * world + rank) % n]);
     const uint64_t nb = drop_last ? per / batch : (per + batch - 1) / batch;
-    // a last partial batch is completed by wrapping around this rank's samples
+    // a last partial batch is filled up by wrapping around this rank's samples (fixed slot
+    // shape); RecordLoader.real_rows() tells the consumer how many rows are real
     for (uint64_t i = order.size(); i < nb * batch; ++i) order.push_back(order[i % per]);
     nbatches = (int64_t)nb;
     nitems = nbatches * chunks_per_batch();

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import itertools
 import json
+import logging
 import os
 import socket
 import threading
@@ -30,6 +31,9 @@ from collections import deque
 from typing import Dict, List, Optional, Tuple
 
 Message = Dict
+
+
+_log = logging.getLogger(__name__)
 
 
 class Broker:
@@ -43,6 +47,10 @@ class Broker:
         raise NotImplementedError
 
     def nack(self, msg_id: str):
+        raise NotImplementedError
+
+    def has(self, msg_id: str) -> bool:
+        """True while the message is queued or leased (not yet acked / revoked)."""
         raise NotImplementedError
 
     def revoke(self, msg_id: str) -> bool:
@@ -106,7 +114,11 @@ class InProcBroker(Broker):
 
     def ack(self, msg_id):
         with self._cv:
-            self._leased.pop(msg_id, None)
+            return self._leased.pop(msg_id, None) is not None
+
+    def has(self, msg_id):
+        with self._cv:
+            return msg_id in self._leased or any(m['id'] == msg_id for dq in self._q.values() for m in dq)
 
     def nack(self, msg_id):
         with self._cv:
@@ -176,8 +188,10 @@ class BrokerClient(Broker):
 
     # safe to re-send after a lost reply: a POP lease dies with the old connection (the
     # broker re-queues it), the others do not change state twice.  PUSH / SET / NACK /
-    # REVOKE are retried only when the request never reached the socket.
-    IDEMPOTENT = frozenset(('PING', 'POP', 'LEN', 'ACK', 'STATS'))
+    # REVOKE are retried only when the request never reached the socket.  A re-sent ACK
+    # whose first copy never arrived finds the lease gone (re-queued when the connection
+    # dropped): the broker answers OK 0 and ack() reports the lost lease.
+    IDEMPOTENT = frozenset(('PING', 'POP', 'LEN', 'ACK', 'STATS', 'HAS'))
 
     def _drop(self):
         if self._sock is not None:
@@ -230,7 +244,17 @@ class BrokerClient(Broker):
         return q, m
 
     def ack(self, msg_id):
-        self._cmd('ACK', msg_id)
+        """True when the lease was released; False when the broker had no lease for it
+        (it was re-queued after a lost connection: the message will be delivered again,
+        and the task status check rejects the duplicate)."""
+        ok = self._cmd('ACK', msg_id) == 'OK 1'
+        if not ok:
+            _log.warning('broker: no lease for message %s at ACK (re-queued after a dropped '
+                         'connection; a duplicate delivery follows)', msg_id)
+        return ok
+
+    def has(self, msg_id):
+        return self._cmd('HAS', msg_id) == 'OK 1'
 
     def nack(self, msg_id):
         self._cmd('NACK', msg_id)

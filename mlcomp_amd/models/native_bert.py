@@ -377,5 +377,30 @@ class NativeBert:
     def logits(self):
         return self._logits[:, :self.c.num_labels]
 
+    def predict(self, ids, tt, key_bias=None):
+        """Inference forward on the native kernels (no dropout, no autograd, no loss
+        accumulators touched): fp32 logits [B, num_labels].  Any batch size / sequence
+        length the kernels take (the eval loader's last batch may be short)."""
+        B, S = ids.shape
+        saved = (self.B, self.S, self.ctx.training)
+        self.B, self.S = B, S
+        self.train(False)
+        try:
+            with torch.no_grad():
+                e = (self.word.bf16[ids].float() + self.pos.bf16[:S][None].float()
+                     + self.tok_type.bf16[tt].float()).to(torch.bfloat16).view(B * S, -1)
+                h = Tx.ln_fwd(e, None, self.ln.g.master, self.ln.b.master, self.c.eps, p_out=0.0,
+                              seed=self.seed, salt_out=1)[0]
+                for layer in self.layers:
+                    h, _ = layer.fwd(h, key_bias)
+                cls = h.view(B, S, -1)[:, 0].contiguous()
+                z, _ = self.pooler.fwd(cls)
+                pooled = torch.tanh(z.float()).to(torch.bfloat16)
+                logits = Fn.linear_fwd(pooled, self.cls_w.bf16, self.cls_b.master)
+            return logits[:, :self.c.num_labels].float()
+        finally:
+            self.B, self.S = saved[0], saved[1]
+            self.train(saved[2])
+
 
 __all__ = ['NativeBert']

@@ -195,6 +195,32 @@ class NativeUnet:
         """BCE + Dice loss (device scalar); ``target`` fp32 [N*H*W*K] in pixel order."""
         return self.head(self.features(x), target)
 
+    def predict(self, x, target=None):
+        """Inference forward on the native kernels (BN running statistics, no autograd):
+        x NHWC bf16 (channels padded to 8, or the stem's s2d image) -> fp32 logits
+        [N, K, H, W]; with ``target`` ([N, K, H, W] / [N, H, W] masks) also the loss the
+        training head computes (bce_w * BCE + dice_w * (1 - dice)) as a device scalar."""
+        h = self.head
+        was = self.ctx.training
+        self.train(False)
+        try:
+            with torch.no_grad():
+                d = self.features(x)
+                N, H, W, _ = d.shape
+                P = N * H * W
+                logits = torch.empty(P, h.K, device=d.device, dtype=torch.float32)
+                t = torch.zeros(P, h.K, device=d.device, dtype=torch.float32)
+                if target is not None:
+                    m = target.to(d.device).float()
+                    t.copy_((m.permute(0, 2, 3, 1) if m.dim() == 4 else m.unsqueeze(-1)).reshape(P, h.K))
+                sums = torch.zeros(4, device=d.device, dtype=torch.float32)
+                seg.seg_head_fwd(d.reshape(P, h.C), h.w.master, h.b.master, t, sums, logits=logits)
+                out = logits.view(N, H, W, h.K).permute(0, 3, 1, 2)
+                loss = seg.seg_loss(sums, P * h.K, h.bce_w, h.dice_w, h.eps) if target is not None else None
+            return out, loss
+        finally:
+            self.train(was)
+
     def train(self, mode=True):
         self.ctx.training = mode
         return self

@@ -115,6 +115,25 @@ class NativeContext:
         self.wt_stale = False
 
 
+def flatten_bn_buffers(units) -> Optional[torch.Tensor]:
+    """One fp32 buffer holding every unit's BatchNorm running mean and variance; the units
+    are re-pointed at views of it.  Call after the units loaded their weights and before a
+    graph is captured: the rank-0 buffer broadcast (:meth:`GraphedStep.broadcast_buffers`)
+    is then one collective of ~2 x sum(C) floats."""
+    units = [u for u in units if getattr(u, 'run_mean', None) is not None]
+    if not units:
+        return None
+    flat = torch.empty(sum(2 * u.run_mean.numel() for u in units), device=units[0].run_mean.device)
+    off = 0
+    for u in units:
+        C = u.run_mean.numel()
+        flat[off:off + C].copy_(u.run_mean)
+        flat[off + C:off + 2 * C].copy_(u.run_var)
+        u.run_mean, u.run_var = flat[off:off + C], flat[off + C:off + 2 * C]
+        off += 2 * C
+    return flat
+
+
 # ---------------------------------------------------------------------------- conv+bn
 class ConvBN:
     """conv (no bias) -> BatchNorm (train-mode batch stats) -> [+residual] -> [ReLU]."""

@@ -21,8 +21,54 @@ import torch.distributed as dist
 
 from mlcomp_amd.ops import _lib
 
+import glob
+import re
+
 _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int64: 3, torch.int32: 4}
 _OP = {'sum': 0, 'max': 1, 'min': 2, 'avg': 3}
+
+
+# RCCL's own INFO log, filtered to the per-channel connection lines ("Channel 00/0 :
+# 0[0] -> 1[1] via P2P/IPC"): which transport each rank's rings / trees use.  Intra-node
+# on MI355X every pair should say P2P (xGMI); SHM means the peers could not map each
+# other's memory (e.g. each process saw only its own GPU) and traffic bounces off the host.
+_VIA = re.compile(r'via (\S+)')
+LAST_TRANSPORTS: dict = {}
+
+
+def enable_transport_log(folder: str) -> Optional[str]:
+    """Route RCCL's INIT/P2P/SHM/NET info lines into ``folder/rccl.<host>.<pid>.log``
+    (must run before the process's first RCCL call; a user-set NCCL_DEBUG wins)."""
+    if os.environ.get('NCCL_DEBUG'):
+        return os.environ.get('NCCL_DEBUG_FILE')
+    os.makedirs(folder, exist_ok=True)
+    path = os.path.join(folder, 'rccl.%h.%p.log')
+    os.environ.update(NCCL_DEBUG='INFO', NCCL_DEBUG_SUBSYS='INIT,P2P,SHM,NET', NCCL_DEBUG_FILE=path)
+    return path
+
+
+def transport_summary(text: str) -> dict:
+    """{transport: number of channel connections} from RCCL INFO log text."""
+    out: dict = {}
+    for line in text.splitlines():
+        if 'Channel' not in line:
+            continue
+        m = _VIA.search(line)
+        if m:
+            out[m.group(1)] = out.get(m.group(1), 0) + 1
+    return out
+
+
+def _read_transport_log() -> dict:
+    pattern = os.environ.get('NCCL_DEBUG_FILE')
+    if not pattern:
+        return {}
+    path = pattern.replace('%h', os.uname().nodename).replace('%p', str(os.getpid()))
+    text = ''
+    for f in ([path] if os.path.exists(path) else glob.glob(pattern.replace('%h', '*').replace('%p', str(os.getpid())))):
+        with open(f, errors='replace') as fh:
+            text += fh.read()
+    return transport_summary(text)
 
 
 class RcclComm:
@@ -48,6 +94,18 @@ class RcclComm:
                                     C.byref(err))
         if not self._h:
             raise RuntimeError(f'ncclCommInitRank failed ({err.value})')
+        # the connections are made lazily by the first collective of each kind: the bucketer's
+        # initial broadcast / first all-reduce; read the log then (transports())
+        self.transports = {}
+
+    def transports_now(self) -> dict:
+        """Transport histogram of this process's RCCL connections so far (needs
+        :func:`enable_transport_log` before the first RCCL call)."""
+        torch.cuda.synchronize(self.device)
+        self.transports = _read_transport_log()
+        LAST_TRANSPORTS.clear()
+        LAST_TRANSPORTS.update(self.transports)
+        return self.transports
 
     def _stream(self, stream):
         s = stream if stream is not None else torch.cuda.current_stream(self.device)

@@ -49,7 +49,10 @@ def _programs(workers: int, with_site: bool = True, with_broker: bool = True):
     log = lambda n: os.path.join(s.LOG_FOLDER, f'{n}.out')  # noqa: E731
     progs = []
     if with_broker:
-        progs.append(Program('broker', [build_broker(), '--port', str(s.BROKER_PORT)], log=log('broker')))
+        # the journal keeps dispatched-but-unfinished task messages across broker restarts
+        os.makedirs(s.DB_FOLDER, exist_ok=True)
+        progs.append(Program('broker', [build_broker(), '--port', str(s.BROKER_PORT), '--journal',
+                                        os.path.join(s.DB_FOLDER, 'broker.journal')], log=log('broker')))
     if with_site:
         progs.append(Program('site', python_module('mlcomp_amd.server', 'start-site'), log=log('site')))
     progs.append(Program('supervisor', python_module('mlcomp_amd.worker', 'worker-supervisor', '--workers', workers),

@@ -38,13 +38,22 @@ from mlcomp_amd.db.providers import (AuxiliaryProvider, ComputerProvider, DagPro
 from mlcomp_amd.utils.logging import create_logger
 from mlcomp_amd.utils.misc import yaml_dump, yaml_load
 
+# complete fatal-error strings of a crashed rank's last log line that make the DAG restart
+# from its last checkpoint (`mlcomp/server/back/supervisor.py:400-407` lists the CUDA/cuDNN
+# ones); a bare library name would also match harmless lines that merely mention it
+ORPHAN_MESSAGE = 'task message lost before the task started'
 FATAL_RESTART_MESSAGES = (
-    'hipErrorIllegalAddress', 'illegal memory access', 'HIP error: an illegal memory access',
-    'device-side assert', 'Memory access fault by GPU', 'GPU Hang', 'unhandled system error',
-    'ncclSystemError', 'RCCL', 'MIOPEN_STATUS_INTERNAL_ERROR',
+    'hipErrorIllegalAddress', 'an illegal memory access was encountered',
+    'device-side assert triggered', 'Memory access fault by GPU', 'GPU Hang', 'HW Exception by GPU',
+    'hipErrorLaunchFailure', 'ncclUnhandledCudaError', 'ncclSystemError: System call',
+    'unhandled system error', 'ncclRemoteError', 'MIOPEN_STATUS_INTERNAL_ERROR',
+    ORPHAN_MESSAGE,
 )
 MAX_AUTO_RESTARTS = 3
 ALIVE_SECONDS = 15
+# a Queued task whose broker message is gone (broker restarted without its journal) or
+# whose queue has been dead this long is taken back: its GPUs return to the ledger
+ORPHAN_SECONDS = 30
 
 
 class SupervisorBuilder:
@@ -56,6 +65,7 @@ class SupervisorBuilder:
         self.commands: _queue.Queue = _queue.Queue()
         self.auxiliary: dict = {}
         self.sent_tasks = 0
+        self._suspect: Dict[int, float] = {}   # Queued task id -> first tick it looked orphaned
         self._providers()
 
     def _providers(self):
@@ -223,6 +233,46 @@ class SupervisorBuilder:
              'dep_status': sorted(TaskStatus(s).name for s in self.dep_status.get(t.id, ()))}
             for t in self.not_ran_tasks[:5]]
 
+    def process_orphans(self):
+        """Queued tasks nobody will run: the message is no longer in the broker (queued or
+        leased - a broker restart without ``--journal``), or the target queue has had no
+        heartbeat for ``ORPHAN_SECONDS``.  After ``ORPHAN_SECONDS`` of that (a worker that
+        just popped the message holds a lease, so a live hand-off never looks orphaned) a
+        plain task goes back to NotRan and is placed again, which also frees its GPUs in the
+        ledger; a DDP rank task is failed with ``ORPHAN_MESSAGE`` - its parent fails, the
+        other ranks are stopped and the bounded fatal-restart resumes the DAG."""
+        t_now = time.time()
+        seen = set()
+        for t in self.tasks:
+            if t.status != TaskStatus.Queued.value or not t.celery_id or not t.computer_assigned:
+                continue
+            q = queue_name(t.computer_assigned, t.docker_assigned or 'default')
+            try:
+                lost = not self.broker.has(t.celery_id)
+            except NotImplementedError:
+                lost = False
+            if not lost and q in self.queues:
+                continue
+            seen.add(t.id)
+            first = self._suspect.setdefault(t.id, t_now)
+            if t_now - first < ORPHAN_SECONDS:
+                continue
+            self._suspect.pop(t.id, None)
+            why = 'its broker message is gone' if lost else f'queue {q} is dead'
+            self.broker.revoke(t.celery_id)
+            if t.type == TaskType.Service.value and t.parent:
+                self.logger.error(f'task {t.id}: {ORPHAN_MESSAGE} ({why})', ComponentType.Supervisor,
+                                  t.computer_assigned, t.id)
+                self.provider.change_status(t, TaskStatus.Failed)
+                continue
+            self.logger.warning(f'task {t.id} re-queued: {why}', ComponentType.Supervisor, t.computer_assigned, t.id)
+            t.status = TaskStatus.NotRan.value
+            t.computer_assigned = t.docker_assigned = t.celery_id = t.gpu_assigned = None
+            self.provider.commit()
+        for tid in list(self._suspect):
+            if tid not in seen:
+                del self._suspect[tid]
+
     def load_computers(self):
         comps = {}
         for name, c in self.computer_provider.computers().items():
@@ -346,10 +396,18 @@ class SupervisorBuilder:
         if len(names) == 1:
             task.computer_assigned = master['name']
         info = yaml_load(task.additional_info) or {}
+        # every rank on a computer sees ALL of the job's GPUs there (HIP_VISIBLE_DEVICES) and
+        # picks its own by local_rank: RCCL then finds its peers and connects them over
+        # xGMI P2P (with one visible GPU per process it cannot, and falls back to host SHM)
+        node_gpus: Dict[str, List[int]] = {}
+        for c, gpu in ranks:
+            node_gpus.setdefault(c['name'], []).append(gpu)
         for rank, (c, gpu) in enumerate(ranks):
             addr = '127.0.0.1' if c['name'] == master['name'] else (master.get('ip') or master['name'])
             child_info = dict(info)
-            child_info['distr_info'] = {'master_addr': addr, 'rank': rank, 'local_rank': gpu,
+            mine = node_gpus[c['name']]
+            child_info['distr_info'] = {'master_addr': addr, 'rank': rank, 'local_rank': mine.index(gpu),
+                                        'gpu': gpu, 'visible_gpus': ','.join(map(str, mine)),
                                         'master_port': port, 'world_size': len(ranks),
                                         'master_computer': master['name']}
             child = Task(name=task.name, computer=task.computer, executor=task.executor,
@@ -407,6 +465,8 @@ class SupervisorBuilder:
             self.create_base()
             self.process_commands()
             self.process_parent_tasks()
+            self.load_tasks()
+            self.process_orphans()
             self.load_tasks()
             self.load_computers()
             self.process_tasks()

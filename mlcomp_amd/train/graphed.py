@@ -19,6 +19,7 @@ step protocol from :class:`GraphedStep`:
 """
 from __future__ import annotations
 
+import os
 import warnings
 
 import torch
@@ -31,6 +32,23 @@ class GraphedStep:
     calls: int = 0
     comm = None
     capture_error = None
+    # BatchNorm running statistics (flat buffer, ops.layers.flatten_bn_buffers) and when rank
+    # 0's copy is broadcast: 'step' (default; PyTorch DDP's broadcast_buffers=True, which the
+    # reference's Catalyst DDP used) = at the end of every step, inside the captured graph;
+    # 'eval' = only when the runner asks (before validation and checkpoints)
+    bn_buffers = None
+    bn_broadcast = os.environ.get('MLC_BN_BROADCAST', 'step')
+
+    def broadcast_buffers(self):
+        """Rank 0's BatchNorm running statistics to every rank: one
+        broadcast of the flat buffer on the current stream.  A no-op on one rank."""
+        if self.comm is None or self.bn_buffers is None or getattr(self.comm, 'world', 1) <= 1:
+            return
+        self.comm.broadcast(self.bn_buffers, 0)
+
+    def _end_of_step_buffers(self):
+        if self.bn_broadcast == 'step':
+            self.broadcast_buffers()
 
     def _body(self):  # pragma: no cover - implemented by the concrete steps
         raise NotImplementedError

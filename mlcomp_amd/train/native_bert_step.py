@@ -18,13 +18,14 @@ from mlcomp_amd.models.native_bert import NativeBert
 from mlcomp_amd.parallel.comm import make_comm
 from mlcomp_amd.parallel.ddp import GradBucketer
 from mlcomp_amd.train.graphed import GraphedStep
-from mlcomp_amd.train.optim import FusedAdam
+from mlcomp_amd.train.optim import FusedAdam, FusedSGD
 
 
 class NativeBertStep(GraphedStep):
     def __init__(self, model_name='bert-base', batch=32, seq_len=128, device=None, world_size=1, use_graph=True,
                  num_labels=2, lr=2e-5, weight_decay=0.01, betas=(0.9, 0.999), eps=1e-6, seed=0, warmup_eager=2,
-                 torch_model=None, dropout: Optional[float] = None, comm=None):
+                 torch_model=None, dropout: Optional[float] = None, comm=None, optimizer='AdamW',
+                 momentum=0.0, nesterov=False, dampening=0.0):
         self.device = torch.device(device or 'cuda')
         torch.manual_seed(seed)
         kw = {'num_labels': num_labels}
@@ -37,8 +38,14 @@ class NativeBertStep(GraphedStep):
         self.comm = comm if comm is not None else (make_comm(self.device) if world_size > 1 else None)
         self.bucketer = GradBucketer(self.net.arena, self.comm)
         self.bucketer.broadcast_params()
-        self.opt = FusedAdam(self.net.arena, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, decoupled=True,
-                             grad_scale=1.0 / world_size)
+        if optimizer in ('Adam', 'AdamW'):
+            self.opt = FusedAdam(self.net.arena, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                                 decoupled=optimizer == 'AdamW', grad_scale=1.0 / world_size)
+        elif optimizer == 'SGD':
+            self.opt = FusedSGD(self.net.arena, lr=lr, momentum=momentum, weight_decay=weight_decay,
+                                nesterov=nesterov, dampening=dampening, grad_scale=1.0 / world_size)
+        else:
+            raise ValueError(f'native optimizers: SGD / Adam / AdamW, not {optimizer!r}')
         # optimizer-in-backward (MLC_OPT_IN_BWD=1): each gradient bucket is updated on the side
         # stream as soon as it is complete (and all-reduced).  Measured slower on MI355X
         # (profiles/round2_ab): the memory-bound update competes with the memory-bound
@@ -76,6 +83,16 @@ class NativeBertStep(GraphedStep):
                 self.key_bias = kb
             else:
                 self.key_bias.copy_(kb)
+
+    def predict(self, ids, token_type_ids=None, attention_mask=None):
+        """Native inference logits [B, num_labels] for one (eval) batch."""
+        ids = ids.to(self.device)
+        tt = token_type_ids.to(self.device) if token_type_ids is not None else torch.zeros_like(ids)
+        kb = None
+        if attention_mask is not None:
+            kb = torch.zeros(attention_mask.shape, device=self.device).masked_fill(
+                attention_mask.to(self.device) == 0, float('-inf'))
+        return self.net.predict(ids, tt, kb)
 
     def _body(self):
         net = self.net

@@ -15,6 +15,7 @@ import torch
 from mlcomp_amd.models.native_resnet import STEM_CIN
 from mlcomp_amd.models.native_unet import NativeUnet
 from mlcomp_amd.ops import functional as Fn
+from mlcomp_amd.ops.layers import flatten_bn_buffers
 from mlcomp_amd.parallel.comm import make_comm
 from mlcomp_amd.parallel.ddp import GradBucketer
 from mlcomp_amd.train.graphed import GraphedStep
@@ -32,23 +33,27 @@ def synthetic_masks(batch, size, device, generator, classes=1):
 class NativeSegmentationStep(GraphedStep):
     def __init__(self, encoder='resnet34', batch=32, image_size=256, device=None, world_size=1, use_graph=True,
                  lr=3e-4, weight_decay=0.0, optimizer='Adam', momentum=0.9, betas=(0.9, 0.999), eps=1e-8,
-                 seed=0, warmup_eager=2, torch_model=None, comm=None, classes=1):
+                 seed=0, warmup_eager=2, torch_model=None, comm=None, classes=1, nesterov=False, dampening=0.0,
+                 bce_w=1.0, dice_w=1.0, loss_eps=1e-7):
         from mlcomp_amd.contrib.segmentation.models import Unet
         self.device = torch.device(device or 'cuda')
         torch.manual_seed(seed)
         tm = torch_model if torch_model is not None else Unet(encoder_name=encoder, classes=classes)
-        self.net = NativeUnet(tm, self.device)
+        self.net = NativeUnet(tm, self.device, bce_w=bce_w, dice_w=dice_w, eps=loss_eps)
         self.net.ctx.grad_prezeroed = True
         self.world = world_size
         self.comm = comm if comm is not None else (make_comm(self.device) if world_size > 1 else None)
         self.bucketer = GradBucketer(self.net.arena, self.comm)
+        self.bn_buffers = flatten_bn_buffers(self.net._units())
         self.bucketer.broadcast_params()
         if optimizer in ('Adam', 'AdamW'):
             self.opt = FusedAdam(self.net.arena, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                                  decoupled=optimizer == 'AdamW', grad_scale=1.0 / world_size)
-        else:
+        elif optimizer == 'SGD':
             self.opt = FusedSGD(self.net.arena, lr=lr, momentum=momentum, weight_decay=weight_decay,
-                                grad_scale=1.0 / world_size)
+                                nesterov=nesterov, dampening=dampening, grad_scale=1.0 / world_size)
+        else:
+            raise ValueError(f'native optimizers: SGD / Adam / AdamW, not {optimizer!r}')
         # optimizer-in-backward (MLC_OPT_IN_BWD=1): each gradient bucket is updated on the side
         # stream as soon as it is complete (and all-reduced).  Measured slower on MI355X
         # (profiles/round2_ab): the memory-bound update competes with the memory-bound
@@ -99,6 +104,7 @@ class NativeSegmentationStep(GraphedStep):
         self.bucketer.finish()
         if not self.opt_in_bwd:
             self.opt.step()
+        self._end_of_step_buffers()
         self._loss = loss.detach()
 
     def set_lr(self, lr):

@@ -19,6 +19,7 @@ import torch
 from mlcomp_amd.models import build_model
 from mlcomp_amd.models.native_resnet import STEM_CIN, NativeResNet
 from mlcomp_amd.ops import functional as Fn
+from mlcomp_amd.ops.layers import flatten_bn_buffers
 from mlcomp_amd.parallel.comm import make_comm
 from mlcomp_amd.parallel.ddp import GradBucketer
 from mlcomp_amd.train.graphed import GraphedStep
@@ -30,7 +31,7 @@ class NativeClassifierStep(GraphedStep):
                  world_size=1, use_graph=True, num_classes=1000, lr=0.1, momentum=0.9,
                  weight_decay=5e-5, nesterov=False, smoothing=0.0, seed=0, warmup_eager=2,
                  torch_model=None, optimizer='SGD', betas=(0.9, 0.999), eps=1e-8,
-                 comm=None):
+                 comm=None, dampening=0.0):
         self.device = torch.device(device or 'cuda')
         torch.manual_seed(seed)
         tm = torch_model if torch_model is not None else build_model(model_name, num_classes=num_classes)
@@ -41,13 +42,16 @@ class NativeClassifierStep(GraphedStep):
         # bucketed all-reduce inside graph capture on a single GPU)
         self.comm = comm if comm is not None else (make_comm(self.device) if world_size > 1 else None)
         self.bucketer = GradBucketer(self.net.arena, self.comm)
+        self.bn_buffers = flatten_bn_buffers(self.net._units())
         self.bucketer.broadcast_params()
         if optimizer in ('Adam', 'AdamW'):
             self.opt = FusedAdam(self.net.arena, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                                  decoupled=optimizer == 'AdamW', grad_scale=1.0 / world_size)
         else:
+            if optimizer != 'SGD':
+                raise ValueError(f'native optimizers: SGD / Adam / AdamW, not {optimizer!r}')
             self.opt = FusedSGD(self.net.arena, lr=lr, momentum=momentum, weight_decay=weight_decay,
-                                nesterov=nesterov, grad_scale=1.0 / world_size)
+                                nesterov=nesterov, dampening=dampening, grad_scale=1.0 / world_size)
         # optimizer-in-backward (MLC_OPT_IN_BWD=1): each gradient bucket is updated on the side
         # stream as soon as it is complete (and all-reduced).  Measured slower on MI355X
         # (profiles/round2_ab): the memory-bound update competes with the memory-bound
@@ -94,6 +98,7 @@ class NativeClassifierStep(GraphedStep):
         self.bucketer.finish()
         if not self.opt_in_bwd:
             self.opt.step()
+        self._end_of_step_buffers()
         self._loss = self.net.head.loss_sum()
 
     def set_lr(self, lr):

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import weakref
 import os
 import struct
 from typing import Iterable, Optional, Sequence, Tuple
@@ -218,6 +219,9 @@ class RecordLoader:
         shuffle = self.train if shuffle is None else shuffle
         drop_last = self.train if drop_last is None else drop_last
         per = math.ceil(self.count / world_size)
+        self._per = per
+        self._drop_last = bool(drop_last)
+        self._live = None
         self._len = per // self.batch_size if drop_last else math.ceil(per / self.batch_size)
         self._loader = rt.mlr_loader_create(self._file, self.batch_size, self.out_h, self.out_w, int(self.train),
                                             float(scale[0]), float(scale[1]), float(ratio[0]), float(ratio[1]),
@@ -291,7 +295,25 @@ class RecordLoader:
         self._used[k % 2] = used
         return out, dlab, done
 
+    def real_rows(self, k: int) -> int:
+        """Samples of batch ``k`` that are not wrap-around padding.  Only the last batch of
+        a ``drop_last=False`` epoch has padding: ``per - (len-1)*batch`` rows are real (the
+        world-size padding of the shard stays, as DistributedSampler does it)."""
+        if k < self._len - 1 or self._drop_last:
+            return self.batch_size
+        return self._per - (self._len - 1) * self.batch_size
+
     def __iter__(self):
+        # an earlier iterator still alive holds an INUSE slot whose async H2D copy may be
+        # pending: close it (its finally releases the slot) before the ring is reset
+        prev = self._live() if self._live is not None else None
+        if prev is not None:
+            prev.close()
+        gen = self._epoch_iter()
+        self._live = weakref.ref(gen)
+        return gen
+
+    def _epoch_iter(self):
         rt = self._rt
         n = rt.mlr_loader_start_epoch(self._loader, self.epoch)
         if n < 0:
@@ -318,6 +340,9 @@ class RecordLoader:
                     pev.synchronize()
                     rt.mlr_loader_release(self._loader, ps)
                 pending = (s, done) if s >= 0 else None
+                real = self.real_rows(k)
+                if real < self.batch_size:   # drop the wrap-around rows of the last batch
+                    x, y = x[:real], y[:real]
                 yield {'features': x, 'targets': y}
         finally:
             if pending is not None:

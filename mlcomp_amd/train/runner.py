@@ -17,6 +17,7 @@ Two engines behind one loop:
 """
 from __future__ import annotations
 
+import logging
 import time
 from collections import OrderedDict, defaultdict
 from typing import Dict, List, Optional
@@ -29,6 +30,8 @@ from mlcomp_amd.utils import faults
 from .callbacks import Callback
 from .data import DeviceSyntheticLoader, make_loader
 from .experiment import ConfigExperiment
+
+_log = logging.getLogger(__name__)
 
 
 class State:
@@ -145,8 +148,19 @@ class Runner:
         if self.engine == 'native' and not _native_capable(self.model, self.device):
             raise RuntimeError('engine: native needs a ResNet-family classifier (groups=1), BERT or a '
                                'ResNet-encoder U-Net (<= 4 sigmoid classes) on a GPU')
-        self.state.native = use_native
         self.native_kind = _native_kind(self.model, self.device) if use_native else None
+        self._native_plan = None
+        if use_native:
+            from .native_spec import NativeUnsupported, native_plan
+            try:
+                self._native_plan = native_plan(self.experiment, stage, self.native_kind)
+            except NativeUnsupported as e:
+                if self.engine == 'native':
+                    raise RuntimeError(f'engine: native cannot run stage {stage!r}: {e}') from e
+                # engine: auto trains what the config asks for, on the PyTorch path
+                _log.warning('stage %s: %s - training on the PyTorch engine', stage, e)
+                use_native, self.native_kind = False, None
+        self.state.native = use_native
         if not use_native:
             self.model.to(self.device)
             if self.device.type == 'cuda':
@@ -159,33 +173,27 @@ class Runner:
                 self.ddp_model = self.model
 
     def _build_native(self, stage, batch):
-        spec = self.experiment.optimizer_spec(stage)
+        plan = dict(self._native_plan or {})
+        use_graph = self.experiment.args.get('graph', True)
         if self.native_kind == 'bert':
             from .native_bert_step import NativeBertStep
             ids = batch['input_ids']
             self.model.to(self.device)
             self.native_step = NativeBertStep(
                 torch_model=self.model, batch=ids.shape[0], seq_len=ids.shape[1], device=self.device,
-                world_size=self.world_size, num_labels=self.model.config.num_labels, lr=spec.get('lr', 2e-5),
-                weight_decay=spec.get('weight_decay', 0.01), betas=tuple(spec.get('betas', (0.9, 0.999))),
-                eps=spec.get('eps', 1e-6), use_graph=self.experiment.args.get('graph', True))
+                world_size=self.world_size, num_labels=self.model.config.num_labels, use_graph=use_graph, **plan)
             self._apply_native_opt_state()
             return
         if self.native_kind == 'unet':
             from .native_seg_step import NativeSegmentationStep
-            name = spec.get('optimizer', 'Adam')
             x = batch['features']
             size = x.shape[1] if x.dtype == torch.bfloat16 and x.shape[-1] == 8 else x.shape[-1]
             self.native_step = NativeSegmentationStep(
                 torch_model=self.model, batch=x.shape[0], image_size=size, device=self.device,
-                world_size=self.world_size, lr=spec.get('lr', 3e-4), optimizer=name,
-                momentum=spec.get('momentum', 0.9), weight_decay=spec.get('weight_decay', 0.0),
-                betas=tuple(spec.get('betas', (0.9, 0.999))), eps=spec.get('eps', 1e-8),
-                use_graph=self.experiment.args.get('graph', True))
+                world_size=self.world_size, use_graph=use_graph, **plan)
             self._apply_native_opt_state()
             return
         from .native_step import NativeClassifierStep
-        name = spec.get('optimizer', 'SGD')
         x = batch['features']
         if x.dtype == torch.bfloat16 and x.shape[-1] == 16:     # stem space-to-depth image (pad 3)
             size = 2 * x.shape[1] - 6
@@ -195,11 +203,7 @@ class Runner:
             size = x.shape[-1]
         self.native_step = NativeClassifierStep(
             torch_model=self.model, batch=x.shape[0], image_size=size, device=self.device,
-            world_size=self.world_size, num_classes=self.model.fc.out_features,
-            lr=spec.get('lr', 0.1), momentum=spec.get('momentum', 0.9 if name == 'SGD' else 0.0),
-            weight_decay=spec.get('weight_decay', 0.0), nesterov=spec.get('nesterov', False),
-            use_graph=self.experiment.args.get('graph', True), optimizer=name,
-            betas=tuple(spec.get('betas', (0.9, 0.999))), eps=spec.get('eps', 1e-8))
+            world_size=self.world_size, num_classes=self.model.fc.out_features, use_graph=use_graph, **plan)
         self._apply_native_opt_state()
 
     def _native_sched(self, stage):
@@ -374,7 +378,6 @@ class Runner:
                 if self.native_kind == 'unet':
                     ns.load_batch(batch['features'], batch['targets'])
                     ns()
-                    self._exported = False
                     st.batch_size = ns.batch
                     if dev_loss is None:
                         dev_loss = torch.zeros(2, device=self.device)
@@ -393,7 +396,6 @@ class Runner:
                     ns.load_batch(batch['features'], batch['targets'])
                     head = ns.net.head
                 ns()
-                self._exported = False
                 st.batch_size = ns.batch
                 if dev_loss is None:
                     dev_loss = torch.zeros(2, device=self.device)
@@ -420,31 +422,35 @@ class Runner:
             st.epoch_metrics[f'{name}_{k}'] = v
 
     def _run_native_eval(self, batch):
+        """Validation / inference batches on the native kernels too (the reference runs
+        train and valid loaders through one runner, `catalyst_.py:423`): inference-mode
+        BatchNorm / no dropout, no autograd, nothing routed to MIOpen or hipBLASLt."""
         st = self.state
+        if self.native_step is None:       # a valid-only stage: build the engine from this batch
+            self._build_native(st.stage, batch)
+            self.sync_lr()
         ns = self.native_step
-        if self.native_kind in ('bert', 'unet') or ns is None and 'input_ids' in batch:
-            if ns is not None and not getattr(self, '_exported', False):
-                ns.net.export_to_torch()
-                self._exported = True
-            self.model.to(self.device).eval()
-            self._run_batch_torch(batch)
-            self.model.train()
-            if self.native_kind == 'unet':
-                st.loss = self.criterion(st.output['logits'], st.input['targets'].float()) \
-                    if self.criterion is not None else None
-            else:
-                st.loss = torch.nn.functional.cross_entropy(st.output['logits'], st.input['targets'])
+        y = batch['targets'].to(self.device)
+        if self.native_kind == 'bert':
+            logits = ns.predict(batch['input_ids'], batch.get('token_type_ids'), batch.get('attention_mask'))
+            st.input = {'input_ids': batch['input_ids'], 'targets': y}
+            st.output = {'logits': logits}
+            st.batch_size = logits.shape[0]
+            st.loss = self._eval_loss(logits, y)
             return
         x = batch['features'].to(self.device)
-        y = batch['targets'].to(self.device)
         if x.dtype != torch.bfloat16:
             from mlcomp_amd.ops import functional as Fn
             from mlcomp_amd.models.native_resnet import STEM_CIN
             x = Fn.nchw_to_nhwc(x.float(), pad_to=STEM_CIN)
-        net = ns.net if ns is not None else None
-        if net is None:
-            self._run_batch_torch(batch)
+        if self.native_kind == 'unet':
+            logits, loss = ns.net.predict(x, y)
+            st.input = {'features': x, 'targets': y}
+            st.output = {'logits': logits}
+            st.batch_size = x.shape[0]
+            st.loss = loss
             return
+        net = ns.net
         net.eval()
         with torch.no_grad():
             logits = net.logits(x).float()
@@ -452,7 +458,13 @@ class Runner:
         st.input = {'features': x, 'targets': y}
         st.output = {'logits': logits}
         st.batch_size = x.shape[0]
-        st.loss = torch.nn.functional.cross_entropy(logits, y)
+        st.loss = self._eval_loss(logits, y)
+
+    def _eval_loss(self, logits, y):
+        """The stage criterion on the native logits (label smoothing included)."""
+        if self.criterion is not None:
+            return self.criterion(logits, y)
+        return torch.nn.functional.cross_entropy(logits, y)
 
     def run_stage(self, stage: str, start_epoch: int = 0):
         st = self.state
@@ -486,6 +498,9 @@ class Runner:
             self._fire('on_epoch_start')
             for name, loader in self.loaders.items():
                 self._run_loader(name, loader)
+                ns = self.native_step
+                if ns is not None and name.startswith('train') and ns.bn_broadcast == 'eval':
+                    ns.broadcast_buffers()     # every rank validates / checkpoints rank 0's BN stats
             valid = 'valid' if 'valid' in self.loaders else next(iter(self.loaders))
             st.valid_metrics = {k[len(valid) + 1:]: v for k, v in st.epoch_metrics.items()
                                 if k.startswith(valid + '_')}

@@ -5,9 +5,11 @@ register and validate their arguments, and fail with a clear message at run time
 the client is missing."""
 from __future__ import annotations
 
+import json
 import os
 import shutil
 import time
+import zipfile
 from typing import List
 
 from mlcomp_amd import config
@@ -50,7 +52,7 @@ class Submit(Executor):
     def __init__(self, competition: str, submit_type: str = 'file', kernel_suffix: str = 'api', message: str = '',
                  wait_seconds: int = 60 * 20, file: str = None, max_size: int = None, datasets: List[str] = (),
                  folders: List[str] = (), files: List[str] = (), model_name: str = None, suffix: str = '',
-                 **kwargs):
+                 notebook: str = 'predict.ipynb', dataset_wait: int = 30, poll_seconds: int = 20, **kwargs):
         super().__init__(**kwargs)
         assert submit_type in ('file', 'kernel'), submit_type
         self.competition, self.submit_type, self.kernel_suffix = competition, submit_type, kernel_suffix
@@ -59,30 +61,89 @@ class Submit(Executor):
         if not file and model_name:
             file = f'data/submissions/{model_name}_{suffix}.csv'
         self.file = file
+        self.notebook, self.dataset_wait, self.poll_seconds = notebook, dataset_wait, poll_seconds
 
     def file_submit(self):
         _api().competition_submit(self.file, message=self.message, competition=self.competition)
 
+    # ------------------------------------------------------------------ kernel submit
+    def dataset_meta(self, username: str) -> dict:
+        """`dataset-metadata.json` of the private dataset that carries the code / weights."""
+        return {'competition': self.competition, 'id': f'{username}/{self.competition}-{self.kernel_suffix}-dataset',
+                'licenses': [{'name': 'CC0-1.0'}], 'title': f'{self.competition} {self.kernel_suffix} (mlcomp)'}
+
+    def kernel_meta(self, username: str, dataset_id: str) -> dict:
+        """`kernel-metadata.json` of the notebook that runs inference over the dataset."""
+        slug = f'{self.competition}-{self.kernel_suffix}'
+        return {'id': f'{username}/{slug}', 'title': slug, 'code_file': os.path.basename(self.notebook),
+                'language': 'python', 'kernel_type': 'notebook', 'is_private': 'true',
+                'enable_gpu': 'true', 'enable_internet': 'false',
+                'dataset_sources': [dataset_id] + list(self.datasets),
+                'competition_sources': [self.competition], 'kernel_sources': []}
+
+    def _size_gb(self) -> float:
+        total = 0
+        for f in self.folders:
+            for root, _, names in os.walk(f):
+                total += sum(os.path.getsize(os.path.join(root, n)) for n in names)
+        total += sum(os.path.getsize(f) for f in self.files)
+        return total / 2 ** 30
+
     def kernel_submit(self):
+        """Zip the folders / files into a private dataset (created, or a new version),
+        then push a notebook kernel that reads it (`mlcomp/worker/executors/kaggle.py:112-186`)
+        and wait for the kernel run to finish."""
         api = _api()
         folder = os.path.expanduser(f'~/.kaggle/competitions/{self.competition}')
         shutil.rmtree(folder, ignore_errors=True)
         os.makedirs(folder, exist_ok=True)
-        for f in self.folders:
-            shutil.make_archive(os.path.join(folder, os.path.basename(f.rstrip('/'))), 'zip', f)
-        for f in self.files:
-            shutil.copy(f, folder)
-        api.dataset_create_version(folder, self.message or 'mlcomp submit', dir_mode='zip')
+        size = self._size_gb()
+        if self.max_size and size >= self.max_size:
+            raise ValueError(f'max_size = {self.max_size} GB, the submission is {size:.2f} GB')
+        username = api.read_config_file()['username']
+        meta = self.dataset_meta(username)
+        with open(os.path.join(folder, 'dataset-metadata.json'), 'w') as f:
+            json.dump(meta, f)
+        self.info('kernel submit: zipping folders')
+        with zipfile.ZipFile(os.path.join(folder, 'dataset.zip'), 'w', zipfile.ZIP_DEFLATED) as z:
+            for d in self.folders:
+                base = os.path.dirname(os.path.abspath(d).rstrip('/'))
+                for root, _, names in os.walk(d):
+                    for n in names:
+                        p = os.path.join(root, n)
+                        z.write(p, os.path.relpath(os.path.abspath(p), base))
+            for p in self.files:
+                z.write(p, os.path.basename(p))
+        self.info('kernel submit: uploading the dataset')
+        if not any(getattr(d, 'ref', None) == meta['id'] for d in api.dataset_list(user=username)):
+            api.dataset_create_new(folder)
+        else:
+            res = api.dataset_create_version(folder, self.message or 'mlcomp submit')
+            if getattr(res, 'status', '') == 'error':
+                raise RuntimeError(f'dataset_create_version: {getattr(res, "error", res)}')
+        time.sleep(self.dataset_wait)     # the new dataset version is processed server-side
+        shutil.copy(self.notebook, os.path.join(folder, os.path.basename(self.notebook)))
+        kmeta = self.kernel_meta(username, meta['id'])
+        with open(os.path.join(folder, 'kernel-metadata.json'), 'w') as f:
+            json.dump(kmeta, f)
+        api.kernels_push(folder)
+        self.info(f'kernel pushed: https://www.kaggle.com/{kmeta["id"]}')
         deadline = time.time() + self.wait_seconds
+        status = None
         while time.time() < deadline:
-            st = api.kernel_status(f'{self.competition}-{self.kernel_suffix}')
-            if getattr(st, 'status', '') in ('complete', 'error'):
+            status = getattr(api.kernels_status(kmeta['id']), 'status', None)
+            if status in ('complete', 'error', 'cancelAcknowledged'):
                 break
-            time.sleep(20)
+            time.sleep(self.poll_seconds)
+        if status == 'error':
+            raise RuntimeError(f'kernel {kmeta["id"]} failed')
+        return {'kernel': kmeta['id'], 'status': status}
 
     def work(self):
-        (self.file_submit if self.submit_type == 'file' else self.kernel_submit)()
-        return {}
+        if self.submit_type == 'file':
+            self.file_submit()
+            return {}
+        return self.kernel_submit()
 
 
 __all__ = ['Download', 'Submit']

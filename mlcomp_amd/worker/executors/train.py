@@ -151,14 +151,37 @@ class Train(Executor):
         os.environ['MASTER_PORT'] = str(info['master_port'])
         os.environ['WORLD_SIZE'] = str(info['world_size'])
         os.environ['RANK'] = str(info['rank'])
-        os.environ['LOCAL_RANK'] = '0'
+        # with distr_info.visible_gpus the rank sees its job's GPUs on this computer and
+        # local_rank indexes them (`catalyst_.py:214-236` saw one GPU and used LOCAL_RANK=0)
+        local = int(info.get('local_rank', 0)) if info.get('visible_gpus') is not None else 0
+        os.environ['LOCAL_RANK'] = str(local)
         cuda = torch.cuda.is_available()
         if cuda:
-            torch.cuda.set_device(0)
+            torch.cuda.set_device(local)
+            from mlcomp_amd.parallel.comm import enable_transport_log
+            enable_transport_log(os.getcwd())
         import torch.distributed as dist
         dist.init_process_group('nccl' if cuda else 'gloo', init_method='env://',
                                 world_size=int(info['world_size']), rank=int(info['rank']))
         self.master = info['rank'] == 0
+
+    def _log_transports(self, runner):
+        """Which RCCL transport this rank's connections use (P2P = xGMI; SHM / NET inside
+        one computer means the peers were not reachable directly)."""
+        from mlcomp_amd.parallel import comm as C
+        ns = runner.native_step
+        cm = getattr(ns, 'comm', None) if ns is not None else None
+        tr = cm.transports_now() if isinstance(cm, C.RcclComm) else C._read_transport_log()
+        if not tr:
+            return
+        msg = 'RCCL transports of rank {}: {}'.format(self.distr_info.get('rank'),
+                                                     ', '.join(f'{k} x{v}' for k, v in sorted(tr.items())))
+        single = len({self.distr_info.get('master_computer')}) == 1 and self.distr_info.get('master_addr') in (
+            '127.0.0.1', 'localhost')
+        if single and any(not k.startswith('P2P') for k in tr):
+            self.warning(msg + ' - intra-node traffic is not on xGMI P2P', db=True)
+        else:
+            self.info(msg, db=True)
 
     def fix_memory(self, experiment):
         if not torch.cuda.is_available():
@@ -250,13 +273,16 @@ class Train(Executor):
         extra = {'mlcomp_db': DbCallback(self)} if self.master else {}
         rank = int(self.distr_info.get('rank', 0))
         world = int(self.distr_info.get('world_size', 1))
-        device = torch.device('cuda', 0) if torch.cuda.is_available() else torch.device('cpu')
+        device = torch.device('cuda', torch.cuda.current_device()) if torch.cuda.is_available() \
+            else torch.device('cpu')
         runner = Runner(experiment, device=device, extra_callbacks=extra, rank=rank, world_size=world)
         if self.resume_path:
             # full state (weights, optimizer, LR schedule, best score), applied when the
             # first remaining stage starts
             runner.resume(self.resume_path)
         runner.run_experiment(stages, start_epoch=start_epoch)
+        if self.distr_info and torch.cuda.is_available():
+            self._log_transports(runner)
         if self.master and self.trace:
             model = runner.model.eval().cpu().float()
             # one real input of the last stage (channels / size as the data has them)

@@ -75,8 +75,12 @@ class ExecuteBuilder:
         self.worker_index = s.WORKER_INDEX
         self.queue_personal = queue_name(hostname(), s.DOCKER_IMG, self.worker_index)
         inherited = os.environ.get('HIP_VISIBLE_DEVICES') or os.environ.get('CUDA_VISIBLE_DEVICES', '')
-        if self.task.gpu_assigned is not None or inherited:
-            vis = map_visible_devices(self.task.gpu_assigned or '', inherited)
+        # a DDP rank sees every GPU of its job on this computer (distr_info.visible_gpus) and
+        # selects its own by local_rank, so RCCL can connect the ranks peer-to-peer over xGMI
+        di = (yaml_load(self.task.additional_info) or {}).get('distr_info') or {}
+        assigned = di.get('visible_gpus') if di.get('visible_gpus') is not None else self.task.gpu_assigned
+        if assigned is not None or inherited:
+            vis = map_visible_devices(assigned or '', inherited)
             env = {'HIP_VISIBLE_DEVICES': vis, 'CUDA_VISIBLE_DEVICES': vis}
         else:
             env = {}

@@ -107,3 +107,24 @@ def test_fused_attention_reference_matches_unfused_path(p):
     o.backward(dctx.float())
     assert (ctx.float() - o).abs().max().item() < 2e-2
     assert _cos(dqkv, x.grad) > 0.999
+
+
+def test_native_bert_predict_matches_torch_eval():
+    """Native validation forward: no dropout, any batch size, no loss accumulators."""
+    torch.manual_seed(0)
+    tm = build_model('bert-tiny', num_classes=3, hidden_dropout=0.1, attention_dropout=0.1)
+    ref = build_model('bert-tiny', num_classes=3, hidden_dropout=0.1, attention_dropout=0.1)
+    ref.load_state_dict(tm.state_dict())
+    ref.eval()
+    net = NativeBert(tm, 'cpu', 4, 16)
+    net.ctx.ws.zero()
+    ids = torch.randint(0, 1024, (5, 16))
+    tt = torch.zeros(5, 16, dtype=torch.long)
+    am = torch.ones(5, 16, dtype=torch.long)
+    am[1, 12:] = 0
+    logits = net.predict(ids, tt, ref.key_bias(am))
+    with torch.no_grad():
+        want = ref(ids, tt, am).float()
+    assert logits.shape == (5, 3)
+    assert _cos(logits, want) > 0.999 and (logits - want).abs().max() < 0.05
+    assert net.loss_sum().item() == 0 and net.ctx.training and net.B == 4

@@ -22,16 +22,19 @@ def _free_port():
 
 
 @contextlib.contextmanager
-def _broker_daemon(sanitize, tmp_path):
+def _broker_daemon(sanitize, tmp_path, journal=None, port=None):
     """Run the broker daemon; with ``sanitize='asan'`` the AddressSanitizer + UBSan build:
     the test's traffic runs against it, then it is stopped with SIGTERM (clean shutdown
     through its destructors, so LeakSanitizer runs) and must exit 0 with no report."""
     from mlcomp_amd.build import build_broker
     binary = build_broker(sanitize=sanitize)
-    port = _free_port()
-    err = open(tmp_path / f'broker-{sanitize or "plain"}.err', 'w+')
-    p = subprocess.Popen([binary, '--host', '127.0.0.1', '--port', str(port)], stdout=subprocess.PIPE, stderr=err)
-    p.stdout.readline()
+    port = port or _free_port()
+    err = open(tmp_path / f'broker-{sanitize or "plain"}.err', 'a+')
+    extra = ['--journal', str(journal)] if journal else []
+    p = subprocess.Popen([binary, '--host', '127.0.0.1', '--port', str(port)] + extra, stdout=subprocess.PIPE,
+                         stderr=err)
+    while not p.stdout.readline().startswith(b'mlcomp-broker listening'):
+        pass
     try:
         yield port
     finally:
@@ -77,7 +80,10 @@ def test_fifo_ack_revoke_results(broker_factory):
     assert b.revoke('999999') is False
     q, m = b.pop(['q0', 'q1'], 0.5)
     assert q == 'q1' and m['args'] == [0] and m['id'] == ids[0]
-    b.ack(m['id'])
+    assert b.has(m['id']) and b.has(ids[2]) and not b.has(ids[1])   # leased / queued / revoked
+    assert b.ack(m['id']) is True
+    assert not b.has(m['id'])
+    assert b.ack(m['id']) is False        # no lease any more
     q, m = b.pop(['q1'], 0.5)
     assert m['args'] == [2]
     b.nack(m['id'])                       # back to the head
@@ -181,3 +187,51 @@ def test_client_does_not_resend_non_idempotent_push(daemon):
         c.push('once', {'task': 'y'})
     time.sleep(0.1)
     assert BrokerClient('127.0.0.1', daemon).queue_len('once') == 1
+
+
+def test_half_closed_client_gets_every_reply(daemon):
+    """A large pipelined batch followed by shutdown(SHUT_WR): every reply arrives (the
+    socket buffer fills, so the broker must keep writing after EOF), and a blocking POP
+    sent last is answered when a message arrives, then the connection closes."""
+    n = 20000
+    s = socket.create_connection(('127.0.0.1', daemon))
+    s.sendall(b''.join(b'PUSH big {"task":"x","pad":"%s"}\n' % (b'y' * 200) for _ in range(n))
+              + b'POP 5000 halfwait\n')
+    s.shutdown(socket.SHUT_WR)
+    time.sleep(0.3)
+    other = BrokerClient('127.0.0.1', daemon)
+    other.push('halfwait', {'task': 'late'})
+    f = s.makefile('rb')
+    lines = f.read().splitlines()
+    s.close()
+    assert len(lines) == n + 1 and all(x.startswith(b'OK ') for x in lines[:n])
+    assert lines[-1].startswith(b'MSG halfwait')
+    # the lease died with the closed connection: the message is queued again
+    deadline = time.time() + 2
+    while other.queue_len('halfwait') == 0 and time.time() < deadline:
+        time.sleep(0.02)
+    assert other.queue_len('halfwait') == 1 and other.queue_len('big') == n
+
+
+def test_journal_survives_broker_restart(tmp_path):
+    """--journal: pushed-but-unacked messages (queued or leased) come back after the
+    broker process is killed; acked and revoked ones do not; ids keep growing."""
+    j = tmp_path / 'broker.journal'
+    port = _free_port()
+    with _broker_daemon(None, tmp_path, journal=j, port=port):
+        c = BrokerClient('127.0.0.1', port)
+        ids = [c.push('jq', {'task': 'execute', 'args': [i]}) for i in range(4)]
+        c.revoke(ids[1])
+        _, m = c.pop(['jq'], 1.0)
+        assert c.ack(m['id'])                  # 0 done
+        _, leased = c.pop(['jq'], 1.0)         # 2 leased when the broker goes down
+        c.close()
+    with _broker_daemon('asan', tmp_path, journal=j, port=port):
+        c = BrokerClient('127.0.0.1', port)
+        assert c.queue_len('jq') == 2
+        assert c.has(ids[2]) and c.has(ids[3]) and not c.has(ids[0]) and not c.has(ids[1])
+        got = [c.pop(['jq'], 1.0)[1]['args'] for _ in range(2)]
+        assert got == [[2], [3]]
+        new = c.push('jq', {'task': 'z'})
+        assert int(new) > int(ids[-1])
+        c.close()

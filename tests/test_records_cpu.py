@@ -73,11 +73,25 @@ def test_eval_centre_crop_matches_numpy(rec):
     L = RecordLoader(path, 7, out_size=16, train=False, layout='nchw', device='cpu', mean=(0, 0, 0),
                      std=(1 / 255,) * 3)
     batches = _all(L)
-    assert len(L) == len(batches) == 9                   # no drop_last: last batch wraps around
+    assert len(L) == len(batches) == 9                   # no drop_last: a short last batch
     x, y = batches[0]
     assert y.tolist() == labs[:7]
     ref = torch.from_numpy(imgs[:7, 2:18, 4:20]).permute(0, 3, 1, 2).float()
     assert torch.equal(x, ref)
+    # the wrap-around rows of the last batch are dropped: every sample counted exactly once
+    assert [b[1].shape[0] for b in batches] == [7] * 8 + [4]
+    assert torch.cat([b[1] for b in batches]).tolist() == labs
+
+
+def test_new_epoch_closes_live_iterator(rec):
+    path, _, labs = rec
+    L = RecordLoader(path, 8, out_size=16, device='cpu', train=False, layout='nchw')
+    it = iter(L)
+    next(it)                                   # a slot is in use by this iterator
+    full = _all(L)                             # a second epoch starts while `it` is alive
+    assert torch.cat([y for _, y in full]).tolist() == labs
+    with pytest.raises(StopIteration):         # the first iterator was closed
+        next(it)
 
 
 def test_augment_reference_layouts():

@@ -137,3 +137,29 @@ def test_native_unet_four_classes_matches_torch():
         step()
         losses.append(step.last_loss())
     assert all(v == v for v in losses)
+
+
+def test_native_unet_predict_matches_torch_eval():
+    """Native validation forward (inference BN, fused head logits + loss) == torch eval."""
+    torch.manual_seed(0)
+    tm = Unet(encoder_name='resnet18', classes=2)
+    with torch.no_grad():
+        for m in tm.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 1.5)
+    ref = Unet(encoder_name='resnet18', classes=2)
+    ref.load_state_dict(tm.state_dict())
+    ref.eval()
+    step = NativeSegmentationStep(torch_model=tm, batch=2, image_size=64, device='cpu', use_graph=False,
+                                  bce_w=0.5, dice_w=2.0)
+    x = torch.randn(3, 3, 64, 64)          # an eval batch of another size than the train batch
+    t = (torch.rand(3, 2, 64, 64) > 0.5).float()
+    logits, loss = step.net.predict(Fn.nchw_to_nhwc(x, pad_to=8), t)
+    with torch.no_grad():
+        want = ref(x.to(torch.bfloat16).float())
+    assert logits.shape == want.shape == (3, 2, 64, 64)
+    assert _cos(logits, want) > 0.999
+    ref_loss = BCEDiceLoss(bce_weight=0.5, dice_weight=2.0)(logits, t)
+    assert abs(loss.item() - ref_loss.item()) < 1e-4
+    assert step.net.ctx.training           # predict restores the training mode
