@@ -138,9 +138,31 @@ def token(data):
 # ---------------------------------------------------------------------------- computers
 @route('computers')
 def computers(data):
+    """Computers with current usage, dockers and ``usage_history`` since
+    ``usage_min_time`` (default: the last day) in the reference's shape
+    {time: [...], mean: [{name: cpu|memory|disk|gpu_<i>, value: [...]}]}
+    (`mlcomp/db/providers/computer.py:71-103`), thinned to at most 300 points."""
+    import datetime
+    from mlcomp_amd.db.providers import parse_time
     o = _opts(data, 'name')
     o.sort_column = 'name'
-    return ComputerProvider(ctx().read).get(data, o)
+    data = data if isinstance(data, dict) else {}
+    cp = ComputerProvider(ctx().read)
+    res = cp.get(data, o)
+    since = parse_time(data['usage_min_time']) if data.get('usage_min_time') else now() - datetime.timedelta(days=1)
+    for item in res['data']:
+        rows = cp.usage_history(item['name'], since)
+        step = max(1, len(rows) // 300)
+        rows = rows[::step]
+        mean = OrderedDict((k, []) for k in ('cpu', 'memory', 'disk'))
+        for r in rows:
+            for k in ('cpu', 'memory', 'disk'):
+                mean[k].append(r.get(k))
+            for i, g in enumerate(r.get('gpu') or []):
+                mean.setdefault(f'gpu_{i}', []).append(g.get('load'))
+        item['usage_history'] = {'time': [r['time'] for r in rows],
+                                 'mean': [{'name': k, 'value': v} for k, v in mean.items()]}
+    return res
 
 
 @route('computer_sync_start')

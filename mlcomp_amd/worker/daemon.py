@@ -218,8 +218,13 @@ class WorkerSupervisor:
         cp.current_usage(self.name, u)
         DockerProvider(self.session).heartbeat(self.name, s.DOCKER_IMG)
         if len(self._usage) >= 6:
-            mean = {k: sum(x[k] for x in self._usage) / len(self._usage) for k in ('cpu', 'memory', 'disk')}
-            mean['gpu'] = u['gpu']
+            n = len(self._usage)
+            mean = {k: sum(x[k] for x in self._usage) / n for k in ('cpu', 'memory', 'disk')}
+            # per-GPU load / memory averaged over the window like the host counters
+            mean['gpu'] = [{'index': g.get('index', i),
+                            **{k: sum((x['gpu'][i].get(k) or 0) for x in self._usage if i < len(x['gpu'])) / n
+                               for k in ('load', 'memory') if k in g}}
+                           for i, g in enumerate(u['gpu'])]
             cp.add_usage(self.name, mean)
             self._usage = []
 

@@ -1,0 +1,135 @@
+"""Whole-network gradient checks on the GPU (verdict r2 #5): the native training steps of
+the full-depth ResNet-50 and of the U-Net with a ResNet-34 encoder against fp32 PyTorch
+autograd of the same model on the same weights and batch, on EVERY parameter.
+
+The native path keeps activations in bf16 between kernels, so it cannot match fp32
+exactly; the bar is stock mixed precision: for each parameter the relative error
+||g_native - g_fp32|| / ||g_fp32|| must stay within 2x (+0.01) of what torch bf16
+autocast of the same model reaches on the same batch, and under an absolute cap.  The
+per-parameter table is printed (pytest -s) for the record."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mlcomp_amd.ops import functional as Fn
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _rel(a, b):
+    a, b = a.float().flatten(), b.float().flatten()
+    return ((a - b).norm() / (b.norm() + 1e-20)).item()
+
+
+def _pairs(net, tm):
+    """(name, native gradient in torch layout, torch parameter of ``tm``) for every trained
+    parameter of a native ResNet / U-Net."""
+    names = {id(p): n for n, p in tm.named_parameters()}
+    out = []
+    for u in net._units():
+        conv, bn = u._src
+        g = u.w.grad
+        if u.s2d:
+            g = Fn.stem_w_from_s2d(g, u.cin)
+        else:
+            g = g[..., :u.cin].permute(0, 3, 1, 2)
+        out.append((names[id(conv.weight)], g, conv.weight))
+        out.append((names[id(bn.weight)], u.gamma.grad, bn.weight))
+        out.append((names[id(bn.bias)], u.beta.grad, bn.bias))
+    h = net.head
+    if hasattr(h, 'fc'):
+        out.append((names[id(h.fc.weight)], h.w.grad[:h.O], h.fc.weight))
+        out.append((names[id(h.fc.bias)], h.b.grad[:h.O], h.fc.bias))
+    else:
+        out.append((names[id(h.conv.weight)], h.w.grad.reshape(h.conv.weight.shape), h.conv.weight))
+        out.append((names[id(h.conv.bias)], h.b.grad, h.conv.bias))
+    assert len({n for n, _, _ in out}) == len(out) == sum(1 for _ in tm.parameters()), 'a parameter is unmapped'
+    return out
+
+
+def _torch_grads(model, x, loss_fn, amp):
+    model.zero_grad(set_to_none=True)
+    model.train()
+    with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp):
+        out = model(x)
+    loss = loss_fn(out.float())
+    loss.backward()
+    return loss.item(), {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+
+
+def _check(pairs, ref_g, amp_g, label, cap):
+    rows, bad = [], []
+    for name, g, _ in pairs:
+        e_nat, e_amp = _rel(g, ref_g[name]), _rel(amp_g[name], ref_g[name])
+        rows.append((name, e_nat, e_amp))
+        if not (e_nat <= 2 * e_amp + 0.01 and e_nat < cap):
+            bad.append((name, round(e_nat, 4), round(e_amp, 4)))
+    print(f'\n{label}: {len(rows)} parameters, relative gradient error native / torch-bf16-autocast vs fp32')
+    for name, a, b in sorted(rows, key=lambda r: -r[1])[:12]:
+        print(f'  {a:8.4f} {b:8.4f}  {name}')
+    med = sorted(r[1] for r in rows)[len(rows) // 2]
+    print(f'  median native {med:.4f}, median autocast {sorted(r[2] for r in rows)[len(rows) // 2]:.4f}')
+    assert not bad, bad
+    return med
+
+
+def _randomize_bn(m):
+    """A well-conditioned random network: BN gammas ~U(0.5, 1) and betas ~U(-0.1, 0.1), but
+    small gammas (~U(0.1, 0.2)) on the BN that closes each residual branch - the residual
+    stream then grows slowly with depth, as after the zero-gamma init that fresh ResNets
+    use.  (Gammas ~1 on every branch of a random ResNet-50 make the fp32 gradients
+    themselves chaotic: torch's own bf16 autocast then lands 100 %+ off on every tensor.)"""
+    from mlcomp_amd.models.resnet import BasicBlock, Bottleneck
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.weight.uniform_(0.5, 1.0)
+                mod.bias.uniform_(-0.1, 0.1)
+        for mod in m.modules():
+            last = mod.cb3 if isinstance(mod, Bottleneck) else mod.cb2 if isinstance(mod, BasicBlock) else None
+            if last is not None:
+                last.bn.weight.uniform_(0.1, 0.2)
+
+
+def test_resnet50_native_gradients_match_fp32_autograd():
+    from mlcomp_amd.models import build_model
+    from mlcomp_amd.train.native_step import NativeClassifierStep
+    torch.manual_seed(0)
+    tm = build_model('resnet50', num_classes=16)
+    _randomize_bn(tm)
+    ref = copy.deepcopy(tm).to(DEV)
+    step = NativeClassifierStep(torch_model=tm, batch=16, image_size=128, device=DEV, num_classes=16, lr=0.0,
+                                momentum=0.0, weight_decay=0.0, use_graph=False)
+    x = Fn.stem_s2d_to_nhwc(step.x).permute(0, 3, 1, 2).float().contiguous()
+    y = step.y
+    step()
+    torch.cuda.synchronize()
+    loss_fp32, ref_g = _torch_grads(ref, x, lambda o: F.cross_entropy(o, y), amp=False)
+    _, amp_g = _torch_grads(ref, x, lambda o: F.cross_entropy(o, y), amp=True)
+    assert abs(step.last_loss() - loss_fp32) / loss_fp32 < 0.02
+    med = _check(_pairs(step.net, tm), ref_g, amp_g, 'ResNet-50', cap=0.25)
+    assert med < 0.05
+
+
+def test_unet_resnet34_native_gradients_match_fp32_autograd():
+    from mlcomp_amd.contrib.criterion import BCEDiceLoss
+    from mlcomp_amd.contrib.segmentation.models import Unet
+    from mlcomp_amd.train.native_seg_step import NativeSegmentationStep
+    torch.manual_seed(0)
+    tm = Unet(encoder_name='resnet34', classes=1)
+    _randomize_bn(tm)
+    ref = copy.deepcopy(tm).to(DEV)
+    step = NativeSegmentationStep(torch_model=tm, batch=4, image_size=128, device=DEV, lr=0.0, use_graph=False)
+    x = Fn.stem_s2d_to_nhwc(step.x).permute(0, 3, 1, 2).float().contiguous()
+    t = step.t.view(4, 128, 128, 1).permute(0, 3, 1, 2).contiguous()
+    step()
+    torch.cuda.synchronize()
+    crit = BCEDiceLoss()
+    loss_fp32, ref_g = _torch_grads(ref, x, lambda o: crit(o, t), amp=False)
+    _, amp_g = _torch_grads(ref, x, lambda o: crit(o, t), amp=True)
+    assert abs(step.last_loss() - loss_fp32) / loss_fp32 < 0.02
+    med = _check(_pairs(step.net, tm), ref_g, amp_g, 'U-Net (ResNet-34)', cap=0.25)
+    assert med < 0.05
