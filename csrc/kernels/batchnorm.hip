@@ -115,7 +115,7 @@ constexpr int NSTAT = 32;
 
 __global__ void __launch_bounds__(NT)
 bn_bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const bf16* __restrict__ y,
-                     const float* __restrict__ mean, float* __restrict__ sums, long rows, int C) {
+                     const float* __restrict__ mean, float* __restrict__ sums, long rows, int C, int ncopy) {
   __shared__ float red[2][NT][9];
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
@@ -162,7 +162,7 @@ bn_bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, co
   __syncthreads();
   const int lanes = NT < G ? NT : G;  // distinct groups present in this block
   const int base_cg = (int)(((long)blockIdx.x * NT) % G);
-  float* dst = sums + (size_t)(blockIdx.x % NSTAT) * 2 * C;
+  float* dst = sums + (size_t)(blockIdx.x % ncopy) * 2 * C;
   if (t < lanes) {
     float a[8], b[8];
 #pragma unroll
@@ -186,12 +186,12 @@ bn_bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, co
 __global__ void __launch_bounds__(NT)
 bn_bwd_finalize_kernel(const float* __restrict__ sums, const float* __restrict__ invstd,
                        const float* __restrict__ gamma, float* __restrict__ coef,
-                       float* __restrict__ dgamma, float* __restrict__ dbeta, long rows, int C) {
+                       float* __restrict__ dgamma, float* __restrict__ dbeta, long rows, int C, int ncopy) {
   const int c = blockIdx.x * (NT / FL) + (threadIdx.x / FL), q = threadIdx.x % FL;
   float S1 = 0.f, S2 = 0.f;
   if (c < C) {
-#pragma unroll
-    for (int k = q; k < NSTAT; k += FL) {
+#pragma unroll 4
+    for (int k = q; k < ncopy; k += FL) {
       S1 += sums[(size_t)k * 2 * C + c];
       S2 += sums[(size_t)k * 2 * C + C + c];
     }
@@ -289,6 +289,19 @@ bool shape_ok(int C) {
 
 }  // namespace
 
+int g_mlc_ncopy = NSTAT;
+int g_mlc_det = 0;
+
+// deterministic mode on/off; ncopy = partial-sum copies of every reduction (>= NSTAT;
+// deterministic mode needs at least one per contributing block, the launchers check)
+MLC_EXPORT int mlc_set_deterministic(int det, int ncopy) {
+  g_mlc_det = det ? 1 : 0;
+  g_mlc_ncopy = ncopy >= NSTAT ? ncopy : NSTAT;
+  return 0;
+}
+MLC_EXPORT int mlc_get_stat_copies() { return g_mlc_ncopy; }
+MLC_EXPORT int mlc_get_deterministic() { return g_mlc_det; }
+
 MLC_EXPORT int mlc_bn_finalize(const float* sum, const float* sumsq, int ncopy, const float* gamma,
                                const float* beta, float* save_mean, float* save_invstd, float* scale,
                                float* shift, float* run_mean, float* run_var, long rows, int C,
@@ -321,7 +334,7 @@ MLC_EXPORT int mlc_bn_fwd_apply(const bf16* y, const bf16* res, bf16* z, const f
   return mlc_bn_fwd_apply2(y, res, z, scale, shift, nullptr, nullptr, rows, C, relu, st);
 }
 
-// sums must hold NSTAT*2*C floats, zeroed by the caller
+// sums must hold ncopy*2*C floats (mlc_get_stat_copies), zeroed by the caller
 MLC_EXPORT int mlc_bn_bwd_reduce(const bf16* dz, const bf16* z, const bf16* y, const float* mean,
                                  float* sums, long rows, int C, hipStream_t st) {
   if (!shape_ok(C)) return -1;
@@ -335,8 +348,9 @@ MLC_EXPORT int mlc_bn_bwd_reduce(const bf16* dz, const bf16* z, const bf16* y, c
     if (G > NT) cap = ((cap + G / NT - 1) / (G / NT)) * (G / NT);
     if (blocks > cap) blocks = cap;
   }
+  if (g_mlc_det && blocks > g_mlc_ncopy) return -2;   // a copy per block or not deterministic
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(NT), 0, st, dz, z, y,
-                     mean, sums, rows, C);
+                     mean, sums, rows, C, g_mlc_ncopy);
   return hipGetLastError();
 }
 
@@ -345,7 +359,7 @@ MLC_EXPORT int mlc_bn_bwd_finalize(const float* sums, const float* invstd, const
                                    float* coef, float* dgamma, float* dbeta, long rows, int C,
                                    hipStream_t st) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + NT / FL - 1) / (NT / FL)), dim3(NT), 0, st, sums, invstd,
-                     gamma, coef, dgamma, dbeta, rows, C);
+                     gamma, coef, dgamma, dbeta, rows, C, g_mlc_ncopy);
   return hipGetLastError();
 }
 

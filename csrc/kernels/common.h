@@ -15,6 +15,17 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define MLC_EXPORT extern "C" __attribute__((visibility("default")))
 
+// Per-channel / per-column reductions (BN statistics in the conv epilogue, BN and LN
+// backward sums, bias column sums) add each block's partial into copy (block % ncopy) of
+// a [ncopy][...] scratch and a finalize kernel folds the copies in a fixed order.  The
+// default ncopy = 32 spreads the same-address float atomics.  Deterministic mode
+// (mlc_set_deterministic, MLC_DETERMINISTIC=1) raises ncopy so that every contributing
+// block owns its copy - one add onto zero, exact and order-free - and runs split-K
+// GEMMs unsplit (one atomic contribution per output element) or through fp32 slabs.
+// Host-side state, defined in batchnorm.hip; launchers pass ncopy to their kernels.
+extern int g_mlc_ncopy;
+extern int g_mlc_det;
+
 static __device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
 static __device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }
 

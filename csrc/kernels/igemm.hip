@@ -212,17 +212,32 @@ struct MatMCSum {
       for (int e = 0; e < 8; ++e) st.s[e] += f[e];
     }
   }
-  __device__ void finish(St& st, bool owner, int tid) const {
-    const int lane = tid & 63;
+  // the 4 waves' partial sums of a column are combined in a fixed order through LDS and
+  // added with ONE atomic per column per block (with one K-split that single add onto
+  // the zeroed gradient is exact, so deterministic mode gets reproducible bias grads)
+  __device__ void finish(St& st, bool owner, int tid, char* lds) const {
+    const int lane = tid & 63, wave = tid >> 6;
 #pragma unroll
     for (int o = R / 8; o < 64; o <<= 1)
 #pragma unroll
       for (int e = 0; e < 8; ++e) st.s[e] += __shfl_xor(st.s[e], o, 64);
-    const int c = st.b.n0 + 8 * (tid % (R / 8));
-    if (owner && lane < R / 8 && c < cols) {
+    float* red = reinterpret_cast<float*>(lds);   // [NTHR/64 waves][R/8 lanes][8]
+    if (owner && lane < R / 8) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) atomicAdd(colsum + c + e, st.s[e]);
+      for (int e = 0; e < 8; ++e) red[(wave * (R / 8) + lane) * 8 + e] = st.s[e];
     }
+    __syncthreads();
+    const int c = st.b.n0 + 8 * lane;
+    if (owner && wave == 0 && lane < R / 8 && c < cols) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float a = 0.f;
+#pragma unroll
+        for (int w = 0; w < NTHR / 64; ++w) a += red[(w * (R / 8) + lane) * 8 + e];
+        atomicAdd(colsum + c + e, a);
+      }
+    }
+    __syncthreads();   // the epilogue reuses the LDS
   }
 };
 template <class L, class = void> struct HasSum { static constexpr bool value = false; };
@@ -623,6 +638,7 @@ struct BnBwdEpi {
   const bf16* y1 = nullptr; const float* mean1 = nullptr; float* sums1 = nullptr;
   const float* msc0 = nullptr; const float* msh0 = nullptr;
   const float* msc1 = nullptr; const float* msh1 = nullptr;
+  int ncopy = NSTAT;   // copies of sums0/sums1 (g_mlc_ncopy at launch)
 };
 
 template <class RowMap = IdentityRows, bool kDense = false>
@@ -632,12 +648,13 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
   // dense-layer extras: out = act(acc + bias) (pre-activation stored to preact), or
   // out = acc * act'(dact) for the backward of an activation (act 1 = exact-erf GELU)
   const float* bias = nullptr; int act = 0; bf16* preact = nullptr; const bf16* dact = nullptr;
+  int ncopy = NSTAT;   // copies of sum / sumsq (g_mlc_ncopy at launch)
   template <int BM, int BN, int MI, int NI>
   __device__ void apply(f32x16 (&acc)[MI][NI], char* lds, int m0, int n0, int M, int N,
                         int wm, int wn, int lane, int tid) const {
     if (sum) {
       // copy slot spreads the per-channel atomics of different blocks over NSTAT rows
-      const int slot = ((m0 / 64) + wm) & (NSTAT - 1);
+      const int slot = (int)((unsigned)((m0 / 64) + wm) % (unsigned)ncopy);
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         float s1 = 0.f, s2 = 0.f;
@@ -827,7 +844,7 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
           a += q[e]; b += q[8 + e]; d += q[16 + e];
         }
         if (n < N) {
-          const int slot = (m0 / BM) & (NSTAT - 1);
+          const int slot = (int)((unsigned)(m0 / BM) % (unsigned)bn.ncopy);
           float* d0 = bn.sums0 + (size_t)slot * 2 * N;
           atomicAdd(d0 + n, a);
           atomicAdd(d0 + N + n, b);
@@ -1204,7 +1221,7 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
       }
     }
   }
-  if constexpr (HasSum<LA>::value) la.finish(sa, tn == 0, tid);
+  if constexpr (HasSum<LA>::value) la.finish(sa, tn == 0, tid, smem);
   epi.template apply<BM, BN, MI, NI>(acc, smem, m0, n0, M, N, wm, wn, lane, tid);
 }
 
@@ -1381,6 +1398,8 @@ MLC_EXPORT int mlc_conv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, f
   const int M = N * Ho * Wo, K = KH * KW * C;
   const int tile = pick_tile(M, Co);
   EpiBF16<> epi{y, Co, sum, sumsq, IdentityRows{}};
+  epi.ncopy = g_mlc_ncopy;
+  if (sum && g_mlc_det && (M + 63) / 64 > g_mlc_ncopy) return -2;   // one copy per 64-row group
   const BnIn bn{in_sc, in_sh};
 #define MKB(R) (MatKC<R>{w, K, Co, K})
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
@@ -1424,7 +1443,8 @@ MLC_EXPORT int mlc_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, const bf1
   if (C % 8 || Co % 8 || KH > 15 || KW > 16 || stride < 1) return -1;
   const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
   BnBwdEpi bn{bn_mask, bn_y0, bn_mean0, bn_sums0, bn_y1, bn_mean1, bn_sums1,
-              bn_msc0, bn_msh0, bn_msc1, bn_msh1};
+              bn_msc0, bn_msh0, bn_msc1, bn_msh1, g_mlc_ncopy};
+  if (bn_y0 && g_mlc_det && ((long)N * H * W + 63) / 64 > g_mlc_ncopy) return -2;
   if (bn_msc0 && (!bn_msh0 || !bn_y0 || (bn_msc1 && (!bn_msh1 || !bn_y1)))) return -1;
   if (bn_y0 && (!bn_mean0 || !bn_sums0 || (bn_y1 && (!bn_mean1 || !bn_sums1)))) return -1;
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
@@ -1477,7 +1497,8 @@ MLC_EXPORT int mlc_conv_dgrad_t(const bf16* dy, const bf16* wt, bf16* dx, const 
   if (bn_msc0 && (!bn_msh0 || !bn_y0 || (bn_msc1 && (!bn_msh1 || !bn_y1)))) return -1;
   if (bn_y0 && (!bn_mean0 || !bn_sums0 || (bn_y1 && (!bn_mean1 || !bn_sums1)))) return -1;
   BnBwdEpi bn{bn_mask, bn_y0, bn_mean0, bn_sums0, bn_y1, bn_mean1, bn_sums1,
-              bn_msc0, bn_msh0, bn_msc1, bn_msh1};
+              bn_msc0, bn_msh0, bn_msc1, bn_msh1, g_mlc_ncopy};
+  if (bn_y0 && g_mlc_det && ((long)N * H * W + 63) / 64 > g_mlc_ncopy) return -2;
   const int ph = dil * (KH - 1) - pad, pw = dil * (KW - 1) - pad;
   if (stride == 1 && ph >= 0 && ph == pw) {
     if (Ho != H + 2 * pad - dil * (KH - 1) || Wo != W + 2 * pad - dil * (KW - 1)) return -1;
@@ -1568,7 +1589,9 @@ MLC_EXPORT int mlc_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, i
   // slabs pay when the partial sums are large (>= 8 MB: atomics ~1.3 TB/s vs two plain
   // passes ~5 TB/s each) and the reduction has enough elements to fill the chip
   bool use_slab = false;
-  if (splits <= 0) {
+  if (g_mlc_det) {
+    splits = 1;   // one contribution per dw element: exact, order-free
+  } else if (splits <= 0) {
     const int ss = auto_splits(Co, KK, P, tile, g_split_target);
     use_slab = ws && slab >= (1u << 18) && (double)ss * slab * 4 >= 8e6 && (long)(ss * slab) <= ws_floats;
     splits = use_slab ? ss : auto_splits(Co, KK, P, tile, plain ? g_split_target_mat : g_split_target);
@@ -1666,6 +1689,7 @@ MLC_EXPORT int mlc_gemm_f32out(const bf16* A, const bf16* B, float* C, const flo
   const int tile = pick_tile(M, N);
   if (out_mode == 1) {
     if (splits <= 0) splits = auto_splits(M, N, K, tile, g_split_target_dense);
+    if (g_mlc_det) splits = 1;
     EpiF32Atomic epi{C, ldc};
     if (!ta && tb) MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_KC, GB_KC);
     if (!ta && !tb) MLC_TILE_DISPATCH(tile, M, N, K, splits, st, epi, GA_KC, GB_MC);
@@ -1690,6 +1714,7 @@ MLC_EXPORT int mlc_linear_wgrad_bias(const bf16* A, const bf16* B, float* C, flo
   if (K % 8 || lda % 8 || ldb % 8 || M % 8 || N % 8) return -1;
   const int tile = pick_tile(M, N);
   if (splits <= 0) splits = auto_splits(M, N, K, tile, g_split_target_dense);
+  if (g_mlc_det) splits = 1;   // one dW atomic and one bias column-sum add per element
   const size_t slab = (size_t)M * N;
 #define GA_MCS(R) (MatMCSum<R>{A, lda, K, M, dbias})
   if (ws && ldc == N && splits > 1 && (long)(splits * slab) <= ws_floats) {

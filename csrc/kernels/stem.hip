@@ -156,7 +156,7 @@ stem_pool_bwd_kernel(const bf16* __restrict__ dp, const uint8_t* __restrict__ id
                      const bf16* __restrict__ y, const float* __restrict__ mean,
                      const float* __restrict__ coef, float* __restrict__ sums, bf16* __restrict__ dy,
                      int H, int W, int C, int Ho, int Wo, int rows_total, int ROWS,
-                     int gshift) {
+                     int gshift, int ncopy) {
   const int G = C >> 3;
   const int cg = threadIdx.x & (G - 1);
   const int c0 = cg * 8;
@@ -213,7 +213,7 @@ stem_pool_bwd_kernel(const bf16* __restrict__ dp, const uint8_t* __restrict__ id
     float acc = 0.f;
 #pragma unroll
     for (int wv = 0; wv < NT / 64; ++wv) acc += red[wv][g][v];
-    float* dst = sums + (size_t)(blockIdx.x % NSTAT) * 2 * C;
+    float* dst = sums + (size_t)(blockIdx.x % ncopy) * 2 * C;
     atomicAdd(dst + (v < 8 ? 0 : C) + g * 8 + (v & 7), acc);
   }
 }
@@ -294,8 +294,10 @@ MLC_EXPORT int mlc_stem_pool_bwd_reduce(const bf16* dp, const uint8_t* idx, cons
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const int rows = N * H;
   const int blocks = (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
+  if (g_mlc_det && blocks > g_mlc_ncopy) return -2;
   hipLaunchKernelGGL(stem_pool_bwd_kernel<false>, dim3(blocks), dim3(NT), 0, st, dp, idx, y, mean,
-                     nullptr, sums, nullptr, H, W, C, Ho, Wo, rows, ROWS_PER_BLOCK, __builtin_ctz(C >> 3));
+                     nullptr, sums, nullptr, H, W, C, Ho, Wo, rows, ROWS_PER_BLOCK, __builtin_ctz(C >> 3),
+                     g_mlc_ncopy);
   return hipGetLastError();
 }
 
@@ -307,7 +309,7 @@ MLC_EXPORT int mlc_stem_pool_bwd_apply(const bf16* dp, const uint8_t* idx, const
   const int rows = N * H;
   const int blocks = (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
   hipLaunchKernelGGL(stem_pool_bwd_kernel<true>, dim3(blocks), dim3(NT), 0, st, dp, idx, y, mean, coef,
-                     nullptr, dy, H, W, C, Ho, Wo, rows, ROWS_PER_BLOCK, __builtin_ctz(C >> 3));
+                     nullptr, dy, H, W, C, Ho, Wo, rows, ROWS_PER_BLOCK, __builtin_ctz(C >> 3), g_mlc_ncopy);
   return hipGetLastError();
 }
 

@@ -125,7 +125,7 @@ ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ s, const flo
               const float* __restrict__ rstd_in, const float* __restrict__ gamma, bf16* __restrict__ ds,
               bf16* __restrict__ dr, float* __restrict__ sums, int T, int H, uint32_t thr_in, float inv_keep_in,
               uint32_t thr_out, float inv_keep_out, const uint32_t* __restrict__ seedp, uint32_t salt_in,
-              uint32_t salt_out) {
+              uint32_t salt_out, int ncopy) {
   __shared__ float red[NT / 64][2][64 * 4 * MAXC];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nch = H >> 2;
@@ -205,7 +205,7 @@ ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ s, const flo
       red[wave][1][col] = db[k][e];
     }
   __syncthreads();
-  float* dst = sums + (size_t)(blockIdx.x % NSTAT) * 2 * H;
+  float* dst = sums + (size_t)(blockIdx.x % ncopy) * 2 * H;
   for (int col = threadIdx.x; col < H; col += NT) {
     float x0 = 0.f, x1 = 0.f;
 #pragma unroll
@@ -217,11 +217,12 @@ ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ s, const flo
 
 // dgamma/dbeta from the NSTAT copies, accumulated into the grad arena slots
 __global__ void __launch_bounds__(NT)
-ln_bwd_finalize_kernel(const float* __restrict__ sums, float* __restrict__ dgamma, float* __restrict__ dbeta, int H) {
+ln_bwd_finalize_kernel(const float* __restrict__ sums, float* __restrict__ dgamma, float* __restrict__ dbeta, int H,
+                       int ncopy) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= H) return;
   float g = 0.f, b = 0.f;
-  for (int k = 0; k < NSTAT; ++k) { g += sums[(size_t)k * 2 * H + c]; b += sums[(size_t)k * 2 * H + H + c]; }
+  for (int k = 0; k < ncopy; ++k) { g += sums[(size_t)k * 2 * H + c]; b += sums[(size_t)k * 2 * H + H + c]; }
   dgamma[c] += g;
   dbeta[c] += b;
 }
@@ -329,7 +330,7 @@ softmax_bwd_kernel(const bf16* __restrict__ P, const bf16* __restrict__ dPd, bf1
 // them into copy (y % NSTAT) of scratch[NSTAT][C] (8 adds per address at most per
 // NSTAT blocks); colsum_finalize folds the copies into out (+=)
 __global__ void __launch_bounds__(NT)
-colsum_partial_kernel(const bf16* __restrict__ g, float* __restrict__ scratch, int R, int C, int RB) {
+colsum_partial_kernel(const bf16* __restrict__ g, float* __restrict__ scratch, int R, int C, int RB, int ncopy) {
   const int c8 = blockIdx.x * NT + threadIdx.x;
   if (c8 * 8 >= C) return;
   const int r0 = blockIdx.y * RB, r1 = min(R, r0 + RB);
@@ -340,17 +341,17 @@ colsum_partial_kernel(const bf16* __restrict__ g, float* __restrict__ scratch, i
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] += f[e];
   }
-  float* dst = scratch + (size_t)(blockIdx.y % NSTAT) * C + c8 * 8;
+  float* dst = scratch + (size_t)(blockIdx.y % ncopy) * C + c8 * 8;
 #pragma unroll
   for (int e = 0; e < 8; ++e) atomicAdd(dst + e, acc[e]);
 }
 
 __global__ void __launch_bounds__(NT)
-colsum_finalize_kernel(float* __restrict__ scratch, float* __restrict__ out, int C) {
+colsum_finalize_kernel(float* __restrict__ scratch, float* __restrict__ out, int C, int ncopy) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= C) return;
   float s = 0.f;
-  for (int k = 0; k < NSTAT; ++k) { s += scratch[(size_t)k * C + c]; scratch[(size_t)k * C + c] = 0.f; }
+  for (int k = 0; k < ncopy; ++k) { s += scratch[(size_t)k * C + c]; scratch[(size_t)k * C + c] = 0.f; }
   out[c] += s;
 }
 
@@ -728,13 +729,15 @@ MLC_EXPORT int mlc_ln_bwd(const bf16* dy, const bf16* s, const float* mean, cons
   // blocks, 7.83 at 512, 7.86 at 256
   int blocks = (T + NT / 64 - 1) / (NT / 64);
   if (blocks > 512) blocks = 512;
+  if (g_mlc_det && blocks > g_mlc_ncopy) return -2;
   int rc = pick_maxc(H, [&](auto mc) {
     hipLaunchKernelGGL((ln_bwd_kernel<decltype(mc)::value>), dim3(blocks), dim3(NT), 0, st, dy, s, mean, rstd, gamma,
-                       ds, dr, sums, T, H, ti, ki, to, ko, seed, salt_in, salt_out);
+                       ds, dr, sums, T, H, ti, ki, to, ko, seed, salt_in, salt_out, g_mlc_ncopy);
     return (int)hipGetLastError();
   });
   if (rc) return rc;
-  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((H + NT - 1) / NT), dim3(NT), 0, st, sums, dgamma, dbeta, H);
+  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((H + NT - 1) / NT), dim3(NT), 0, st, sums, dgamma, dbeta, H,
+                     g_mlc_ncopy);
   return hipGetLastError();
 }
 
@@ -773,8 +776,9 @@ MLC_EXPORT int mlc_colsum_acc(const bf16* g, float* out, float* scratch, int R, 
   int RB = (R * xb + 511) / 512;       // ~512 blocks
   if (RB < 16) RB = 16;
   dim3 grid(xb, (R + RB - 1) / RB);
-  hipLaunchKernelGGL(colsum_partial_kernel, grid, dim3(NT), 0, st, g, scratch, R, C, RB);
-  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, st, scratch, out, C);
+  if (g_mlc_det && (int)grid.y > g_mlc_ncopy) return -2;
+  hipLaunchKernelGGL(colsum_partial_kernel, grid, dim3(NT), 0, st, g, scratch, R, C, RB, g_mlc_ncopy);
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, st, scratch, out, C, g_mlc_ncopy);
   return hipGetLastError();
 }
 

@@ -27,6 +27,7 @@ import os
 
 import torch
 
+from mlcomp_amd.ops import _lib
 from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops import transformer as Tx
 from mlcomp_amd.ops.layers import NativeContext
@@ -244,9 +245,17 @@ class _EmbedFn(torch.autograd.Function):
         net.ln.mark()
         B, S = ids.shape
         d = ds.float().view(B, S, -1)
-        net.word.grad.index_add_(0, ids.reshape(-1), d.reshape(B * S, -1))
+        if _lib.DETERMINISTIC:
+            # index_add_ races float atomics on repeated ids (and the sort-based scatter
+            # orders ties arbitrarily): a one-hot GEMM sums every row in a fixed order
+            dd = d.reshape(B * S, -1)
+            for tbl, ix in ((net.word, ids), (net.tok_type, tt)):
+                oh = torch.nn.functional.one_hot(ix.reshape(-1), tbl.grad.shape[0]).to(dd.dtype)
+                tbl.grad.add_(oh.t() @ dd)
+        else:
+            net.word.grad.index_add_(0, ids.reshape(-1), d.reshape(B * S, -1))
+            net.tok_type.grad.index_add_(0, tt.reshape(-1), d.reshape(B * S, -1))
         net.pos.grad[:S].add_(d.sum(0))
-        net.tok_type.grad.index_add_(0, tt.reshape(-1), d.reshape(B * S, -1))
         for sl in (net.word, net.pos, net.tok_type):
             net.ctx.arena.mark_ready(sl)
         return None, None, None, None

@@ -16,6 +16,13 @@ import torch
 _LIB = None
 _LOCK = threading.Lock()
 
+# Deterministic mode (MLC_DETERMINISTIC=1): every reduction gets one partial-sum copy per
+# contributing block (MLC_DET_COPIES of them, default 4096) and split-K GEMMs run unsplit,
+# so no two float adds race and a step is bitwise reproducible (graph replay == eager).
+# Slower (no split-K) and heavier (bigger reduction scratch): a debugging / testing mode.
+DETERMINISTIC = os.environ.get('MLC_DETERMINISTIC', '0') == '1'
+DET_COPIES = int(os.environ.get('MLC_DET_COPIES', '4096'))
+
 vp, i32, i64, f32, u32 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_uint
 
 _SIGS = {
@@ -47,6 +54,9 @@ _SIGS = {
     'mlc_colsum_acc': [vp, vp, vp, i32, i32, vp],
     'mlc_dropout': [vp, vp, i64, f32, vp, u32, vp],
     'mlc_bn_stat_copies': [],
+    'mlc_set_deterministic': [i32, i32],
+    'mlc_get_stat_copies': [],
+    'mlc_get_deterministic': [],
     'mlc_gemm_config': [i32],
     'mlc_gemm_get_set': [i32, i32],
     'mlc_bn_get_set': [i32, i32],
@@ -116,6 +126,11 @@ def load():
         for key, env in ((0, 'MLC_BN_UNROLL'), (1, 'MLC_BN_BLOCKS')):   # BN elementwise passes
             if os.environ.get(env):
                 lib.mlc_bn_get_set(key, int(os.environ[env]))
+        if DETERMINISTIC:
+            lib.mlc_set_deterministic(1, DET_COPIES)
+            # torch's own scatter-adds (the BERT embedding gradients) take their
+            # deterministic (sort-based) implementations too
+            torch.use_deterministic_algorithms(True, warn_only=True)
         _LIB = lib
     return _LIB
 
@@ -136,6 +151,9 @@ def ptr(t):
 
 def call(name, *args):
     rc = getattr(load(), name)(*args)
+    if rc == -2 and DETERMINISTIC:
+        raise RuntimeError(f'{name}: deterministic mode needs more partial-sum copies than '
+                           f'MLC_DET_COPIES={DET_COPIES} (one per contributing block; raise it)')
     if rc != 0:
         raise RuntimeError(f'{name} failed (rc={rc}); check shape constraints '
                            f'(channels % 8 == 0) or HIP error')

@@ -285,7 +285,10 @@ def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride=1, pad=0, di
 
 
 # ---------------------------------------------------------------- batch norm
-NSTAT = 32  # == mlc_bn_stat_copies(): partial-sum copies written by the conv epilogue
+# partial-sum copies of the per-channel reductions (conv-epilogue BN statistics, BN / LN
+# backward sums, bias column sums): 32 (== mlc_bn_stat_copies()), or one per contributing
+# block in deterministic mode (_lib.DET_COPIES, see mlc_set_deterministic)
+NSTAT = _lib.DET_COPIES if _lib.DETERMINISTIC else 32
 
 
 def stat_buffers(C, device):

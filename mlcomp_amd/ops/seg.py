@@ -45,7 +45,7 @@ def seg_head_fwd(x, w, b, target, sums, logits=None):
     sum t) into ``sums`` [4]; writes logits [P, K] if given."""
     P, C = x.shape
     K = w.numel() // C
-    if _cuda(x):
+    if _cuda(x) and not _lib.DETERMINISTIC:     # the kernel's loss sums use float atomics
         _lib.call('mlc_seg_head_fwd', _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(target), _lib.ptr(logits),
                   _lib.ptr(sums), P, C, K, _lib.stream())
         return sums
@@ -70,7 +70,7 @@ def seg_head_bwd(x, w, b, target, sums, dw, db, bce_w=1.0, dice_w=1.0, eps=1e-7)
     """Returns dx [P, C] bf16; dw [K, C] / db [K] are ACCUMULATED (+=)."""
     P, C = x.shape
     K = w.numel() // C
-    if _cuda(x):
+    if _cuda(x) and not _lib.DETERMINISTIC:     # dw / db use float atomics
         dx = torch.empty_like(x)
         _lib.call('mlc_seg_head_bwd', _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(target), _lib.ptr(sums),
                   _lib.ptr(dx), _lib.ptr(dw), _lib.ptr(db), P, C, K, float(bce_w), float(dice_w), float(eps),

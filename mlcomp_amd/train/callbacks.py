@@ -44,7 +44,17 @@ class TimerCallback(Callback):
     = whole-node throughput), ``data_time``, ``model_time``, ``batch_time``."""
     order = 0
 
+    @staticmethod
+    def _sync(state):
+        # the step is asynchronous GPU work: bracket the loader with a device sync so the
+        # loader's wall time (and _fps) is the device's, not the launch queue's
+        dev = getattr(getattr(state, 'runner', None), 'device', None)
+        if dev is not None and dev.type == 'cuda':
+            import torch
+            torch.cuda.synchronize(dev)
+
     def on_loader_start(self, state):
+        self._sync(state)
         self.t_end = time.time()
         self.acc = {'data_time': 0.0, 'model_time': 0.0, 'batch_time': 0.0, 'n': 0, 'samples': 0}
 
@@ -62,6 +72,8 @@ class TimerCallback(Callback):
         self.t_end = now
 
     def on_loader_end(self, state):
+        self._sync(state)
+        self.acc['batch_time'] += time.time() - self.t_end   # the queued work drained by the sync
         n = max(1, self.acc['n'])
         for k in ('data_time', 'model_time', 'batch_time'):
             state.loader_metrics[f'_timer/{k}'] = self.acc[k] / n

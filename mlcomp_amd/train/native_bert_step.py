@@ -69,7 +69,15 @@ class NativeBertStep(GraphedStep):
         self.graph = None
         self.calls = 0
 
+    def _check_ids(self, ids):
+        """Token ids past the vocabulary would make the embedding gather read out of bounds
+        on the GPU (a device fault): refuse them while they are still on the host."""
+        v = self.net.c.vocab_size
+        if ids.device.type == 'cpu' and ids.numel() and (int(ids.max()) >= v or int(ids.min()) < 0):
+            raise ValueError(f'token ids must be in [0, {v}) for this model (got [{int(ids.min())}, {int(ids.max())}])')
+
     def load_batch(self, ids, labels, token_type_ids=None, attention_mask=None):
+        self._check_ids(ids)
         self.ids.copy_(ids.to(self.device, non_blocking=True))
         self.y.copy_(labels.to(self.device, non_blocking=True))
         if token_type_ids is not None:
@@ -86,6 +94,7 @@ class NativeBertStep(GraphedStep):
 
     def predict(self, ids, token_type_ids=None, attention_mask=None):
         """Native inference logits [B, num_labels] for one (eval) batch."""
+        self._check_ids(ids)
         ids = ids.to(self.device)
         tt = token_type_ids.to(self.device) if token_type_ids is not None else torch.zeros_like(ids)
         kb = None

@@ -33,8 +33,8 @@ CASES = {
              {'criterion': 'BCEDiceLoss'}, {'optimizer': 'Adam', 'lr': 3e-4},
              {'dice': {'callback': 'DiceCallback'}}, 'dice'),
     'bert': ({'model': 'bert-tiny', 'num_labels': 2},
-             {'dataset': 'synthetic_text_classification', 'seq_len': 32, 'num_samples': 32, 'valid_samples': 20,
-              'batch_size': 8},
+             {'dataset': 'synthetic_text_classification', 'seq_len': 32, 'vocab_size': 1024, 'num_samples': 32,
+              'valid_samples': 20, 'batch_size': 8},
              {'criterion': 'CrossEntropyLoss'}, {'optimizer': 'AdamW', 'lr': 1e-4},
              {'accuracy': {'callback': 'AccuracyCallback'}}, 'accuracy01'),
 }

@@ -25,29 +25,28 @@ def test_native_resnet18_overfits_fixed_batch():
 
 
 def test_graph_replay_matches_eager():
+    """Default (fast) mode: split-K weight gradients and BN statistics add with float
+    atomics, so a graph replay and an eager step differ in the last bits; after a few
+    moderate SGD steps that stays under 1e-3.  (Deterministic mode makes the two bitwise
+    equal: tests/test_deterministic_gpu.py.)"""
     torch.manual_seed(3)
     from mlcomp_amd.models import build_model
     tm1 = build_model('resnet18', num_classes=10)
     tm2 = build_model('resnet18', num_classes=10)
     tm2.load_state_dict(tm1.state_dict())
-    a = _step(torch_model=tm1, batch=16, image_size=64, device='cuda', num_classes=10,
-              use_graph=False)
-    b = _step(torch_model=tm2, batch=16, image_size=64, device='cuda', num_classes=10,
-              use_graph=True, warmup_eager=2)
-    for _ in range(5):
+    kw = dict(batch=16, image_size=64, device='cuda', num_classes=10, lr=0.02, momentum=0.9)
+    a = _step(torch_model=tm1, use_graph=False, **kw)
+    b = _step(torch_model=tm2, use_graph=True, warmup_eager=2, **kw)
+    for _ in range(4):
         a()
         b()
     torch.cuda.synchronize()
     assert b.graph is not None
     la, lb = a.last_loss(), b.last_loss()
-    # float-atomic accumulation order differs run to run; on this fast-overfitting batch
-    # two eager/graph pairs measured |la - lb| between 1e-4 and 1.3e-3 (scripts/graph_noise_probe.py)
-    assert abs(la - lb) <= 3e-3 * max(1.0, abs(la)), (la, lb)
+    assert abs(la - lb) <= 1e-3 * max(1.0, abs(la)), (la, lb)
     pa = a.net.arena.decay.master
     pb = b.net.arena.decay.master
-    # split-K weight gradients and BN statistics are accumulated with float atomics, so
-    # two runs differ in the last bits; after 5 SGD steps the drift stays ~1e-4
-    assert ((pa - pb).norm() / pa.norm()).item() < 5e-3
+    assert ((pa - pb).norm() / pa.norm()).item() < 1e-3
 
 
 def test_rccl_single_rank():
