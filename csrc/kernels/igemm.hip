@@ -687,6 +687,10 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
     __syncthreads();
     constexpr int CPR = BN / 8;              // 16 B chunks per row
     constexpr int RPI = NTHR / CPR;          // rows per iteration
+    // three-wide tiles: CPR does not divide the block (12 / 24 / 36 chunks per row), so
+    // the last NTHR % CPR threads idle and the last iteration is partial
+    constexpr bool EXACT = RPI * CPR == NTHR && BM % RPI == 0;
+    const bool tok = EXACT || tid < RPI * CPR;
     const int c = tid % CPR;
     const int nc = n0 + c * 8;
     const bool red = !kDense && bn.y0 != nullptr;
@@ -711,12 +715,13 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
 #pragma unroll
     for (int e = 0; e < 8; ++e) bz[e] = 0.f;
     if (kDense && bias) ldg8f(bias + (nc < N ? nc : 0), bz);
+    constexpr int ITERS = (BM + RPI - 1) / RPI;
     if (!addend && !red && !dense) {  // plain store (forward convs / GEMMs)
 #pragma unroll
-      for (int it = 0; it < BM / RPI; ++it) {
+      for (int it = 0; it < ITERS; ++it) {
         const int row = tid / CPR + RPI * it;
         const int m = m0 + row;
-        if (m < M && nc < N)
+        if ((EXACT || (tok && row < BM)) && m < M && nc < N)
           *reinterpret_cast<uint4*>(out + rowmap(m) * ld + nc) =
               *reinterpret_cast<const uint4*>(lds + row * RS + c * 16);
       }
@@ -725,7 +730,6 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
     // rows are processed U at a time: every global load of a chunk (addend, mask, y) is
     // issued before the chunk's stores, so the loads overlap instead of serialising
     // behind stores the compiler must assume alias them (out may alias addend)
-    constexpr int ITERS = BM / RPI;
     constexpr int UMAX = kDense ? 4 : 8;   // conv epilogues: every row's loads in flight at once
     constexpr int U = ITERS < UMAX ? ITERS : UMAX;
     const bool has_add = addend != nullptr, has_mask = red && bn.mask, has_y1 = red && bn.y1;
@@ -738,9 +742,11 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
       bool ok[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int row = tid / CPR + RPI * (it0 + u);
+        int row = tid / CPR + RPI * (it0 + u);
+        const bool rin = EXACT || (tok && row < BM);
+        if (!rin) row = 0;                          // idle thread / past the tile: read row 0, no store
         const int m = m0 + row;
-        ok[u] = m < M && nc < N;
+        ok[u] = rin && m < M && nc < N;
         off[u] = ok[u] ? rowmap(m) * ld + nc : 0;   // rows/cols outside: element 0 (valid)
         vv[u] = *reinterpret_cast<const uint4*>(lds + row * RS + c * 16);
         const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
@@ -1064,12 +1070,19 @@ struct EpiF32 {  // fp32 [M][ld] = acc (+ bias[n]) (+= if accumulate)
 // 64x64 wave tile (2x2) reads one LDS fragment per MFMA; the 128x64 wave tile of the
 // 256x128 / 128x256 blocks reads 0.75 and halves the global->LDS bytes per MFMA, at one
 // block per CU (96 KB of double-buffered LDS).
+// Three-wide dense tiles (128 x 96 / 192 / 288, both operands K-contiguous only): sized so
+// that a 4096-token dense layer's output is exactly 256 or 512 tiles - one or two per CU,
+// no partial last round - where 128x128 leaves 768/2304/3072-wide outputs at 192, 576 and
+// 768 tiles.  128x96: 4x1 waves of 32x96; 128x192: 2x2 waves of 64x96 (80 KB of LDS, two
+// blocks fill the 160 KB); 128x288: 4x1 waves of 32x288 at one block per CU.
 template <int BM, int BN> struct TileCfg {
-  static constexpr bool BIG = BM * BN > 128 * 128;
+  static constexpr bool WIDE3 = BM == 128 && (BN == 96 || BN == 192 || BN == 288);
+  static constexpr bool BIG = !WIDE3 && BM * BN > 128 * 128;
   // 128x64 (dense GEMMs with a 768-wide output): 2x2 waves of 64x32 (MI = 2, NI = 1)
   static constexpr bool NARROW = BM == 128 && BN == 64;
-  static constexpr int MI = (BIG && BM > BN) ? 4 : 2, NI = NARROW ? 1 : (BIG && BN > BM) ? 4 : 2;
-  static constexpr int OCC = BIG ? 1 : 2;
+  static constexpr int MI = WIDE3 ? (BN == 192 ? 2 : 1) : (BIG && BM > BN) ? 4 : 2;
+  static constexpr int NI = WIDE3 ? (BN == 192 ? 3 : BN / 32) : NARROW ? 1 : (BIG && BN > BM) ? 4 : 2;
+  static constexpr int OCC = WIDE3 ? (BN == 288 ? 1 : 2) : BIG ? 1 : 2;
 };
 
 template <int BM, int BN, class LA, class LB, class EPI, int PF>
@@ -1296,6 +1309,34 @@ static int g_splitk_fused = 0;
 // 128x64 tiles instead of split-K for narrow dense outputs (A/B knob 7); -1: read
 // MLC_DENSE_NARROW on first use (default 0: measured neutral on BERT-base)
 static int g_dense_narrow = -1;
+// three-wide tile (5: 128x96, 6: 128x192, 7: 128x288) for a dense GEMM whose operands are
+// both K-contiguous; 0 keeps the 128x128 / split-K path.  MLC_DENSE_TILE forces a tile
+// (A/B; MLC_DENSE_SPLIT a split-K factor with it); unset: picked by pick_dense_tile's model.
+static int g_dense_tile = -2, g_dense_split = 1;
+static int pick_dense_tile(int M, int N, int K, int& split) {
+  if (g_dense_tile == -2) {
+    const char* e = getenv("MLC_DENSE_TILE");
+    g_dense_tile = e ? atoi(e) : -1;
+    const char* s = getenv("MLC_DENSE_SPLIT");
+    g_dense_split = s ? atoi(s) : 1;
+  }
+  split = g_dense_split > 1 ? g_dense_split : 1;
+  if (g_dense_tile >= 0) return g_dense_tile;
+  // Model from scripts/bench_dense_tiles.py on BERT-base (M = 4096 tokens, graph-timed):
+  // a three-wide tile pays when it turns the output into 256-640 tiles (one or two per CU,
+  // 128x128 leaves a partial last round): 2304/3072-wide outputs on 128x192 (-9 / -12 %),
+  // 768-wide on 128x96 (-33 % at K = 768), split-K 2 on top from K >= 2560 (-6 %).  The
+  // 128x288 tile (one block per CU) lost on every shape.
+  split = 1;
+  const long tm = (M + 127) / 128;
+  const long t192 = tm * ((N + 191) / 192), t96 = tm * ((N + 95) / 96);
+  if (t192 >= 256 && t192 <= 640) return 6;
+  if (t96 >= 128 && t96 <= 640) {
+    if (K >= 2560 && t96 <= 256) split = 2;
+    return 5;
+  }
+  return 0;
+}
 constexpr int kSplitCounters = 1 << 16;
 // per-device tile counters for EpiSlabFused, allocated (zeroed) on first use outside stream
 // capture; nullptr -> the caller falls back to the separate reduction kernel
@@ -1369,16 +1410,26 @@ MLC_EXPORT int mlc_gemm_config(int prefetch) {
 }
 
 // tuning knobs for A/B measurements: key 0 = prefetch depth (1, 2), key 1 / 2 = split-K
-// block target of gathered / plain-matrix weight-gradient GEMMs; returns the previous
-// value (-1: bad key)
+// block target of gathered / plain-matrix weight-gradient GEMMs, ..., 10 / 11 = three-wide
+// dense tile (-1 auto, 0 off, 5-7) / its split-K factor; returns the previous value
+// (-1: bad key)
 MLC_EXPORT int mlc_gemm_get_set(int key, int value) {
   int* k = key == 0 ? &igemm::g_prefetch : key == 1 ? &igemm::g_split_target
           : key == 2 ? &igemm::g_split_target_mat : key == 3 ? &igemm::g_big_tiles
           : key == 4 ? &igemm::g_big_min_blocks : key == 5 ? &igemm::g_single_stage
           : key == 6 ? &igemm::g_splitk_fused : key == 7 ? &igemm::g_dense_narrow
-          : key == 8 ? &igemm::g_gemm_dma : key == 9 ? &igemm::g_split_target_dense : nullptr;
+          : key == 8 ? &igemm::g_gemm_dma : key == 9 ? &igemm::g_split_target_dense
+          : key == 10 ? &igemm::g_dense_tile : key == 11 ? &igemm::g_dense_split : nullptr;
   if (!k) return -1;
+  if (key == 10 || key == 11) {   // resolve the env defaults before the first override
+    int sp = 1;
+    (void)igemm::pick_dense_tile(4096, 768, 768, sp);
+  }
   const int old = *k;
+  if (key == 10) {                // -1 = auto (pick_dense_tile's model), 0 = off, 5-7 = forced
+    if (value >= -1) *k = value;
+    return old;
+  }
   if (value >= 0 && (value > 0 || key == 3 || key == 5 || key == 6 || key == 7 || key == 8)) *k = value;
   return old;
 }
@@ -1786,12 +1837,37 @@ MLC_EXPORT int mlc_gemm_bf16_ex(const bf16* A, const bf16* B, bf16* C, int M, in
                                 const bf16* addend, const bf16* dact, float* ws, long ws_floats,
                                 hipStream_t st) {
   if (K % 8 || N % 8 || ldc % 8 || lda % 8 || ldb % 8 || (ta && M % 8)) return -1;
+  const int ktiles = (K + BK - 1) / BK;
+  const long slab = (long)M * N;
+  if (!ta && tb) {  // both operands K-contiguous: the three-wide tiles apply
+    int dsplit = 1;
+    const int dt = pick_dense_tile(M, N, K, dsplit);
+    if (dt >= 5 && dt <= 7) {
+      if (dsplit > 1 && ws && slab * dsplit <= ws_floats && ktiles >= 2 * dsplit) {
+        const int per = (ktiles + dsplit - 1) / dsplit;
+        dsplit = (ktiles + per - 1) / per;
+        EpiF32Slab epi{ws, N, (size_t)slab};
+        hipError_t e = dt == 5 ? launch<128, 96>(GA_KC(128), GB_KC(96), epi, M, N, K, dsplit, st)
+                     : dt == 6 ? launch<128, 192>(GA_KC(128), GB_KC(192), epi, M, N, K, dsplit, st)
+                               : launch<128, 288>(GA_KC(128), GB_KC(288), epi, M, N, K, dsplit, st);
+        if (e != hipSuccess) return e;
+        const DenseFinish fin{C, ldc, bias, act, preact, addend, dact};
+        long blocks = ((long)M * (N / 8) + 255) / 256;
+        if (blocks > 8192) blocks = 8192;
+        hipLaunchKernelGGL(dense_finalize_kernel, dim3(blocks), dim3(256), 0, st, ws, dsplit, fin, M, N);
+        return hipGetLastError();
+      }
+      EpiBF16<IdentityRows, true> epi{C, ldc, nullptr, nullptr, IdentityRows{}, addend};
+      epi.bias = bias; epi.act = act; epi.preact = preact; epi.dact = dact;
+      if (dt == 5) return launch<128, 96>(GA_KC(128), GB_KC(96), epi, M, N, K, 1, st);
+      if (dt == 6) return launch<128, 192>(GA_KC(128), GB_KC(192), epi, M, N, K, 1, st);
+      return launch<128, 288>(GA_KC(128), GB_KC(288), epi, M, N, K, 1, st);
+    }
+  }
   const int tile = pick_tile(M, N);
   const int BMv = tile_bm(tile), BNv = tile_bn(tile);
   const int tiles = ((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
-  const int ktiles = (K + BK - 1) / BK;
   int splits = 1;
-  const long slab = (long)M * N;
   // a narrow output (N <= 1024, e.g. BERT's 768-wide projections) on 128x64 tiles fills
   // the chip without split-K: no fp32 slabs, no finalize pass (MLC_DENSE_NARROW=1; measured
   // neutral on the BERT-base step against split-K 2 + finalize, so off by default)

@@ -79,18 +79,27 @@ def test_softmax_fwd_bwd(L, p, masked):
     assert rel(dS_g, dS_r) < 2e-2
 
 
-@pytest.fixture(params=[0, 1], ids=['splitk', 'narrow'])
+@pytest.fixture(params=[(0, 0, 1), (1, 0, 1), (0, 5, 1), (0, 6, 1), (0, 7, 1), (0, 5, 2), (0, -1, 1)],
+                ids=['splitk', 'narrow', 'wide96', 'wide192', 'wide288', 'wide96s2', 'auto'])
 def dense_narrow(request):
-    """Dense GEMMs with a narrow output: split-K + finalize (default) and 128x64 tiles."""
+    """Dense GEMMs over every tile policy: 128x128 + split-K finalize, 128x64 tiles, the
+    three-wide tiles 128x96 / 128x192 / 128x288 (forced, and 128x96 with split-K 2), and the
+    automatic choice (igemm pick_dense_tile)."""
     from mlcomp_amd.ops import _lib
     lib = _lib.load()
-    old = lib.mlc_gemm_get_set(7, request.param)
+    narrow, tile, split = request.param
+    old = lib.mlc_gemm_get_set(7, narrow)
+    old_t = lib.mlc_gemm_get_set(10, tile)
+    old_s = lib.mlc_gemm_get_set(11, split)
     yield
     lib.mlc_gemm_get_set(7, max(old, 0))
+    lib.mlc_gemm_get_set(10, old_t)
+    lib.mlc_gemm_get_set(11, max(old_s, 1))
 
 
 @pytest.mark.parametrize('M,N,K', [(512, 3072, 768), (300, 768, 3072), (4096, 2304, 768), (64, 8, 128),
-                                   (4096, 768, 3072), (4096, 776, 256)])   # last two: 128x64 narrow tiles
+                                   (4096, 768, 3072), (4096, 776, 256),    # 128x64 narrow tiles
+                                   (4096, 3072, 768), (4096, 768, 768), (1000, 680, 200)])  # three-wide tiles
 def test_dense_epilogues(M, N, K, dense_narrow):
     x, w = _bf(M, K, seed=6), _bf(N, K, seed=7, scale=K ** -0.5)
     bias = torch.randn(N) * 0.1
