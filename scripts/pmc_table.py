@@ -11,7 +11,7 @@ for path in sys.argv[1:]:
         name = r['Kernel_Name']
         m = re.search(r'gemm_kernel<(\d+), (\d+), igemm::(\w+)<\d+>, igemm::(\w+)<\d+>, igemm::(\w+)', name)
         short = f'{m.group(1)}x{m.group(2)} {m.group(3)}/{m.group(4)}/{m.group(5)}' if m else name[:40]
-        if not m and 'bn_' not in name:
+        if not m and 'bn_' not in name and 'Cijk' not in name:
             continue
         key = (path.split('/')[-3], int(r['Dispatch_Id']))
         d = rows.setdefault(key, {'name': short, 'us': (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3,
