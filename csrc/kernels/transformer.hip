@@ -219,10 +219,19 @@ ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ s, const flo
 __global__ void __launch_bounds__(NT)
 ln_bwd_finalize_kernel(const float* __restrict__ sums, float* __restrict__ dgamma, float* __restrict__ dbeta, int H,
                        int ncopy) {
-  const int c = blockIdx.x * NT + threadIdx.x;
-  if (c >= H) return;
+  // 8 lanes per column, each summing every 8th copy, then a fixed-order shuffle reduction
+  // (deterministic): one lane per column looping over all copies ran 3 blocks of serial
+  // loads, 11 us per call on BERT-base (24 calls per step)
+  constexpr int FL = 8;
+  const int c = blockIdx.x * (NT / FL) + (int)(threadIdx.x / FL), q = threadIdx.x % FL;
   float g = 0.f, b = 0.f;
-  for (int k = 0; k < ncopy; ++k) { g += sums[(size_t)k * 2 * H + c]; b += sums[(size_t)k * 2 * H + H + c]; }
+  if (c < H) {
+#pragma unroll 4
+    for (int k = q; k < ncopy; k += FL) { g += sums[(size_t)k * 2 * H + c]; b += sums[(size_t)k * 2 * H + H + c]; }
+  }
+#pragma unroll
+  for (int o = 1; o < FL; o <<= 1) { g += __shfl_xor(g, o, 64); b += __shfl_xor(b, o, 64); }
+  if (c >= H || q != 0) return;
   dgamma[c] += g;
   dbeta[c] += b;
 }
@@ -348,11 +357,16 @@ colsum_partial_kernel(const bf16* __restrict__ g, float* __restrict__ scratch, i
 
 __global__ void __launch_bounds__(NT)
 colsum_finalize_kernel(float* __restrict__ scratch, float* __restrict__ out, int C, int ncopy) {
-  const int c = blockIdx.x * NT + threadIdx.x;
-  if (c >= C) return;
+  constexpr int FL = 8;   // 8 lanes per column + fixed-order shuffle (as ln_bwd_finalize_kernel)
+  const int c = blockIdx.x * (NT / FL) + (int)(threadIdx.x / FL), q = threadIdx.x % FL;
   float s = 0.f;
-  for (int k = 0; k < ncopy; ++k) { s += scratch[(size_t)k * C + c]; scratch[(size_t)k * C + c] = 0.f; }
-  out[c] += s;
+  if (c < C) {
+#pragma unroll 4
+    for (int k = q; k < ncopy; k += FL) { s += scratch[(size_t)k * C + c]; scratch[(size_t)k * C + c] = 0.f; }
+  }
+#pragma unroll
+  for (int o = 1; o < FL; o <<= 1) s += __shfl_xor(s, o, 64);
+  if (c < C && q == 0) out[c] += s;
 }
 
 // ------------------------------------------------------------------ dropout (standalone)
@@ -736,7 +750,7 @@ MLC_EXPORT int mlc_ln_bwd(const bf16* dy, const bf16* s, const float* mean, cons
     return (int)hipGetLastError();
   });
   if (rc) return rc;
-  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((H + NT - 1) / NT), dim3(NT), 0, st, sums, dgamma, dbeta, H,
+  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((H + NT / 8 - 1) / (NT / 8)), dim3(NT), 0, st, sums, dgamma, dbeta, H,
                      g_mlc_ncopy);
   return hipGetLastError();
 }
@@ -778,7 +792,8 @@ MLC_EXPORT int mlc_colsum_acc(const bf16* g, float* out, float* scratch, int R, 
   dim3 grid(xb, (R + RB - 1) / RB);
   if (g_mlc_det && (int)grid.y > g_mlc_ncopy) return -2;
   hipLaunchKernelGGL(colsum_partial_kernel, grid, dim3(NT), 0, st, g, scratch, R, C, RB, g_mlc_ncopy);
-  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, st, scratch, out, C, g_mlc_ncopy);
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((C + NT / 8 - 1) / (NT / 8)), dim3(NT), 0, st, scratch, out, C,
+                     g_mlc_ncopy);
   return hipGetLastError();
 }
 

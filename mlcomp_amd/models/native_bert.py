@@ -81,18 +81,39 @@ class _Dense:
         self.ctx.arena.mark_ready(self.w)
         self.ctx.arena.mark_ready(self.b)
 
-    def bwd_params_async(self, dy, x):
-        """:meth:`bwd_params` on the context's weight-gradient stream (when there is one);
-        returns a join callable for after the layer's dgrad."""
+    def bwd_params_async(self, dy, x, fork=None):
+        """:meth:`bwd_params` on the context's weight-gradient stream (when there is one),
+        forked from event ``fork`` (default: now); returns a join callable for after the
+        layer's dgrad."""
         side = self.ctx.wgrad_stream
         if side is None:
             self.bwd_params(dy, x)
             return lambda: None
         main = torch.cuda.current_stream(self.ctx.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
+        if fork is None:
+            side.wait_stream(main)
+        else:
+            side.wait_event(fork)
+        with Fn.side_stream(side):
             self.bwd_params(dy, x)
         return lambda: main.wait_stream(side)
+
+    def backward(self, dy, x, **dgrad_kw):
+        """Input gradient (returned) + weight/bias gradients (side stream), then mark the
+        slots.  With ``ctx.dgrad_first`` the dgrad is captured first and the wgrad
+        forked from the point before it, so graph replay keeps the dgrad chain on one
+        hardware queue (see mlcomp_amd.ops.layers)."""
+        if self.ctx.dgrad_first and self.ctx.wgrad_stream is not None:
+            fork = torch.cuda.Event()
+            fork.record(torch.cuda.current_stream(self.ctx.device))
+            dx = self.dgrad(dy, **dgrad_kw)
+            join = self.bwd_params_async(dy, x, fork)
+        else:
+            join = self.bwd_params_async(dy, x)
+            dx = self.dgrad(dy, **dgrad_kw)
+        join()
+        self.mark()
+        return dx
 
 
 class _LN:
@@ -175,21 +196,12 @@ class NativeBertLayer:
         ds2, df = Tx.ln_bwd(dh2, s2, m2, r2, self.ln2.g.master, self.ln2.g.grad, self.ln2.b.grad,
                             ws[self.ln2.k_sums], p_in=ph, seed=net.seed, salt_in=self.salt + 2, want_dr=True)
         self.ln2.mark()
-        join = self.ffn2.bwd_params_async(df, g)
-        du = self.ffn2.dgrad(df, dact_u=u)          # grad of the GELU input
-        join()
-        self.ffn2.mark()
-        join = self.ffn1.bwd_params_async(du, h1)
-        dh1 = self.ffn1.dgrad(du, addend=ds2)       # + residual branch
-        join()
-        self.ffn1.mark()
+        du = self.ffn2.backward(df, g, dact_u=u)          # grad of the GELU input
+        dh1 = self.ffn1.backward(du, h1, addend=ds2)      # + residual branch
         ds1, dao = Tx.ln_bwd(dh1, s1, m1, r1, self.ln1.g.master, self.ln1.g.grad, self.ln1.b.grad,
                              ws[self.ln1.k_sums], p_in=ph, seed=net.seed, salt_in=self.salt + 1, want_dr=True)
         self.ln1.mark()
-        join = self.out.bwd_params_async(dao, ctx2)
-        dctx2 = self.out.dgrad(dao)
-        join()
-        self.out.mark()
+        dctx2 = self.out.backward(dao, ctx2)
         if fused:
             qkv, lse = att
             dqkv = Tx.attn_bwd(qkv, key_bias, dctx2, lse, B, S, nh, 1.0 / math.sqrt(dh), pa, net.seed, self.salt,
@@ -203,11 +215,7 @@ class NativeBertLayer:
             dq = torch.bmm(dS, k)
             dk = torch.bmm(dS.transpose(1, 2), q)
             dqkv = torch.stack([dq, dk, dv]).view(3, B, nh, S, dh).permute(1, 3, 0, 2, 4).reshape(B * S, 3 * nh * dh)
-        join = self.qkv.bwd_params_async(dqkv, x)
-        dx = self.qkv.dgrad(dqkv, addend=ds1)
-        join()
-        self.qkv.mark()
-        return dx
+        return self.qkv.backward(dqkv, x, addend=ds1)
 
 
 class _BertLayerFn(torch.autograd.Function):

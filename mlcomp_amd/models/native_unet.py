@@ -133,6 +133,7 @@ class NativeUnet:
             raise NotImplementedError('native U-Net: center block not supported')
         self.torch_model = model
         ctx = self.ctx = NativeContext()
+        ctx.default_dgrad_first(True)     # +1.8 % here (profiles/round3/README.md)
         self.stem, self.pool, self.blocks, self.ends = lower_resnet_body(ctx, enc.body, prefix='encoder.body.',
                                                                           s2d_stem=True)
         for e in self.ends[:3]:          # stage outputs 1-3 feed skips (see module doc)

@@ -14,7 +14,9 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
+import contextlib
 import os
+import threading
 
 import torch
 import torch.nn.functional as F
@@ -223,21 +225,34 @@ _SLAB = {}
 _SLAB_OLD = []   # superseded buffers stay alive: a captured graph may still point at them
 
 
-_SIDE_STREAMS = set()
+_ROLE = threading.local()
 
 
 def register_side_stream(stream) -> None:
-    """GEMMs issued on ``stream`` (e.g. the weight-gradient stream) get workspaces of their
-    own, so they can run concurrently with GEMMs on the main stream."""
-    _SIDE_STREAMS.add((stream.device.index, stream.stream_id))
+    """Kept for callers of the old API: the workspace role is now explicit (side_role)."""
+
+
+@contextlib.contextmanager
+def side_stream(stream):
+    """``with torch.cuda.stream(stream)`` for work that runs CONCURRENTLY with the main
+    stream (weight gradients, the shortcut branch): its split-K GEMMs get workspaces of
+    their own.  The role is explicit, not derived from the stream id: pool stream ids are
+    recycled, so the pool stream a graph warm-up or capture runs the main work on can carry
+    the id of an earlier context's side stream - main and side GEMMs then shared one
+    workspace while running concurrently."""
+    prev = getattr(_ROLE, 'side', False)
+    _ROLE.side = True
+    try:
+        with torch.cuda.stream(stream):
+            yield
+    finally:
+        _ROLE.side = prev
 
 
 def workspace_key(device) -> str:
     device = torch.device(device)
-    if device.type == 'cuda' and _SIDE_STREAMS:
-        cs = torch.cuda.current_stream(device)
-        if (cs.device.index, cs.stream_id) in _SIDE_STREAMS:
-            return f'{device}/side'
+    if device.type == 'cuda' and getattr(_ROLE, 'side', False):
+        return f'{device}/side'
     return str(device)
 
 

@@ -24,6 +24,13 @@ import torch.nn as nn
 from . import functional as Fn
 from .arena import ParamArena, Slot
 
+# MLC_DGRAD_FIRST=1/0: capture a layer's input-gradient GEMM before / after its side-stream
+# weight gradient (both forked from the same point).  It changes which hardware queue the
+# HIP graph executor gives each chain, and the measured effect is engine-dependent
+# (profiles/round3/README.md): U-Net +1.8 % with dgrad first, ResNet-50 -1 %, BERT-base -3 %.
+# Unset: the engine's default (NativeContext.dgrad_first; the U-Net engine turns it on).
+DGRAD_FIRST_ENV = os.environ.get('MLC_DGRAD_FIRST')
+
 
 class Workspace:
     """One zero-per-step fp32 buffer carved into named views."""
@@ -80,6 +87,12 @@ class NativeContext:
         # not stall on a just-finished wgrad; flush_wgrad joins the last one
         self.wgrad_lag = os.environ.get('MLC_WGRAD_LAG', '0') == '1'
         self._pending_wgrad = None
+        self.dgrad_first = DGRAD_FIRST_ENV == '1'
+
+    def default_dgrad_first(self, on: bool):
+        """Engine default for the capture order (MLC_DGRAD_FIRST overrides it)."""
+        if DGRAD_FIRST_ENV is None:
+            self.dgrad_first = on
 
     def finalize(self, device):
         self.device = torch.device(device)
@@ -91,7 +104,6 @@ class NativeContext:
         self.arena.flush = self.flush_wgrad
         if self.device.type == 'cuda' and os.environ.get('MLC_WGRAD_STREAM', '1') in ('1', '2'):
             self.wgrad_stream = torch.cuda.Stream(self.device)
-            Fn.register_side_stream(self.wgrad_stream)
 
     def flush_wgrad(self):
         """Join the lagged weight gradient (if any) into the current stream and mark its
@@ -279,11 +291,15 @@ class ConvBN:
         side = self.ctx.wgrad_stream if need_dx else None
         if side is not None and torch.cuda.current_stream(self.ctx.device) == side:
             side = None            # already on the side stream (a forked branch): run inline
+        fork = None
         if side is not None:
             main = torch.cuda.current_stream(self.ctx.device)
-            side.wait_stream(main)                 # dy, x and the grad slot are ready
-            with torch.cuda.stream(side):
-                self.wgrad(dy, x, in_affine)
+            fork = torch.cuda.Event()
+            fork.record(main)                      # dy, x and the grad slot are ready
+            if not self.ctx.dgrad_first:
+                side.wait_event(fork)
+                with Fn.side_stream(side):
+                    self.wgrad(dy, x, in_affine)
         else:
             self.wgrad(dy, x, in_affine)
         dx = None
@@ -296,6 +312,13 @@ class ConvBN:
                 wt = self.ctx.wt[self.wt_idx]
             dx = Fn.conv2d_dgrad(dy, self.w.bf16, x.shape, self.stride, self.pad, self.dil,
                                  addend=dx_addend, out=dx_out, bn=dgrad_bn, wt=wt)
+        if side is not None and self.ctx.dgrad_first:
+            # captured after the dgrad but forked from the point before it: the dgrad is the
+            # first child of the previous node, so graph replay keeps the dgrad -> BN chain
+            # on one hardware queue and only the weight gradient crosses queues
+            side.wait_event(fork)
+            with Fn.side_stream(side):
+                self.wgrad(dy, x, in_affine)
         if side is not None and defer is not None:
             defer.append((dy, x, self.w))
             return dx, dres
@@ -405,7 +428,7 @@ class _ResidualBlockFn(torch.autograd.Function):
         if blk.down is not None:
             # the downsample BN (no activation) is applied inside the last unit's pass
             if side is not None:
-                with torch.cuda.stream(side):
+                with Fn.side_stream(side):
                     _, rd = blk.down.fwd(x, defer=not blk.down.act)
             else:
                 _, rd = blk.down.fwd(x, defer=not blk.down.act)
@@ -476,7 +499,7 @@ class _ResidualBlockFn(torch.autograd.Function):
             main = torch.cuda.current_stream(units[0].ctx.device)
             short_buf = torch.empty(rd[0].shape, device=rd[0].device, dtype=rd[0].dtype) if need_dx else None
             down_side.wait_stream(main)
-            with torch.cuda.stream(down_side):
+            with Fn.side_stream(down_side):
                 short, _ = blk.down.bwd(dres, rd, need_dx=need_dx, prereduced=pre, dx_out=short_buf)
         for i in range(len(units) - 2, 0, -1):
             sp = spec_for(i - 1)
