@@ -20,65 +20,100 @@ __device__ __forceinline__ void store_bf16x4(bf16* dst, const float* f) {
 }
 }  // namespace
 
+typedef float v4f __attribute__((ext_vector_type(4)));
+// U float4 chunks per thread in flight: every load of an iteration (issued through
+// ext-vector types from clamped, always-valid indices) precedes its compute and stores, so
+// the loads of U chunks overlap instead of each waiting for the previous chunk's stores
+constexpr int OPT_U = 2;
+
 // hyper[0] = lr, hyper[1] = grad scale (e.g. 1/world_size / loss scale)
 __global__ void __launch_bounds__(NT)
 sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
            bf16* __restrict__ pbf, const float* __restrict__ hyper, long n4, long ndecay4,
            long nbf4, float momentum, float dampening, float wd, int nesterov, int first) {
   const float lr = hyper[0], gs = hyper[1];
-  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
-    float4 pv = reinterpret_cast<float4*>(p)[i];
-    float4 gv = reinterpret_cast<const float4*>(g)[i];
-    float pp[4] = {pv.x, pv.y, pv.z, pv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
-    const float w = i < ndecay4 ? wd : 0.f;
-    float mm[4];
-    if (momentum != 0.f) {
-      float4 mv = reinterpret_cast<float4*>(m)[i];
-      mm[0] = mv.x; mm[1] = mv.y; mm[2] = mv.z; mm[3] = mv.w;
+  const long stride = (long)gridDim.x * NT;
+  v4f* P = reinterpret_cast<v4f*>(p);
+  const v4f* Gr = reinterpret_cast<const v4f*>(g);
+  v4f* Mo = reinterpret_cast<v4f*>(m);
+  const bool mom = momentum != 0.f;
+  for (long i0 = (long)blockIdx.x * NT + threadIdx.x; i0 < n4; i0 += stride * OPT_U) {
+    v4f pv[OPT_U], gv[OPT_U], mv[OPT_U];
+#pragma unroll
+    for (int u = 0; u < OPT_U; ++u) {
+      const long i = min(i0 + u * stride, n4 - 1);
+      pv[u] = P[i];
+      gv[u] = Gr[i];
+      mv[u] = mom && !first ? Mo[i] : (v4f){0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float d = gg[j] * gs + w * pp[j];
-      if (momentum != 0.f) {
-        mm[j] = first ? d : momentum * mm[j] + (1.f - dampening) * d;
-        d = nesterov ? d + momentum * mm[j] : mm[j];
+    for (int u = 0; u < OPT_U; ++u) {
+      const long i = i0 + u * stride;
+      if (i >= n4) break;
+      const float w = i < ndecay4 ? wd : 0.f;
+      float pp[4], mm[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pp[j] = pv[u][j];
+        float d = gv[u][j] * gs + w * pp[j];
+        if (mom) {
+          mm[j] = first ? d : momentum * mv[u][j] + (1.f - dampening) * d;
+          d = nesterov ? d + momentum * mm[j] : mm[j];
+        }
+        pp[j] -= lr * d;
       }
-      pp[j] -= lr * d;
+      P[i] = (v4f){pp[0], pp[1], pp[2], pp[3]};
+      if (mom) Mo[i] = (v4f){mm[0], mm[1], mm[2], mm[3]};
+      if (pbf && i < nbf4) store_bf16x4(pbf + i * 4, pp);
     }
-    reinterpret_cast<float4*>(p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
-    if (momentum != 0.f) reinterpret_cast<float4*>(m)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
-    if (pbf && i < nbf4) store_bf16x4(pbf + i * 4, pp);
   }
 }
 
-// Adam / AdamW.  hyper: [lr, grad_scale, bias_correction1, bias_correction2]
+// Adam / AdamW, in torch.optim.Adam(W)'s form: m = b1 m + (1-b1) d, v = b2 v + (1-b2) d^2,
+// p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)  (AdamW: p *= 1 - lr*wd first).
+// hyper: [lr, grad_scale, bias_correction1, bias_correction2]
 __global__ void __launch_bounds__(NT)
 adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
             float* __restrict__ v, bf16* __restrict__ pbf, const float* __restrict__ hyper, long n4,
             long ndecay4, long nbf4, float b1, float b2, float eps, float wd, int decoupled) {
-  const float lr = hyper[0], gs = hyper[1], bc1 = hyper[2], bc2 = hyper[3];
-  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
-    float4 pv = reinterpret_cast<float4*>(p)[i];
-    float4 gv = reinterpret_cast<const float4*>(g)[i];
-    float4 mv = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
-    float pp[4] = {pv.x, pv.y, pv.z, pv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
-    float mm[4] = {mv.x, mv.y, mv.z, mv.w}, ww[4] = {vv.x, vv.y, vv.z, vv.w};
-    const float wdi = i < ndecay4 ? wd : 0.f;
+  const float lr = hyper[0], gs = hyper[1];
+  const float step_size = lr / hyper[2], bc2s = sqrtf(hyper[3]);
+  const long stride = (long)gridDim.x * NT;
+  v4f* P = reinterpret_cast<v4f*>(p);
+  const v4f* Gr = reinterpret_cast<const v4f*>(g);
+  v4f* Mo = reinterpret_cast<v4f*>(m);
+  v4f* Vo = reinterpret_cast<v4f*>(v);
+  for (long i0 = (long)blockIdx.x * NT + threadIdx.x; i0 < n4; i0 += stride * OPT_U) {
+    v4f pv[OPT_U], gv[OPT_U], mv[OPT_U], vv[OPT_U];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float d = gg[j] * gs;
-      if (!decoupled) d += wdi * pp[j];
-      mm[j] = b1 * mm[j] + (1.f - b1) * d;
-      ww[j] = b2 * ww[j] + (1.f - b2) * d * d;
-      const float upd = (mm[j] / bc1) / (sqrtf(ww[j] / bc2) + eps);
-      if (decoupled) pp[j] -= lr * wdi * pp[j];
-      pp[j] -= lr * upd;
+    for (int u = 0; u < OPT_U; ++u) {
+      const long i = min(i0 + u * stride, n4 - 1);
+      pv[u] = P[i];
+      gv[u] = Gr[i];
+      mv[u] = Mo[i];
+      vv[u] = Vo[i];
     }
-    reinterpret_cast<float4*>(p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
-    reinterpret_cast<float4*>(m)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
-    reinterpret_cast<float4*>(v)[i] = make_float4(ww[0], ww[1], ww[2], ww[3]);
-    if (pbf && i < nbf4) store_bf16x4(pbf + i * 4, pp);
+#pragma unroll
+    for (int u = 0; u < OPT_U; ++u) {
+      const long i = i0 + u * stride;
+      if (i >= n4) break;
+      const float wdi = i < ndecay4 ? wd : 0.f;
+      float pp[4], mm[4], ww[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pp[j] = pv[u][j];
+        float d = gv[u][j] * gs;
+        if (!decoupled) d += wdi * pp[j];
+        mm[j] = b1 * mv[u][j] + (1.f - b1) * d;
+        ww[j] = b2 * vv[u][j] + (1.f - b2) * d * d;
+        if (decoupled) pp[j] -= lr * wdi * pp[j];
+        pp[j] -= step_size * mm[j] / (sqrtf(ww[j]) / bc2s + eps);
+      }
+      P[i] = (v4f){pp[0], pp[1], pp[2], pp[3]};
+      Mo[i] = (v4f){mm[0], mm[1], mm[2], mm[3]};
+      Vo[i] = (v4f){ww[0], ww[1], ww[2], ww[3]};
+      if (pbf && i < nbf4) store_bf16x4(pbf + i * 4, pp);
+    }
   }
 }
 
@@ -102,7 +137,7 @@ sqnorm_kernel(const float* __restrict__ x, long n, float* __restrict__ out, floa
 }
 
 static int blocks_for(long work) {
-  long b = (work + NT - 1) / NT;
+  long b = (work + NT * OPT_U - 1) / (NT * OPT_U);
   if (b > 8192) b = 8192;
   return (int)(b < 1 ? 1 : b);
 }

@@ -33,6 +33,11 @@ from mlcomp_amd.ops import transformer as Tx
 from mlcomp_amd.ops.layers import NativeContext
 from .bert import BertForSequenceClassification
 
+# MLC_GELU_DERIV=1 (default): the FFN's first GEMM stores gelu'(pre-activation) instead of
+# the pre-activation, so the input-gradient GEMM of the second only multiplies by it (no erf
+# / exp in that epilogue); 0 keeps the pre-activation and recomputes the derivative.
+GELU_DERIV = os.environ.get('MLC_GELU_DERIV', '1') == '1'
+
 
 class _Dense:
     def __init__(self, ctx: NativeContext, name: str, lin: torch.nn.Linear):
@@ -59,14 +64,14 @@ class _Dense:
         self.ctx.wt_stale = True
         return Tx.dense_fwd(x, self.w.bf16, self.b.master, act, want_preact)
 
-    def dgrad(self, dy, dact_u=None, addend=None):
-        """dx = dy @ W [* gelu'(dact_u)] [+ addend]."""
+    def dgrad(self, dy, dact_u=None, addend=None, dact_is_deriv=False):
+        """dx = dy @ W [* gelu'(dact_u)] [+ addend] (``dact_is_deriv``: dact_u = gelu'(u))."""
         wt = None
         if self.wt_idx is not None:
             if self.ctx.wt_stale:
                 raise RuntimeError('transposed weights are stale: refresh_wt() must follow the forward pass')
             wt = self.ctx.wt[self.wt_idx]
-        return Tx.dense_dgrad(dy, self.w.bf16, dact_u=dact_u, addend=addend, wt=wt)
+        return Tx.dense_dgrad(dy, self.w.bf16, dact_u=dact_u, addend=addend, wt=wt, dact_is_deriv=dact_is_deriv)
 
     def bwd_params(self, dy, x):
         """dW += dy^T x, db += colsum(dy) (straight into the grad arena); the caller calls
@@ -179,7 +184,8 @@ class NativeBertLayer:
         ao, _ = self.out.fwd(ctx2)
         h1, s1, m1, r1 = Tx.ln_fwd(x, ao, self.ln1.g.master, self.ln1.b.master, net.c.eps, p_in=ph,
                                    seed=net.seed, salt_in=self.salt + 1)
-        g, u = self.ffn1.fwd(h1, act=1, want_preact=True)
+        # act 2: the GEMM epilogue stores gelu'(pre-activation) for the backward (not u)
+        g, u = self.ffn1.fwd(h1, act=2 if GELU_DERIV else 1, want_preact=True)
         f, _ = self.ffn2.fwd(g)
         h2, s2, m2, r2 = Tx.ln_fwd(h1, f, self.ln2.g.master, self.ln2.b.master, net.c.eps, p_in=ph,
                                    seed=net.seed, salt_in=self.salt + 2)
@@ -196,7 +202,7 @@ class NativeBertLayer:
         ds2, df = Tx.ln_bwd(dh2, s2, m2, r2, self.ln2.g.master, self.ln2.g.grad, self.ln2.b.grad,
                             ws[self.ln2.k_sums], p_in=ph, seed=net.seed, salt_in=self.salt + 2, want_dr=True)
         self.ln2.mark()
-        du = self.ffn2.backward(df, g, dact_u=u)          # grad of the GELU input
+        du = self.ffn2.backward(df, g, dact_u=u, dact_is_deriv=GELU_DERIV)   # grad of the GELU input
         dh1 = self.ffn1.backward(du, h1, addend=ds2)      # + residual branch
         ds1, dao = Tx.ln_bwd(dh1, s1, m1, r1, self.ln1.g.master, self.ln1.g.grad, self.ln1.b.grad,
                              ws[self.ln1.k_sums], p_in=ph, seed=net.seed, salt_in=self.salt + 1, want_dr=True)

@@ -271,7 +271,9 @@ def _dgelu(u):
 
 def dense_fwd(x, w, bias=None, act: int = 0, want_preact: bool = False):
     """y = act(x @ w^T + bias): x [M, K] bf16, w [N, K] bf16, bias fp32 [N].  Returns
-    (y, u) with u the bf16 pre-activation (when ``want_preact``)."""
+    (y, u) with u the bf16 pre-activation (when ``want_preact``).  ``act`` 1 = exact-erf
+    GELU; 2 = GELU returning u = gelu'(pre-activation) instead, for
+    ``dense_dgrad(..., dact_is_deriv=True)`` (the backward epilogue then only multiplies)."""
     M, K = x.shape
     N = w.shape[0]
     if _cuda(x):
@@ -284,14 +286,18 @@ def dense_fwd(x, w, bias=None, act: int = 0, want_preact: bool = False):
     z = x.float() @ w.float().t()
     if bias is not None:
         z = z + bias
-    u = z.to(torch.bfloat16) if want_preact else None
-    if act == 1:
+    if act == 2:
+        u = _dgelu(z).to(torch.bfloat16) if want_preact else None
+    else:
+        u = z.to(torch.bfloat16) if want_preact else None
+    if act in (1, 2):
         z = _gelu(z)
     return z.to(torch.bfloat16), u
 
 
-def dense_dgrad(dy, w, dact_u=None, addend=None, wt=None):
+def dense_dgrad(dy, w, dact_u=None, addend=None, wt=None, dact_is_deriv=False):
     """dx = (dy @ w) [* gelu'(dact_u)] [+ addend]: dy [M, N], w [N, K] -> [M, K] bf16.
+    ``dact_is_deriv``: ``dact_u`` already holds gelu'(u) (``dense_fwd(act=2)``), multiply.
     ``wt`` = w^T ([K, N], e.g. a ``Fn.WtTable`` view): the GEMM reads both operands
     K-contiguous (the LDS-DMA main loop) instead of w as an MN-contiguous tile."""
     M, N = dy.shape
@@ -301,7 +307,8 @@ def dense_dgrad(dy, w, dact_u=None, addend=None, wt=None):
         b, ldb, tb = (wt, N, 1) if wt is not None else (w, K, 0)
         if wt is not None:
             assert tuple(wt.shape) == (K, N), (wt.shape, w.shape)
-        _lib.call('mlc_gemm_bf16_ex', _lib.ptr(dy), _lib.ptr(b), _lib.ptr(dx), M, K, N, N, ldb, K, 0, tb, None, 0,
+        _lib.call('mlc_gemm_bf16_ex', _lib.ptr(dy), _lib.ptr(b), _lib.ptr(dx), M, K, N, N, ldb, K, 0, tb, None,
+                  4 if (dact_u is not None and dact_is_deriv) else 0,
                   None, _lib.ptr(addend), _lib.ptr(dact_u), _lib.ptr(gemm_workspace(dy.device, 4 * M * K)),
                   4 * M * K, _lib.stream())
         return dx
@@ -310,7 +317,7 @@ def dense_dgrad(dy, w, dact_u=None, addend=None, wt=None):
     z = dy.float() @ w.float()
     z = z.to(torch.bfloat16).float()
     if dact_u is not None:
-        z = z * _dgelu(dact_u.float())
+        z = z * (dact_u.float() if dact_is_deriv else _dgelu(dact_u.float()))
     if addend is not None:
         z = z + addend.float()
     return z.to(torch.bfloat16)

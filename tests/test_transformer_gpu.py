@@ -120,6 +120,14 @@ def test_dense_epilogues(M, N, K, dense_narrow):
     g = Tx.dense_dgrad(dy2.to(DEV), w2.to(DEV), dact_u=u_g)
     torch.cuda.synchronize()
     assert rel(g, r) < 2e-2
+    # act 2: the forward stores gelu'(pre-activation); the backward multiplies by it (act 4)
+    y2_r, d_r = Tx.dense_fwd(x, w, bias, act=2, want_preact=True)
+    y2_g, d_g = Tx.dense_fwd(x.to(DEV), w.to(DEV), bias.to(DEV), act=2, want_preact=True)
+    assert rel(y2_g, y_r) < 1e-2 and rel(d_g, d_r) < 1e-2
+    r2 = Tx.dense_dgrad(dy2, w2, dact_u=d_r, dact_is_deriv=True)
+    g2 = Tx.dense_dgrad(dy2.to(DEV), w2.to(DEV), dact_u=d_g, dact_is_deriv=True)
+    torch.cuda.synchronize()
+    assert rel(g2, r2) < 2e-2 and rel(g2, r) < 2e-2
     o_r, o_g = torch.zeros(N), torch.zeros(N, device=DEV)
     Tx.colsum_acc(dy, o_r)
     Tx.colsum_acc(dy.to(DEV), o_g)
