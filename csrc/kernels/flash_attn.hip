@@ -34,6 +34,7 @@
 // guide's dual-use image (b), D=64 a swizzle over row bits 1, 3, 4 found the same way).
 #include "common.h"
 #include "dropout.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -471,6 +472,171 @@ dkv_kernel(const bf16* __restrict__ qkv, const float* __restrict__ key_bias, con
   }
 }
 
+// ------------------------------------------------------------------ backward, S = 128: fused
+// One block per (b, h) holds the whole 128-query x 128-key problem, so P is recomputed once
+// (not once per dq / dkv kernel) and there is one launch instead of two:
+// * phase 0: every wave forms dot = rowsum(dO * O) for its 32 queries; Q, dO (as the
+//   dkv_kernel's swap23 images) and K (natural row order, for the dQ GEMM's transposed
+//   reads) are staged in LDS;
+// * phase A (dkv_kernel orientation, lane = key): wave w owns keys 32w..32w+31, computes
+//   S = Q K^T and dP = dO V^T over both 64-query tiles, P from the saved log-sum-exp, dS,
+//   accumulates dV^T = dO^T Pd and dK^T = Q^T dS in registers, and writes dS (bf16) into a
+//   [query][key] LDS image;
+// * phase B (lane = query): wave w owns queries 32w..32w+31 and forms dQ^T = K^T dS^T from
+//   the K and dS images.
+// LDS: 3 x 16 KB operand images + the 32 KB dS image + lse / dot = 81 KB (one block per CU).
+// (A 65 KB variant with K staged over Q after phase A, two blocks per CU at 231 VGPRs,
+// measured 36.5 vs 28.3 us on BERT-base: the co-resident blocks share the matrix pipe and
+// the extra barrier/staging did not pay.)
+template <int D, bool DROP>
+__global__ void __launch_bounds__(NT)
+bwd128_kernel(const bf16* __restrict__ qkv, const float* __restrict__ key_bias, const bf16* __restrict__ out,
+              const bf16* __restrict__ dout, const float* __restrict__ lse, bf16* __restrict__ dqkv, int H,
+              float scale, float sl2, uint32_t thr, float inv_keep, const uint32_t* __restrict__ seedp,
+              uint32_t salt) {
+  constexpr int S = 128, NS = D / 16, NJ = D / 32, IMG = KT * D * 2;
+  constexpr int DS_BYTES = S * S * 2;
+  __shared__ __attribute__((aligned(16))) char smem[6 * IMG + DS_BYTES + 2 * S * 4];
+  char* Qi = smem;               // two 64-row images each, rows at swap23 (as Tile::store)
+  char* Oi = smem + 2 * IMG;
+  char* Ki = smem + 4 * IMG;     // 128 rows in natural order
+  char* dSi = smem + 6 * IMG;    // [query at swap23][key] bf16, 256-B rows
+  float* Ls = reinterpret_cast<float*>(dSi + DS_BYTES);
+  float* Dt = Ls + S;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, l32 = lane & 31;
+  const Geo G = geo(H, 1);
+  const int E = H * D, ld = 3 * E;
+  const bf16* Qg = qkv + (size_t)G.b * S * ld + G.hd * D;
+  const bf16* Kg = Qg + E;
+  const bf16* Vg = Qg + 2 * E;
+  const bf16* Og = out + (size_t)G.b * S * E + G.hd * D;
+  const bf16* dOg = dout + (size_t)G.b * S * E + G.hd * D;
+  const uint32_t seed = seedp ? *seedp : 0u;
+  // ---- phase 0
+  {
+    Tile<D> q0, q1, o0, o1, k0, k1;
+    q0.load(Qg, ld, tid);
+    q1.load(Qg + (size_t)KT * ld, ld, tid);
+    o0.load(dOg, E, tid);
+    o1.load(dOg + (size_t)KT * E, E, tid);
+    k0.load(Kg, ld, tid);
+    k1.load(Kg + (size_t)KT * ld, ld, tid);
+    const int qr = 32 * w + l32;
+    float dt = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const bf16x8 of = gfrag(dOg, E, qr, s, lane), ov = gfrag(Og, E, qr, s, lane);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dt += (float)of[e] * (float)ov[e];
+    }
+    dt += __shfl_xor(dt, 32, 64);
+    if (hh == 0) {
+      Dt[qr] = dt;
+      Ls[qr] = lse[(size_t)G.bh * S + qr] * LOG2E;
+    }
+    q0.store(Qi, tid);
+    q1.store(Qi + IMG, tid);
+    o0.store(Oi, tid);
+    o1.store(Oi + IMG, tid);
+    constexpr int CH = D / 8;
+#pragma unroll
+    for (int j = 0; j < Tile<D>::N; ++j) {   // K rows in natural order
+      const int c = tid + NT * j, r = c / CH, ch = c % CH;
+      *reinterpret_cast<uint4*>(Ki + off<D>(r, ch)) = k0.v[j];
+      *reinterpret_cast<uint4*>(Ki + off<D>(r + KT, ch)) = k1.v[j];
+    }
+  }
+  // this wave's keys: K / V fragments (B operands) and the key bias
+  const int key = 32 * w + l32;
+  bf16x8 kf[NS], vf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    kf[s] = gfrag(Kg, ld, key, s, lane);
+    vf[s] = gfrag(Vg, ld, key, s, lane);
+  }
+  const float kbl = key_bias ? key_bias[(size_t)G.b * S + key] * LOG2E : 0.f;
+  __syncthreads();
+  // ---- phase A
+  f32x16 dk[NJ], dv[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    zero(dk[j]);
+    zero(dv[j]);
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const char* Qt = Qi + t * IMG;
+    const char* Ot = Oi + t * IMG;
+    f32x16 sc[2], dp[2];   // C[q][key]: lane = key, register r = query 64t + 32i + acc_row(r, hh)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      zero(sc[i]);
+      zero(dp[i]);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        sc[i] = mfma(rowf<D>(Qt, 32 * i + l32, s, lane), kf[s], sc[i]);
+        dp[i] = mfma(rowf<D>(Ot, 32 * i + l32, s, lane), vf[s], dp[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int q0 = KT * t + 32 * i + 8 * g + 4 * hh;   // registers 4g..4g+3: queries q0..q0+3
+        const f32x4 L4 = *reinterpret_cast<const f32x4*>(Ls + q0);
+        const f32x4 D4 = *reinterpret_cast<const f32x4*>(Dt + q0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e;
+          const float p = __builtin_amdgcn_exp2f(sc[i][r] * sl2 + kbl - L4[e]);
+          float d = dp[i][r], pd = p;
+          if constexpr (DROP) {
+            const bool kp = keep(seed, salt, ((uint32_t)G.bh * S + q0 + e) * S + key, thr);
+            d = kp ? d * inv_keep : 0.f;
+            pd = kp ? p * inv_keep : 0.f;
+          }
+          const float ds = scale * p * (d - D4[e]);
+          dp[i][r] = ds;
+          sc[i][r] = pd;
+          *reinterpret_cast<bf16*>(dSi + off<128>(swap23(q0 + e), key >> 3) + (key & 7) * 2) = (bf16)ds;
+        }
+      }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pb = acc_frag(sc[i], s);
+        const bf16x8 sb = acc_frag(dp[i], s);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          dv[j] = mfma(trf<D>(Ot, 32 * j, 32 * i + 16 * s, lane), pb, dv[j]);
+          dk[j] = mfma(trf<D>(Qt, 32 * j, 32 * i + 16 * s, lane), sb, dk[j]);
+        }
+      }
+  }
+  {
+    bf16* dst = dqkv + ((size_t)G.b * S + key) * ld + G.hd * D;
+    store_rows<NJ>(dst + E, dk, lane);
+    store_rows<NJ>(dst + 2 * E, dv, lane);
+  }
+  __syncthreads();   // every wave's dS is in the image
+  // ---- phase B: dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q], lane = query 32w + l32
+  f32x16 dq[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) zero(dq[j]);
+  const int qr = 32 * w + l32;
+#pragma unroll
+  for (int s = 0; s < S / 16; ++s) {
+    const bf16x8 sb = rowf<128>(dSi, qr, s, lane);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) dq[j] = mfma(trf<D>(Ki, 32 * j, 16 * s, lane), sb, dq[j]);
+  }
+  store_rows<NJ>(dqkv + ((size_t)G.b * S + qr) * ld + G.hd * D, dq, lane);
+}
+
+// MLC_ATTN_BWD128=0 routes S = 128, D = 64 back to the dq / dkv kernel pair
+int g_bwd128 = -1;
+
 bool flash_shape_ok(int B, int S, int H, int D) {
   return B > 0 && H > 0 && S >= KT && S % KT == 0 && (D == 64 || D == 128);
 }
@@ -499,9 +665,23 @@ MLC_EXPORT int mlc_flash_fwd(const bf16* qkv, const float* key_bias, bf16* out, 
 MLC_EXPORT int mlc_flash_bwd(const bf16* qkv, const float* key_bias, const bf16* out, const bf16* dout,
                              const float* lse, float* dot, bf16* dqkv, int B, int S, int H, int D, float scale,
                              float p, const uint32_t* seed, uint32_t salt, hipStream_t st) {
+  if (g_bwd128 < 0) {
+    const char* e = getenv("MLC_ATTN_BWD128");
+    g_bwd128 = e ? atoi(e) : 1;
+  }
   if (!flash_shape_ok(B, S, H, D)) return -1;
   const uint32_t t = p > 0.f ? drop_threshold(p) : 0u;
   const float k = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  if (S == 128 && D == 64 && g_bwd128) {   // whole-problem fused backward (MLC_ATTN_BWD128)
+    const dim3 grid(B * H);
+    if (t)
+      hipLaunchKernelGGL((bwd128_kernel<64, true>), grid, dim3(NT), 0, st, qkv, key_bias, out, dout, lse, dqkv, H,
+                         scale, scale * LOG2E, t, k, seed, salt);
+    else
+      hipLaunchKernelGGL((bwd128_kernel<64, false>), grid, dim3(NT), 0, st, qkv, key_bias, out, dout, lse, dqkv, H,
+                         scale, scale * LOG2E, t, k, seed, salt);
+    return hipGetLastError();
+  }
   const int nb = (S + 127) / 128;
   const dim3 grid(B * H * nb);
 #define BWD(DD, DR)                                                                                              \
@@ -516,3 +696,16 @@ MLC_EXPORT int mlc_flash_bwd(const bf16* qkv, const float* key_bias, const bf16*
 #undef BWD
   return hipGetLastError();
 }
+
+// A/B knob of the S = 128 fused backward: value 0 / 1 sets it, < 0 only reads; returns the
+// previous setting (resolving MLC_ATTN_BWD128 first)
+MLC_EXPORT int mlc_flash_bwd128(int value) {
+  if (g_bwd128 < 0) {
+    const char* e = getenv("MLC_ATTN_BWD128");
+    g_bwd128 = e ? atoi(e) : 1;
+  }
+  const int old = g_bwd128;
+  if (value >= 0) g_bwd128 = value ? 1 : 0;
+  return old;
+}
+

@@ -51,6 +51,7 @@ _SIGS = {
     'mlc_attn_bwd': [vp] * 5 + [i32, i32, i32, f32, f32, vp, u32, vp],
     'mlc_flash_fwd': [vp] * 4 + [i32] * 4 + [f32, f32, vp, u32, vp],
     'mlc_flash_bwd': [vp] * 7 + [i32] * 4 + [f32, f32, vp, u32, vp],
+    'mlc_flash_bwd128': [i32],
     'mlc_colsum_acc': [vp, vp, vp, i32, i32, vp],
     'mlc_dropout': [vp, vp, i64, f32, vp, u32, vp],
     'mlc_bn_stat_copies': [],

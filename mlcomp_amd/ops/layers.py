@@ -376,9 +376,12 @@ class ResidualBlock:
         # reads y_i and applies BN+ReLU in its conv and weight-gradient operand loaders.
         # Measured on MI355X (docs/kernels.md): the loader transform costs the 3x3 convs
         # more than the saved pass, so the default is off.
+        # Mode 3: only into 1x1 consumers over <= 64 channels, whose GEMM is a single K-tile
+        # on the register-staged loop anyway (no LDS-DMA given up for the transform).
         mode = int(os.environ.get('MLC_FUSE_BN_FWD', '0'))
+        one = lambda u: u.k == (1, 1) and u.stride == 1 and u.pad == 0  # noqa: E731
         self.fuse_into = [False] + [
-            mode >= 1 and prev.act and (mode >= 2 or (u.k == (1, 1) and u.stride == 1 and u.pad == 0))
+            mode >= 1 and prev.act and (mode == 2 or (one(u) and (mode != 3 or u.cin <= 64)))
             for prev, u in zip(units[:-1], units[1:])]
         self.dout_prereduced = False
         self._last = None   # (rec of the last unit, rec of down) of the latest forward

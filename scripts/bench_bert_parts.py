@@ -31,6 +31,16 @@ def main():
     scale = 1 / math.sqrt(D)
     fns = {}
     res = {}
+    lib = _lib.load()
+    for b128 in (0, 1):      # S = 128 fused backward off / on (flash path)
+        Tx._FLASH_ONLY = True
+        ctx, lse = Tx.attn_fwd(qkv, kb, B, S, H, scale, 0.1, seed, 7)
+
+        def f(b128=b128, c=ctx, l=lse):
+            lib.mlc_flash_bwd128(b128)
+            Tx._FLASH_ONLY = True
+            return Tx.attn_bwd(qkv, kb, dctx, l, B, S, H, scale, 0.1, seed, 7, ctx=c)
+        fns[f'attn_bwd_flash_p0.1_b128_{b128}'] = ({}, f)
     for kern in ('tile', 'flash'):
         Tx._FLASH_ONLY = kern == 'flash'
         for p in (0.0, 0.1):

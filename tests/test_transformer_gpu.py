@@ -195,6 +195,49 @@ def test_flash_attention_fwd_bwd(B, S, H, D, p, masked, monkeypatch):
         assert rel(dq_g[:, sl], dq_r[:, sl]) < 2e-2, part
 
 
+@pytest.mark.parametrize('B,H,p,masked', [(3, 4, 0.1, True), (2, 12, 0.0, False), (4, 2, 0.1, False)])
+def test_attention_bwd128_fused_matches_pair_and_reference(B, H, p, masked, monkeypatch):
+    """S = 128, head dim 64: the one-launch fused backward (bwd128_kernel) against the fp32
+    reference and against the dq / dkv kernel pair (MLC_ATTN_BWD128 off)."""
+    import math
+    from mlcomp_amd.ops import _lib
+    monkeypatch.setattr(Tx, '_FLASH_ONLY', True)
+    S, D = 128, 64
+    qkv = _bf(B * S, 3 * H * D, seed=26, scale=0.7)
+    dctx = _bf(B * S, H * D, seed=27)
+    kb = None
+    if masked:
+        kb = torch.zeros(B, S)
+        kb[0, S - 37:] = float('-inf')
+        kb[-1, :5] = -2.5
+        if B > 2:
+            kb[1] = float('-inf')         # a fully masked sequence
+    seed = torch.tensor([31], dtype=torch.int32)
+    scale = 1.0 / math.sqrt(D)
+    ctx_r, lse_r = Tx.attn_fwd(qkv, kb, B, S, H, scale, p, seed, 35, head_dim=D)
+    dq_r = Tx.attn_bwd(qkv, kb, dctx, lse_r, B, S, H, scale, p, seed, 35, head_dim=D, ctx=ctx_r)
+    kbg = kb.to(DEV) if kb is not None else None
+    ctx_g, lse_g = Tx.attn_fwd(qkv.to(DEV), kbg, B, S, H, scale, p, seed.to(DEV), 35, head_dim=D)
+    lib = _lib.load()
+    old = lib.mlc_flash_bwd128(-1)
+    outs = {}
+    try:
+        for mode in (1, 0):
+            lib.mlc_flash_bwd128(mode)
+            outs[mode] = Tx.attn_bwd(qkv.to(DEV), kbg, dctx.to(DEV), lse_g, B, S, H, scale, p, seed.to(DEV), 35,
+                                     head_dim=D, ctx=ctx_g)
+    finally:
+        lib.mlc_flash_bwd128(old)
+    torch.cuda.synchronize()
+    E = H * D
+    for part in range(3):   # dQ, dK, dV separately
+        sl = slice(part * E, (part + 1) * E)
+        assert rel(outs[1][:, sl], dq_r[:, sl]) < 2e-2, part
+        assert rel(outs[1][:, sl], outs[0][:, sl]) < 1e-2, part
+    if masked and B > 2:
+        assert outs[1][S:2 * S].abs().max().item() == 0
+
+
 def test_flash_attention_fully_masked_sequence(monkeypatch):
     """A sequence whose keys are all masked: zero context, lse = +inf, zero gradients (the
     reference softmax is NaN there and is zeroed the same way)."""
