@@ -82,6 +82,7 @@ _SIGS = {
     'mlc_sgd': [vp] * 5 + [i64, i64, i64, f32, f32, f32, i32, i32, vp],
     'mlc_adam': [vp] * 6 + [i64, i64, i64, f32, f32, f32, f32, i32, vp],
     'mlc_sqnorm': [vp, i64, vp, f32, vp],
+    'mlc_opt_config': [i32, i32],
     'mlc_comm_unique_id_bytes': [],
     'mlc_comm_get_unique_id': [vp],
     'mlc_comm_init': [vp, i32, i32, i32, vp],

@@ -15,6 +15,7 @@ from __future__ import annotations
 from typing import Optional, Tuple
 
 import contextlib
+import math
 import os
 import threading
 
@@ -738,10 +739,11 @@ def adam_step(p, g, m, v, pbf, hyper, ndecay, nbf, b1=0.9, b2=0.999, eps=1e-8, w
         d = d + wdv * p
     m.mul_(b1).add_((1 - b1) * d)
     v.mul_(b2).add_((1 - b2) * d * d)
-    upd = (m / bc1) / ((v / bc2).sqrt() + eps)
+    # torch.optim.Adam(W)'s form (csrc/kernels/optim.hip adam_kernel computes the same)
+    upd = m / (v.sqrt() / math.sqrt(bc2) + eps)
     if decoupled:
         p.sub_(lr * wdv * p)
-    p.sub_(lr * upd)
+    p.sub_((lr / bc1) * upd)
     if pbf is not None and nbf:
         pbf[:nbf].copy_(p[:nbf].to(torch.bfloat16))
 

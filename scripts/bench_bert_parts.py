@@ -71,11 +71,15 @@ def main():
     v = torch.zeros(n, device=dev)
     pbf = torch.empty(n, device=dev, dtype=torch.bfloat16)
     hyper = torch.tensor([1e-4, 1.0, 0.1, 0.001], device=dev)
-    fns['adam_110M'] = ({}, lambda: _lib.call('mlc_adam', _lib.ptr(pa), _lib.ptr(gr), _lib.ptr(m), _lib.ptr(v),
-                                              _lib.ptr(pbf), _lib.ptr(hyper), n, n - 1_000_000, n - 1_000_000,
-                                              0.9, 0.999, 1e-8, 0.01, 1, _lib.stream()))
+    for var in (0, 1, 2):    # Adam kernel variants (mlc_opt_config key 0)
+        def adam(var=var):
+            _lib.load().mlc_opt_config(0, var)
+            _lib.call('mlc_adam', _lib.ptr(pa), _lib.ptr(gr), _lib.ptr(m), _lib.ptr(v), _lib.ptr(pbf),
+                      _lib.ptr(hyper), n, n - 1_000_000, n - 1_000_000, 0.9, 0.999, 1e-8, 0.01, 1, _lib.stream())
+        fns[f'adam_110M_v{var}'] = ({}, adam)
     t = graph_time(fns, rounds=5, iters=10)
-    t['adam_110M_TBps'] = round(n * 30 / (t['adam_110M'] * 1e-6) / 1e12, 2)
+    for var in (0, 1, 2):
+        t[f'adam_110M_v{var}_TBps'] = round(n * 30 / (t[f'adam_110M_v{var}'] * 1e-6) / 1e12, 2)
     print(json.dumps(t), flush=True)
 
 

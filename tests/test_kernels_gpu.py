@@ -283,6 +283,29 @@ def test_sgd_adam():
     assert rel_err(pg, pc) < 1e-5
 
 
+@pytest.mark.parametrize('variant', [0, 1, 2])
+def test_adam_kernel_variants(variant):
+    """Every Adam kernel variant (float4 pairs / 8-float chunks / nontemporal) against the
+    CPU reference, with n % 8 == 4 and the decay / bf16-mirror boundaries inside a chunk."""
+    from mlcomp_amd.ops import _lib
+    lib = _lib.load()
+    old = lib.mlc_opt_config(0, variant)
+    try:
+        n, nd, nb = 8196, 4100, 4100
+        p, g = torch.randn(n), torch.randn(n)
+        hyper = torch.tensor([0.01, 0.5, 0.9, 0.99])
+        pc, mc, vc = p.clone(), torch.randn(n) * 0.1, torch.rand(n) * 0.1
+        pg, mg, vg = pc.to(DEV), mc.to(DEV), vc.to(DEV)
+        bfc, bfg = torch.zeros(n, dtype=torch.bfloat16), torch.zeros(n, dtype=torch.bfloat16, device=DEV)
+        Fn.adam_step(pc, g, mc, vc, bfc, hyper, nd, nb, wd=0.01)
+        Fn.adam_step(pg, g.to(DEV), mg, vg, bfg, hyper.to(DEV), nd, nb, wd=0.01)
+        torch.cuda.synchronize()
+        assert rel_err(pg, pc) < 1e-5 and rel_err(mg, mc) < 1e-6 and rel_err(vg, vc) < 1e-6
+        assert rel_err(bfg[:nb], bfc[:nb]) < 1e-2 and bfg[nb:].abs().max().item() == 0
+    finally:
+        lib.mlc_opt_config(0, old)
+
+
 @pytest.mark.parametrize('case', [(2, 16, 16, 64, 128, 1, 2, 0), (2, 14, 14, 64, 64, 3, 1, 1),
                                   (2, 16, 16, 64, 128, 3, 2, 1)])
 def test_conv_dgrad_addend(case):
