@@ -236,6 +236,87 @@ ln_bwd_finalize_kernel(const float* __restrict__ sums, float* __restrict__ dgamm
   dbeta[c] += b;
 }
 
+// all LayerNorms of a model in one launch: blockIdx.y picks the LayerNorm (its NSTAT sums
+// scratch, grad slots and width), the rest is ln_bwd_finalize_kernel.  The native BERT runs
+// it once at the end of backward instead of 25 finalize launches on the critical path.
+struct LnFin {
+  const float* sums;
+  float* dgamma;
+  float* dbeta;
+  long H;
+};
+__global__ void __launch_bounds__(NT)
+ln_finalize_many_kernel(const LnFin* __restrict__ d, int ncopy) {
+  constexpr int FL = 8;
+  const LnFin f = d[blockIdx.y];
+  const int H = (int)f.H;
+  const int c = blockIdx.x * (NT / FL) + (int)(threadIdx.x / FL), q = threadIdx.x % FL;
+  float g = 0.f, b = 0.f;
+  if (c < H) {
+#pragma unroll 4
+    for (int k = q; k < ncopy; k += FL) { g += f.sums[(size_t)k * 2 * H + c]; b += f.sums[(size_t)k * 2 * H + H + c]; }
+  }
+#pragma unroll
+  for (int o = 1; o < FL; o <<= 1) { g += __shfl_xor(g, o, 64); b += __shfl_xor(b, o, 64); }
+  if (c >= H || q != 0) return;
+  f.dgamma[c] += g;
+  f.dbeta[c] += b;
+}
+
+// ------------------------------------------------------------------ embedding backward
+// dE = ds [B*S][H] bf16 scattered into the three embedding gradients, two launches:
+// * embed_bwd_kernel, block (s, y) = position s, batch rows y*BB .. y*BB+BB-1, threads along
+//   the columns (4 each) so every atomic wave-instruction covers 256 contiguous bytes of one
+//   row (64 lanes in 64 rows run ~17x slower, MI355X_MICROARCH.md float atomics):
+//   word[ids[t]] += ds[t] (fp32 atomics, as index_add) and pt[s][k] += the block's sum over
+//   its tokens of type k (gridDim.y adders per address);
+// * embed_bwd_finish_kernel: pos[s] += sum_k pt[s][k], tok[k] += sum_s pt[s][k], and pt is
+//   zeroed again for the next step.  (Summing tok_type straight from every block put ~500
+//   adders on each address of one 3 KB row: the whole pass took 98 us.)
+constexpr int EMB_MAXT = 4;
+__global__ void __launch_bounds__(NT)
+embed_bwd_kernel(const bf16* __restrict__ ds, const long* __restrict__ ids, const long* __restrict__ tt,
+                 float* __restrict__ word, float* __restrict__ pt, int B, int S, int H, int ntypes, int BB) {
+  const int s = blockIdx.x;
+  const int b0 = blockIdx.y * BB, b1 = min(B, b0 + BB);
+  // lane-consecutive columns: each atomic wave-instruction is 64 consecutive floats
+  for (int c = threadIdx.x; c < H; c += NT) {
+    float ta[EMB_MAXT] = {0.f, 0.f, 0.f, 0.f};
+    for (int b = b0; b < b1; ++b) {
+      const long t = (long)b * S + s;
+      const float d = (float)ds[t * H + c];
+      atomicAdd(word + ids[t] * H + c, d);
+      const int ty = tt ? (int)tt[t] : 0;
+#pragma unroll
+      for (int k = 0; k < EMB_MAXT; ++k) ta[k] += ty == k ? d : 0.f;
+    }
+    for (int k = 0; k < ntypes; ++k) atomicAdd(pt + ((long)s * ntypes + k) * H + c, ta[k]);
+  }
+}
+
+constexpr int EMB_SB = 8;   // positions per finish thread
+__global__ void __launch_bounds__(NT)
+embed_bwd_finish_kernel(float* __restrict__ pt, float* __restrict__ pos, float* __restrict__ tok, int S, int H,
+                        int ntypes) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= H) return;
+  const int s0 = blockIdx.y * EMB_SB, s1 = min(S, s0 + EMB_SB);
+  float tk[EMB_MAXT] = {0.f, 0.f, 0.f, 0.f};
+  for (int s = s0; s < s1; ++s) {
+    float ps = 0.f;
+    for (int k = 0; k < ntypes; ++k) {
+      float* q = pt + ((long)s * ntypes + k) * H + c;
+      const float v = *q;
+      *q = 0.f;
+      ps += v;
+      tk[k] += v;
+    }
+    pos[(long)s * H + c] += ps;
+  }
+  if (tok)
+    for (int k = 0; k < ntypes; ++k) atomicAdd(tok + (long)k * H + c, tk[k]);
+}
+
 // ------------------------------------------------------------------ softmax
 // rows of length L (keys); row r belongs to batch (r / rows_per_batch) for the key bias
 template <int MAXC>
@@ -749,9 +830,35 @@ MLC_EXPORT int mlc_ln_bwd(const bf16* dy, const bf16* s, const float* mean, cons
                        ds, dr, sums, T, H, ti, ki, to, ko, seed, salt_in, salt_out, g_mlc_ncopy);
     return (int)hipGetLastError();
   });
-  if (rc) return rc;
+  if (rc || !dgamma) return rc;   // no dgamma: the caller finalizes later (mlc_ln_finalize_many)
   hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((H + NT / 8 - 1) / (NT / 8)), dim3(NT), 0, st, sums, dgamma, dbeta, H,
                      g_mlc_ncopy);
+  return hipGetLastError();
+}
+
+// word/pos/tok += the embedding gradient ds (see embed_bwd_kernel); ids/tt int64 [B*S]
+// (token types < ntypes <= 4; tt and tok null: one type, no token-type table); pt: fp32
+// scratch [S][ntypes][H], zero on entry and left zeroed.  H % 4 == 0.
+MLC_EXPORT int mlc_embed_bwd(const bf16* ds, const long* ids, const long* tt, float* word, float* pos, float* tok,
+                             float* pt, int B, int S, int H, int ntypes, hipStream_t st) {
+  if (H % 4 || S < 1 || ntypes < 1 || ntypes > EMB_MAXT || (tok != nullptr) != (tt != nullptr)) return -1;
+  int ny = (512 + S - 1) / S;                  // ~512 blocks: split the batch rows
+  if (ny > B) ny = B;
+  if (ny < 1) ny = 1;
+  const int BB = (B + ny - 1) / ny;
+  const dim3 grid(S, (B + BB - 1) / BB);
+  hipLaunchKernelGGL(embed_bwd_kernel, grid, dim3(NT), 0, st, ds, ids, tt, word, pt, B, S, H, ntypes, BB);
+  hipLaunchKernelGGL(embed_bwd_finish_kernel, dim3((H + NT - 1) / NT, (S + EMB_SB - 1) / EMB_SB), dim3(NT), 0, st, pt,
+                     pos, tok, S, H, ntypes);
+  return hipGetLastError();
+}
+
+// desc: n LnFin entries in device memory (sums scratch of NSTAT copies, dgamma, dbeta, H);
+// every dgamma/dbeta += the sum of its copies.  maxH bounds the widths.
+MLC_EXPORT int mlc_ln_finalize_many(const void* desc, int n, int maxH, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(ln_finalize_many_kernel, dim3((maxH + NT / 8 - 1) / (NT / 8), n), dim3(NT), 0, st,
+                     reinterpret_cast<const LnFin*>(desc), g_mlc_ncopy);
   return hipGetLastError();
 }
 

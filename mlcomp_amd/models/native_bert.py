@@ -37,6 +37,11 @@ from .bert import BertForSequenceClassification
 # the pre-activation, so the input-gradient GEMM of the second only multiplies by it (no erf
 # / exp in that epilogue); 0 keeps the pre-activation and recomputes the derivative.
 GELU_DERIV = os.environ.get('MLC_GELU_DERIV', '1') == '1'
+# MLC_LN_DEFER=1 (default): the LayerNorm backward kernels leave their dgamma/dbeta partial
+# sums in the workspace and ONE launch at the end of backward (Tx.LnFinalizer) adds all 25 of
+# them into the gradient arena, instead of a finalize launch after each LayerNorm backward;
+# the LayerNorm slots are marked ready for the bucketer then.
+LN_DEFER = os.environ.get('MLC_LN_DEFER', '1') == '1'
 
 
 class _Dense:
@@ -141,6 +146,15 @@ class _LN:
         self.ctx.arena.mark_ready(self.g)
         self.ctx.arena.mark_ready(self.b)
 
+    def bwd(self, dy, s, mean, rstd, **kw):
+        """Tx.ln_bwd into this LayerNorm's slots; with LN_DEFER the finalize (and the
+        mark) waits for the model's LnFinalizer."""
+        out = Tx.ln_bwd(dy, s, mean, rstd, self.g.master, self.g.grad, self.b.grad, self.ctx.ws[self.k_sums],
+                        defer_finalize=LN_DEFER, **kw)
+        if not LN_DEFER:
+            self.mark()
+        return out
+
 
 class NativeBertLayer:
     def __init__(self, net: 'NativeBert', idx: int, layer):
@@ -193,20 +207,15 @@ class NativeBertLayer:
 
     def bwd(self, dh2, saved, key_bias):
         net = self.net
-        ws = net.ctx.ws
         B, S, nh, dh = net.B, net.S, net.c.heads, net.c.head_dim
         pa, ph = net.p_attn, net.p_hidden
         fused = Tx.attn_supported(S, dh)
         x, att = saved[0], saved[1:3] if fused else saved[1:6]
         ctx2, s1, m1, r1, h1, u, g, s2, m2, r2 = saved[len(att) + 1:]
-        ds2, df = Tx.ln_bwd(dh2, s2, m2, r2, self.ln2.g.master, self.ln2.g.grad, self.ln2.b.grad,
-                            ws[self.ln2.k_sums], p_in=ph, seed=net.seed, salt_in=self.salt + 2, want_dr=True)
-        self.ln2.mark()
+        ds2, df = self.ln2.bwd(dh2, s2, m2, r2, p_in=ph, seed=net.seed, salt_in=self.salt + 2, want_dr=True)
         du = self.ffn2.backward(df, g, dact_u=u, dact_is_deriv=GELU_DERIV)   # grad of the GELU input
         dh1 = self.ffn1.backward(du, h1, addend=ds2)      # + residual branch
-        ds1, dao = Tx.ln_bwd(dh1, s1, m1, r1, self.ln1.g.master, self.ln1.g.grad, self.ln1.b.grad,
-                             ws[self.ln1.k_sums], p_in=ph, seed=net.seed, salt_in=self.salt + 1, want_dr=True)
-        self.ln1.mark()
+        ds1, dao = self.ln1.bwd(dh1, s1, m1, r1, p_in=ph, seed=net.seed, salt_in=self.salt + 1, want_dr=True)
         dctx2 = self.out.backward(dao, ctx2)
         if fused:
             qkv, lse = att
@@ -254,10 +263,18 @@ class _EmbedFn(torch.autograd.Function):
     def backward(ctx, dy):
         net = ctx.net
         ids, tt, s, m, r = ctx.saved_tensors
-        ds, _ = Tx.ln_bwd(dy.contiguous(), s, m, r, net.ln.g.master, net.ln.g.grad, net.ln.b.grad,
-                          net.ctx.ws[net.ln.k_sums], p_out=net.p_hidden, seed=net.seed, salt_out=1)
-        net.ln.mark()
+        ds, _ = net.ln.bwd(dy.contiguous(), s, m, r, p_out=net.p_hidden, seed=net.seed, salt_out=1)
+        if LN_DEFER:   # the last LayerNorm backward of the step: finalize all of them at once
+            net.ln_fin.run()
+            for ln in net.all_lns():
+                ln.mark()
         B, S = ids.shape
+        if not _lib.DETERMINISTIC and net.tok_type.grad.shape[0] <= 4:
+            # one kernel: word atomics, per-position and per-type sums (Tx.embed_bwd)
+            Tx.embed_bwd(ds, ids, tt, net.word.grad, net.pos.grad, net.tok_type.grad)
+            for sl in (net.word, net.pos, net.tok_type):
+                net.ctx.arena.mark_ready(sl)
+            return None, None, None, None
         d = ds.float().view(B, S, -1)
         if _lib.DETERMINISTIC:
             # index_add_ races float atomics on repeated ids (and the sort-based scatter
@@ -338,7 +355,17 @@ class NativeBert:
         ctx.finalize(device)
         self.device = ctx.device
         self.seed = torch.zeros(1, device=self.device, dtype=torch.int32)
+        self.ln_fin = Tx.LnFinalizer()
+        for ln in self.all_lns():
+            self.ln_fin.add(ctx.ws[ln.k_sums], ln.g.grad, ln.b.grad)
+        self.ln_fin.build()
         self.load_from_torch()
+
+    def all_lns(self):
+        yield self.ln
+        for l in self.layers:
+            yield l.ln1
+            yield l.ln2
 
     # ------------------------------------------------------------------ weights
     def _dense_parts(self):

@@ -40,6 +40,8 @@ _SIGS = {
     'mlc_gemm_bf16_ex': [vp, vp, vp] + [i32] * 8 + [vp, i32, vp, vp, vp, vp, i64, vp],
     'mlc_ln_fwd': [vp] * 8 + [i32, i32, f32, f32, f32, vp, u32, u32, vp],
     'mlc_ln_bwd': [vp] * 10 + [i32, i32, f32, f32, vp, u32, u32, vp],
+    'mlc_ln_finalize_many': [vp, i32, i32, vp],
+    'mlc_embed_bwd': [vp] * 7 + [i32] * 4 + [vp],
     'mlc_softmax_fwd': [vp] * 4 + [i64, i32, i32, f32, f32, vp, u32, vp],
     'mlc_softmax_bwd': [vp] * 3 + [i64, i32, f32, f32, vp, u32, vp],
     'mlc_linear_wgrad_bias': [vp] * 4 + [i32] * 7 + [vp, i64, vp],

@@ -73,17 +73,21 @@ def ln_fwd(x, r, gamma, beta, eps=1e-12, p_in=0.0, p_out=0.0, seed=None, salt_in
 
 
 def ln_bwd(dy, s, mean, rstd, gamma, dgamma, dbeta, sums=None, p_in=0.0, p_out=0.0, seed=None, salt_in=0,
-           salt_out=0, want_dr=False):
+           salt_out=0, want_dr=False, defer_finalize=False):
     """Returns (ds, dr): ds = dLoss/ds, dr = dropout_in'(ds) (None unless ``want_dr``).
-    dgamma / dbeta are ACCUMULATED (+=)."""
+    dgamma / dbeta are ACCUMULATED (+=).  ``defer_finalize`` (GPU): leave the per-copy
+    partial sums in ``sums`` for a later :class:`LnFinalizer` launch (dgamma/dbeta untouched
+    until then)."""
     T, H = dy.shape
     if _cuda(dy):
         ds = torch.empty_like(dy)
         dr = torch.empty_like(dy) if want_dr else None
         if sums is None:
+            assert not defer_finalize, 'a deferred finalize needs a persistent sums scratch'
             sums = torch.zeros(NSTAT * 2 * H, device=dy.device, dtype=torch.float32)
+        dg, db = (None, None) if defer_finalize else (dgamma, dbeta)
         _lib.call('mlc_ln_bwd', _lib.ptr(dy), _lib.ptr(s), _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(gamma),
-                  _lib.ptr(ds), _lib.ptr(dr), _lib.ptr(sums), _lib.ptr(dgamma), _lib.ptr(dbeta), T, H, float(p_in),
+                  _lib.ptr(ds), _lib.ptr(dr), _lib.ptr(sums), _lib.ptr(dg), _lib.ptr(db), T, H, float(p_in),
                   float(p_out), _lib.ptr(seed), salt_in, salt_out, _lib.stream())
         return ds, dr
     sd = _seed_val(seed)
@@ -105,6 +109,60 @@ def ln_bwd(dy, s, mean, rstd, gamma, dgamma, dbeta, sums=None, p_in=0.0, p_out=0
             drf = torch.where(keep_mask((T, H), p_in, sd, salt_in), dsf / (1 - p_in), torch.zeros_like(dsf))
         dr = drf.to(torch.bfloat16)
     return ds, dr
+
+
+_EMB_SCRATCH = {}
+
+
+def embed_bwd(ds, ids, tt, word_grad, pos_grad, tok_grad):
+    """Embedding gradients from ds [B*S, H] (bf16): word_grad[ids] += ds, pos_grad[s] +=
+    sum over the batch, tok_grad[tt] += ds (all fp32, accumulated).  ids / tt int64 [B, S]."""
+    B, S = ids.shape
+    H = ds.shape[-1]
+    if _cuda(ds):
+        ntypes = tok_grad.shape[0] if tok_grad is not None else 1
+        key = (str(ds.device), S * ntypes * H)
+        pt = _EMB_SCRATCH.get(key)
+        if pt is None:    # [S][ntypes][H] partial sums, left zeroed by the kernel
+            pt = _EMB_SCRATCH[key] = torch.zeros(S * ntypes * H, device=ds.device, dtype=torch.float32)
+        _lib.call('mlc_embed_bwd', _lib.ptr(ds.contiguous()), _lib.ptr(ids.contiguous()),
+                  _lib.ptr(tt.contiguous() if tok_grad is not None else None), _lib.ptr(word_grad),
+                  _lib.ptr(pos_grad), _lib.ptr(tok_grad), _lib.ptr(pt), B, S, H, ntypes, _lib.stream())
+        return
+    d = ds.float().reshape(B * S, H)
+    word_grad.index_add_(0, ids.reshape(-1), d)
+    if tok_grad is not None:
+        tok_grad.index_add_(0, tt.reshape(-1), d)
+    pos_grad[:S].add_(d.view(B, S, H).sum(0))
+
+
+class LnFinalizer:
+    """Finalizes the dgamma / dbeta of many LayerNorms in ONE launch
+    (``mlc_ln_finalize_many``): each entry's ``ln_bwd(..., defer_finalize=True)`` left its
+    partial sums in a persistent NSTAT-copy scratch; ``run()`` adds every sum into its grad
+    slots.  The descriptor table is built once (pointers must stay put), outside capture."""
+
+    def __init__(self):
+        self.entries = []        # (sums [NSTAT*2*H], dgamma [H], dbeta [H])
+        self.desc = None
+        self.max_h = 0
+
+    def add(self, sums, dgamma, dbeta):
+        self.entries.append((sums, dgamma, dbeta))
+
+    def build(self):
+        if not self.entries or not self.entries[0][0].is_cuda:
+            return
+        rows = [[s.data_ptr(), g.data_ptr(), b.data_ptr(), g.numel()] for s, g, b in self.entries]
+        self.desc = torch.tensor(rows, dtype=torch.int64).to(self.entries[0][0].device)
+        self.max_h = max(g.numel() for _, g, _ in self.entries)
+
+    def run(self):
+        if not self.entries or not self.entries[0][0].is_cuda:
+            return       # the CPU path of ln_bwd accumulates immediately
+        if self.desc is None:
+            self.build()
+        _lib.call('mlc_ln_finalize_many', _lib.ptr(self.desc), len(self.entries), self.max_h, _lib.stream())
 
 
 # ---------------------------------------------------------------------------- softmax
@@ -366,5 +424,5 @@ def dropout(x, p, seed, salt):
     return torch.where(m, x.float() / (1 - p), torch.zeros_like(x, dtype=torch.float32)).to(x.dtype)
 
 
-__all__ = ['ln_fwd', 'ln_bwd', 'softmax_fwd', 'softmax_bwd', 'dense_fwd', 'dense_dgrad', 'dact_gelu', 'colsum_acc',
+__all__ = ['ln_fwd', 'ln_bwd', 'LnFinalizer', 'embed_bwd', 'softmax_fwd', 'softmax_bwd', 'dense_fwd', 'dense_dgrad', 'dact_gelu', 'colsum_acc',
            'dropout', 'keep_mask']

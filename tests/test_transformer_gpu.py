@@ -344,3 +344,21 @@ def test_native_bert_step_trains_and_graph_matches():
     assert abs(a.last_loss() - b.last_loss()) < 1e-2 * max(1.0, abs(a.last_loss()))
     pa, pb = a.net.arena.decay.master, b.net.arena.decay.master
     assert ((pa - pb).norm() / pa.norm()).item() < 1e-3
+
+
+@pytest.mark.parametrize('B,S,H,ntypes', [(4, 128, 768, 2), (3, 40, 64, 1), (2, 512, 128, 4)])
+def test_embed_bwd_matches_index_add(B, S, H, ntypes):
+    """One-kernel embedding backward (word atomics, per-position and per-type sums) against
+    index_add on the CPU; repeated ids (a padding token) included."""
+    g = torch.Generator().manual_seed(3)
+    ds = (torch.randn(B * S, H, generator=g)).to(torch.bfloat16)
+    ids = torch.randint(0, 1000, (B, S), generator=g)
+    ids[:, S // 2:] = 0                       # many [PAD] rows hitting one word row
+    tt = torch.randint(0, ntypes, (B, S), generator=g)
+    ref = [torch.zeros(1000, H), torch.zeros(S + 3, H), torch.zeros(ntypes, H)]
+    Tx.embed_bwd(ds, ids, tt, *ref)
+    out = [t.to(DEV) for t in (torch.zeros(1000, H), torch.zeros(S + 3, H), torch.zeros(ntypes, H))]
+    Tx.embed_bwd(ds.to(DEV), ids.to(DEV), tt.to(DEV), *out)
+    torch.cuda.synchronize()
+    for o, r in zip(out, ref):
+        assert rel(o, r) < 1e-5
