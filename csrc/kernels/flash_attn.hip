@@ -634,7 +634,107 @@ bwd128_kernel(const bf16* __restrict__ qkv, const float* __restrict__ key_bias, 
   store_rows<NJ>(dqkv + ((size_t)G.b * S + qr) * ld + G.hd * D, dq, lane);
 }
 
-// MLC_ATTN_BWD128=0 routes S = 128, D = 64 back to the dq / dkv kernel pair
+// ------------------------------------------------------------------ forward, S = 128
+// The whole key range at once: K and V (128 rows each, two consecutive swap23 images = one
+// 128-row image) land in LDS behind ONE barrier, the 4 key tiles of S^T = K Q^T are formed,
+// and the softmax runs over the complete row (no running max / rescale), then O^T = V^T P^T.
+// Same numerics and dropout indexing as fwd_kernel.
+template <int D, bool DROP>
+__global__ void __launch_bounds__(NT)
+fwd128_kernel(const bf16* __restrict__ qkv, const float* __restrict__ key_bias, bf16* __restrict__ out,
+              float* __restrict__ lse, int H, float sl2, uint32_t thr, float inv_keep,
+              const uint32_t* __restrict__ seedp, uint32_t salt) {
+  constexpr int S = 128, NS = D / 16, NJ = D / 32, IMG = KT * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + S * 4];   // K (2 images) | V (2) | bias
+  char* Ki = smem;
+  char* Vi = smem + 2 * IMG;
+  float* Kb = reinterpret_cast<float*>(smem + 4 * IMG);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, l32 = lane & 31;
+  const Geo G = geo(H, 1);
+  const int E = H * D, ld = 3 * E;
+  const bf16* Qg = qkv + (size_t)G.b * S * ld + G.hd * D;
+  const bf16* Kg = Qg + E;
+  const bf16* Vg = Qg + 2 * E;
+  const int q = 32 * w + l32;
+  {
+    Tile<D> k0, k1, v0, v1;
+    k0.load(Kg, ld, tid);
+    k1.load(Kg + (size_t)KT * ld, ld, tid);
+    v0.load(Vg, ld, tid);
+    v1.load(Vg + (size_t)KT * ld, ld, tid);
+    if (tid < S) Kb[tid] = key_bias ? key_bias[(size_t)G.b * S + tid] * LOG2E : 0.f;
+    k0.store(Ki, tid);
+    k1.store(Ki + IMG, tid);
+    v0.store(Vi, tid);
+    v1.store(Vi + IMG, tid);
+  }
+  bf16x8 qf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) qf[s] = gfrag(Qg, ld, q, s, lane);
+  const uint32_t seed = seedp ? *seedp : 0u;
+  const uint32_t rowidx = ((uint32_t)G.bh * S + q) * S;
+  __syncthreads();
+  f32x16 a[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    zero(a[i]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) a[i] = mfma(rowf<D>(Ki, 32 * i + l32, s, lane), qf[s], a[i]);
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 k4 = *reinterpret_cast<const f32x4*>(Kb + 32 * i + 8 * g + 4 * hh);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = a[i][4 * g + e] * sl2 + k4[e];
+        a[i][4 * g + e] = x;
+        m = fmaxf(m, x);
+      }
+    }
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  const float mref = m == -INFINITY ? 0.f : m;
+  float l = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = __builtin_amdgcn_exp2f(a[i][r] - mref);
+      l += e;
+      a[i][r] = e;
+    }
+  if constexpr (DROP) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        a[i][r] = keep(seed, salt, rowidx + 32 * i + acc_row(r, hh), thr) ? a[i][r] * inv_keep : 0.f;
+  }
+  f32x16 o[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) zero(o[j]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 pb = acc_frag(a[i], s);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) o[j] = mfma(trf<D>(Vi, 32 * j, 32 * i + 16 * s, lane), pb, o[j]);
+    }
+  l += __shfl_xor(l, 32, 64);
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[j][r] *= inv;
+  if (hh == 0) lse[(size_t)G.bh * S + q] = l > 0.f ? (m + __log2f(l)) * LN2 : INFINITY;
+  store_rows<NJ>(out + ((size_t)G.b * S + q) * E + G.hd * D, o, lane);
+}
+
+// MLC_ATTN_BWD128=0 routes S = 128, D = 64 back to the streaming kernels (fwd_kernel and the
+// dq / dkv pair)
 int g_bwd128 = -1;
 
 bool flash_shape_ok(int B, int S, int H, int D) {
@@ -650,6 +750,20 @@ MLC_EXPORT int mlc_flash_fwd(const bf16* qkv, const float* key_bias, bf16* out, 
   if (!flash_shape_ok(B, S, H, D)) return -1;
   const uint32_t t = p > 0.f ? drop_threshold(p) : 0u;
   const float k = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  if (g_bwd128 < 0) {
+    const char* e = getenv("MLC_ATTN_BWD128");
+    g_bwd128 = e ? atoi(e) : 1;
+  }
+  if (S == 128 && D == 64 && g_bwd128) {   // whole-key-range forward (MLC_ATTN_BWD128 covers both)
+    const dim3 grid(B * H);
+    if (t)
+      hipLaunchKernelGGL((fwd128_kernel<64, true>), grid, dim3(NT), 0, st, qkv, key_bias, out, lse, H, scale * LOG2E,
+                         t, k, seed, salt);
+    else
+      hipLaunchKernelGGL((fwd128_kernel<64, false>), grid, dim3(NT), 0, st, qkv, key_bias, out, lse, H, scale * LOG2E,
+                         t, k, seed, salt);
+    return hipGetLastError();
+  }
   const int nqb = (S + 127) / 128;
   const dim3 grid(B * H * nqb);
 #define FWD(DD, DR) hipLaunchKernelGGL((fwd_kernel<DD, DR>), grid, dim3(NT), 0, st, qkv, key_bias, out, lse, S, H, nqb, \

@@ -41,6 +41,12 @@ def main():
             Tx._FLASH_ONLY = True
             return Tx.attn_bwd(qkv, kb, dctx, l, B, S, H, scale, 0.1, seed, 7, ctx=c)
         fns[f'attn_bwd_flash_p0.1_b128_{b128}'] = ({}, f)
+
+        def ff(b128=b128):
+            lib.mlc_flash_bwd128(b128)
+            Tx._FLASH_ONLY = True
+            return Tx.attn_fwd(qkv, kb, B, S, H, scale, 0.1, seed, 7)
+        fns[f'attn_fwd_flash_p0.1_b128_{b128}'] = ({}, ff)
     for kern in ('tile', 'flash'):
         Tx._FLASH_ONLY = kern == 'flash'
         for p in (0.0, 0.1):
