@@ -626,3 +626,4 @@ def test_linear_lds_dma(B, I, O, gemm_dma):
     dg = Tx.dense_dgrad(dy.to(DEV), w.to(DEV))
     torch.cuda.synchronize()
     assert rel_err(dg, dr) < 1e-2
+
