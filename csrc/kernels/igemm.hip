@@ -1270,9 +1270,17 @@ static int g_split_target = 384;
 // single-LDS-stage variant for single-K-tile splits (A/B knob 5)
 static int g_single_stage = 1;
 static int g_split_target_mat = 128;
-// dense-layer weight gradients (mlc_linear_wgrad_bias, mlc_gemm_f32out) keep 256: at 128
-// the BERT-base step lost 3 % (A/B knob 9)
-static int g_split_target_dense = 256;
+// dense-layer weight gradients (mlc_linear_wgrad_bias, mlc_gemm_f32out), A/B knob 9.
+// Round 2 kept 256 (128 lost 3 %); once the bf16 dgrads stopped splitting (knob 12 = 0)
+// 128 became the better point: BERT-base 5041/5096 vs 5021/4991 seq/s at 256, 64 lost
+// 2 % (profiles/round3/session2/wgrad_split_ab.txt)
+static int g_split_target_dense = 128;
+// bf16-output dense GEMMs on the 128x128 path (BERT's input gradients with MN-contiguous
+// weights) split K until tiles * splits reaches this (A/B knob 12, MLC_DENSE_SPLIT_TARGET;
+// 0 never splits).  Default 0 since round 3: unsplit 192-tile dgrads with the epilogue in
+// the GEMM beat split-K 2 + slab finalize by 4.3 % on the BERT-base step (5041/5058 vs
+// 4853/4821 seq/s, profiles/round3/session2/dense_split_ab.txt); 768 lost 4.5 %.
+static int g_dense_bf16_split_target = 0;
 // LDS-DMA main loop (PF = 3) for GEMMs whose two operands both have an enabled DMA copy
 // (the K-contiguous MatKC / ConvFwdA: forward convs, stride-1 dgrads, dense forward):
 // A/B knob 8; -1: read MLC_GEMM_DMA on first use (default 1: ResNet-50 +1.2 %, U-Net
@@ -1436,7 +1444,8 @@ MLC_EXPORT int mlc_gemm_get_set(int key, int value) {
           : key == 4 ? &igemm::g_big_min_blocks : key == 5 ? &igemm::g_single_stage
           : key == 6 ? &igemm::g_splitk_fused : key == 7 ? &igemm::g_dense_narrow
           : key == 8 ? &igemm::g_gemm_dma : key == 9 ? &igemm::g_split_target_dense
-          : key == 10 ? &igemm::g_dense_tile : key == 11 ? &igemm::g_dense_split : nullptr;
+          : key == 10 ? &igemm::g_dense_tile : key == 11 ? &igemm::g_dense_split
+          : key == 12 ? &igemm::g_dense_bf16_split_target : nullptr;
   if (!k) return -1;
   if (key == 10 || key == 11) {   // resolve the env defaults before the first override
     int sp = 1;
@@ -1447,7 +1456,7 @@ MLC_EXPORT int mlc_gemm_get_set(int key, int value) {
     if (value >= -1) *k = value;
     return old;
   }
-  if (value >= 0 && (value > 0 || key == 3 || key == 5 || key == 6 || key == 7 || key == 8)) *k = value;
+  if (value >= 0 && (value > 0 || key == 3 || key == 5 || key == 6 || key == 7 || key == 8 || key == 12)) *k = value;
   return old;
 }
 
@@ -1899,7 +1908,8 @@ MLC_EXPORT int mlc_gemm_bf16_ex(const bf16* A, const bf16* B, bf16* C, int M, in
     if (!ta && !tb) return launch<128, 64>(GA_KC(128), GB_MC(64), epi, M, N, K, 1, st);
   }
   if (ws)
-    while (tiles * splits < 384 && ktiles / (splits * 2) >= 4 && slab * splits * 2 <= ws_floats) splits *= 2;
+    while (tiles * splits < g_dense_bf16_split_target && ktiles / (splits * 2) >= 4 && slab * splits * 2 <= ws_floats)
+      splits *= 2;
   if (splits > 1) {
     {  // the launch rounds splits so that no split is empty: finish exactly those slabs
       const int per = (ktiles + splits - 1) / splits;
