@@ -71,7 +71,7 @@ def main():
         dist.init_process_group('nccl', device_id=device)
 
     is_bert = args.model.startswith('bert')
-    is_unet = args.model.startswith('unet')
+    is_unet = args.model.startswith('unet') or args.model.startswith('linknet')
     if args.batch is None:
         args.batch = 32 if (is_bert or is_unet) else 256
     if is_unet:
@@ -79,9 +79,11 @@ def main():
         from mlcomp_amd.train.segment import build_seg_step
         if args.image_size == 224:
             args.image_size = 256
+        # (--model linknet[-<encoder>]: the LinkNet decoder on the same data / loss / optimizer)
         enc = args.model.split('-', 1)[1] if '-' in args.model else 'resnet34'
         step = build_seg_step(enc, batch=args.batch, impl=args.impl, image_size=args.image_size, device=device,
-                              world_size=world, use_graph=(args.graph if args.graph >= 0 else None))
+                              world_size=world, use_graph=(args.graph if args.graph >= 0 else None),
+                              arch=args.model.split('-', 1)[0])
     elif is_bert:
         from mlcomp_amd.train.bert import build_bert_step
         step = build_bert_step(args.model, batch=args.batch, seq_len=args.seq_len, impl=args.impl,
@@ -158,7 +160,8 @@ def main():
         print(json.dumps(out), flush=True)
     elif rank == 0 and is_unet:
         out = {
-            'metric': 'images/sec (whole node) U-Net segmentation DAG train task',
+            'metric': f"images/sec (whole node) {'LinkNet' if args.model.startswith('linknet') else 'U-Net'} "
+                      'segmentation DAG train task',
             'value': round(value, 2), 'unit': 'images/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': 'bf16',

@@ -1510,14 +1510,16 @@ MLC_EXPORT int mlc_conv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, f
 // A strided conv runs one GEMM per stride-parity class of dx (only the filter taps that
 // reach the class are in its K loop; a class no tap reaches gets K = 0), so every dx row
 // is written by a GEMM epilogue and no structurally-zero products are computed.
-MLC_EXPORT int mlc_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, const bf16* addend, int N,
-                              int H, int W, int C, int Co, int KH, int KW, int stride, int pad,
-                              int dil, int Ho, int Wo, const bf16* bn_mask, const bf16* bn_y0,
-                              const float* bn_mean0, float* bn_sums0, const bf16* bn_y1,
-                              const float* bn_mean1, float* bn_sums1, const float* bn_msc0,
-                              const float* bn_msh0, const float* bn_msc1, const float* bn_msh1,
-                              hipStream_t st) {
-  if (C % 8 || Co % 8 || KH > 15 || KW > 16 || stride < 1) return -1;
+// sum/sumsq (optional): per-column BN forward statistics of dx, as in mlc_conv_fwd - the
+// transposed-conv forward (mlc_conv_tr_fwd) is this GEMM with a BatchNorm after it.
+static int conv_dgrad_impl(const bf16* dy, const bf16* w, bf16* dx, const bf16* addend, int N,
+                           int H, int W, int C, int Co, int KH, int KW, int stride, int pad,
+                           int dil, int Ho, int Wo, const bf16* bn_mask, const bf16* bn_y0,
+                           const float* bn_mean0, float* bn_sums0, const bf16* bn_y1,
+                           const float* bn_mean1, float* bn_sums1, const float* bn_msc0,
+                           const float* bn_msh0, const float* bn_msc1, const float* bn_msh1,
+                           float* sum, float* sumsq, hipStream_t st) {
+  if (C % 8 || Co % 8 || KH > 15 || KW > 16 || stride < 1 || ((sum == nullptr) != (sumsq == nullptr))) return -1;
   const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
   BnBwdEpi bn{bn_mask, bn_y0, bn_mean0, bn_sums0, bn_y1, bn_mean1, bn_sums1,
               bn_msc0, bn_msh0, bn_msc1, bn_msh1, g_mlc_ncopy};
@@ -1527,27 +1529,34 @@ MLC_EXPORT int mlc_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, const bf1
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
     const DgradClass cl = mkclass(1, 0, 0, H, W, Ho, Wo, Co, 1, 1, 0, dil);
     const int M = N * H * W, K = cl.ncb * BK;
+    if (sum && g_mlc_det && (M + 63) / 64 > g_mlc_ncopy) return -2;
     const int tile = pick_tile(M, C);
-    EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}, addend, bn};
+    EpiBF16<> epi{dx, C, sum, sumsq, IdentityRows{}, addend, bn};
+    epi.ncopy = g_mlc_ncopy;
 #define MKA(R) (MatKC<R>{dy, Co, M, Co})
 #define MKB(R) (ConvDgradB<R>{w, g, cl})
     MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB);
 #undef MKA
   }
   hipError_t err = hipSuccess;
+  // the parity-class GEMMs run one after another on the stream, so in deterministic mode
+  // the statistics stay reproducible as long as each launch has a copy per 64-row group
   for (int ph = 0; ph < stride && ph < H; ++ph)
     for (int pw = 0; pw < stride && pw < W; ++pw) {
       const DgradClass cl = mkclass(stride, ph, pw, H, W, Ho, Wo, Co, KH, KW, pad, dil);
       if (cl.nr > 15 || cl.ns > 16) return -1;
       const int M = N * cl.Hc * cl.Wc, K = cl.nr * cl.ns * cl.ncb * BK;
       if (M <= 0) continue;
+      if (sum && g_mlc_det && (M + 63) / 64 > g_mlc_ncopy) return -2;
       const int tile = pick_tile(M, C);
 #define MKA(R) (ConvDgradA<R>{dy, g, M, K, cl})
       if (stride == 1) {
-        EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}, addend, bn};
+        EpiBF16<> epi{dx, C, sum, sumsq, IdentityRows{}, addend, bn};
+        epi.ncopy = g_mlc_ncopy;
         err = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB); }();
       } else {
-        EpiBF16<ClassRows> epi{dx, C, nullptr, nullptr, ClassRows{cl, H, W}, addend, bn};
+        EpiBF16<ClassRows> epi{dx, C, sum, sumsq, ClassRows{cl, H, W}, addend, bn};
+        epi.ncopy = g_mlc_ncopy;
         err = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB); }();
       }
 #undef MKA
@@ -1555,6 +1564,36 @@ MLC_EXPORT int mlc_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, const bf1
     }
   return err;
 #undef MKB
+}
+
+MLC_EXPORT int mlc_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, const bf16* addend, int N,
+                              int H, int W, int C, int Co, int KH, int KW, int stride, int pad,
+                              int dil, int Ho, int Wo, const bf16* bn_mask, const bf16* bn_y0,
+                              const float* bn_mean0, float* bn_sums0, const bf16* bn_y1,
+                              const float* bn_mean1, float* bn_sums1, const float* bn_msc0,
+                              const float* bn_msh0, const float* bn_msc1, const float* bn_msh1,
+                              hipStream_t st) {
+  return conv_dgrad_impl(dy, w, dx, addend, N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo, bn_mask, bn_y0,
+                         bn_mean0, bn_sums0, bn_y1, bn_mean1, bn_sums1, bn_msc0, bn_msh0, bn_msc1, bn_msh1,
+                         nullptr, nullptr, st);
+}
+
+// Transposed convolution (nn.ConvTranspose2d, no bias): y[N, Ho, Wo, Cout] from
+// x[N, Hi, Wi, Cin] and w[Cin][KH][KW][Cout] (the ConvTranspose2d weight [Cin, Cout, KH, KW]
+// with its taps moved before the output channels).  It is the input gradient of the conv
+// y -> x with that filter, so it runs the dgrad's parity-class GEMMs (a 4x4 / stride-2
+// LinkNet up-conv: 4 classes of 2x2 taps, no structurally-zero products), with the
+// following BatchNorm's sum / sum-of-squares in the epilogue as in mlc_conv_fwd.
+// The input gradient of this op is mlc_conv_fwd of dy over the same w, its weight
+// gradient mlc_conv_wgrad with the roles of x and y swapped.
+MLC_EXPORT int mlc_conv_tr_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, float* sumsq, int N, int Hi,
+                               int Wi, int Cin, int Cout, int KH, int KW, int stride, int pad, int dil, int Ho,
+                               int Wo, hipStream_t st) {
+  if (Hi != (Ho + 2 * pad - dil * (KH - 1) - 1) / stride + 1 || Wi != (Wo + 2 * pad - dil * (KW - 1) - 1) / stride + 1)
+    return -1;
+  return conv_dgrad_impl(x, w, y, nullptr, N, Ho, Wo, Cout, Cin, KH, KW, stride, pad, dil, Hi, Wi, nullptr,
+                         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                         nullptr, sum, sumsq, st);
 }
 
 // dgrad from the transposed, flipped filter wt[C][KH][KW][Co] (wtrans.hip), same

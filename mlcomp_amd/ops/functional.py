@@ -74,6 +74,35 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, stride=1, pad=0, dil=1,
     return y
 
 
+def conv_transpose2d_fwd(x: torch.Tensor, w: torch.Tensor, out_hw, stride=2, pad=1, dil=1,
+                         stats: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+    """y = conv_transpose(x, w) in NHWC, no bias: x [N, Hi, Wi, Cin], w [Cin, KH, KW, Cout]
+    (nn.ConvTranspose2d's [Cin, Cout, KH, KW] with the taps first), y [N, *out_hw, Cout].
+    It is the input gradient of the conv y -> x over w, so the GPU path runs the dgrad's
+    parity-class GEMMs (``mlc_conv_tr_fwd``); ``stats`` as in :func:`conv2d_fwd`.  Its own
+    input gradient is :func:`conv2d_fwd` of dy over w, its weight gradient
+    :func:`conv2d_wgrad` (dy=x, x=dy)."""
+    N, Hi, Wi, Cin = x.shape
+    Cw, KH, KW, Cout = w.shape
+    assert Cw == Cin, (w.shape, x.shape)
+    Ho, Wo = out_hw
+    assert conv_out_hw(Ho, Wo, KH, KW, stride, pad, dil) == (Hi, Wi), (out_hw, x.shape)
+    if _cuda(x):
+        y = torch.empty(N, Ho, Wo, Cout, device=x.device, dtype=torch.bfloat16)
+        s1, s2 = (stats if stats is not None else (None, None))
+        _lib.call('mlc_conv_tr_fwd', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(s1), _lib.ptr(s2),
+                  N, Hi, Wi, Cin, Cout, KH, KW, stride, pad, dil, Ho, Wo, _lib.stream())
+        return y
+    oph = Ho - ((Hi - 1) * stride - 2 * pad + dil * (KH - 1) + 1)
+    opw = Wo - ((Wi - 1) * stride - 2 * pad + dil * (KW - 1) + 1)
+    yf = F.conv_transpose2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), None, stride, pad,
+                            (oph, opw), 1, dil)
+    if stats is not None:
+        stats[0][:Cout].add_(yf.sum(dim=(0, 2, 3)))
+        stats[1][:Cout].add_((yf * yf).sum(dim=(0, 2, 3)))
+    return yf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+
+
 class BnBwdSpec:
     """Backward reduction of up to two BatchNorms fused into a dgrad epilogue: the dgrad
     output is their (shared) output gradient dU.  ``mask`` (the BN output z, or None)

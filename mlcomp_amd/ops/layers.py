@@ -237,7 +237,7 @@ class ConvBN:
             res, rs, rh = res
             raff = (rs, rh)
         if not self.ctx.training:  # inference BN: running statistics, no stat epilogue
-            y = Fn.conv2d_fwd(x, self.w.bf16, self.stride, self.pad, self.dil, in_affine=in_affine)
+            y = self._conv(x, None, in_affine)
             torch.rsqrt(self.run_var + self.eps, out=self.scale).mul_(self.gamma.master)
             torch.sub(self.beta.master, self.run_mean * self.scale, out=self.shift)
             if defer:
@@ -246,13 +246,27 @@ class ConvBN:
             return z, (x, y, z)
         s1, s2 = ws[self.k_s1], ws[self.k_s2]
         self.ctx.wt_stale = True
-        y = Fn.conv2d_fwd(x, self.w.bf16, self.stride, self.pad, self.dil, stats=(s1, s2), in_affine=in_affine)
+        y = self._conv(x, (s1, s2), in_affine)
         training = self.ctx.training
         z = Fn.bn_fwd_apply(y, res, s1, s2, self.gamma.master, self.beta.master, self.save_mean,
                             self.save_invstd, self.run_mean if training else None,
                             self.run_var if training else None, self.eps, self.momentum, self.act,
                             scale=self.scale, shift=self.shift, res_affine=raff, apply=not defer)
         return z, (x, y, z)
+
+    # the three GEMMs of the unit (overridden by ConvTBN)
+    def _conv(self, x, stats, in_affine=None):
+        return Fn.conv2d_fwd(x, self.w.bf16, self.stride, self.pad, self.dil, stats=stats, in_affine=in_affine)
+
+    def _dgrad(self, dy, x_shape, addend=None, out=None, bn=None):
+        wt = None
+        if self.wt_idx is not None:
+            if self.ctx.wt_stale:
+                raise RuntimeError('transposed filters are stale: the model must call '
+                                   'ctx.refresh_wt() after its training forward pass')
+            wt = self.ctx.wt[self.wt_idx]
+        return Fn.conv2d_dgrad(dy, self.w.bf16, x_shape, self.stride, self.pad, self.dil,
+                               addend=addend, out=out, bn=bn, wt=wt)
 
     def dgrad_covers_all(self) -> bool:
         """True when the dgrad GEMM epilogue writes every dx row, i.e. a BN-backward
@@ -304,14 +318,7 @@ class ConvBN:
             self.wgrad(dy, x, in_affine)
         dx = None
         if need_dx:
-            wt = None
-            if self.wt_idx is not None:
-                if self.ctx.wt_stale:
-                    raise RuntimeError('transposed filters are stale: the model must call '
-                                       'ctx.refresh_wt() after its training forward pass')
-                wt = self.ctx.wt[self.wt_idx]
-            dx = Fn.conv2d_dgrad(dy, self.w.bf16, x.shape, self.stride, self.pad, self.dil,
-                                 addend=dx_addend, out=dx_out, bn=dgrad_bn, wt=wt)
+            dx = self._dgrad(dy, x.shape, addend=dx_addend, out=dx_out, bn=dgrad_bn)
         if side is not None and self.ctx.dgrad_first:
             # captured after the dgrad but forked from the point before it: the dgrad is the
             # first child of the previous node, so graph replay keeps the dgrad -> BN chain
@@ -332,6 +339,83 @@ class ConvBN:
             main.wait_stream(side)                 # join: the weight gradient is complete
         arena.mark_ready(self.w)   # after the dgrad: the last reader of w in backward
         return dx, dres
+
+
+class ConvTBN(ConvBN):
+    """transposed conv (``nn.ConvTranspose2d``) -> BatchNorm (train-mode batch stats) ->
+    [ReLU]: LinkNet's x2 up-convolution (`mlcomp/contrib/segmentation/linknet/decoder.py`,
+    4x4 / stride 2 / pad 1).  Its three GEMMs are the conv GEMMs with the roles turned
+    round (:func:`Fn.conv_transpose2d_fwd`): forward = the dgrad parity-class GEMMs with the
+    BN statistics in their epilogue, input gradient = a forward conv over the same filter,
+    weight gradient = the conv wgrad with x and dy swapped.
+
+    The conv's bias is not applied: a training-mode BatchNorm subtracts the batch mean, so
+    the bias changes neither the output nor any gradient (its gradient is exactly zero and it
+    stays untouched).  It only shifts the running mean, which is kept bias-free here and
+    converted on load / export."""
+
+    def __init__(self, ctx: NativeContext, name: str, conv: nn.ConvTranspose2d, bn: nn.BatchNorm2d, act: bool):
+        assert conv.groups == 1 and conv.dilation[0] == conv.dilation[1], 'native ConvTBN: groups=1'
+        assert conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
+        self.ctx = ctx
+        self.name = name
+        Cin, Cout, KH, KW = conv.weight.shape
+        assert bn.num_features == Cout
+        self.cin = self.cin_p = Cout          # last dim of the [Cin, KH, KW, Cout] filter
+        self.Co = Cout
+        self.k = (KH, KW)
+        self.stride, self.pad, self.dil = conv.stride[0], conv.padding[0], conv.dilation[0]
+        self.out_pad = conv.output_padding
+        self.s2d = False
+        self.act = act
+        self.eps = bn.eps
+        self.momentum = bn.momentum if bn.momentum is not None else 0.1
+        self.w = ctx.arena.weight(f'{name}.conv.weight', (Cin, KH, KW, Cout))
+        self.wt_idx = None
+        self.gamma = ctx.arena.vector(f'{name}.bn.weight', (Cout,))
+        self.beta = ctx.arena.vector(f'{name}.bn.bias', (Cout,))
+        self._src = (conv, bn)
+        self.k_s1 = ctx.ws.request(f'{name}.s1', Fn.NSTAT * Cout)
+        self.k_s2 = ctx.ws.request(f'{name}.s2', Fn.NSTAT * Cout)
+        self.k_bw = ctx.ws.request(f'{name}.bwd', Fn.NSTAT * 2 * Cout)
+
+    def _bias(self):
+        conv = self._src[0]
+        return conv.bias.detach().float().to(self.ctx.device) if conv.bias is not None else None
+
+    def load_from_torch(self):
+        super().load_from_torch()
+        b = self._bias()
+        if b is not None:
+            self.run_mean.sub_(b)
+
+    def export_to_torch(self):
+        super().export_to_torch()
+        b = self._bias()
+        if b is not None:
+            bn = self._src[1]
+            bn.running_mean.add_(b.to(bn.running_mean.device))
+
+    def out_hw(self, H, W):
+        KH, KW = self.k
+        return ((H - 1) * self.stride - 2 * self.pad + self.dil * (KH - 1) + self.out_pad[0] + 1,
+                (W - 1) * self.stride - 2 * self.pad + self.dil * (KW - 1) + self.out_pad[1] + 1)
+
+    def _conv(self, x, stats, in_affine=None):
+        assert in_affine is None
+        return Fn.conv_transpose2d_fwd(x, self.w.bf16, self.out_hw(x.shape[1], x.shape[2]), self.stride,
+                                       self.pad, self.dil, stats=stats)
+
+    def _dgrad(self, dy, x_shape, addend=None, out=None, bn=None):
+        assert addend is None and out is None and bn is None, 'ConvTBN input gradient: plain conv'
+        dx = Fn.conv2d_fwd(dy, self.w.bf16, self.stride, self.pad, self.dil)
+        assert tuple(dx.shape) == tuple(x_shape), (dx.shape, x_shape)
+        return dx
+
+    def wgrad(self, dy, x, in_affine=None):
+        assert in_affine is None
+        Fn.conv2d_wgrad(x, dy, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad,
+                        accumulate=self.ctx.grad_prezeroed)
 
 
 class _ConvBNFn(torch.autograd.Function):

@@ -1,4 +1,4 @@
-"""The native training step for U-Net segmentation (BASELINE config 3).
+"""The native training step for U-Net (BASELINE config 3) and LinkNet segmentation.
 
 forward (fused conv+BN+ReLU nodes, fused upsample+concat) -> fused 1x1 head + BCE + Dice
 -> backward (wgrad straight into the flat grad arena, bucketed RCCL all-reduce on a side
@@ -13,6 +13,7 @@ from typing import Optional
 import torch
 
 from mlcomp_amd.models.native_resnet import STEM_CIN
+from mlcomp_amd.models.native_linknet import NativeLinknet
 from mlcomp_amd.models.native_unet import NativeUnet
 from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops.layers import flatten_bn_buffers
@@ -34,12 +35,15 @@ class NativeSegmentationStep(GraphedStep):
     def __init__(self, encoder='resnet34', batch=32, image_size=256, device=None, world_size=1, use_graph=True,
                  lr=3e-4, weight_decay=0.0, optimizer='Adam', momentum=0.9, betas=(0.9, 0.999), eps=1e-8,
                  seed=0, warmup_eager=2, torch_model=None, comm=None, classes=1, nesterov=False, dampening=0.0,
-                 bce_w=1.0, dice_w=1.0, loss_eps=1e-7):
-        from mlcomp_amd.contrib.segmentation.models import Unet
+                 bce_w=1.0, dice_w=1.0, loss_eps=1e-7, arch='unet'):
+        from mlcomp_amd.contrib.segmentation.models import Linknet, Unet
         self.device = torch.device(device or 'cuda')
         torch.manual_seed(seed)
-        tm = torch_model if torch_model is not None else Unet(encoder_name=encoder, classes=classes)
-        self.net = NativeUnet(tm, self.device, bce_w=bce_w, dice_w=dice_w, eps=loss_eps)
+        if torch_model is None:
+            torch_model = (Linknet if arch.lower() == 'linknet' else Unet)(encoder_name=encoder, classes=classes)
+        tm = torch_model
+        engine = NativeLinknet if isinstance(tm, Linknet) else NativeUnet
+        self.net = engine(tm, self.device, bce_w=bce_w, dice_w=dice_w, eps=loss_eps)
         self.net.ctx.grad_prezeroed = True
         self.world = world_size
         self.comm = comm if comm is not None else (make_comm(self.device) if world_size > 1 else None)
