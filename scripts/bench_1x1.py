@@ -25,9 +25,10 @@ SHAPES = [
     ('l3 512>256', 28, 512, 256, 1), ('l3 256>1024', 14, 256, 1024, 6), ('l3 1024>256', 14, 1024, 256, 5),
     ('l4 1024>512', 14, 1024, 512, 1), ('l4 512>2048', 7, 512, 2048, 3), ('l4 2048>512', 7, 2048, 512, 2),
 ]
-# (tag, {knob: value}) - knob 12: single-stage (4 blocks/CU) up to this many K-tiles,
-# knob 8: LDS-DMA main loop on/off, knob 0: register prefetch depth
-CONFIGS = [('base', {}), ('ss4', {12: 4}), ('ss16', {12: 16}), ('nodma', {8: 0}), ('nodma_pf1', {8: 0, 0: 1})]
+# (tag, {knob: value}) - knob 8: LDS-DMA main loop on/off, knob 0: register prefetch depth.
+# (The ss4 / ss16 columns of profiles/round3/streamk/bench_1x1.jsonl came from a
+# single-stage knob that was removed with the variant; knob 12 is now a dense-GEMM knob.)
+CONFIGS = [('base', {}), ('nodma', {8: 0}), ('nodma_pf1', {8: 0, 0: 1})]
 
 
 def set_knobs(kn):

@@ -185,3 +185,32 @@ def test_native_linknet_step_trains_and_graph_matches():
     assert abs(le[0] - lg[0]) < 1e-3 * abs(le[0]) + 1e-4, (le, lg)
     for a, b in zip(le, lg):
         assert abs(a - b) < 6e-2 * abs(a) + 1e-3, (le, lg)
+
+
+def test_runner_native_linknet_train_valid(tmp_path):
+    """The config-driven runner trains and validates a LinkNet on the native engine."""
+    from mlcomp_amd.train.experiment import ConfigExperiment
+    from mlcomp_amd.train.runner import Runner
+    cfg = {'model_params': {'model': 'Linknet', 'encoder_name': 'resnet34', 'classes': 1},
+           'args': {'logdir': str(tmp_path), 'engine': 'auto'},
+           'stages': {
+               'data_params': {'dataset': 'synthetic_segmentation', 'image_size': 64, 'num_classes': 1,
+                               'num_samples': 64, 'valid_samples': 16, 'batch_size': 8, 'num_workers': 0},
+               'state_params': {'num_epochs': 2, 'main_metric': 'dice', 'minimize_metric': False},
+               'criterion_params': {'criterion': 'BCEDiceLoss'},
+               'optimizer_params': {'optimizer': 'Adam', 'lr': 3e-4},
+               'callbacks_params': {'loss': {'callback': 'CriterionCallback'},
+                                    'opt': {'callback': 'OptimizerCallback'},
+                                    'dice': {'callback': 'DiceCallback'},
+                                    'saver': {'callback': 'CheckpointCallback'}},
+               'stage1': {}}}
+    r = Runner(ConfigExperiment(cfg), device='cuda')
+    st = r.run_experiment()
+    assert st.native and r.native_kind == 'unet'
+    from mlcomp_amd.models.native_linknet import NativeLinknet
+    assert isinstance(r.native_step.net, NativeLinknet)
+    m = st.epoch_metrics
+    assert m['train_loss'] == m['train_loss'] and m['train_loss'] > 0
+    assert m['valid_loss'] == m['valid_loss'] and 0 <= m['valid_dice'] <= 1
+    ck = torch.load(tmp_path / 'checkpoints' / 'last_full.pth', weights_only=True)
+    assert torch.isfinite(ck['model_state_dict']['decoder.final_conv.weight']).all()
