@@ -1,0 +1,327 @@
+"""Native execution of the FPN segmentation model
+(:class:`mlcomp_amd.contrib.segmentation.models.FPN`; the reference's
+`mlcomp/contrib/segmentation/fpn/{model,decoder}.py`) with a ResNet encoder.
+
+* encoder: the native ResNet body shared with the U-Net engine
+  (:meth:`NativeUnet._lower_encoder`): fused conv+BN(+residual)(+ReLU) nodes.
+* every decoder convolution runs on the native MFMA GEMMs:
+  - the 1x1 lateral convs (+ bias) and the 1x1 output conv are dense GEMMs over the NHWC
+    pixel rows with the bias in the epilogue (``transformer.dense_fwd``), their weight and
+    bias gradients one GEMM (``Fn.linear_wgrad_bias``), the input gradient ``dense_dgrad``;
+  - the 3x3 convs of the segmentation heads are the implicit-GEMM conv kernels.
+* the GroupNorm(32) + ReLU of the heads, the nearest / bilinear upsamplings, the pyramid
+  additions, Dropout2d and the BCE + Dice loss on the x4-upsampled logits are PyTorch tensor
+  ops on the NHWC activations (no MIOpen / hipBLASLt call in the step); GroupNorm's backward
+  is written out (:class:`_GNReluFn`) so its parameter gradients land in the flat arena.
+
+Parameters live in the flat arenas (fused Adam, bucketed all-reduce) like the other engines.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from mlcomp_amd.ops import functional as Fn
+from mlcomp_amd.ops import seg
+from mlcomp_amd.ops import transformer as Tx
+from .native_unet import NativeUnet
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def _up(x, scale, mode):
+    """NHWC upsampling (channels_last views, so no layout copies)."""
+    kw = {'align_corners': True} if mode == 'bilinear' else {}
+    return _nhwc(F.interpolate(_nchw(x), scale_factor=scale, mode=mode, **kw))
+
+
+# ---------------------------------------------------------------------------- units
+class Conv1x1Bias:
+    """1x1 conv with bias as a dense GEMM over pixel rows (NHWC)."""
+
+    def __init__(self, ctx, name, conv: nn.Conv2d, f32_out=False):
+        assert conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.groups == 1
+        self.ctx, self.conv, self.f32_out = ctx, conv, f32_out
+        self.Co, self.Ci = conv.out_channels, conv.in_channels
+        self.w = ctx.arena.weight(f'{name}.weight', (self.Co, self.Ci))
+        self.b = ctx.arena.vector(f'{name}.bias', (self.Co,))
+
+    def load_from_torch(self):
+        dev = self.ctx.device
+        self.w.master.copy_(self.conv.weight.detach().float().reshape(self.Co, self.Ci).to(dev))
+        b = self.conv.bias.detach().float() if self.conv.bias is not None else torch.zeros(self.Co)
+        self.b.master.copy_(b.to(dev))
+
+    def export_to_torch(self):
+        self.conv.weight.data.copy_(self.w.master.reshape(self.conv.weight.shape).to(self.conv.weight.device))
+        if self.conv.bias is not None:
+            self.conv.bias.data.copy_(self.b.master.to(self.conv.bias.device))
+
+    def __call__(self, x):
+        return _Conv1x1BiasFn.apply(x, self.ctx.anchor, self)
+
+
+class _Conv1x1BiasFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, u: Conv1x1Bias):
+        N, H, W, C = x.shape
+        x2 = x.reshape(-1, C)
+        if u.f32_out:
+            y = Fn.linear_fwd(x2, u.w.bf16, u.b.master)
+        else:
+            y, _ = Tx.dense_fwd(x2, u.w.bf16, u.b.master)
+        ctx.u = u
+        ctx.save_for_backward(x2)
+        return y.view(N, H, W, u.Co)
+
+    @staticmethod
+    def backward(ctx, dy):
+        u: Conv1x1Bias = ctx.u
+        (x2,) = ctx.saved_tensors
+        shp = dy.shape
+        d2 = dy.reshape(-1, u.Co).to(torch.bfloat16).contiguous()
+        Fn.linear_wgrad_bias(d2, x2, u.w.grad, u.b.grad)
+        dx = Tx.dense_dgrad(d2, u.w.bf16).view(*shp[:3], u.Ci) if ctx.needs_input_grad[0] else None
+        u.ctx.arena.mark_ready(u.w)
+        u.ctx.arena.mark_ready(u.b)
+        return dx, None, None
+
+
+class Conv3x3:
+    """3x3 / stride 1 / pad 1 conv without bias on the implicit-GEMM kernels."""
+
+    def __init__(self, ctx, name, conv: nn.Conv2d):
+        assert conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
+        assert conv.groups == 1 and conv.bias is None
+        self.ctx, self.conv = ctx, conv
+        self.Co, self.Ci = conv.out_channels, conv.in_channels
+        self.w = ctx.arena.weight(f'{name}.weight', (self.Co, 3, 3, self.Ci))
+
+    def load_from_torch(self):
+        self.w.master.copy_(self.conv.weight.detach().permute(0, 2, 3, 1).float().to(self.ctx.device))
+
+    def export_to_torch(self):
+        self.conv.weight.data.copy_(self.w.master.permute(0, 3, 1, 2).to(self.conv.weight.device))
+
+    def __call__(self, x):
+        return _Conv3x3Fn.apply(x, self.ctx.anchor, self)
+
+
+class _Conv3x3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, u: Conv3x3):
+        ctx.u = u
+        ctx.save_for_backward(x)
+        return Fn.conv2d_fwd(x, u.w.bf16, 1, 1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        u: Conv3x3 = ctx.u
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        Fn.conv2d_wgrad(dy, x, u.w.shape, 1, 1, out=u.w.grad, accumulate=True)
+        dx = Fn.conv2d_dgrad(dy, u.w.bf16, x.shape, 1, 1) if ctx.needs_input_grad[0] else None
+        u.ctx.arena.mark_ready(u.w)
+        return dx, None, None
+
+
+class GNRelu:
+    """GroupNorm + ReLU over NHWC activations, parameters in the arena."""
+
+    def __init__(self, ctx, name, gn: nn.GroupNorm):
+        self.ctx, self.gn = ctx, gn
+        self.G, self.C, self.eps = gn.num_groups, gn.num_channels, gn.eps
+        self.g = ctx.arena.vector(f'{name}.weight', (self.C,))
+        self.b = ctx.arena.vector(f'{name}.bias', (self.C,))
+
+    def load_from_torch(self):
+        self.g.master.copy_(self.gn.weight.detach().float().to(self.ctx.device))
+        self.b.master.copy_(self.gn.bias.detach().float().to(self.ctx.device))
+
+    def export_to_torch(self):
+        self.gn.weight.data.copy_(self.g.master.to(self.gn.weight.device))
+        self.gn.bias.data.copy_(self.b.master.to(self.gn.bias.device))
+
+    def __call__(self, x):
+        return _GNReluFn.apply(x, self.ctx.anchor, self)
+
+
+def _gn_stats(u: GNRelu, x):
+    N, H, W, C = x.shape
+    xf = x.float().view(N, H * W, u.G, C // u.G)
+    mean = xf.mean((1, 3), keepdim=True)
+    rstd = torch.rsqrt(xf.var((1, 3), unbiased=False, keepdim=True) + u.eps)
+    return xf, mean, rstd
+
+
+class _GNReluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, u: GNRelu):
+        xf, mean, rstd = _gn_stats(u, x)
+        shape = (1, 1, u.G, u.C // u.G)
+        y = (xf - mean) * rstd * u.g.master.view(shape) + u.b.master.view(shape)
+        ctx.u = u
+        ctx.save_for_backward(x, mean, rstd)
+        return torch.relu(y).to(torch.bfloat16).view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dz):
+        u: GNRelu = ctx.u
+        x, mean, rstd = ctx.saved_tensors
+        N, H, W, C = x.shape
+        shape = (1, 1, u.G, C // u.G)
+        xhat = (x.float().view(N, H * W, u.G, C // u.G) - mean) * rstd
+        gam = u.g.master.view(shape)
+        dy = dz.float().view(xhat.shape) * ((xhat * gam + u.b.master.view(shape)) > 0)
+        u.g.grad.add_((dy * xhat).sum((0, 1)).reshape(C))
+        u.b.grad.add_(dy.sum((0, 1)).reshape(C))
+        u.ctx.arena.mark_ready(u.g)
+        u.ctx.arena.mark_ready(u.b)
+        dxh = dy * gam
+        dx = rstd * (dxh - dxh.mean((1, 3), keepdim=True) - xhat * (dxh * xhat).mean((1, 3), keepdim=True))
+        return dx.to(torch.bfloat16).view(x.shape), None, None
+
+
+class FPNHead:
+    """Output conv (1x1 + bias, fp32 logits at stride 4) -> x4 bilinear -> BCE + soft Dice
+    (contrib.criterion.BCEDiceLoss) with the loss sums [BCE sum, sum s*t, sum s, sum t]
+    kept in the workspace like :class:`~.native_unet.SegHead`."""
+
+    def __init__(self, ctx, conv: nn.Conv2d, bce_w=1.0, dice_w=1.0, eps=1e-7):
+        assert conv.out_channels <= 4
+        self.ctx = ctx
+        self.conv = Conv1x1Bias(ctx, 'decoder.final_conv', conv, f32_out=True)
+        self.K = conv.out_channels
+        self.bce_w, self.dice_w, self.eps = bce_w, dice_w, eps
+        self.k_sums = ctx.ws.request('decoder.head.sums', 4)
+
+    def sums(self):
+        return self.ctx.ws[self.k_sums]
+
+    def logits(self, x):
+        """[N, H/4, W/4, C] bf16 -> fp32 logits [N, H, W, K] (NHWC)."""
+        return _up(self.conv(x), 4, 'bilinear')
+
+    def loss(self, z, target):
+        zf = z.reshape(-1)
+        t = target.reshape(-1).float()
+        s = torch.sigmoid(zf)
+        sums = self.sums()
+        bce = F.binary_cross_entropy_with_logits(zf, t, reduction='sum')
+        st = (s * t).sum()
+        ss = s.sum()
+        with torch.no_grad():
+            sums.copy_(torch.stack([bce.detach(), st.detach(), ss.detach(), t.sum()]))
+        dice = (2 * st + self.eps) / (ss + t.sum() + self.eps)
+        return self.bce_w * bce / zf.numel() + self.dice_w * (1 - dice)
+
+
+class NativeFPN(NativeUnet):
+    """Same encoder / step interface as :class:`NativeUnet`; FPN decoder."""
+
+    def __init__(self, model, device, bce_w=1.0, dice_w=1.0, eps=1e-7):
+        from mlcomp_amd.contrib.segmentation.decoders import FPNDecoder
+        dec = model.decoder
+        if not isinstance(dec, FPNDecoder):
+            raise NotImplementedError('NativeFPN: an FPNDecoder model')
+        ctx = self._lower_encoder(model)
+        self.dec_m = dec
+        self.lat_top = Conv1x1Bias(ctx, 'decoder.lateral_top', dec.lateral_top)
+        self.laterals = [Conv1x1Bias(ctx, f'decoder.laterals.{i}', c) for i, c in enumerate(dec.laterals)]
+        self.heads = []
+        for i, h in enumerate(dec.heads):
+            layers = []
+            for j, gu in enumerate(h):
+                pre = f'decoder.heads.{i}.{j}'
+                layers.append((Conv3x3(ctx, f'{pre}.0', gu[0]), GNRelu(ctx, f'{pre}.1', gu[1]), gu.upsample))
+            self.heads.append(layers)
+        self.drop = dec.dropout.p
+        self.head = FPNHead(ctx, dec.final_conv, bce_w, dice_w, eps)
+        self._finish_init(device)
+
+    def _units(self):
+        yield self.stem
+        for blk in self.blocks:
+            yield from blk.units
+            if blk.down is not None:
+                yield blk.down
+
+    def _dec_units(self):
+        yield self.lat_top
+        yield from self.laterals
+        for layers in self.heads:
+            for conv, gn, _ in layers:
+                yield conv
+                yield gn
+        yield self.head.conv
+
+    def _finish_init(self, device):
+        self.ctx.finalize(device)
+        for u in self._units():
+            u.load_from_torch()
+        for u in self._dec_units():
+            u.load_from_torch()
+        self.ctx.arena.decay.refresh_mirror()
+
+    def features(self, x):
+        """x: NHWC bf16 image -> the summed stride-4 head features [N, H/4, W/4, 128] bf16."""
+        anchor = self.ctx.anchor
+        x0 = self.stem(x)
+        y = self.pool(x0, anchor)
+        feats = []
+        for i, blk in enumerate(self.blocks):
+            y = blk(y)
+            if i in self.ends:
+                feats.append(y)
+        x1, x2, x3, x4 = feats
+        p = self.lat_top(x4)
+        pyramid = [p]
+        for lat, c in zip(self.laterals, (x3, x2, x1)):
+            p = _up(p, 2, 'nearest') + lat(c)
+            pyramid.append(p)
+        acc = None
+        for layers, t in zip(self.heads, pyramid):
+            for conv, gn, up in layers:
+                t = gn(conv(t))
+                if up:
+                    t = _up(t, 2, 'bilinear')
+            acc = t.float() if acc is None else acc + t.float()
+        self.ctx.refresh_wt()    # transposed filters for the encoder's backward dgrads
+        if self.ctx.training and self.drop > 0:
+            acc = _nhwc(F.dropout2d(_nchw(acc), self.drop, True))
+        return acc.to(torch.bfloat16)
+
+    def loss(self, x, target):
+        """BCE + Dice loss (device scalar); ``target`` fp32 [N*H*W*K] in pixel order."""
+        return self.head.loss(self.head.logits(self.features(x)), target)
+
+    def predict(self, x, target=None):
+        h = self.head
+        was = self.ctx.training
+        self.train(False)
+        try:
+            with torch.no_grad():
+                z = h.logits(self.features(x))
+                out = z.permute(0, 3, 1, 2)
+                loss = None
+                if target is not None:
+                    m = target.to(z.device).float()
+                    t = m.permute(0, 2, 3, 1) if m.dim() == 4 else m.unsqueeze(-1)
+                    loss = h.loss(z, t.contiguous())
+            return out, loss
+        finally:
+            self.train(was)
+
+    def export_to_torch(self):
+        for u in self._units():
+            u.export_to_torch()
+        for u in self._dec_units():
+            u.export_to_torch()
+        return self.torch_model

@@ -214,3 +214,38 @@ def test_runner_native_linknet_train_valid(tmp_path):
     assert m['valid_loss'] == m['valid_loss'] and 0 <= m['valid_dice'] <= 1
     ck = torch.load(tmp_path / 'checkpoints' / 'last_full.pth', weights_only=True)
     assert torch.isfinite(ck['model_state_dict']['decoder.final_conv.weight']).all()
+
+
+def test_native_fpn_step_trains_and_graph_matches():
+    """The native FPN engine (ResNet-34 encoder) trains, under graph replay too (dropout
+    off here so eager and replay see the same function)."""
+    from mlcomp_amd.contrib.segmentation.models import FPN
+    from mlcomp_amd.train.native_seg_step import NativeSegmentationStep
+
+    def mk(graph):
+        torch.manual_seed(3)
+        tm = FPN(encoder_name='resnet34', classes=1, dropout=0.0)
+        return NativeSegmentationStep(torch_model=tm, batch=4, image_size=128, device=DEV, use_graph=graph,
+                                      seed=3, warmup_eager=1)
+    eager, graph = mk(False), mk(True)
+    le, lg = [], []
+    for _ in range(6):
+        eager()
+        graph()
+        le.append(eager.last_loss())
+        lg.append(graph.last_loss())
+    torch.cuda.synchronize()
+    assert graph.graph is not None
+    assert all(v == v for v in le) and le[-1] < le[0], le
+    assert abs(le[0] - lg[0]) < 1e-3 * abs(le[0]) + 1e-4, (le, lg)
+    for a, b in zip(le, lg):
+        assert abs(a - b) < 6e-2 * abs(a) + 1e-3, (le, lg)
+    # with dropout (the model default) the captured step trains as well
+    st = NativeSegmentationStep('resnet34', batch=4, image_size=128, device=DEV, use_graph=True, seed=4,
+                                warmup_eager=1, arch='fpn')
+    ls = []
+    for _ in range(6):
+        st()
+        ls.append(st.last_loss())
+    torch.cuda.synchronize()
+    assert all(v == v for v in ls) and ls[-1] < ls[0], ls
