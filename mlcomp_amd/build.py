@@ -77,6 +77,19 @@ SANITIZERS = {'asan': ['-fsanitize=address,undefined', '-fno-omit-frame-pointer'
               'tsan': ['-fsanitize=thread']}
 
 
+def _link_atomic(cmd, out, srcs):
+    """Build into a private temp name, then rename over ``out``: a process that is running
+    (or loading) the old file keeps its inode, so concurrent test workers never see a
+    half-written binary ("Text file busy" / truncated ELF)."""
+    tmp = f'{out}.tmp{os.getpid()}'
+    try:
+        _run(cmd + [tmp] + srcs)
+        os.replace(tmp, out)
+    finally:
+        if os.path.exists(tmp):
+            os.remove(tmp)
+
+
 def build_broker(verbose=False, sanitize=None):
     """The C++ broker daemon; ``sanitize='asan'`` (AddressSanitizer + UBSan, any report
     aborts) or ``'tsan'`` builds an instrumented twin ``mlcomp-broker-<san>`` for the
@@ -90,7 +103,7 @@ def build_broker(verbose=False, sanitize=None):
     if _newer(out, srcs + hdrs):
         cxx = shutil.which('g++') or 'c++'
         flags = ['-O2'] if not sanitize else ['-O1', '-g'] + SANITIZERS[sanitize]
-        _run([cxx] + flags + ['-std=c++17', '-pthread', '-Wall', '-o', out] + srcs)
+        _link_atomic([cxx] + flags + ['-std=c++17', '-pthread', '-Wall', '-o'], out, srcs)
     if verbose:
         print(f'[build] broker -> {out}')
     return out
@@ -109,8 +122,7 @@ def build_runtime(verbose=False):
         return None
     if _newer(RUNTIME_LIB, srcs + hdrs):
         cxx = shutil.which('g++') or 'c++'
-        _run([cxx, '-O3', '-std=c++17', '-pthread', '-fPIC', '-shared', '-Wall', '-o', RUNTIME_LIB]
-             + srcs)
+        _link_atomic([cxx, '-O3', '-std=c++17', '-pthread', '-fPIC', '-shared', '-Wall', '-o'], RUNTIME_LIB, srcs)
     if verbose:
         print(f'[build] runtime -> {RUNTIME_LIB}')
     return RUNTIME_LIB
@@ -125,7 +137,7 @@ def build_runtime_selftest(sanitize='tsan', verbose=False):
     out = os.path.join(OUT, f'mlcomp-records-selftest-{sanitize}')
     if _newer(out, srcs + glob.glob(os.path.join(ROOT, 'csrc', 'runtime', '*.h'))):
         cxx = shutil.which('g++') or 'c++'
-        _run([cxx, '-O1', '-g', '-std=c++17', '-pthread', '-Wall'] + SANITIZERS[sanitize] + ['-o', out] + srcs)
+        _link_atomic([cxx, '-O1', '-g', '-std=c++17', '-pthread', '-Wall'] + SANITIZERS[sanitize] + ['-o'], out, srcs)
     if verbose:
         print(f'[build] runtime selftest -> {out}')
     return out

@@ -49,20 +49,28 @@ class Conv1x1Bias:
     def __init__(self, ctx, name, conv: nn.Conv2d, f32_out=False):
         assert conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.groups == 1
         self.ctx, self.conv, self.f32_out = ctx, conv, f32_out
-        self.Co, self.Ci = conv.out_channels, conv.in_channels
+        self.Ci = conv.in_channels
+        self.O = conv.out_channels
+        # output channels padded to 8 (the GEMMs' column granularity: a 1-class output conv
+        # is a [P, 8] GEMM); the padding rows stay zero (zero gradient, zero update) and
+        # the caller slices the first O channels
+        self.Co = (self.O + 7) // 8 * 8
         self.w = ctx.arena.weight(f'{name}.weight', (self.Co, self.Ci))
         self.b = ctx.arena.vector(f'{name}.bias', (self.Co,))
 
     def load_from_torch(self):
         dev = self.ctx.device
-        self.w.master.copy_(self.conv.weight.detach().float().reshape(self.Co, self.Ci).to(dev))
-        b = self.conv.bias.detach().float() if self.conv.bias is not None else torch.zeros(self.Co)
-        self.b.master.copy_(b.to(dev))
+        self.w.master.zero_()
+        self.b.master.zero_()
+        self.w.master[:self.O].copy_(self.conv.weight.detach().float().reshape(self.O, self.Ci).to(dev))
+        if self.conv.bias is not None:
+            self.b.master[:self.O].copy_(self.conv.bias.detach().float().to(dev))
 
     def export_to_torch(self):
-        self.conv.weight.data.copy_(self.w.master.reshape(self.conv.weight.shape).to(self.conv.weight.device))
+        self.conv.weight.data.copy_(self.w.master[:self.O].reshape(self.conv.weight.shape)
+                                    .to(self.conv.weight.device))
         if self.conv.bias is not None:
-            self.conv.bias.data.copy_(self.b.master.to(self.conv.bias.device))
+            self.conv.bias.data.copy_(self.b.master[:self.O].to(self.conv.bias.device))
 
     def __call__(self, x):
         return _Conv1x1BiasFn.apply(x, self.ctx.anchor, self)
@@ -207,7 +215,7 @@ class FPNHead:
 
     def logits(self, x):
         """[N, H/4, W/4, C] bf16 -> fp32 logits [N, H, W, K] (NHWC)."""
-        return _up(self.conv(x), 4, 'bilinear')
+        return _up(self.conv(x)[..., :self.K], 4, 'bilinear')
 
     def loss(self, z, target):
         zf = z.reshape(-1)

@@ -70,8 +70,10 @@ def test_native_fpn_matches_torch_autograd():
     assert abs(l_nat.item() - loss.item()) / loss.item() < 0.03
     a = net.arena.by_name
     d = ref.decoder
-    assert _cos(a['decoder.final_conv.weight'].grad, d.final_conv.weight.grad) > 0.95
-    assert _cos(a['decoder.final_conv.bias'].grad, d.final_conv.bias.grad) > 0.95
+    # the output conv's rows are padded to 8 (zero, with zero gradient)
+    assert a['decoder.final_conv.weight'].grad[1:].abs().max() == 0
+    assert _cos(a['decoder.final_conv.weight'].grad[:1], d.final_conv.weight.grad) > 0.95
+    assert _cos(a['decoder.final_conv.bias'].grad[:1], d.final_conv.bias.grad) > 0.95
     g = a['decoder.heads.3.0.0.weight'].grad.permute(0, 3, 1, 2)
     assert _cos(g, d.heads[3][0][0].weight.grad) > 0.9
     assert _cos(a['decoder.heads.0.2.1.weight'].grad, d.heads[0][2][1].weight.grad) > 0.9
