@@ -12,6 +12,8 @@
 //   dw / db block-reduced into the grad arena.
 //   loss = bce_w * mean(BCE) + dice_w * (1 - (2*I + eps) / (U + eps)),  I = sum s*t,
 //   U = sum s + sum t  (contrib/criterion.BCEDiceLoss).
+// * bilinear x2 upsampling (align_corners=True) of the FPN heads: forward 4 taps per
+//   output chunk, backward as a gather over the outputs that read an input pixel.
 #include "common.h"
 
 namespace {
@@ -225,6 +227,90 @@ seg_head_bwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w, con
   }
 }
 
+// Bilinear upsampling with align_corners=True (FPN's segmentation heads,
+// `mlcomp/contrib/segmentation/fpn/decoder.py`), NHWC bf16, C % 8 == 0.  Source coordinate
+// of output o: f = o * (In-1)/(Out-1) in fp32 as PyTorch computes it, i0 = floor(f),
+// i1 = min(i0+1, In-1), weight f - i0 on i1.
+struct Lerp { int i0, i1; float l; };
+__device__ __forceinline__ Lerp lerp_at(int o, float scale, int in) {
+  const float f = scale * (float)o;
+  int i0 = (int)f;
+  i0 = i0 < in - 1 ? i0 : in - 1;
+  return Lerp{i0, i0 + (i0 < in - 1 ? 1 : 0), f - (float)i0};
+}
+__device__ __forceinline__ float lerp_w(const Lerp& a, int i) {
+  return (a.i0 == i ? 1.f - a.l : 0.f) + (a.i1 == i ? a.l : 0.f);
+}
+
+__global__ void __launch_bounds__(NT)
+bilinear_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N, int H, int W, int C, int Ho, int Wo,
+                    float sy, float sx) {
+  const int cpr = C / 8;
+  const long total = (long)N * Ho * Wo * cpr;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cpr);
+    const long p = i / cpr;
+    const int ox = (int)(p % Wo);
+    const long t = p / Wo;
+    const int oy = (int)(t % Ho);
+    const long n = t / Ho;
+    const Lerp ly = lerp_at(oy, sy, H), lx = lerp_at(ox, sx, W);
+    const bf16* b = x + n * H * W * (long)C + c8 * 8;
+    float v00[8], v01[8], v10[8], v11[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(b + ((long)ly.i0 * W + lx.i0) * C), v00);
+    unpack8(*reinterpret_cast<const uint4*>(b + ((long)ly.i0 * W + lx.i1) * C), v01);
+    unpack8(*reinterpret_cast<const uint4*>(b + ((long)ly.i1 * W + lx.i0) * C), v10);
+    unpack8(*reinterpret_cast<const uint4*>(b + ((long)ly.i1 * W + lx.i1) * C), v11);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      o[e] = (1.f - ly.l) * ((1.f - lx.l) * v00[e] + lx.l * v01[e]) + ly.l * ((1.f - lx.l) * v10[e] + lx.l * v11[e]);
+    *reinterpret_cast<uint4*>(y + p * C + c8 * 8) = pack8(o);
+  }
+}
+
+// first output whose floor(o * scale) reaches i (one below it to absorb fp32 rounding;
+// outputs outside the exact range get weight 0 from lerp_w)
+__device__ __forceinline__ int first_out(int i, int in, int out) {
+  if (in <= 1 || i <= 0) return 0;
+  const long num = (long)i * (out - 1);
+  const int o = (int)((num + (in - 1) - 1) / (in - 1)) - 1;
+  return o > 0 ? o : 0;
+}
+
+// gather form of the backward: input pixel (iy, ix) sums the outputs whose interpolation
+// reads it (source index i0 or i1 equal to it) - no atomics, every dx written once
+__global__ void __launch_bounds__(NT)
+bilinear_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx, int N, int H, int W, int C, int Ho, int Wo,
+                    float sy, float sx) {
+  const int cpr = C / 8;
+  const long total = (long)N * H * W * cpr;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cpr);
+    const long p = i / cpr;
+    const int ix = (int)(p % W);
+    const long t = p / W;
+    const int iy = (int)(t % H);
+    const long n = t / H;
+    const int oy0 = first_out(iy - 1, H, Ho), oy1 = iy + 1 >= H ? Ho : first_out(iy + 1, H, Ho) + 2;
+    const int ox0 = first_out(ix - 1, W, Wo), ox1 = ix + 1 >= W ? Wo : first_out(ix + 1, W, Wo) + 2;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const bf16* b = dy + n * Ho * Wo * (long)C + c8 * 8;
+    for (int oy = oy0; oy < (oy1 < Ho ? oy1 : Ho); ++oy) {
+      const float wy = lerp_w(lerp_at(oy, sy, H), iy);
+      if (wy == 0.f) continue;
+      for (int ox = ox0; ox < (ox1 < Wo ? ox1 : Wo); ++ox) {
+        const float w = wy * lerp_w(lerp_at(ox, sx, W), ix);
+        if (w == 0.f) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(b + ((long)oy * Wo + ox) * C), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += w * f[e];
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + p * C + c8 * 8) = pack8(acc);
+  }
+}
+
 inline int grid_for(long work) {
   long b = (work + NT - 1) / NT;
   return (int)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
@@ -250,6 +336,26 @@ MLC_EXPORT int mlc_upcat_bwd(const bf16* dout, bf16* dlo, bf16* dskip, int N, in
     const long P = (long)N * 4 * h * w;
     hipLaunchKernelGGL(upcat_bwd_skip_kernel, dim3(grid_for(P * (C2 / 8))), dim3(NT), 0, st, dout, dskip, P, C1, C2);
   }
+  return hipGetLastError();
+}
+
+// y [N,Ho,Wo,C] = bilinear upsampling (align_corners=True) of x [N,H,W,C]; C % 8 == 0
+MLC_EXPORT int mlc_bilinear_up_fwd(const bf16* x, bf16* y, int N, int H, int W, int C, int Ho, int Wo,
+                                   hipStream_t st) {
+  if (C % 8 || H < 1 || W < 1 || Ho < 1 || Wo < 1) return -1;
+  const float sy = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.f, sx = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
+  hipLaunchKernelGGL(bilinear_fwd_kernel, dim3(grid_for((long)N * Ho * Wo * (C / 8))), dim3(NT), 0, st, x, y, N, H, W,
+                     C, Ho, Wo, sy, sx);
+  return hipGetLastError();
+}
+
+// dx [N,H,W,C] from dy [N,Ho,Wo,C] (gather, fp32 accumulate); C % 8 == 0
+MLC_EXPORT int mlc_bilinear_up_bwd(const bf16* dy, bf16* dx, int N, int H, int W, int C, int Ho, int Wo,
+                                   hipStream_t st) {
+  if (C % 8 || H < 1 || W < 1 || Ho < 1 || Wo < 1) return -1;
+  const float sy = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.f, sx = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
+  hipLaunchKernelGGL(bilinear_bwd_kernel, dim3(grid_for((long)N * H * W * (C / 8))), dim3(NT), 0, st, dy, dx, N, H, W,
+                     C, Ho, Wo, sy, sx);
   return hipGetLastError();
 }
 

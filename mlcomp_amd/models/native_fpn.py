@@ -37,9 +37,24 @@ def _nhwc(x):
 
 
 def _up(x, scale, mode):
-    """NHWC upsampling (channels_last views, so no layout copies)."""
+    """NHWC upsampling (channels_last views, so no layout copies); the heads' bf16 bilinear
+    x2 runs on the native kernels (:class:`_BilinearFn`)."""
+    if mode == 'bilinear' and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
+        return _BilinearFn.apply(x.contiguous(), scale)
     kw = {'align_corners': True} if mode == 'bilinear' else {}
     return _nhwc(F.interpolate(_nchw(x), scale_factor=scale, mode=mode, **kw))
+
+
+class _BilinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, scale):
+        N, H, W, C = x.shape
+        ctx.hw = (H, W)
+        return seg.bilinear_up_fwd(x, H * scale, W * scale)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return seg.bilinear_up_bwd(dy.contiguous(), *ctx.hw), None
 
 
 # ---------------------------------------------------------------------------- units

@@ -89,3 +89,28 @@ def seg_head_bwd(x, w, b, target, sums, dw, db, bce_w=1.0, dice_w=1.0, eps=1e-7)
 
 
 __all__ = ['upcat_fwd', 'upcat_bwd', 'seg_head_fwd', 'seg_head_bwd', 'seg_loss']
+
+
+def bilinear_up_fwd(x, Ho, Wo):
+    """NHWC bf16 bilinear upsampling with align_corners=True (C % 8 == 0 on the GPU)."""
+    N, H, W, C = x.shape
+    if _cuda(x):
+        y = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.bfloat16)
+        _lib.call('mlc_bilinear_up_fwd', _lib.ptr(x), _lib.ptr(y), N, H, W, C, Ho, Wo, _lib.stream())
+        return y
+    y = torch.nn.functional.interpolate(x.permute(0, 3, 1, 2).float(), size=(Ho, Wo), mode='bilinear',
+                                        align_corners=True)
+    return y.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+
+
+def bilinear_up_bwd(dy, H, W):
+    """Input gradient of :func:`bilinear_up_fwd` (gather over the reading outputs, fp32)."""
+    N, Ho, Wo, C = dy.shape
+    if _cuda(dy):
+        dx = torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
+        _lib.call('mlc_bilinear_up_bwd', _lib.ptr(dy.contiguous()), _lib.ptr(dx), N, H, W, C, Ho, Wo, _lib.stream())
+        return dx
+    x = torch.zeros(N, C, H, W, requires_grad=True)
+    y = torch.nn.functional.interpolate(x, size=(Ho, Wo), mode='bilinear', align_corners=True)
+    (g,) = torch.autograd.grad(y, x, dy.permute(0, 3, 1, 2).float())
+    return g.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
