@@ -110,7 +110,8 @@ def bilinear_up_bwd(dy, H, W):
         dx = torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
         _lib.call('mlc_bilinear_up_bwd', _lib.ptr(dy.contiguous()), _lib.ptr(dx), N, H, W, C, Ho, Wo, _lib.stream())
         return dx
-    x = torch.zeros(N, C, H, W, requires_grad=True)
-    y = torch.nn.functional.interpolate(x, size=(Ho, Wo), mode='bilinear', align_corners=True)
-    (g,) = torch.autograd.grad(y, x, dy.permute(0, 3, 1, 2).float())
+    with torch.enable_grad():     # (called from inside an autograd backward)
+        x = torch.zeros(N, C, H, W, requires_grad=True)
+        y = torch.nn.functional.interpolate(x, size=(Ho, Wo), mode='bilinear', align_corners=True)
+        (g,) = torch.autograd.grad(y, x, dy.permute(0, 3, 1, 2).float())
     return g.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
