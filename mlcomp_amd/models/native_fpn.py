@@ -48,9 +48,11 @@ def _up(x, scale, mode):
 class _BilinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, scale):
+        """``scale``: an integer factor or the output size (Ho, Wo)."""
         N, H, W, C = x.shape
         ctx.hw = (H, W)
-        return seg.bilinear_up_fwd(x, H * scale, W * scale)
+        Ho, Wo = scale if isinstance(scale, tuple) else (H * scale, W * scale)
+        return seg.bilinear_up_fwd(x, Ho, Wo)
 
     @staticmethod
     def backward(ctx, dy):
@@ -118,20 +120,31 @@ class _Conv1x1BiasFn(torch.autograd.Function):
 
 
 class Conv3x3:
-    """3x3 / stride 1 / pad 1 conv without bias on the implicit-GEMM kernels."""
+    """3x3 / stride 1 / pad 1 conv on the implicit-GEMM kernels.  With a bias (an output
+    conv: PSPNet's head) the output channels are padded to 8 (zero filters, zero gradient)
+    and the result is fp32 ``conv + bias`` over all padded channels (the caller slices)."""
 
     def __init__(self, ctx, name, conv: nn.Conv2d):
         assert conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
-        assert conv.groups == 1 and conv.bias is None
+        assert conv.groups == 1
         self.ctx, self.conv = ctx, conv
-        self.Co, self.Ci = conv.out_channels, conv.in_channels
+        self.O, self.Ci = conv.out_channels, conv.in_channels
+        self.has_bias = conv.bias is not None
+        self.Co = (self.O + 7) // 8 * 8 if self.has_bias else self.O
         self.w = ctx.arena.weight(f'{name}.weight', (self.Co, 3, 3, self.Ci))
+        self.b = ctx.arena.vector(f'{name}.bias', (self.Co,)) if self.has_bias else None
 
     def load_from_torch(self):
-        self.w.master.copy_(self.conv.weight.detach().permute(0, 2, 3, 1).float().to(self.ctx.device))
+        self.w.master.zero_()
+        self.w.master[:self.O].copy_(self.conv.weight.detach().permute(0, 2, 3, 1).float().to(self.ctx.device))
+        if self.has_bias:
+            self.b.master.zero_()
+            self.b.master[:self.O].copy_(self.conv.bias.detach().float().to(self.ctx.device))
 
     def export_to_torch(self):
-        self.conv.weight.data.copy_(self.w.master.permute(0, 3, 1, 2).to(self.conv.weight.device))
+        self.conv.weight.data.copy_(self.w.master[:self.O].permute(0, 3, 1, 2).to(self.conv.weight.device))
+        if self.has_bias:
+            self.conv.bias.data.copy_(self.b.master[:self.O].to(self.conv.bias.device))
 
     def __call__(self, x):
         return _Conv3x3Fn.apply(x, self.ctx.anchor, self)
@@ -142,13 +155,17 @@ class _Conv3x3Fn(torch.autograd.Function):
     def forward(ctx, x, anchor, u: Conv3x3):
         ctx.u = u
         ctx.save_for_backward(x)
-        return Fn.conv2d_fwd(x, u.w.bf16, 1, 1)
+        y = Fn.conv2d_fwd(x, u.w.bf16, 1, 1)
+        return y.float() + u.b.master if u.has_bias else y
 
     @staticmethod
     def backward(ctx, dy):
         u: Conv3x3 = ctx.u
         (x,) = ctx.saved_tensors
-        dy = dy.contiguous()
+        if u.has_bias:
+            u.b.grad.add_(dy.float().sum((0, 1, 2)))
+            u.ctx.arena.mark_ready(u.b)
+        dy = dy.to(torch.bfloat16).contiguous()
         Fn.conv2d_wgrad(dy, x, u.w.shape, 1, 1, out=u.w.grad, accumulate=True)
         dx = Fn.conv2d_dgrad(dy, u.w.bf16, x.shape, 1, 1) if ctx.needs_input_grad[0] else None
         u.ctx.arena.mark_ready(u.w)
@@ -212,16 +229,17 @@ class _GNReluFn(torch.autograd.Function):
         return dx.to(torch.bfloat16).view(x.shape), None, None
 
 
-class FPNHead:
-    """Output conv (1x1 + bias, fp32 logits at stride 4) -> x4 bilinear -> BCE + soft Dice
-    (contrib.criterion.BCEDiceLoss) with the loss sums [BCE sum, sum s*t, sum s, sum t]
-    kept in the workspace like :class:`~.native_unet.SegHead`."""
+class UpsampledSegHead:
+    """Output conv (``conv``: a :class:`Conv1x1Bias` with fp32 output or a biased
+    :class:`Conv3x3`) -> x ``scale`` bilinear -> BCE + soft Dice (contrib.criterion.
+    BCEDiceLoss) with the loss sums [BCE sum, sum s*t, sum s, sum t] kept in the workspace
+    like :class:`~.native_unet.SegHead` (FPN: 1x1 at stride 4; PSPNet: 3x3 at stride 8)."""
 
-    def __init__(self, ctx, conv: nn.Conv2d, bce_w=1.0, dice_w=1.0, eps=1e-7):
-        assert conv.out_channels <= 4
+    def __init__(self, ctx, conv, K, scale, bce_w=1.0, dice_w=1.0, eps=1e-7):
+        assert K <= 4
         self.ctx = ctx
-        self.conv = Conv1x1Bias(ctx, 'decoder.final_conv', conv, f32_out=True)
-        self.K = conv.out_channels
+        self.conv = conv
+        self.K, self.scale = K, scale
         self.bce_w, self.dice_w, self.eps = bce_w, dice_w, eps
         self.k_sums = ctx.ws.request('decoder.head.sums', 4)
 
@@ -229,8 +247,8 @@ class FPNHead:
         return self.ctx.ws[self.k_sums]
 
     def logits(self, x):
-        """[N, H/4, W/4, C] bf16 -> fp32 logits [N, H, W, K] (NHWC)."""
-        return _up(self.conv(x)[..., :self.K], 4, 'bilinear')
+        """[N, H/scale, W/scale, C] bf16 -> fp32 logits [N, H, W, K] (NHWC)."""
+        return _up(self.conv(x)[..., :self.K].float(), self.scale, 'bilinear')
 
     def loss(self, z, target):
         zf = z.reshape(-1)
@@ -266,7 +284,8 @@ class NativeFPN(NativeUnet):
                 layers.append((Conv3x3(ctx, f'{pre}.0', gu[0]), GNRelu(ctx, f'{pre}.1', gu[1]), gu.upsample))
             self.heads.append(layers)
         self.drop = dec.dropout.p
-        self.head = FPNHead(ctx, dec.final_conv, bce_w, dice_w, eps)
+        self.head = UpsampledSegHead(ctx, Conv1x1Bias(ctx, 'decoder.final_conv', dec.final_conv, f32_out=True),
+                                     dec.final_conv.out_channels, 4, bce_w, dice_w, eps)
         self._finish_init(device)
 
     def _units(self):

@@ -1,4 +1,4 @@
-"""The native training step for U-Net (BASELINE config 3), LinkNet and FPN segmentation.
+"""The native training step for U-Net (BASELINE config 3), LinkNet, FPN and PSPNet segmentation.
 
 forward (fused conv+BN+ReLU nodes, fused upsample+concat) -> fused 1x1 head + BCE + Dice
 -> backward (wgrad straight into the flat grad arena, bucketed RCCL all-reduce on a side
@@ -15,6 +15,7 @@ import torch
 from mlcomp_amd.models.native_resnet import STEM_CIN
 from mlcomp_amd.models.native_fpn import NativeFPN
 from mlcomp_amd.models.native_linknet import NativeLinknet
+from mlcomp_amd.models.native_psp import NativePSPNet
 from mlcomp_amd.models.native_unet import NativeUnet
 from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops.layers import flatten_bn_buffers
@@ -37,14 +38,15 @@ class NativeSegmentationStep(GraphedStep):
                  lr=3e-4, weight_decay=0.0, optimizer='Adam', momentum=0.9, betas=(0.9, 0.999), eps=1e-8,
                  seed=0, warmup_eager=2, torch_model=None, comm=None, classes=1, nesterov=False, dampening=0.0,
                  bce_w=1.0, dice_w=1.0, loss_eps=1e-7, arch='unet'):
-        from mlcomp_amd.contrib.segmentation.models import FPN, Linknet, Unet
+        from mlcomp_amd.contrib.segmentation.models import FPN, Linknet, PSPNet, Unet
         self.device = torch.device(device or 'cuda')
         torch.manual_seed(seed)
-        archs = {'unet': Unet, 'linknet': Linknet, 'fpn': FPN}
+        archs = {'unet': Unet, 'linknet': Linknet, 'fpn': FPN, 'pspnet': PSPNet}
         if torch_model is None:
             torch_model = archs[arch.lower()](encoder_name=encoder, classes=classes)
         tm = torch_model
-        engine = NativeLinknet if isinstance(tm, Linknet) else NativeFPN if isinstance(tm, FPN) else NativeUnet
+        engine = (NativeLinknet if isinstance(tm, Linknet) else NativeFPN if isinstance(tm, FPN)
+                  else NativePSPNet if isinstance(tm, PSPNet) else NativeUnet)
         self.net = engine(tm, self.device, bce_w=bce_w, dice_w=dice_w, eps=loss_eps)
         self.net.ctx.grad_prezeroed = True
         self.world = world_size

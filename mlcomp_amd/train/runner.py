@@ -95,7 +95,7 @@ class State:
 
 
 def _native_kind(model: nn.Module, device: torch.device) -> Optional[str]:
-    """'resnet' / 'bert' / 'unet' (U-Net, LinkNet and FPN segmentation) when the model runs on a
+    """'resnet' / 'bert' / 'unet' (U-Net, LinkNet, FPN, PSPNet segmentation) when the model runs on a
     native engine on this device."""
     if device.type != 'cuda':
         return None
@@ -105,7 +105,14 @@ def _native_kind(model: nn.Module, device: torch.device) -> Optional[str]:
         return 'resnet'
     if isinstance(model, BertForSequenceClassification):
         return 'bert'
-    from mlcomp_amd.contrib.segmentation.models import FPN, Linknet, Unet
+    from mlcomp_amd.contrib.segmentation.models import FPN, Linknet, PSPNet, Unet
+    if isinstance(model, PSPNet):      # sigmoid heads of <= 4 classes (BCE + Dice)
+        from mlcomp_amd.contrib.segmentation.encoders import ResNetEncoder
+        dec = model.decoder
+        if isinstance(model.encoder, ResNetEncoder) and model.encoder.body.groups == 1 \
+                and dec.final_conv.out_channels <= 4 and dec.aux is None \
+                and isinstance(dec.conv[1], nn.BatchNorm2d):
+            return 'unet'
     if isinstance(model, FPN):         # the segmentation engine kind ('unet': BCE+Dice head)
         from mlcomp_amd.contrib.segmentation.encoders import ResNetEncoder
         if isinstance(model.encoder, ResNetEncoder) and model.encoder.body.groups == 1 \

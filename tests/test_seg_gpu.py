@@ -272,3 +272,36 @@ def test_bilinear_up_align_corners(N, H, W, C, s):
     torch.cuda.synchronize()
     assert rel(got, ref) < 1e-2
     assert rel(gd, rd) < 1e-2
+
+
+def test_native_pspnet_step_matches_torch_and_graph():
+    """The native PSPNet engine (ResNet-34 encoder, 1 sigmoid class): first loss == fp32
+    PyTorch on the same weights / batch; graph replay == eager (dropout off)."""
+    from mlcomp_amd.contrib.criterion import BCEDiceLoss
+    from mlcomp_amd.contrib.segmentation.models import PSPNet
+    from mlcomp_amd.ops import functional as Fn
+    from mlcomp_amd.train.native_seg_step import NativeSegmentationStep
+
+    def mk(graph):
+        torch.manual_seed(3)
+        tm = PSPNet(encoder_name='resnet34', classes=1, dropout=0.0)
+        ref = PSPNet(encoder_name='resnet34', classes=1, dropout=0.0)
+        ref.load_state_dict(tm.state_dict())
+        st = NativeSegmentationStep(torch_model=tm, batch=4, image_size=128, device=DEV, use_graph=graph,
+                                    seed=3, warmup_eager=1)
+        return st, ref
+    (eager, ref), (graph, _) = mk(False), mk(True)
+    x = Fn.stem_s2d_to_nhwc(eager.x).permute(0, 3, 1, 2).float().contiguous()
+    with torch.no_grad():
+        want = BCEDiceLoss()(ref.to(DEV).train()(x), eager.t.view(4, 1, 128, 128)).item()
+    le, lg = [], []
+    for _ in range(4):
+        eager()
+        graph()
+        le.append(eager.last_loss())
+        lg.append(graph.last_loss())
+    torch.cuda.synchronize()
+    assert graph.graph is not None and all(v == v for v in le + lg), (le, lg)
+    assert abs(le[0] - want) < 0.03 * want, (le[0], want)
+    assert abs(le[0] - lg[0]) < 1e-3 * abs(le[0]) + 1e-4, (le, lg)
+    assert abs(le[1] - lg[1]) < 6e-2 * abs(le[1]) + 1e-3, (le, lg)
