@@ -659,6 +659,13 @@ def linear_wgrad_bias(dout, x, dw, db):
     summed from dout's tiles as the wgrad kernel stages them (``mlc_linear_wgrad_bias``)."""
     B, O = dout.shape
     I = x.shape[1]
+    if _cuda(dout) and B % 8:
+        # the GEMM reduces over the rows in 8-row chunks: zero rows add nothing (PSPNet's
+        # 1x1 pyramid level has batch x 1 x 1 rows)
+        pad = 8 - B % 8
+        dout = torch.nn.functional.pad(dout, (0, 0, 0, pad))
+        x = torch.nn.functional.pad(x, (0, 0, 0, pad))
+        B += pad
     if _cuda(dout):
         assert dout.is_contiguous() and x.is_contiguous() and x.shape[0] == B
         assert tuple(dw.shape) == (O, I) and dw.is_contiguous() and db.numel() == O
