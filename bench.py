@@ -71,7 +71,7 @@ def main():
         dist.init_process_group('nccl', device_id=device)
 
     is_bert = args.model.startswith('bert')
-    is_unet = args.model.split('-')[0] in ('unet', 'linknet', 'fpn', 'pspnet')
+    is_unet = args.model.split('-')[0] in ('unet', 'linknet', 'fpn', 'pspnet', 'deeplab')
     if args.batch is None:
         args.batch = 32 if (is_bert or is_unet) else 256
     if is_unet:
@@ -79,7 +79,7 @@ def main():
         from mlcomp_amd.train.segment import build_seg_step
         if args.image_size == 224:
             args.image_size = 256
-        # (--model linknet|fpn|pspnet[-<encoder>]: that decoder on the same data / loss / optimizer)
+        # (--model linknet|fpn|pspnet[-<encoder>] / deeplab: that model on the same data / loss / optimizer)
         enc = args.model.split('-', 1)[1] if '-' in args.model else 'resnet34'
         step = build_seg_step(enc, batch=args.batch, impl=args.impl, image_size=args.image_size, device=device,
                               world_size=world, use_graph=(args.graph if args.graph >= 0 else None),
@@ -160,7 +160,7 @@ def main():
         print(json.dumps(out), flush=True)
     elif rank == 0 and is_unet:
         out = {
-            'metric': f"images/sec (whole node) {dict(linknet='LinkNet', fpn='FPN', pspnet='PSPNet').get(args.model.split('-')[0], 'U-Net')} "
+            'metric': f"images/sec (whole node) {dict(linknet='LinkNet', fpn='FPN', pspnet='PSPNet', deeplab='DeepLab').get(args.model.split('-')[0], 'U-Net')} "
                       'segmentation DAG train task',
             'value': round(value, 2), 'unit': 'images/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',

@@ -1,4 +1,5 @@
-"""The native training step for U-Net (BASELINE config 3), LinkNet, FPN and PSPNet segmentation.
+"""The native training step for U-Net (BASELINE config 3), LinkNet, FPN, PSPNet and DeepLab
+(ResNet backbone) segmentation.
 
 forward (fused conv+BN+ReLU nodes, fused upsample+concat) -> fused 1x1 head + BCE + Dice
 -> backward (wgrad straight into the flat grad arena, bucketed RCCL all-reduce on a side
@@ -13,6 +14,7 @@ from typing import Optional
 import torch
 
 from mlcomp_amd.models.native_resnet import STEM_CIN
+from mlcomp_amd.models.native_deeplab import NativeDeepLab
 from mlcomp_amd.models.native_fpn import NativeFPN
 from mlcomp_amd.models.native_linknet import NativeLinknet
 from mlcomp_amd.models.native_psp import NativePSPNet
@@ -41,12 +43,17 @@ class NativeSegmentationStep(GraphedStep):
         from mlcomp_amd.contrib.segmentation.models import FPN, Linknet, PSPNet, Unet
         self.device = torch.device(device or 'cuda')
         torch.manual_seed(seed)
+        from mlcomp_amd.contrib.segmentation.deeplab import DeepLab
         archs = {'unet': Unet, 'linknet': Linknet, 'fpn': FPN, 'pspnet': PSPNet}
         if torch_model is None:
-            torch_model = archs[arch.lower()](encoder_name=encoder, classes=classes)
+            if arch.lower() == 'deeplab':
+                torch_model = DeepLab(backbone='resnet', num_classes=classes)
+            else:
+                torch_model = archs[arch.lower()](encoder_name=encoder, classes=classes)
         tm = torch_model
         engine = (NativeLinknet if isinstance(tm, Linknet) else NativeFPN if isinstance(tm, FPN)
-                  else NativePSPNet if isinstance(tm, PSPNet) else NativeUnet)
+                  else NativePSPNet if isinstance(tm, PSPNet) else NativeDeepLab if isinstance(tm, DeepLab)
+                  else NativeUnet)
         self.net = engine(tm, self.device, bce_w=bce_w, dice_w=dice_w, eps=loss_eps)
         self.net.ctx.grad_prezeroed = True
         self.world = world_size

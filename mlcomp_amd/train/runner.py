@@ -95,7 +95,7 @@ class State:
 
 
 def _native_kind(model: nn.Module, device: torch.device) -> Optional[str]:
-    """'resnet' / 'bert' / 'unet' (U-Net, LinkNet, FPN, PSPNet segmentation) when the model runs on a
+    """'resnet' / 'bert' / 'unet' (U-Net, LinkNet, FPN, PSPNet, DeepLab segmentation) when the model runs on a
     native engine on this device."""
     if device.type != 'cuda':
         return None
@@ -105,7 +105,12 @@ def _native_kind(model: nn.Module, device: torch.device) -> Optional[str]:
         return 'resnet'
     if isinstance(model, BertForSequenceClassification):
         return 'bert'
+    from mlcomp_amd.contrib.segmentation.deeplab import DeepLab, ResNetBackbone
     from mlcomp_amd.contrib.segmentation.models import FPN, Linknet, PSPNet, Unet
+    if isinstance(model, DeepLab):     # dilated-ResNet backbone, sigmoid heads of <= 4 classes
+        if isinstance(model.backbone, ResNetBackbone) and model.backbone.body.groups == 1 \
+                and not model._freeze and model.decoder.body[4].out_channels <= 4:
+            return 'unet'
     if isinstance(model, PSPNet):      # sigmoid heads of <= 4 classes (BCE + Dice)
         from mlcomp_amd.contrib.segmentation.encoders import ResNetEncoder
         dec = model.decoder

@@ -305,3 +305,40 @@ def test_native_pspnet_step_matches_torch_and_graph():
     assert abs(le[0] - want) < 0.03 * want, (le[0], want)
     assert abs(le[0] - lg[0]) < 1e-3 * abs(le[0]) + 1e-4, (le, lg)
     assert abs(le[1] - lg[1]) < 6e-2 * abs(le[1]) + 1e-3, (le, lg)
+
+
+def test_native_deeplab_step_matches_torch_and_graph():
+    """The native DeepLab v3+ engine (dilated ResNet-101 backbone, ASPP, 1 sigmoid class):
+    first loss == fp32 PyTorch on the same weights / batch; graph replay == eager (dropout
+    off so both see the same function)."""
+    from mlcomp_amd.contrib.criterion import BCEDiceLoss
+    from mlcomp_amd.contrib.segmentation.deeplab import DeepLab
+    from mlcomp_amd.ops import functional as Fn
+    from mlcomp_amd.train.native_seg_step import NativeSegmentationStep
+
+    def mk(graph):
+        torch.manual_seed(3)
+        tm = DeepLab(backbone='resnet', num_classes=1)
+        ref = DeepLab(backbone='resnet', num_classes=1)
+        for m in (tm, ref):
+            for mod in m.modules():
+                if isinstance(mod, torch.nn.Dropout):
+                    mod.p = 0.0
+        ref.load_state_dict(tm.state_dict())
+        st = NativeSegmentationStep(torch_model=tm, batch=4, image_size=128, device=DEV, use_graph=graph,
+                                    seed=3, warmup_eager=1)
+        return st, ref
+    (eager, ref), (graph, _) = mk(False), mk(True)
+    x = Fn.stem_s2d_to_nhwc(eager.x).permute(0, 3, 1, 2).float().contiguous()
+    with torch.no_grad():
+        want = BCEDiceLoss()(ref.to(DEV).train()(x), eager.t.view(4, 1, 128, 128)).item()
+    le, lg = [], []
+    for _ in range(3):
+        eager()
+        graph()
+        le.append(eager.last_loss())
+        lg.append(graph.last_loss())
+    torch.cuda.synchronize()
+    assert graph.graph is not None and all(v == v for v in le + lg), (le, lg)
+    assert abs(le[0] - want) < 0.03 * want, (le[0], want)
+    assert abs(le[0] - lg[0]) < 1e-3 * abs(le[0]) + 1e-4, (le, lg)
