@@ -186,7 +186,8 @@ def bn_unroll(request):
 
 
 @pytest.mark.parametrize('relu,res', [(True, True), (True, False), (False, False)])
-@pytest.mark.parametrize('C,shape', [(64, (4, 5, 3)), (256, (4, 5, 3)), (2048, (4, 5, 3)), (256, (4, 50, 31))])
+@pytest.mark.parametrize('C,shape', [(64, (4, 5, 3)), (256, (4, 5, 3)), (2048, (4, 5, 3)), (256, (4, 50, 31)),
+                                     (48, (4, 9, 7)), (768, (4, 50, 31))])   # channel groups not dividing 256
 def test_bn_fwd_bwd(relu, res, C, shape, bn_unroll):
     rows_shape = (*shape, C)
     y = _bf(*rows_shape, scale=2.0, seed=7) + 0.5
