@@ -14,6 +14,8 @@
 //   U = sum s + sum t  (contrib/criterion.BCEDiceLoss).
 // * bilinear x2 upsampling (align_corners=True) of the FPN heads: forward 4 taps per
 //   output chunk, backward as a gather over the outputs that read an input pixel.
+// * GroupNorm + ReLU of the FPN heads: per-(sample, channel) sums, then one elementwise pass
+//   (forward and backward each: a reduction pass + an apply pass).
 #include "common.h"
 
 namespace {
@@ -311,6 +313,112 @@ bilinear_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx, int N, i
   }
 }
 
+// GroupNorm + ReLU over NHWC bf16 (FPN's segmentation heads, GroupNorm(32, 128)), C % 8 == 0
+// and C/8 dividing 256.  Statistics are per (sample, channel) partial sums reduced per
+// block and added with one atomic per channel; the per-group mean / rstd (and in the
+// backward the per-group means of gamma*dy and gamma*dy*xhat) are combined from them on the
+// fly by the elementwise passes, so each tensor is read once per pass.
+constexpr int GN_ROWS = 256;   // pixel rows per block of the reduction passes
+
+// MODE 0: st[n][c] += (sum x, sum x^2);  MODE 1: st[n][c] += (sum dym*xhat, sum dym) with
+// dym = dz * [xhat*gamma + beta > 0] (ReLU mask recomputed), xhat from fst (forward stats)
+template <int MODE>
+__global__ void __launch_bounds__(NT)
+gn_reduce_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dz, const float* __restrict__ fst,
+                 const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ st, int HW,
+                 int C, int G, float eps) {
+  __shared__ float red[NT][17];
+  const int cpr = C / 8, rg = NT / cpr, t = threadIdx.x;
+  const int n = blockIdx.y, c8 = t % cpr, r0 = blockIdx.x * GN_ROWS + t / cpr;
+  const int Cg = C / G;
+  const float cnt = (float)HW * (float)Cg;
+  float s1[8], s2[8], mu[8], rs[8], ga[8], be[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  if (MODE == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c8 * 8 + e, g0 = (c / Cg) * Cg;
+      float a = 0.f, b = 0.f;
+      for (int k = 0; k < Cg; ++k) { a += fst[((long)n * C + g0 + k) * 2]; b += fst[((long)n * C + g0 + k) * 2 + 1]; }
+      mu[e] = a / cnt;
+      rs[e] = rsqrtf(fmaxf(b / cnt - mu[e] * mu[e], 0.f) + eps);
+      ga[e] = gamma[c];
+      be[e] = beta[c];
+    }
+  }
+  const long base = (long)n * HW;
+  const int rend = min(HW, (int)(blockIdx.x + 1) * GN_ROWS);
+  for (int r = r0; r < rend; r += rg) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + (base + r) * C + c8 * 8), f);
+    if (MODE == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1[e] += f[e]; s2[e] += f[e] * f[e]; }
+    } else {
+      float d[8];
+      unpack8(*reinterpret_cast<const uint4*>(dz + (base + r) * C + c8 * 8), d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh = (f[e] - mu[e]) * rs[e];
+        const float dm = xh * ga[e] + be[e] > 0.f ? d[e] : 0.f;
+        s1[e] += dm * xh;
+        s2[e] += dm;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[t][e] = s1[e]; red[t][8 + e] = s2[e]; }
+  __syncthreads();
+  if (t < C) {
+    const int cc8 = t / 8, e = t % 8;
+    float a = 0.f, b = 0.f;
+    for (int j = 0; j < rg; ++j) { a += red[j * cpr + cc8][e]; b += red[j * cpr + cc8][8 + e]; }
+    atomicAdd(st + ((long)n * C + t) * 2, a);
+    atomicAdd(st + ((long)n * C + t) * 2 + 1, b);
+  }
+}
+
+// MODE 0: z = relu(xhat*gamma + beta);  MODE 1: dx from dz and the backward sums bst
+template <int MODE>
+__global__ void __launch_bounds__(NT)
+gn_apply_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dz, const float* __restrict__ fst,
+                const float* __restrict__ bst, const float* __restrict__ gamma, const float* __restrict__ beta,
+                bf16* __restrict__ out, int N, int HW, int C, int G, float eps) {
+  const int cpr = C / 8, Cg = C / G;
+  const float cnt = (float)HW * (float)Cg;
+  const long total = (long)N * HW * cpr;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cpr);
+    const long p = i / cpr;
+    const int n = (int)(p / HW);
+    float f[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + p * C + c8 * 8), f);
+    float d[8];
+    if (MODE == 1) unpack8(*reinterpret_cast<const uint4*>(dz + p * C + c8 * 8), d);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c8 * 8 + e, g0 = (c / Cg) * Cg;
+      float a = 0.f, b = 0.f, A = 0.f, B = 0.f;
+      for (int k = 0; k < Cg; ++k) {
+        const long q = ((long)n * C + g0 + k) * 2;
+        a += fst[q];
+        b += fst[q + 1];
+        if (MODE == 1) { A += gamma[g0 + k] * bst[q]; B += gamma[g0 + k] * bst[q + 1]; }
+      }
+      const float mu = a / cnt, rs = rsqrtf(fmaxf(b / cnt - mu * mu, 0.f) + eps);
+      const float xh = (f[e] - mu) * rs, y = xh * gamma[c] + beta[c];
+      if (MODE == 0) {
+        o[e] = fmaxf(y, 0.f);
+      } else {
+        const float dm = y > 0.f ? d[e] : 0.f;
+        o[e] = rs * (gamma[c] * dm - B / cnt - xh * (A / cnt));
+      }
+    }
+    *reinterpret_cast<uint4*>(out + p * C + c8 * 8) = pack8(o);
+  }
+}
+
 inline int grid_for(long work) {
   long b = (work + NT - 1) / NT;
   return (int)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
@@ -356,6 +464,32 @@ MLC_EXPORT int mlc_bilinear_up_bwd(const bf16* dy, bf16* dx, int N, int H, int W
   const float sy = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.f, sx = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
   hipLaunchKernelGGL(bilinear_bwd_kernel, dim3(grid_for((long)N * H * W * (C / 8))), dim3(NT), 0, st, dy, dx, N, H, W,
                      C, Ho, Wo, sy, sx);
+  return hipGetLastError();
+}
+
+// GroupNorm + ReLU forward: z [N,HW,C] from x; fst [N][C][2] fp32 (zeroed by the caller)
+// receives the per-channel sums the backward reuses.  C % 8 == 0, 256 % (C/8) == 0, G | C.
+MLC_EXPORT int mlc_gn_relu_fwd(const bf16* x, const float* gamma, const float* beta, bf16* z, float* fst, int N,
+                               int HW, int C, int G, float eps, hipStream_t st) {
+  if (C % 8 || NT % (C / 8) || C % G || C > NT * 8) return -1;
+  const dim3 rgrid((HW + GN_ROWS - 1) / GN_ROWS, N);
+  hipLaunchKernelGGL(gn_reduce_kernel<0>, rgrid, dim3(NT), 0, st, x, nullptr, nullptr, nullptr, nullptr, fst, HW,
+                     C, G, eps);
+  hipLaunchKernelGGL(gn_apply_kernel<0>, dim3(grid_for((long)N * HW * (C / 8))), dim3(NT), 0, st, x, nullptr, fst,
+                     nullptr, gamma, beta, z, N, HW, C, G, eps);
+  return hipGetLastError();
+}
+
+// backward: dx from dz (ReLU mask recomputed), bst [N][C][2] fp32 scratch (zeroed by the
+// caller) = per-channel (sum dym*xhat, sum dym): dgamma / dbeta are its sums over n
+MLC_EXPORT int mlc_gn_relu_bwd(const bf16* x, const bf16* dz, const float* gamma, const float* beta,
+                               const float* fst, float* bst, bf16* dx, int N, int HW, int C, int G, float eps,
+                               hipStream_t st) {
+  if (C % 8 || NT % (C / 8) || C % G || C > NT * 8) return -1;
+  const dim3 rgrid((HW + GN_ROWS - 1) / GN_ROWS, N);
+  hipLaunchKernelGGL(gn_reduce_kernel<1>, rgrid, dim3(NT), 0, st, x, dz, fst, gamma, beta, bst, HW, C, G, eps);
+  hipLaunchKernelGGL(gn_apply_kernel<1>, dim3(grid_for((long)N * HW * (C / 8))), dim3(NT), 0, st, x, dz, fst, bst,
+                     gamma, beta, dx, N, HW, C, G, eps);
   return hipGetLastError();
 }
 

@@ -9,10 +9,11 @@
     pixel rows with the bias in the epilogue (``transformer.dense_fwd``), their weight and
     bias gradients one GEMM (``Fn.linear_wgrad_bias``), the input gradient ``dense_dgrad``;
   - the 3x3 convs of the segmentation heads are the implicit-GEMM conv kernels.
-* the GroupNorm(32) + ReLU of the heads, the nearest / bilinear upsamplings, the pyramid
-  additions, Dropout2d and the BCE + Dice loss on the x4-upsampled logits are PyTorch tensor
-  ops on the NHWC activations (no MIOpen / hipBLASLt call in the step); GroupNorm's backward
-  is written out (:class:`_GNReluFn`) so its parameter gradients land in the flat arena.
+* the GroupNorm(32) + ReLU of the heads and the bilinear x2 upsamplings are native kernels
+  (seg.hip; the CPU path uses tensor ops with the same explicit backward, :class:`_GNReluFn`);
+  the nearest upsamplings, pyramid additions, Dropout2d and the BCE + Dice loss on the
+  x4-upsampled logits are PyTorch tensor ops on the NHWC activations (no MIOpen / hipBLASLt
+  call in the step).
 
 Parameters live in the flat arenas (fused Adam, bucketed all-reduce) like the other engines.
 """
@@ -22,6 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from mlcomp_amd.ops import _lib
 from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops import seg
 from mlcomp_amd.ops import transformer as Tx
@@ -201,19 +203,48 @@ def _gn_stats(u: GNRelu, x):
     return xf, mean, rstd
 
 
+def _gn_native(u: GNRelu, x) -> bool:
+    C = x.shape[-1]
+    return x.is_cuda and C % 8 == 0 and 256 % (C // 8) == 0 and C % u.G == 0
+
+
 class _GNReluFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, u: GNRelu):
+        ctx.u = u
+        if _gn_native(u, x):      # seg.hip: per-(sample, channel) sums + one apply pass
+            N, H, W, C = x.shape
+            fst = torch.zeros(N, C, 2, device=x.device, dtype=torch.float32)
+            z = torch.empty_like(x)
+            _lib.call('mlc_gn_relu_fwd', _lib.ptr(x), _lib.ptr(u.g.master), _lib.ptr(u.b.master), _lib.ptr(z),
+                      _lib.ptr(fst), N, H * W, C, u.G, float(u.eps), _lib.stream())
+            ctx.native = True
+            ctx.save_for_backward(x, fst)
+            return z
+        ctx.native = False
         xf, mean, rstd = _gn_stats(u, x)
         shape = (1, 1, u.G, u.C // u.G)
         y = (xf - mean) * rstd * u.g.master.view(shape) + u.b.master.view(shape)
-        ctx.u = u
         ctx.save_for_backward(x, mean, rstd)
         return torch.relu(y).to(torch.bfloat16).view(x.shape)
 
     @staticmethod
     def backward(ctx, dz):
         u: GNRelu = ctx.u
+        if ctx.native:
+            x, fst = ctx.saved_tensors
+            N, H, W, C = x.shape
+            bst = torch.zeros(N, C, 2, device=x.device, dtype=torch.float32)
+            dx = torch.empty_like(x)
+            _lib.call('mlc_gn_relu_bwd', _lib.ptr(x), _lib.ptr(dz.contiguous()), _lib.ptr(u.g.master),
+                      _lib.ptr(u.b.master), _lib.ptr(fst), _lib.ptr(bst), _lib.ptr(dx), N, H * W, C, u.G,
+                      float(u.eps), _lib.stream())
+            sums = bst.sum(0)
+            u.g.grad.add_(sums[:, 0])
+            u.b.grad.add_(sums[:, 1])
+            u.ctx.arena.mark_ready(u.g)
+            u.ctx.arena.mark_ready(u.b)
+            return dx, None, None
         x, mean, rstd = ctx.saved_tensors
         N, H, W, C = x.shape
         shape = (1, 1, u.G, C // u.G)

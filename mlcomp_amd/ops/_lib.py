@@ -31,6 +31,8 @@ _SIGS = {
     'mlc_conv_dgrad_t': [vp] * 4 + [i32] * 12 + [vp] * 11 + [vp],
     'mlc_bilinear_up_fwd': [vp, vp] + [i32] * 6 + [vp],
     'mlc_bilinear_up_bwd': [vp, vp] + [i32] * 6 + [vp],
+    'mlc_gn_relu_fwd': [vp, vp, vp, vp, vp] + [i32] * 4 + [f32, vp],
+    'mlc_gn_relu_bwd': [vp] * 7 + [i32] * 4 + [f32, vp],
     'mlc_conv_tr_fwd': [vp] * 5 + [i32] * 12 + [vp],
     'mlc_wt_transpose': [vp, i32, i64, vp],
     'mlc_conv_wgrad': [vp, vp, vp] + [i32] * 14 + [vp, i64, vp, vp, vp],

@@ -342,3 +342,31 @@ def test_native_deeplab_step_matches_torch_and_graph():
     assert graph.graph is not None and all(v == v for v in le + lg), (le, lg)
     assert abs(le[0] - want) < 0.03 * want, (le[0], want)
     assert abs(le[0] - lg[0]) < 1e-3 * abs(le[0]) + 1e-4, (le, lg)
+
+
+@pytest.mark.parametrize('N,H,W,C,G', [(4, 16, 16, 128, 32), (2, 33, 7, 64, 8), (3, 5, 9, 256, 32)])
+def test_gn_relu_native_vs_fp32(N, H, W, C, G):
+    """FPN's GroupNorm + ReLU on the native kernels vs fp32 autograd of nn.GroupNorm + ReLU."""
+    from mlcomp_amd.models.native_fpn import GNRelu
+    from mlcomp_amd.ops.layers import NativeContext
+    torch.manual_seed(0)
+    gn = torch.nn.GroupNorm(G, C)
+    with torch.no_grad():
+        gn.weight.uniform_(0.5, 1.5)
+        gn.bias.uniform_(-0.3, 0.3)
+    ctx = NativeContext()
+    u = GNRelu(ctx, 'gn', gn)
+    ctx.finalize(DEV)
+    u.load_from_torch()
+    x = (torch.randn(N, H, W, C) * 2 + 0.5).to(torch.bfloat16)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_()
+    ref = torch.relu(gn(xr))
+    d = torch.randn_like(ref)
+    (ref * d).sum().backward()
+    xn = x.to(DEV).requires_grad_()
+    z = u(xn)
+    (z.float() * d.permute(0, 2, 3, 1).to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel(z.permute(0, 3, 1, 2), ref.detach()) < 1e-2
+    assert rel(xn.grad.permute(0, 3, 1, 2), xr.grad) < 2e-2
+    assert rel(u.g.grad, gn.weight.grad) < 1e-2 and rel(u.b.grad, gn.bias.grad) < 1e-2
