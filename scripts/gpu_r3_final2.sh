@@ -8,7 +8,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 tail -1 $OUT/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -20 $OUT/smoke.log; exit 1; }
 tail -1 $OUT/smoke.log
-for m in resnet50 bert-base unet; do
+for m in resnet50 bert-base unet fpn; do
   timeout -k 10 300 python bench.py --model $m > $OUT/bench_$m.log 2>&1 || { echo "bench $m rc=$?"; tail -20 $OUT/bench_$m.log; exit 1; }
   tail -1 $OUT/bench_$m.log | cut -c1-160
 done
