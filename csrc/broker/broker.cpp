@@ -26,7 +26,7 @@
 // whenever it grows past 4x that set.  It survives a crash of the broker process (the
 // writes are flushed to the kernel), not a power loss (no fsync).
 //
-// usage: mlcomp-broker [--host 127.0.0.1] [--port 6380] [--journal FILE]
+// usage: mlcomp-broker [--host 127.0.0.1] [--port 6380] [--journal FILE] [--compact-every N]
 #include <arpa/inet.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -103,6 +103,9 @@ class Broker {
   std::string jpath_;
   FILE* jf_ = nullptr;
   size_t jlines_ = 0;
+ public:
+  size_t compact_every_ = 0;   // --compact-every N (tests): compact whenever N lines accrued
+ private:
 
   void journal(const char* tag, const std::string& id, const Msg* m = nullptr);
   void compact_journal();
@@ -272,9 +275,11 @@ void Broker::handle(Conn* c, const std::string& line) {
     auto a = split(rest, 2);
     if (a.size() < 2) { reply(c, "ERR usage: PUSH queue payload"); return; }
     Msg m{std::to_string(next_id_++), a[0], a[1]};
-    journal("P", m.id, &m);
+    // state first, journal after: a compaction triggered by this line rewrites the
+    // journal from the live state, which must already hold the message
     queues_[a[0]].push_back(m);
     queued_ids_.insert(m.id);
+    journal("P", m.id, &m);
     reply(c, "OK " + m.id);
     wake();
     return;
@@ -296,13 +301,14 @@ void Broker::handle(Conn* c, const std::string& line) {
     const bool had = l != leased_.end();
     if (had) {
       if (cmd == "NACK") enqueue_front(l->second);
-      else journal("A", rest);
       leased_.erase(l);
       for (auto& kv : conns_) {
         auto& v = kv.second->leased;
         for (auto it = v.begin(); it != v.end(); ++it)
           if (*it == rest) { v.erase(it); break; }
       }
+      // after the lease is gone: a compaction at this line must not write it back as live
+      if (cmd == "ACK") journal("A", rest);
     }
     reply(c, had ? "OK 1" : "OK 0");
     if (cmd == "NACK") wake();
@@ -406,7 +412,10 @@ void Broker::journal(const char* tag, const std::string& id, const Msg* m) {
   else
     fprintf(jf_, "%s %s\n", tag, id.c_str());
   fflush(jf_);
-  if (++jlines_ > 10000 && jlines_ > 4 * (queued_ids_.size() + leased_.size())) compact_journal();
+  ++jlines_;
+  if (compact_every_ ? jlines_ >= compact_every_
+                     : jlines_ > 10000 && jlines_ > 4 * (queued_ids_.size() + leased_.size()))
+    compact_journal();
 }
 
 // rewrite the journal to the live set (queued + leased, in id order) via tmp + rename
@@ -508,10 +517,12 @@ void Broker::run() {
 int main(int argc, char** argv) {
   std::string host = "127.0.0.1", jpath;
   int port = 6380;
+  long compact_every = 0;
   for (int i = 1; i + 1 < argc; i += 2) {
     if (!strcmp(argv[i], "--host")) host = argv[i + 1];
     else if (!strcmp(argv[i], "--port")) port = atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "--journal")) jpath = argv[i + 1];
+    else if (!strcmp(argv[i], "--compact-every")) compact_every = atol(argv[i + 1]);
   }
   signal(SIGPIPE, SIG_IGN);
   struct sigaction sa{};
@@ -534,6 +545,7 @@ int main(int argc, char** argv) {
   if (listen(lfd, 512) < 0) { perror("listen"); return 1; }
   set_nonblock(lfd);
   Broker broker(lfd);
+  broker.compact_every_ = compact_every > 0 ? (size_t)compact_every : 0;
   if (!jpath.empty() && !broker.open_journal(jpath)) {
     fprintf(stderr, "cannot open journal %s\n", jpath.c_str());
     return 1;

@@ -370,12 +370,13 @@ gn_reduce_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dz, const 
 #pragma unroll
   for (int e = 0; e < 8; ++e) { red[t][e] = s1[e]; red[t][8 + e] = s2[e]; }
   __syncthreads();
-  if (t < C) {
-    const int cc8 = t / 8, e = t % 8;
+  // one thread per channel; C may exceed the block (up to 8 * NT channels), so loop
+  for (int c = t; c < C; c += NT) {
+    const int cc8 = c / 8, e = c % 8;
     float a = 0.f, b = 0.f;
     for (int j = 0; j < rg; ++j) { a += red[j * cpr + cc8][e]; b += red[j * cpr + cc8][8 + e]; }
-    atomicAdd(st + ((long)n * C + t) * 2, a);
-    atomicAdd(st + ((long)n * C + t) * 2 + 1, b);
+    atomicAdd(st + ((long)n * C + c) * 2, a);
+    atomicAdd(st + ((long)n * C + c) * 2 + 1, b);
   }
 }
 

@@ -39,6 +39,13 @@ class NativePSPNet(NativeUnet):
             raise NotImplementedError('native PSPNet: <= 4 sigmoid classes (BCE + Dice)')
         ctx = self._lower_encoder(model)
         self.level, self.factor = dec.level, dec.factor
+        # encoder blocks past the decoder's level are never run (see features()): their
+        # slots are frozen, so the optimizer neither updates nor weight-decays them - what
+        # torch.optim does with parameters whose grad stays None
+        last = self.ends[3 - self.level]
+        for blk in self.blocks[last + 1:]:
+            for u in list(blk.units) + ([blk.down] if blk.down is not None else []):
+                u.w.frozen = u.gamma.frozen = u.beta.frozen = True
         self.stages = []
         for i, st in enumerate(dec.psp.stages):
             pool, cbr = st[0], st[1]

@@ -21,7 +21,10 @@ _LOCK = threading.Lock()
 # so no two float adds race and a step is bitwise reproducible (graph replay == eager).
 # Slower (no split-K) and heavier (bigger reduction scratch): a debugging / testing mode.
 DETERMINISTIC = os.environ.get('MLC_DETERMINISTIC', '0') == '1'
-DET_COPIES = int(os.environ.get('MLC_DET_COPIES', '4096'))
+# mlc_set_deterministic never uses fewer than the default 32 copies (batchnorm.hip NSTAT), so
+# the Python side sizes its reduction buffers with the same floor: fewer would let kernels
+# index copies the buffers do not have
+DET_COPIES = max(32, int(os.environ.get('MLC_DET_COPIES', '4096')))
 
 vp, i32, i64, f32, u32 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_uint
 

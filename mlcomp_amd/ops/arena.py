@@ -36,6 +36,9 @@ class Slot:
     numel: int
     offset: int = 0
     arena: 'Arena' = None
+    # frozen: the optimizer skips the slot entirely (no update, no weight decay) - the
+    # parameters a model never runs, which torch.optim skips because their grad is None
+    frozen: bool = False
 
     @property
     def master(self) -> torch.Tensor:
@@ -90,6 +93,22 @@ class Arena:
 
     def slots_in_backward_order(self) -> List[Slot]:
         return sorted(self.slots, key=lambda s: s.offset)
+
+    def segments(self) -> List[Tuple[int, int]]:
+        """[start, end) element ranges the optimizer updates: the whole arena, minus the
+        (padded) extents of frozen slots, neighbouring live slots merged."""
+        if not any(s.frozen for s in self.slots):
+            return [(0, self.numel)]
+        out: List[Tuple[int, int]] = []
+        for s in self.slots_in_backward_order():
+            if s.frozen:
+                continue
+            end = s.offset + (s.numel + _ALIGN - 1) // _ALIGN * _ALIGN
+            if out and out[-1][1] == s.offset:
+                out[-1] = (out[-1][0], end)
+            else:
+                out.append((s.offset, end))
+        return out
 
 
 class ParamArena:

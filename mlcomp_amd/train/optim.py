@@ -72,6 +72,11 @@ class FusedSGD(_ArenaStateMixin):
         # buffers "mu*0 + (1-dampening)*g" equals that when dampening == 0, which keeps
         # the kernel arguments identical across steps (HIP-graph friendly).
         for a in self.arena.arenas():
+            segs = a.segments()
+            if segs != [(0, a.numel)]:       # frozen slots: update the live ranges only
+                for s, e in segs:
+                    self.step_slice(a, s, e)
+                continue
             Fn.sgd_step(a.master, a.grad, a.state['momentum'], a.mirror, self.hyper,
                         a.numel if a.decay else 0, a.numel if a.mirror is not None else 0,
                         self.momentum, self.dampening, self.wd, self.nesterov, False)
@@ -116,6 +121,11 @@ class FusedAdam(_ArenaStateMixin):
 
     def step(self):
         for a in self.arena.arenas():
+            segs = a.segments()
+            if segs != [(0, a.numel)]:       # frozen slots: update the live ranges only
+                for s, e in segs:
+                    self.step_slice(a, s, e)
+                continue
             Fn.adam_step(a.master, a.grad, a.state['exp_avg'], a.state['exp_avg_sq'], a.mirror,
                          self.hyper, a.numel if a.decay else 0,
                          a.numel if a.mirror is not None else 0, self.b1, self.b2, self.eps,

@@ -3,9 +3,11 @@ Catalyst runner the reference executes, `catalyst_.py:365-430`).
 
 Two engines behind one loop:
 
-* ``torch`` - any ``nn.Module``: autocast(bf16) forward, criterion, backward,
-  ``torch.optim`` step; DDP through ``torch.nn.parallel.DistributedDataParallel``
-  (backend "nccl" == RCCL on ROCm) when ``world_size > 1``.
+* ``torch`` - any ``nn.Module``: forward under autocast(bf16) (``args.precision: bf16``,
+  default) or in plain fp32 (``precision: fp32``, the reference's Catalyst default),
+  criterion, backward, ``torch.optim`` step; DDP through
+  ``torch.nn.parallel.DistributedDataParallel`` (backend "nccl" == RCCL on ROCm) when
+  ``world_size > 1``.
 * ``native`` - ResNet-family classifiers (``groups == 1``), BERT and ResNet-encoder
   U-Nets (:class:`~mlcomp_amd.train.native_seg_step.NativeSegmentationStep`) on a GPU: the whole step
   runs through :class:`~mlcomp_amd.train.native_step.NativeClassifierStep` (hand-written
@@ -153,6 +155,16 @@ class Runner:
         self.extra_callbacks = extra_callbacks or OrderedDict()
         self.rank, self.world_size = rank, world_size
         self.engine = engine or experiment.args.get('engine', 'auto')
+        if self.engine not in ('auto', 'native', 'torch'):
+            raise ValueError(f'args.engine: auto / native / torch, not {self.engine!r}')
+        # torch engine compute precision: bf16 (autocast, the default) or fp32 (the
+        # reference's Catalyst default: no autocast at all); the native engines are bf16
+        self.precision = str(experiment.args.get('precision', 'bf16')).lower()
+        if self.precision not in ('bf16', 'fp32'):
+            raise ValueError(f'args.precision: bf16 / fp32, not {self.precision!r}')
+        # one entry per built stage: which engine ran it and why (see _select_engine)
+        self.engine_log: List[dict] = []
+        self.engine_hook = None     # callable(entry), set by the train executor
         self.model: Optional[nn.Module] = None
         self.ddp_model = None
         self.native_step = None
@@ -166,25 +178,47 @@ class Runner:
         self._native_opt_state: Optional[dict] = None  # applied when the native step is built
 
     # ------------------------------------------------------------------ setup
+    def _select_engine(self, stage) -> dict:
+        """Which engine trains ``stage`` and why: ``{'engine': 'native'|'torch', 'kind',
+        'precision', 'reason'}``.  ``engine: native`` raises when the stage cannot run
+        natively; ``engine: auto`` falls back to the torch engine and the reason is kept
+        (``engine_log``, reported to the task by the train executor)."""
+        forced = self.engine == 'native'
+        kind = _native_kind(self.model, self.device) if self.device.type == 'cuda' else None
+        reason = None
+        if self.engine == 'torch':
+            reason = 'engine: torch requested'
+        elif self.precision != 'bf16':
+            reason = f'precision {self.precision}: the native engines compute in bf16 (fp32 master weights)'
+        elif self.device.type != 'cuda':
+            reason = 'no HIP device: the native engines run on MI355X GPUs'
+        elif kind is None:
+            reason = f'{type(self.model).__name__} has no native lowering'
+        if reason is None:
+            from .native_spec import NativeUnsupported, native_plan
+            try:
+                self._native_plan = native_plan(self.experiment, stage, kind)
+            except NativeUnsupported as e:
+                reason = str(e)
+        if reason is not None and forced:
+            raise RuntimeError(f'engine: native cannot run stage {stage!r}: {reason}')
+        if reason is not None:
+            return {'stage': stage, 'engine': 'torch', 'kind': None, 'precision': self.precision,
+                    'reason': reason}
+        return {'stage': stage, 'engine': 'native', 'kind': kind, 'precision': 'bf16', 'reason': None}
+
     def _build_model(self, stage):
         if self.model is None:
             self.model = self.experiment.get_model(stage)
-        use_native = self.engine == 'native' or (self.engine == 'auto' and _native_capable(self.model, self.device))
-        if self.engine == 'native' and not _native_capable(self.model, self.device):
-            raise RuntimeError('engine: native needs a ResNet-family classifier (groups=1), BERT or a '
-                               'ResNet-encoder U-Net (<= 4 sigmoid classes) on a GPU')
-        self.native_kind = _native_kind(self.model, self.device) if use_native else None
         self._native_plan = None
-        if use_native:
-            from .native_spec import NativeUnsupported, native_plan
-            try:
-                self._native_plan = native_plan(self.experiment, stage, self.native_kind)
-            except NativeUnsupported as e:
-                if self.engine == 'native':
-                    raise RuntimeError(f'engine: native cannot run stage {stage!r}: {e}') from e
-                # engine: auto trains what the config asks for, on the PyTorch path
-                _log.warning('stage %s: %s - training on the PyTorch engine', stage, e)
-                use_native, self.native_kind = False, None
+        choice = self._select_engine(stage)
+        use_native = choice['engine'] == 'native'
+        self.native_kind = choice['kind']
+        self.engine_log.append(choice)
+        if choice['reason'] and self.engine == 'auto' and self.device.type == 'cuda':
+            _log.warning('stage %s: %s - training on the PyTorch engine', stage, choice['reason'])
+        if self.engine_hook is not None:
+            self.engine_hook(choice)
         self.state.native = use_native
         if not use_native:
             self.model.to(self.device)
@@ -353,8 +387,7 @@ class Runner:
             dev = lambda k: batch[k].to(self.device, non_blocking=True) if batch.get(k) is not None else None  # noqa
             ids, y = dev('input_ids'), dev('targets')
             st.input = {'input_ids': ids, 'targets': y}
-            with torch.set_grad_enabled(st.is_train), \
-                    torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.device.type == 'cuda'):
+            with torch.set_grad_enabled(st.is_train), self._autocast():
                 out = (self.ddp_model if st.is_train else self.model)(ids, dev('token_type_ids'),
                                                                      dev('attention_mask'))
             st.output = {'logits': out.float()}
@@ -365,11 +398,15 @@ class Runner:
         if self.device.type == 'cuda' and x.dim() == 4:
             x = x.contiguous(memory_format=torch.channels_last)
         st.input = {'features': x, 'targets': y}
-        with torch.set_grad_enabled(st.is_train), \
-                torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.device.type == 'cuda'):
+        with torch.set_grad_enabled(st.is_train), self._autocast():
             out = (self.ddp_model if st.is_train else self.model)(x)
         st.output = {'logits': out.float() if isinstance(out, torch.Tensor) else out}
         st.batch_size = x.shape[0]
+
+    def _autocast(self):
+        """bf16 autocast on a GPU for ``precision: bf16``; a no-op context for fp32."""
+        return torch.autocast(self.device.type, dtype=torch.bfloat16,
+                              enabled=self.device.type == 'cuda' and self.precision == 'bf16')
 
     def _run_loader(self, name, loader):
         st = self.state

@@ -244,6 +244,20 @@ class Train(Executor):
         self.info(f'resuming from {path} (stage {ckpt["stage"]}, epoch {ckpt["checkpoint_data"]["epoch"]})')
         return start
 
+    def _engine_chosen(self, e: dict):
+        """Record which engine trains a stage (and why not the native one) in the task's
+        DB log and ``additional_info['engine'][stage]`` - a fallback is never silent."""
+        msg = f"stage {e['stage']}: {e['engine']} engine" + (f" ({e['kind']})" if e['kind'] else '') + \
+            f", {e['precision']}" + (f" - {e['reason']}" if e['reason'] else '')
+        if e['reason'] and e['engine'] == 'torch' and 'requested' not in e['reason']:
+            self.warning(msg, db=True)
+        else:
+            self.info(msg, db=True)
+        info = yaml_load(self.task.additional_info) or {}
+        info.setdefault('engine', {})[e['stage']] = {k: e[k] for k in ('engine', 'kind', 'precision', 'reason')}
+        self.task.additional_info = yaml_dump(info)
+        self.task_provider.commit()
+
     # ------------------------------------------------------------------ run
     def work(self):
         cfg = self.load_config()
@@ -276,6 +290,7 @@ class Train(Executor):
         device = torch.device('cuda', torch.cuda.current_device()) if torch.cuda.is_available() \
             else torch.device('cpu')
         runner = Runner(experiment, device=device, extra_callbacks=extra, rank=rank, world_size=world)
+        runner.engine_hook = self._engine_chosen
         if self.resume_path:
             # full state (weights, optimizer, LR schedule, best score), applied when the
             # first remaining stage starts

@@ -141,7 +141,11 @@ class ExecuteBuilder:
                 self.executor.info(f'stage {res["stage"]} done, next {res["stages"][i + 1]}')
                 self.task.status = TaskStatus.Queued.value
                 self.provider.commit()
-                get_broker().send_task(self.queue_personal, 'execute', self.id)
+                mid = get_broker().send_task(self.queue_personal, 'execute', self.id)
+                # the scheduler's orphan pass checks the broker for task.celery_id: point it
+                # at the continuation message (the stage's own message is acked by now)
+                self.task.celery_id = mid
+                self.provider.commit()
                 return
         self.executor.step.finish()
         self.provider.change_status(self.task, TaskStatus.Success)

@@ -22,7 +22,7 @@ def _free_port():
 
 
 @contextlib.contextmanager
-def _broker_daemon(sanitize, tmp_path, journal=None, port=None):
+def _broker_daemon(sanitize, tmp_path, journal=None, port=None, compact_every=None):
     """Run the broker daemon; with ``sanitize='asan'`` the AddressSanitizer + UBSan build:
     the test's traffic runs against it, then it is stopped with SIGTERM (clean shutdown
     through its destructors, so LeakSanitizer runs) and must exit 0 with no report."""
@@ -31,6 +31,8 @@ def _broker_daemon(sanitize, tmp_path, journal=None, port=None):
     port = port or _free_port()
     err = open(tmp_path / f'broker-{sanitize or "plain"}.err', 'a+')
     extra = ['--journal', str(journal)] if journal else []
+    if compact_every:
+        extra += ['--compact-every', str(compact_every)]
     p = subprocess.Popen([binary, '--host', '127.0.0.1', '--port', str(port)] + extra, stdout=subprocess.PIPE,
                          stderr=err)
     while not p.stdout.readline().startswith(b'mlcomp-broker listening'):
@@ -234,4 +236,26 @@ def test_journal_survives_broker_restart(tmp_path):
         assert got == [[2], [3]]
         new = c.push('jq', {'task': 'z'})
         assert int(new) > int(ids[-1])
+        c.close()
+
+
+@pytest.mark.parametrize('sanitize', [None, 'asan'])
+def test_journal_compaction_at_push_and_ack(tmp_path, sanitize):
+    """A compaction triggered by the very line a PUSH / ACK journals (--compact-every 1:
+    after every line) rewrites the journal from the live state: the pushed message must
+    already be in it, and the acked one must already be gone (journal after
+    the state change, not before)."""
+    j = tmp_path / 'broker.journal'
+    port = _free_port()
+    with _broker_daemon(sanitize, tmp_path, journal=j, port=port, compact_every=1):
+        c = BrokerClient('127.0.0.1', port)
+        ids = [c.push('cq', {'task': 'execute', 'args': [i]}) for i in range(3)]
+        _, m = c.pop(['cq'], 1.0)
+        assert m['args'] == [0] and c.ack(m['id'])
+        c.close()
+    with _broker_daemon(sanitize, tmp_path, journal=j, port=port, compact_every=1):
+        c = BrokerClient('127.0.0.1', port)
+        assert c.queue_len('cq') == 2, j.read_text()
+        assert not c.has(ids[0]) and c.has(ids[1]) and c.has(ids[2])
+        assert [c.pop(['cq'], 1.0)[1]['args'] for _ in range(2)] == [[1], [2]]
         c.close()

@@ -42,3 +42,15 @@ def test_library_exports():
     lib = ctypes.CDLL(path)
     for name in _lib._SIGS:
         assert hasattr(lib, name), name
+
+
+def test_det_copies_floor_matches_kernels():
+    """mlc_set_deterministic raises ncopy to >= 32 (batchnorm.hip NSTAT); the Python side
+    must size its partial-sum buffers with the same floor."""
+    import subprocess
+    import sys
+    out = subprocess.run([sys.executable, '-c', 'from mlcomp_amd.ops import _lib, functional as F; '
+                          'print(_lib.DET_COPIES, F.NSTAT)'],
+                         env=dict(os.environ, MLC_DETERMINISTIC='1', MLC_DET_COPIES='8'),
+                         capture_output=True, text=True, check=True)
+    assert out.stdout.split() == ['32', '32'], out.stdout

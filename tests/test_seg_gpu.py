@@ -344,7 +344,8 @@ def test_native_deeplab_step_matches_torch_and_graph():
     assert abs(le[0] - lg[0]) < 1e-3 * abs(le[0]) + 1e-4, (le, lg)
 
 
-@pytest.mark.parametrize('N,H,W,C,G', [(4, 16, 16, 128, 32), (2, 33, 7, 64, 8), (3, 5, 9, 256, 32)])
+@pytest.mark.parametrize('N,H,W,C,G', [(4, 16, 16, 128, 32), (2, 33, 7, 64, 8), (3, 5, 9, 256, 32),
+                                       (2, 8, 8, 512, 32), (2, 4, 6, 2048, 32)])
 def test_gn_relu_native_vs_fp32(N, H, W, C, G):
     """FPN's GroupNorm + ReLU on the native kernels vs fp32 autograd of nn.GroupNorm + ReLU."""
     from mlcomp_amd.models.native_fpn import GNRelu

@@ -185,6 +185,14 @@ def test_train_executor_through_dag(cluster, tmp_path):
     assert {'warm', 'main'} <= {st.name for st in steps}
     t = s.get(Task, tid)
     assert t.score is not None and t.loss is not None
+    # the engine that trained each stage (and why) is stored on the task and in its DB log
+    from mlcomp_amd.db.models import Log
+    from mlcomp_amd.utils.misc import yaml_load
+    eng = (yaml_load(t.additional_info) or {})['engine']
+    assert set(eng) == {'warm', 'main'} and eng['main']['engine'] == 'torch', eng
+    assert eng['main']['reason'] == 'engine: torch requested' and eng['main']['precision'] == 'bf16'
+    msgs = [lg.message for lg in s.query(Log).filter(Log.task == tid).all()]
+    assert any('stage main: torch engine' in m for m in msgs), msgs[-20:]
 
 
 # ---------------------------------------------------------------------------- native DP
@@ -317,3 +325,62 @@ def test_optimizer_in_backward_matches_step_at_end(kind, monkeypatch):
     a, b = run('1'), run('0')
     assert torch.isfinite(a).all()
     assert torch.allclose(a, b, atol=1e-6, rtol=1e-5), (a - b).abs().max()
+
+
+# ---------------------------------------------------------------------------- engine choice
+def test_engine_choice_records_the_fallback_reason(tmp_path, monkeypatch):
+    """engine: auto never falls back silently: the reason lands in runner.engine_log (and
+    the hook the train executor turns into a task log line + additional_info)."""
+    import mlcomp_amd.train.runner as R
+    cfg = _cfg(tmp_path, epochs=1)
+    cfg['args']['engine'] = 'auto'
+    seen = []
+    r = Runner(ConfigExperiment(cfg), device='cpu')
+    r.engine_hook = seen.append
+    r.run_experiment()
+    assert seen == r.engine_log and len(seen) == 1
+    assert seen[0]['engine'] == 'torch' and 'no HIP device' in seen[0]['reason']
+    # a GPU-capable model whose stage asks for an optimizer the native engines lack
+    cfg['stages']['optimizer_params'] = {'optimizer': 'RMSprop', 'lr': 0.01}
+    r = Runner(ConfigExperiment(cfg), device='cpu')
+    r.model = r.experiment.get_model('stage1')
+    monkeypatch.setattr(R, '_native_kind', lambda m, d: 'resnet')
+    r.device = torch.device('cuda')          # selection only; nothing is built
+    got = r._select_engine('stage1')
+    assert got['engine'] == 'torch' and 'RMSprop' in got['reason']
+    r.engine = 'native'
+    with pytest.raises(RuntimeError, match='RMSprop'):
+        r._select_engine('stage1')
+    # precision fp32 keeps the stage on the torch engine, and says so
+    cfg['stages']['optimizer_params'] = {'optimizer': 'Adam', 'lr': 0.01}
+    cfg['args']['precision'] = 'fp32'
+    r = Runner(ConfigExperiment(cfg), device='cpu')
+    r.model = r.experiment.get_model('stage1')
+    r.device = torch.device('cuda')
+    got = r._select_engine('stage1')
+    assert got['engine'] == 'torch' and got['precision'] == 'fp32' and 'fp32' in got['reason']
+    with pytest.raises(ValueError, match='precision'):
+        Runner(ConfigExperiment(dict(cfg, args=dict(cfg['args'], precision='fp16'))), device='cpu')
+
+
+def test_fp32_torch_engine_matches_plain_fp32_training(tmp_path):
+    """precision: fp32 is plain fp32 autograd + torch.optim (no autocast): the runner's
+    weights after an epoch equal a hand-written fp32 loop over the same batches."""
+    cfg = _cfg(tmp_path, epochs=1, n=32)
+    cfg['args']['precision'] = 'fp32'
+    cfg['stages']['callbacks_params'].pop('saver')
+    torch.manual_seed(3)
+    r = Runner(ConfigExperiment(cfg), device='cpu')
+    r.run_experiment()
+    torch.manual_seed(3)
+    e = ConfigExperiment(cfg)
+    m = e.get_model('stage1')
+    opt = torch.optim.Adam(m.parameters(), lr=0.01)
+    for b in r.loaders['train']:
+        m.train()
+        loss = torch.nn.functional.cross_entropy(m(b['features']), b['targets'])
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    for k, v in m.state_dict().items():
+        assert torch.allclose(v, r.model.state_dict()[k], atol=1e-6, rtol=1e-5), k
