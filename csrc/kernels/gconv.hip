@@ -1,0 +1,594 @@
+// Grouped and depthwise convolutions, NHWC bf16, for the generic native engine
+// (ResNeXt / SE-ResNeXt grouped 3x3s, EfficientNet / MobileNet depthwise kxk).
+//
+// Grouped (groups > 1, Cg = channels per group, in == out, Cg | 16 or 16 | Cg) on the
+// v_mfma_f32_16x16x32_bf16 matrix cores.  The GEMM is block-diagonal: an output block of
+// 16 channels reads KB = max(16, Cg) input channels per filter tap (for Cg < 16 the 16
+// channels of the 16/Cg groups the block spans, with the off-group weights zero).  That
+// wastes 16/Cg of the MFMA work for Cg < 16 but keeps every operand a 16-byte NHWC chunk;
+// these layers are bound by HBM / L1 traffic, not by the matrix cores.
+//   forward     y[p][oc]   = sum_{t,kb} x[p@t][cbase+kb] * WB[ob][j][t*KB+kb]
+//   dgrad       dx[q][ic]  = the same kernel over dy, with the stride-fractional tap map
+//               (a tap reaches q iff (q + pad - r*dil) % S == 0) and WB built from the
+//               transposed weight
+//   wgrad       dw[oc][t][ci] = sum_p dy[p][oc] * x[p@t][ci]: K = pixels, both operands
+//               staged through LDS [px][16] and read with ds_read_b64_tr_b16
+// WB is the 16-column-block expansion of the [Co][KH][KW][Cg] filter (one tiny kernel per
+// use), laid out [ob][j][Kpad] so a lane's B fragment is one 16-byte load.
+//
+// Depthwise (groups == C, one filter per channel) on the VALU: 18 FLOP per output, pure
+// bandwidth.  Threads own a fixed 8-channel group (16 B accesses, grid = multiple of C/8
+// threads, as the BatchNorm passes) and walk pixels; the weight gradient reduces per
+// thread, then per block (LDS), then over 32 partial copies.
+#include "common.h"
+
+namespace gconv {
+
+constexpr int NT = 256;
+constexpr int NCOPY = 32;   // partial-sum copies of the cross-block reductions
+
+struct GGeom {
+  int N, Hi, Wi, Ci;        // operand image (x; dy for the transposed map)
+  int Ho, Wo, Co;           // output image (y; dx for the transposed map)
+  int KH, KW, S, P, D;
+  int Cg, KB, T, Kp;        // group width, K channels per tap, taps, padded K (mult. of 32)
+  long M;                   // output pixels
+};
+
+__device__ __forceinline__ bf16x8 ldfrag(const bf16* p) {
+  return *reinterpret_cast<const bf16x8*>(p);
+}
+
+// ------------------------------------------------------------------ weight expansion
+// WB[ob][j][k] (k < Kp): the B operand of the 16-column output block ob.  tr = 0: the
+// forward filter w[Co][T][Cg]; tr = 1: the dgrad filter (output channel = the conv's
+// input channel, K over the conv's output channels of the group).
+__global__ void __launch_bounds__(NT)
+expand_kernel(const bf16* __restrict__ w, bf16* __restrict__ wb, int Cout, int T, int Cg, int KB, int Kp,
+              int tr) {
+  const long total = (long)Cout * Kp;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int k = (int)(i % Kp);
+    const int oc = (int)(i / Kp);           // = ob*16 + j
+    float v = 0.f;
+    if (k < T * KB) {
+      const int t = k / KB, kb = k % KB;
+      const int g = oc / Cg;
+      const int cbase = Cg >= 16 ? g * Cg : (oc / 16) * 16;
+      const int ci = cbase + kb;            // the K-side channel
+      if (ci / Cg == g) {
+        // forward: w[oc][t][ci - g*Cg]; transposed: the conv's output channel is ci
+        v = tr ? (float)w[((long)ci * T + t) * Cg + (oc - g * Cg)] : (float)w[((long)oc * T + t) * Cg + (ci - g * Cg)];
+      }
+    }
+    wb[i] = (bf16)v;
+  }
+}
+
+// ------------------------------------------------------------------ grouped fwd / dgrad
+// Block: 4 waves x 2 sub-tiles of 16 output pixels = 128 pixels, one 16-channel output
+// block (blockIdx.y).  Optional per-channel sum / sum-of-squares into NCOPY copies.
+template <bool TR>
+__global__ void __launch_bounds__(NT)
+gconv_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wb, bf16* __restrict__ out,
+             float* __restrict__ sum, float* __restrict__ sumsq, GGeom g) {
+  __shared__ __attribute__((aligned(16))) bf16 stage[4][32 * 16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ob = blockIdx.y;
+  const int oc0 = ob * 16;
+  const int grp = oc0 / g.Cg;
+  const int cbase = g.Cg >= 16 ? grp * g.Cg : oc0;   // first K-side channel of the block
+  const long m0 = (long)blockIdx.x * 128 + wave * 32;
+  const int hl = lane >> 4;                          // k-chunk (8 channels) of the lane
+  // the two sub-tiles' rows of this lane
+  int n[2], ph[2], pw[2];
+  bool ok[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const long m = m0 + 16 * s + (lane & 15);
+    ok[s] = m < g.M;
+    const long mm = ok[s] ? m : 0;
+    pw[s] = (int)(mm % g.Wo);
+    const long t = mm / g.Wo;
+    ph[s] = (int)(t % g.Ho);
+    n[s] = (int)(t / g.Ho);
+  }
+  f32x4 acc[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) acc[s] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const bf16* wrow = wb + (long)(oc0 + (lane & 15)) * g.Kp + 8 * hl;
+  const bf16x8 zero = {};
+  for (int k0 = 0; k0 < g.Kp; k0 += 32) {
+    const int k = k0 + 8 * hl;
+    const bf16x8 b = ldfrag(wrow + k0);
+    const int t = k / g.KB, kb = k - t * g.KB;
+    const bool kv = t < g.T;
+    const int r = kv ? t / g.KW : 0, c = kv ? t - r * g.KW : 0;
+    bf16x8 a[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      int hi, wi;
+      bool v = kv && ok[s];
+      if (!TR) {
+        hi = ph[s] * g.S - g.P + r * g.D;
+        wi = pw[s] * g.S - g.P + c * g.D;
+      } else {
+        const int nh = ph[s] + g.P - r * g.D, nw = pw[s] + g.P - c * g.D;
+        v = v && nh >= 0 && nw >= 0 && nh % g.S == 0 && nw % g.S == 0;
+        hi = nh / g.S;
+        wi = nw / g.S;
+      }
+      v = v && (unsigned)hi < (unsigned)g.Hi && (unsigned)wi < (unsigned)g.Wi;
+      a[s] = v ? ldfrag(in + (((long)n[s] * g.Hi + hi) * g.Wi + wi) * g.Ci + cbase + kb) : zero;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) acc[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], b, acc[s], 0, 0, 0);
+  }
+  // C/D map: lane -> column j = lane & 15, rows 4*(lane>>4) + i
+  const int j = lane & 15;
+  if (sum) {
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long m = m0 + 16 * s + 4 * hl + i;
+        const float v = m < g.M ? acc[s][i] : 0.f;
+        s1 += v;
+        s2 += v * v;
+      }
+    s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
+    if (lane < 16) {
+      const int slot = (int)((blockIdx.x * 4 + wave) % NCOPY);
+      atomicAdd(sum + (long)slot * g.Co + oc0 + j, s1);
+      atomicAdd(sumsq + (long)slot * g.Co + oc0 + j, s2);
+    }
+  }
+  // stage the 32 x 16 bf16 tile, then 16-byte row-chunk stores (2 lanes per row)
+  bf16* st = stage[wave];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st[(16 * s + 4 * hl + i) * 16 + j] = (bf16)acc[s][i];
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  {
+    const long m = m0 + (lane >> 1);
+    if (m < g.M)
+      *reinterpret_cast<uint4*>(out + m * g.Co + oc0 + 8 * (lane & 1)) =
+          *reinterpret_cast<const uint4*>(st + (lane >> 1) * 16 + 8 * (lane & 1));
+  }
+}
+
+// ------------------------------------------------------------------ grouped wgrad
+// dw[oc][t][cl] (+)= sum_p dy[p][oc] x[p@t][ci].  Block: 4 waves, one 16-channel output
+// block (blockIdx.y), up to NCB column blocks (tap, 16-channel input block) (blockIdx.z
+// selects which), a pixel chunk (blockIdx.x).  Each wave stages 32 pixels of dy [32][16]
+// and of every column block's x gather [32][16] in its own LDS region and feeds the
+// MFMA with ds_read_b64_tr_b16 transposed reads (K = pixels).
+typedef short s16x4t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* tile, int lane) {
+  // 16x16x32 operand whose K index is the tile row (32 rows x 16 cols, 32-byte rows):
+  // lane l gets column (l & 15), rows 8*(l>>4) + 0..7
+  const int q = (lane & 15) >> 2, p = lane & 3, g = lane >> 4;
+  const bf16* a0 = tile + (8 * g + q) * 16 + 4 * p;
+  const bf16* a1 = tile + (8 * g + 4 + q) * 16 + 4 * p;
+  const s16x4t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4t))(a0));
+  const s16x4t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4t))(a1));
+  typedef short s16x8t __attribute__((ext_vector_type(8)));
+  const s16x8t r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+constexpr int WG_NCB = 9;   // column blocks per block (3x3 taps of one 16-channel block)
+
+__global__ void __launch_bounds__(NT)
+gconv_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* __restrict__ dw, GGeom g,
+                   int ncb_total, long chunk) {
+  // per wave: dy tile + WG_NCB x tiles, 32 x 16 bf16 each
+  __shared__ __attribute__((aligned(16))) bf16 lds[4][(1 + WG_NCB) * 32 * 16];
+  __shared__ float red[4][WG_NCB][16][17];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ob = blockIdx.y, oc0 = ob * 16;
+  const int grp = oc0 / g.Cg;
+  const int cbase = g.Cg >= 16 ? grp * g.Cg : oc0;
+  const int nsub = g.KB / 16;                       // 16-channel input blocks per tap
+  const int cb0 = blockIdx.z * WG_NCB;
+  const int ncb = min(WG_NCB, ncb_total - cb0);
+  bf16* tA = lds[wave];
+  f32x4 acc[WG_NCB];
+#pragma unroll
+  for (int c = 0; c < WG_NCB; ++c) acc[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // this lane's staging role: pixel row (lane >> 1), 8-channel half (lane & 1)
+  const int prow = lane >> 1, half = lane & 1;
+  // per column block of this block: tap (r, s) and input-channel offset
+  int tr_[WG_NCB], ts_[WG_NCB], tc_[WG_NCB];
+#pragma unroll
+  for (int c = 0; c < WG_NCB; ++c) {
+    const int cb = cb0 + (c < ncb ? c : 0);
+    const int t = cb / nsub, sb = cb - t * nsub;
+    tr_[c] = t / g.KW;
+    ts_[c] = t - tr_[c] * g.KW;
+    tc_[c] = cbase + 16 * sb + 8 * half;
+  }
+  const long pbeg = (long)blockIdx.x * chunk, pend = min(g.M, pbeg + chunk);
+  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  for (long p0 = pbeg + 32 * wave; p0 < pend; p0 += 128) {
+    const long p = p0 + prow;
+    const bool pv = p < pend;
+    int n = 0, ho = 0, wo = 0;
+    if (pv) {
+      wo = (int)(p % g.Wo);
+      const long t = p / g.Wo;
+      ho = (int)(t % g.Ho);
+      n = (int)(t / g.Ho);
+    }
+    uint4 va = pv ? ldg16(dy + p * g.Co + oc0 + 8 * half) : z4;
+    uint4 vb[WG_NCB];
+#pragma unroll
+    for (int c = 0; c < WG_NCB; ++c) {
+      const int hi = ho * g.S - g.P + tr_[c] * g.D, wi = wo * g.S - g.P + ts_[c] * g.D;
+      const bool v = pv && c < ncb && (unsigned)hi < (unsigned)g.Hi && (unsigned)wi < (unsigned)g.Wi;
+      vb[c] = v ? ldg16(x + (((long)n * g.Hi + hi) * g.Wi + wi) * g.Ci + tc_[c]) : z4;
+    }
+    __builtin_amdgcn_wave_barrier();   // the previous iteration's reads are done (same wave)
+    *reinterpret_cast<uint4*>(tA + prow * 16 + 8 * half) = va;
+#pragma unroll
+    for (int c = 0; c < WG_NCB; ++c)
+      *reinterpret_cast<uint4*>(tA + (1 + c) * 512 + prow * 16 + 8 * half) = vb[c];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    const bf16x8 fa = tr_frag(tA, lane);
+#pragma unroll
+    for (int c = 0; c < WG_NCB; ++c) {
+      if (c < ncb) {   // wave-uniform
+        const bf16x8 fb = tr_frag(tA + (1 + c) * 512, lane);
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[c], 0, 0, 0);
+      }
+    }
+  }
+  // C map: column (input channel within the block) = lane & 15, row (oc) = 4*(lane>>4)+i.
+  // Reduce the 4 waves through LDS, then one atomic per kept element.
+  const int col = lane & 15;
+#pragma unroll
+  for (int c = 0; c < WG_NCB; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[wave][c][4 * (lane >> 4) + i][col] = acc[c][i];
+  __syncthreads();
+  for (int e = threadIdx.x; e < ncb * 256; e += NT) {
+    const int c = e >> 8, row = (e >> 4) & 15, cl = e & 15;
+    const float v = red[0][c][row][cl] + red[1][c][row][cl] + red[2][c][row][cl] + red[3][c][row][cl];
+    const int cb = cb0 + c, t = cb / nsub, sb = cb - t * nsub;
+    const int oc = oc0 + row, ci = cbase + 16 * sb + cl;
+    if (ci / g.Cg != oc / g.Cg) continue;              // off the block diagonal
+    atomicAdd(dw + ((long)oc * g.T + t) * g.Cg + (ci - (oc / g.Cg) * g.Cg), v);
+  }
+}
+
+// ------------------------------------------------------------------ depthwise
+// weights [T][C] (tap-major, bf16), C % 8 == 0; y[n,ho,wo,c] = sum_t x[..@t][c] * w[t][c]
+constexpr int DW_OW = 4;   // outputs per thread along W
+
+__device__ __forceinline__ void red_stats(float (&s1)[8], float (&s2)[8], float* sum, float* sumsq, int C, int G) {
+  __shared__ float rb[NT][17];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { rb[t][e] = s1[e]; rb[t][8 + e] = s2[e]; }
+  __syncthreads();
+  const int lanes = NT < G ? NT : G;
+  const int base_cg = (int)(((long)blockIdx.x * NT) % G);
+  if (t < lanes) {
+    float a[8], b[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { a[e] = 0.f; b[e] = 0.f; }
+    for (int u = t; u < NT; u += G)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { a[e] += rb[u][e]; b[e] += rb[u][8 + e]; }
+    const int cg = (base_cg + t) % G;
+    const long slot = blockIdx.x % NCOPY;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      atomicAdd(sum + slot * C + cg * 8 + e, a[e]);
+      atomicAdd(sumsq + slot * C + cg * 8 + e, b[e]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(NT)
+dw_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, bf16* __restrict__ y, float* __restrict__ sum,
+              float* __restrict__ sumsq, int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int S, int P,
+              int D) {
+  const int G = C >> 3;
+  const int Wq = (Wo + DW_OW - 1) / DW_OW;
+  const long total = (long)N * Ho * Wq * G;
+  const long gtid = (long)blockIdx.x * NT + threadIdx.x;
+  const int cg = (int)(gtid % G);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  for (long i = gtid; i < total; i += (long)gridDim.x * NT) {
+    long t = i / G;
+    const int wq = (int)(t % Wq); t /= Wq;
+    const int ho = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    const int wo0 = wq * DW_OW;
+    float acc[DW_OW][8];
+#pragma unroll
+    for (int o = 0; o < DW_OW; ++o)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[o][e] = 0.f;
+    for (int r = 0; r < KH; ++r) {
+      const int hi = ho * S - P + r * D;
+      if ((unsigned)hi >= (unsigned)H) continue;
+      const bf16* xr = x + ((long)n * H + hi) * W * C + cg * 8;
+      for (int s = 0; s < KW; ++s) {
+        float wv[8];
+        unpack8(ldg16(w + (long)(r * KW + s) * C + cg * 8), wv);
+#pragma unroll
+        for (int o = 0; o < DW_OW; ++o) {
+          const int wi = (wo0 + o) * S - P + s * D;
+          if (wo0 + o < Wo && (unsigned)wi < (unsigned)W) {
+            float xv[8];
+            unpack8(ldg16(xr + (long)wi * C), xv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[o][e] += xv[e] * wv[e];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < DW_OW; ++o) {
+      if (wo0 + o >= Wo) break;
+      *reinterpret_cast<uint4*>(y + (((long)n * Ho + ho) * Wo + wo0 + o) * C + cg * 8) = pack8(acc[o]);
+      if (sum) {   // statistics of the fp32 accumulators, as the implicit-GEMM epilogues
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { s1[e] += acc[o][e]; s2[e] += acc[o][e] * acc[o][e]; }
+      }
+    }
+  }
+  if (sum) red_stats(s1, s2, sum, sumsq, C, G);
+}
+
+// dx[n,h,w,c] = sum over taps reaching (h, w) of dy[n,ho,wo,c] * w[t][c]
+__global__ void __launch_bounds__(NT)
+dw_dgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ w, bf16* __restrict__ dx, int N, int H, int W,
+                int C, int Ho, int Wo, int KH, int KW, int S, int P, int D) {
+  const int G = C >> 3;
+  const long total = (long)N * H * W * G;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int cg = (int)(i % G);
+    long t = i / G;
+    const int wi = (int)(t % W); t /= W;
+    const int hi = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int r = 0; r < KH; ++r) {
+      const int nh = hi + P - r * D;
+      if (nh < 0 || nh % S) continue;
+      const int ho = nh / S;
+      if (ho >= Ho) continue;
+      for (int s = 0; s < KW; ++s) {
+        const int nw = wi + P - s * D;
+        if (nw < 0 || nw % S) continue;
+        const int wo = nw / S;
+        if (wo >= Wo) continue;
+        float gv[8], wv[8];
+        unpack8(ldg16(dy + (((long)n * Ho + ho) * Wo + wo) * C + cg * 8), gv);
+        unpack8(ldg16(w + (long)(r * KW + s) * C + cg * 8), wv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += gv[e] * wv[e];
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + i * 8) = pack8(acc);
+  }
+}
+
+// partial dw over this thread's output pixels for taps [t0, t0 + TC), reduced per block
+// and added into copy (block % NCOPY) of ws[NCOPY][T][C]
+constexpr int DW_TC = 9;
+
+__global__ void __launch_bounds__(NT)
+dw_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* __restrict__ ws, int N, int H, int W,
+                int C, int Ho, int Wo, int KH, int KW, int S, int P, int D, int t0) {
+  __shared__ float rb[NT][DW_TC * 8 + 1];
+  const int G = C >> 3;
+  const int T = KH * KW;
+  const int tc = min(DW_TC, T - t0);
+  const long total = (long)N * Ho * Wo * G;
+  const long gtid = (long)blockIdx.x * NT + threadIdx.x;
+  const int cg = (int)(gtid % G);
+  float acc[DW_TC][8];
+#pragma unroll
+  for (int k = 0; k < DW_TC; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
+  int tr[DW_TC], ts[DW_TC];
+#pragma unroll
+  for (int k = 0; k < DW_TC; ++k) {
+    const int tt = t0 + (k < tc ? k : 0);
+    tr[k] = tt / KW;
+    ts[k] = tt - tr[k] * KW;
+  }
+  for (long i = gtid; i < total; i += (long)gridDim.x * NT) {
+    long t = i / G;
+    const int wo = (int)(t % Wo); t /= Wo;
+    const int ho = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    float gv[8];
+    unpack8(ldg16(dy + i * 8), gv);
+#pragma unroll
+    for (int k = 0; k < DW_TC; ++k) {
+      if (k >= tc) break;
+      const int hi = ho * S - P + tr[k] * D, wi = wo * S - P + ts[k] * D;
+      if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) continue;
+      float xv[8];
+      unpack8(ldg16(x + (((long)n * H + hi) * W + wi) * C + cg * 8), xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[k][e] += gv[e] * xv[e];
+    }
+  }
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < DW_TC; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) rb[tid][k * 8 + e] = acc[k][e];
+  __syncthreads();
+  const int lanes = NT < G ? NT : G;
+  const int base_cg = (int)(((long)blockIdx.x * NT) % G);
+  float* dst = ws + (long)(blockIdx.x % NCOPY) * T * C;
+  for (int q = tid; q < lanes * tc * 8; q += NT) {
+    const int l = q % lanes, ke = q / lanes;
+    const int k = ke >> 3, e = ke & 7;
+    float a = 0.f;
+    for (int u = l; u < NT; u += G) a += rb[u][k * 8 + e];
+    const int c = ((base_cg + l) % G) * 8 + e;
+    atomicAdd(dst + (long)(t0 + k) * C + c, a);
+  }
+}
+
+// dw[t][c] (+)= sum over the NCOPY copies
+__global__ void __launch_bounds__(NT)
+copies_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n, int accumulate) {
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
+    float a = accumulate ? out[i] : 0.f;
+    for (int k = 0; k < NCOPY; ++k) a += ws[(long)k * n + i];
+    out[i] = a;
+  }
+}
+
+// threads of a grid-stride pass over (row, 8-channel group) keep one group when the thread
+// count is a multiple of G = C/8 (as batchnorm.hip's grid_for)
+inline int grid_groups(long work, int G, int cap) {
+  long blocks = (work + NT * 4 - 1) / (NT * 4);
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  long m;
+  if (G > NT) {
+    m = G % NT == 0 ? G / NT : G;
+  } else {
+    int a = G, b = NT;
+    while (b) { const int r = a % b; a = b; b = r; }
+    m = G / a;
+  }
+  blocks = ((blocks + m - 1) / m) * m;
+  return (int)blocks;
+}
+
+inline int blocks_for(long work) {
+  long b = (work + NT - 1) / NT;
+  return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
+}
+
+inline bool grouped_ok(int C, int Co, int groups) {
+  if (groups < 2 || C % groups || Co % groups || C / groups != Co / groups) return false;
+  const int Cg = C / groups;
+  return (16 % Cg == 0 || Cg % 16 == 0) && C % 16 == 0 && Co % 16 == 0;
+}
+
+inline GGeom mkg(int N, int Hi, int Wi, int Ci, int Ho, int Wo, int Co, int KH, int KW, int S, int P, int D,
+                 int Cg) {
+  GGeom g;
+  g.N = N; g.Hi = Hi; g.Wi = Wi; g.Ci = Ci; g.Ho = Ho; g.Wo = Wo; g.Co = Co;
+  g.KH = KH; g.KW = KW; g.S = S; g.P = P; g.D = D;
+  g.Cg = Cg; g.KB = Cg > 16 ? Cg : 16; g.T = KH * KW; g.Kp = (g.T * g.KB + 31) / 32 * 32;
+  g.M = (long)N * Ho * Wo;
+  return g;
+}
+
+}  // namespace gconv
+
+using namespace gconv;
+
+// bytes of the expanded filter (bf16) that mlc_gconv_fwd / _dgrad need in `wb`
+MLC_EXPORT long mlc_gconv_wb_elems(int Cout, int KH, int KW, int Cg) {
+  const int KB = Cg > 16 ? Cg : 16;
+  return (long)Cout * ((KH * KW * KB + 31) / 32 * 32);
+}
+
+// y[N,Ho,Wo,Co] = grouped conv of x[N,H,W,C] with w[Co][KH][KW][C/groups]; wb: scratch of
+// mlc_gconv_wb_elems bf16; sum/sumsq (optional, zeroed, 32*Co fp32 each): BN statistics
+MLC_EXPORT int mlc_gconv_fwd(const bf16* x, const bf16* w, bf16* wb, bf16* y, float* sum, float* sumsq, int N, int H,
+                             int W, int C, int Co, int KH, int KW, int S, int P, int D, int Ho, int Wo, int groups,
+                             hipStream_t st) {
+  if (!grouped_ok(C, Co, groups) || ((sum == nullptr) != (sumsq == nullptr))) return -1;
+  const GGeom g = mkg(N, H, W, C, Ho, Wo, Co, KH, KW, S, P, D, C / groups);
+  hipLaunchKernelGGL(expand_kernel, dim3(blocks_for((long)Co * g.Kp)), dim3(NT), 0, st, w, wb, Co, g.T, g.Cg, g.KB,
+                     g.Kp, 0);
+  const dim3 grid((unsigned)((g.M + 127) / 128), Co / 16);
+  hipLaunchKernelGGL(gconv_kernel<false>, grid, dim3(NT), 0, st, x, wb, y, sum, sumsq, g);
+  return hipGetLastError();
+}
+
+// dx[N,H,W,C] from dy[N,Ho,Wo,Co] (same w, groups): the stride-fractional tap map
+MLC_EXPORT int mlc_gconv_dgrad(const bf16* dy, const bf16* w, bf16* wb, bf16* dx, int N, int H, int W, int C, int Co,
+                               int KH, int KW, int S, int P, int D, int Ho, int Wo, int groups, hipStream_t st) {
+  if (!grouped_ok(C, Co, groups)) return -1;
+  // the roles swap: operand image dy (Co channels), output dx (C channels)
+  const GGeom g = mkg(N, Ho, Wo, Co, H, W, C, KH, KW, S, P, D, C / groups);
+  hipLaunchKernelGGL(expand_kernel, dim3(blocks_for((long)C * g.Kp)), dim3(NT), 0, st, w, wb, C, g.T, g.Cg, g.KB,
+                     g.Kp, 1);
+  const dim3 grid((unsigned)((g.M + 127) / 128), C / 16);
+  hipLaunchKernelGGL(gconv_kernel<true>, grid, dim3(NT), 0, st, dy, wb, dx, nullptr, nullptr, g);
+  return hipGetLastError();
+}
+
+// dw[Co][KH][KW][C/groups] fp32 (+)= grouped weight gradient
+MLC_EXPORT int mlc_gconv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int Co, int KH,
+                               int KW, int S, int P, int D, int Ho, int Wo, int groups, int accumulate, hipStream_t st) {
+  if (!grouped_ok(C, Co, groups)) return -1;
+  const GGeom g = mkg(N, H, W, C, Ho, Wo, Co, KH, KW, S, P, D, C / groups);
+  if (!accumulate) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)Co * g.T * g.Cg, st);
+  const int ncb = g.T * (g.KB / 16);
+  const int zb = (ncb + WG_NCB - 1) / WG_NCB;
+  const int base = (Co / 16) * zb;
+  // enough pixel chunks to give the chip ~2048 blocks, at least 128 pixels each
+  long chunks = (2048 + base - 1) / base;
+  const long maxc = (g.M + 127) / 128;
+  if (chunks > maxc) chunks = maxc;
+  if (chunks < 1) chunks = 1;
+  long chunk = (g.M + chunks - 1) / chunks;
+  chunk = (chunk + 127) / 128 * 128;
+  chunks = (g.M + chunk - 1) / chunk;
+  const dim3 grid((unsigned)chunks, Co / 16, zb);
+  hipLaunchKernelGGL(gconv_wgrad_kernel, grid, dim3(NT), 0, st, dy, x, dw, g, ncb, chunk);
+  return hipGetLastError();
+}
+
+// depthwise: w [KH][KW][C] bf16 (tap-major); C % 8 == 0
+MLC_EXPORT int mlc_dwconv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, float* sumsq, int N, int H, int W,
+                              int C, int KH, int KW, int S, int P, int D, int Ho, int Wo, hipStream_t st) {
+  if (C % 8 || ((sum == nullptr) != (sumsq == nullptr))) return -1;
+  const int G = C / 8;
+  const long work = (long)N * Ho * ((Wo + DW_OW - 1) / DW_OW) * G;
+  hipLaunchKernelGGL(dw_fwd_kernel, dim3(grid_groups(work, G, 2048)), dim3(NT), 0, st, x, w, y, sum, sumsq, N, H, W,
+                     C, Ho, Wo, KH, KW, S, P, D);
+  return hipGetLastError();
+}
+
+MLC_EXPORT int mlc_dwconv_dgrad(const bf16* dy, const bf16* w, bf16* dx, int N, int H, int W, int C, int KH, int KW,
+                                int S, int P, int D, int Ho, int Wo, hipStream_t st) {
+  if (C % 8) return -1;
+  hipLaunchKernelGGL(dw_dgrad_kernel, dim3(blocks_for((long)N * H * W * (C / 8))), dim3(NT), 0, st, dy, w, dx, N, H,
+                     W, C, Ho, Wo, KH, KW, S, P, D);
+  return hipGetLastError();
+}
+
+// dw [KH][KW][C] fp32 (+)=; ws: scratch of 32*KH*KW*C fp32 (zeroed here)
+MLC_EXPORT int mlc_dwconv_wgrad(const bf16* dy, const bf16* x, float* dw, float* ws, int N, int H, int W, int C,
+                                int KH, int KW, int S, int P, int D, int Ho, int Wo, int accumulate, hipStream_t st) {
+  if (C % 8) return -1;
+  const int G = C / 8, T = KH * KW;
+  (void)hipMemsetAsync(ws, 0, sizeof(float) * (size_t)NCOPY * T * C, st);
+  const long work = (long)N * Ho * Wo * G;
+  const int blocks = grid_groups(work, G, 1024);
+  for (int t0 = 0; t0 < T; t0 += DW_TC)
+    hipLaunchKernelGGL(dw_wgrad_kernel, dim3(blocks), dim3(NT), 0, st, dy, x, ws, N, H, W, C, Ho, Wo, KH, KW, S, P, D,
+                       t0);
+  hipLaunchKernelGGL(copies_reduce_kernel, dim3(blocks_for((long)T * C)), dim3(NT), 0, st, ws, dw, (long)T * C,
+                     accumulate);
+  return hipGetLastError();
+}

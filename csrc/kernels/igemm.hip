@@ -647,6 +647,12 @@ struct BnBwdEpi {
 // exp in the input-gradient epilogue, which cost BERT-base's FFN dgrad ~40 % of its time).
 __device__ __forceinline__ void dense_act8(float (&a)[8], int act, bf16* pre) {
   const int mode = act & 3;
+  if (mode == 3) {   // ReLU (generic engine: conv / linear + bias + ReLU)
+    if (pre) *reinterpret_cast<uint4*>(pre) = pack8(a);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = fmaxf(a[e], 0.f);
+    return;
+  }
   if (mode == 2) {
     float d[8];
 #pragma unroll
@@ -666,13 +672,18 @@ __device__ __forceinline__ void dense_act8(float (&a)[8], int act, bf16* pre) {
   }
 }
 // backward of the activation: a *= gelu'(z) for z the stored pre-activation, or a *= z when
-// z already holds the derivative (act & 4, written by dense_act8 mode 2)
+// z already holds the derivative (act & 4, written by dense_act8 mode 2); act 3: ReLU mask
 __device__ __forceinline__ void dense_dact8(float (&a)[8], int act, uint4 zv) {
   float z[8];
   unpack8(zv, z);
   if (act & 4) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) a[e] *= z[e];
+    return;
+  }
+  if ((act & 3) == 3) {   // ReLU: z is the pre-activation or the output, either gives the mask
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = z[e] > 0.f ? a[e] : 0.f;
     return;
   }
 #pragma unroll
@@ -1777,6 +1788,78 @@ MLC_EXPORT int mlc_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, i
     MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
 #undef MKB
   }
+  if (plain) {
+#define MKB(R) (MatMC<R>{x, C, P, C})
+    MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
+#undef MKB
+  }
+#define MKB(R) (ConvWgradB<R>{x, g, P, KK})
+  MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);
+#undef MKB
+#undef MKA
+}
+
+// Conv forward with a dense epilogue: y = act(conv(x, w) + bias) (act 0 / 3 = ReLU; the
+// GELU codes of the dense layers apply too) - the generic engine's convs that carry a bias
+// and no BatchNorm (LeNet-style nets, 1x1 squeeze-excitation convs, segmentation heads).
+MLC_EXPORT int mlc_conv_fwd_ex(const bf16* x, const bf16* w, bf16* y, const float* bias, int act, int N, int H,
+                               int W, int C, int Co, int KH, int KW, int stride, int pad, int dil, int Ho, int Wo,
+                               hipStream_t st) {
+  if (C % 8 || Co % 8 || KH > 15 || KW > 16) return -1;
+  const int M = N * Ho * Wo, K = KH * KW * C;
+  const int tile = pick_tile(M, Co);
+  EpiBF16<IdentityRows, true> epi{y, Co, nullptr, nullptr, IdentityRows{}, nullptr};
+  epi.bias = bias;
+  epi.act = act;
+#define MKB(R) (MatKC<R>{w, K, Co, K})
+  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
+#define MKA(R) (MatKC<R>{x, C, M, K})
+    MLC_TILE_DISPATCH(tile, M, Co, K, 1, st, epi, MKA, MKB);
+#undef MKA
+  }
+  const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
+#define MKA(R) (ConvFwdA<R>{x, g, M, K})
+  MLC_TILE_DISPATCH(tile, M, Co, K, 1, st, epi, MKA, MKB);
+#undef MKA
+#undef MKB
+}
+
+// Conv weight gradient plus the bias gradient: dw[Co][KH*KW*C] (+)= as mlc_conv_wgrad and
+// dbias[Co] += the column sums of dy, summed from dy's staged tiles (MatMCSum) in the same
+// GEMM.  Split-K partial tiles go to fp32 slabs of ws (+ one reduction pass) when it is big
+// enough, else fp32 atomics.
+MLC_EXPORT int mlc_conv_wgrad_bias(const bf16* dy, const bf16* x, float* dw, float* dbias, int N, int H, int W,
+                                   int C, int Co, int KH, int KW, int stride, int pad, int dil, int Ho, int Wo,
+                                   int accumulate, float* ws, long ws_floats, hipStream_t st) {
+  if (C % 8 || Co % 8 || !dbias) return -1;
+  const int P = N * Ho * Wo, KK = KH * KW * C;
+  const int tile = pick_tile(Co, KK);
+  const bool plain = KH == 1 && KW == 1 && stride == 1 && pad == 0;
+  const size_t slab = (size_t)Co * KK;
+  int splits = g_mlc_det ? 1 : auto_splits(Co, KK, P, tile, plain ? g_split_target_mat : g_split_target);
+  const ConvGeom g = mkgeom(N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo);
+#define MKA(R) (MatMCSum<R>{dy, Co, P, Co, dbias})
+  if (ws && splits > 1 && (long)(splits * slab) <= ws_floats) {
+    const int ktiles = (P + BK - 1) / BK;
+    const int per = (ktiles + splits - 1) / splits;
+    splits = (ktiles + per - 1) / per;
+    EpiF32Slab epi{ws, KK, slab};
+    hipError_t e;
+#define MKB(R) (MatMC<R>{x, C, P, C})
+    if (plain) e = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB); }();
+#undef MKB
+#define MKB(R) (ConvWgradB<R>{x, g, P, KK})
+    else e = [&]() -> hipError_t { MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB); }();
+#undef MKB
+    if (e != hipSuccess) return e;
+    const long n4 = (long)slab / 4;
+    long blocks = (n4 + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, dw, n4, splits, n4, accumulate);
+    return hipGetLastError();
+  }
+  if (!accumulate) (void)hipMemsetAsync(dw, 0, slab * sizeof(float), st);
+  EpiF32Atomic epi{dw, KK};
   if (plain) {
 #define MKB(R) (MatMC<R>{x, C, P, C})
     MLC_TILE_DISPATCH(tile, Co, KK, P, splits, st, epi, MKA, MKB);

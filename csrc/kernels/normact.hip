@@ -1,0 +1,347 @@
+// BatchNorm with any activation, for the generic native engine (batchnorm.hip keeps the
+// ReLU-only passes the ResNet engine is tuned on).  NHWC bf16, 16 B per lane, threads own
+// a fixed 8-channel group (grid = multiple of C/8 threads).
+//
+//   stats      per-channel sum / sum-of-squares of x into 32 partial copies (a BatchNorm
+//              whose input no conv epilogue reduced: after a pool, a concat, a torch op)
+//   apply      z = act(y*scale + shift [+ res*rscale + rshift])
+//   bwd        dU = dz * act'(a) (a = the pre-activation, recomputed from y [and res], or the
+//              derivative read off z), S1 = sum dU, S2 = sum dU*(y - mean) per channel, then
+//              dy = k1*dU + k2 + k3*(y - mean) and dres = dU (mlc_bn_bwd_finalize gives k*)
+//
+// Activation codes (ACT_*): 0 identity, 1 ReLU, 2 ReLU6, 3 SiLU, 4 sigmoid, 5 tanh,
+// 6 hardswish, 7 leaky ReLU (slope `alpha`), 8 GELU (erf), 9 ELU (alpha), 10 hardsigmoid.
+#include "common.h"
+
+namespace normact {
+
+constexpr int NT = 256;
+constexpr int NCOPY = 32;
+
+__device__ __forceinline__ float sigm(float a) { return 1.f / (1.f + __expf(-a)); }
+
+__device__ __forceinline__ float act_f(float a, int act, float alpha) {
+  switch (act) {
+    case 1: return fmaxf(a, 0.f);
+    case 2: return fminf(fmaxf(a, 0.f), 6.f);
+    case 3: return a * sigm(a);
+    case 4: return sigm(a);
+    case 5: return tanhf(a);
+    case 6: return a * fminf(fmaxf(a + 3.f, 0.f), 6.f) * (1.f / 6.f);
+    case 7: return a > 0.f ? a : alpha * a;
+    case 8: return 0.5f * a * (1.f + erff(a * 0.70710678118654752f));
+    case 9: return a > 0.f ? a : alpha * (__expf(a) - 1.f);
+    case 10: return fminf(fmaxf(a + 3.f, 0.f), 6.f) * (1.f / 6.f);
+    default: return a;
+  }
+}
+
+// d act / d a at pre-activation a (z = act(a) as stored, used where it is the cheaper input;
+// the masks of the piecewise-linear codes are taken from a, which matches torch: ReLU'(0) = 0,
+// ReLU6'(6) = 0, hardswish at +-3 as torch's hardswish_backward)
+__device__ __forceinline__ float act_df(float a, float z, int act, float alpha) {
+  switch (act) {
+    case 1: return a > 0.f ? 1.f : 0.f;
+    case 2: return (a > 0.f && a < 6.f) ? 1.f : 0.f;
+    case 3: { const float s = sigm(a); return s * (1.f + a * (1.f - s)); }
+    case 4: return z * (1.f - z);
+    case 5: return 1.f - z * z;
+    case 6: return a < -3.f ? 0.f : (a <= 3.f ? (2.f * a + 3.f) * (1.f / 6.f) : 1.f);
+    case 7: return a > 0.f ? 1.f : alpha;
+    case 8: {
+      const float cdf = 0.5f * (1.f + erff(a * 0.70710678118654752f));
+      return cdf + a * 0.3989422804014327f * __expf(-0.5f * a * a);
+    }
+    case 9: return a > 0.f ? 1.f : alpha * __expf(a);
+    case 10: return (a > -3.f && a < 3.f) ? (1.f / 6.f) : 0.f;
+    default: return 1.f;
+  }
+}
+
+// per-thread constants of its channel group
+struct Ch {
+  float sc[8], sh[8], rs[8], rh[8];
+};
+__device__ __forceinline__ void load_ch(Ch& c, const float* scale, const float* shift, const float* rscale,
+                                        const float* rshift, int c0) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    c.sc[j] = scale[c0 + j];
+    c.sh[j] = shift[c0 + j];
+    c.rs[j] = rscale ? rscale[c0 + j] : 1.f;
+    c.rh[j] = rscale ? rshift[c0 + j] : 0.f;
+  }
+}
+
+__global__ void __launch_bounds__(NT)
+stats_kernel(const bf16* __restrict__ x, float* __restrict__ sum, float* __restrict__ sumsq, long rows, int C) {
+  __shared__ float rb[NT][17];
+  const int G = C >> 3;
+  const long gtid = (long)blockIdx.x * NT + threadIdx.x;
+  const long stride = (long)gridDim.x * NT;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  const long total = rows * G;
+  for (long i = gtid; i < total; i += stride) {
+    float f[8];
+    unpack8(ldg16(x + i * 8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s1[e] += f[e]; s2[e] += f[e] * f[e]; }
+  }
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { rb[t][e] = s1[e]; rb[t][8 + e] = s2[e]; }
+  __syncthreads();
+  const int lanes = NT < G ? NT : G;
+  const int base_cg = (int)(((long)blockIdx.x * NT) % G);
+  if (t < lanes) {
+    float a[8], b[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { a[e] = 0.f; b[e] = 0.f; }
+    for (int u = t; u < NT; u += G)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { a[e] += rb[u][e]; b[e] += rb[u][8 + e]; }
+    const int cg = (base_cg + t) % G;
+    const long slot = blockIdx.x % NCOPY;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      atomicAdd(sum + slot * C + cg * 8 + e, a[e]);
+      atomicAdd(sumsq + slot * C + cg * 8 + e, b[e]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(NT)
+apply_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf16* __restrict__ z,
+             const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ rscale,
+             const float* __restrict__ rshift, long rows, int C, int act, float alpha) {
+  const int G = C >> 3;
+  const long gtid = (long)blockIdx.x * NT + threadIdx.x;
+  const long stride = (long)gridDim.x * NT;
+  const int c0 = (int)(gtid % G) * 8;
+  Ch c;
+  load_ch(c, scale, shift, rscale, rshift, c0);
+  const long total = rows * G;
+  for (long i = gtid; i < total; i += stride) {
+    float f[8];
+    unpack8(ldg16(y + i * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = f[j] * c.sc[j] + c.sh[j];
+    if (res) {
+      float r[8];
+      unpack8(ldg16(res + i * 8), r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += r[j] * c.rs[j] + c.rh[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = act_f(f[j], act, alpha);
+    *reinterpret_cast<uint4*>(z + i * 8) = pack8(f);
+  }
+}
+
+// dU of one chunk: dz * act'(a), a recomputed from y (and res) with the forward's affine
+__device__ __forceinline__ void dU8(float (&d)[8], const uint4& zv, const uint4& yv, const uint4& rv, bool has_res,
+                                    const Ch& c, int act, float alpha) {
+  if (act == 0) return;
+  float yy[8], zz[8], a[8];
+  unpack8(yv, yy);
+  unpack8(zv, zz);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = yy[j] * c.sc[j] + c.sh[j];
+  if (has_res) {
+    float r[8];
+    unpack8(rv, r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += r[j] * c.rs[j] + c.rh[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d[j] *= act_df(a[j], zz[j], act, alpha);
+}
+
+__global__ void __launch_bounds__(NT)
+bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const bf16* __restrict__ y,
+                  const bf16* __restrict__ res, const float* __restrict__ mean, const float* __restrict__ scale,
+                  const float* __restrict__ shift, const float* __restrict__ rscale, const float* __restrict__ rshift,
+                  float* __restrict__ sums, long rows, int C, int act, float alpha) {
+  __shared__ float rb[NT][17];
+  const int G = C >> 3;
+  const long gtid = (long)blockIdx.x * NT + threadIdx.x;
+  const long stride = (long)gridDim.x * NT;
+  const int c0 = (int)(gtid % G) * 8;
+  Ch c;
+  load_ch(c, scale, shift, rscale, rshift, c0);
+  float mu[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; s1[j] = 0.f; s2[j] = 0.f; }
+  const long total = rows * G;
+  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  for (long i = gtid; i < total; i += stride) {
+    const uint4 dv = ldg16(dz + i * 8), yv = ldg16(y + i * 8);
+    const uint4 zv = z ? ldg16(z + i * 8) : z4, rv = res ? ldg16(res + i * 8) : z4;
+    float d[8], yy[8];
+    unpack8(dv, d);
+    unpack8(yv, yy);
+    dU8(d, zv, yv, rv, res != nullptr, c, act, alpha);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s1[j] += d[j]; s2[j] += d[j] * (yy[j] - mu[j]); }
+  }
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { rb[t][e] = s1[e]; rb[t][8 + e] = s2[e]; }
+  __syncthreads();
+  const int lanes = NT < G ? NT : G;
+  const int base_cg = (int)(((long)blockIdx.x * NT) % G);
+  if (t < lanes) {
+    float a[8], b[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { a[e] = 0.f; b[e] = 0.f; }
+    for (int u = t; u < NT; u += G)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { a[e] += rb[u][e]; b[e] += rb[u][8 + e]; }
+    const int cg = (base_cg + t) % G;
+    float* dst = sums + (long)(blockIdx.x % NCOPY) * 2 * C;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      atomicAdd(dst + cg * 8 + e, a[e]);
+      atomicAdd(dst + C + cg * 8 + e, b[e]);
+    }
+  }
+}
+
+// dy = k1*dU + k2 + k3*(y - mean) (coef from mlc_bn_bwd_finalize), dres = dU
+__global__ void __launch_bounds__(NT)
+bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const bf16* __restrict__ y,
+                 const bf16* __restrict__ res, const float* __restrict__ mean, const float* __restrict__ coef,
+                 const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ rscale,
+                 const float* __restrict__ rshift, bf16* __restrict__ dy, bf16* __restrict__ dres, long rows, int C,
+                 int act, float alpha) {
+  const int G = C >> 3;
+  const long gtid = (long)blockIdx.x * NT + threadIdx.x;
+  const long stride = (long)gridDim.x * NT;
+  const int c0 = (int)(gtid % G) * 8;
+  Ch c;
+  load_ch(c, scale, shift, rscale, rshift, c0);
+  float mu[8], k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mu[j] = mean[c0 + j];
+    k1[j] = coef[c0 + j];
+    k2[j] = coef[C + c0 + j];
+    k3[j] = coef[2 * C + c0 + j];
+  }
+  const long total = rows * G;
+  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  for (long i = gtid; i < total; i += stride) {
+    const uint4 dv = ldg16(dz + i * 8), yv = ldg16(y + i * 8);
+    const uint4 zv = z ? ldg16(z + i * 8) : z4, rv = res ? ldg16(res + i * 8) : z4;
+    float d[8], yy[8], o[8];
+    unpack8(dv, d);
+    unpack8(yv, yy);
+    dU8(d, zv, yv, rv, res != nullptr, c, act, alpha);
+    if (dres) *reinterpret_cast<uint4*>(dres + i * 8) = pack8(d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = k1[j] * d[j] + k2[j] + k3[j] * (yy[j] - mu[j]);
+    *reinterpret_cast<uint4*>(dy + i * 8) = pack8(o);
+  }
+}
+
+// y = act(x) and dx = dy * act'(x) for a torch-free activation between native ops
+__global__ void __launch_bounds__(NT)
+act_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long n8, int act, float alpha) {
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    float f[8];
+    unpack8(ldg16(x + i * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = act_f(f[j], act, alpha);
+    *reinterpret_cast<uint4*>(y + i * 8) = pack8(f);
+  }
+}
+
+__global__ void __launch_bounds__(NT)
+act_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, const bf16* __restrict__ y,
+               bf16* __restrict__ dx, long n8, int act, float alpha) {
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    float d[8], a[8], z[8];
+    unpack8(ldg16(dy + i * 8), d);
+    unpack8(ldg16(x + i * 8), a);
+    unpack8(ldg16(y + i * 8), z);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] *= act_df(a[j], z[j], act, alpha);
+    *reinterpret_cast<uint4*>(dx + i * 8) = pack8(d);
+  }
+}
+
+inline int grid_for(long rows, int C, int cap = 1024) {
+  const int G = C >> 3;
+  long blocks = (rows * G + NT * 4 - 1) / (NT * 4);
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  long m;
+  if (G > NT) {
+    m = G % NT == 0 ? G / NT : G;
+  } else {
+    int a = G, b = NT;
+    while (b) { const int r = a % b; a = b; b = r; }
+    m = G / a;
+  }
+  return (int)(((blocks + m - 1) / m) * m);
+}
+
+inline int blocks_for(long work) {
+  long b = (work + NT - 1) / NT;
+  return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
+}
+
+}  // namespace normact
+
+using namespace normact;
+
+// sum/sumsq: 32*C fp32 each, zeroed by the caller; C % 8 == 0
+MLC_EXPORT int mlc_bn_stats(const bf16* x, float* sum, float* sumsq, long rows, int C, hipStream_t st) {
+  if (C % 8) return -1;
+  hipLaunchKernelGGL(stats_kernel, dim3(grid_for(rows, C)), dim3(NT), 0, st, x, sum, sumsq, rows, C);
+  return hipGetLastError();
+}
+
+MLC_EXPORT int mlc_bnact_apply(const bf16* y, const bf16* res, bf16* z, const float* scale, const float* shift,
+                               const float* rscale, const float* rshift, long rows, int C, int act, float alpha,
+                               hipStream_t st) {
+  if (C % 8 || (rscale && !rshift)) return -1;
+  hipLaunchKernelGGL(apply_kernel, dim3(grid_for(rows, C, 768)), dim3(NT), 0, st, y, res, z, scale, shift, rscale,
+                     rshift, rows, C, act, alpha);
+  return hipGetLastError();
+}
+
+// sums: 32*2*C fp32, zeroed by the caller
+MLC_EXPORT int mlc_bnact_bwd_reduce(const bf16* dz, const bf16* z, const bf16* y, const bf16* res, const float* mean,
+                                    const float* scale, const float* shift, const float* rscale, const float* rshift,
+                                    float* sums, long rows, int C, int act, float alpha, hipStream_t st) {
+  if (C % 8) return -1;
+  hipLaunchKernelGGL(bwd_reduce_kernel, dim3(grid_for(rows, C)), dim3(NT), 0, st, dz, z, y, res, mean, scale, shift,
+                     rscale, rshift, sums, rows, C, act, alpha);
+  return hipGetLastError();
+}
+
+MLC_EXPORT int mlc_bnact_bwd_apply(const bf16* dz, const bf16* z, const bf16* y, const bf16* res, const float* mean,
+                                   const float* coef, const float* scale, const float* shift, const float* rscale,
+                                   const float* rshift, bf16* dy, bf16* dres, long rows, int C, int act, float alpha,
+                                   hipStream_t st) {
+  if (C % 8) return -1;
+  hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_for(rows, C, 768)), dim3(NT), 0, st, dz, z, y, res, mean, coef,
+                     scale, shift, rscale, rshift, dy, dres, rows, C, act, alpha);
+  return hipGetLastError();
+}
+
+MLC_EXPORT int mlc_act_fwd(const bf16* x, bf16* y, long n, int act, float alpha, hipStream_t st) {
+  if (n % 8) return -1;
+  hipLaunchKernelGGL(act_fwd_kernel, dim3(blocks_for(n / 8)), dim3(NT), 0, st, x, y, n / 8, act, alpha);
+  return hipGetLastError();
+}
+
+MLC_EXPORT int mlc_act_bwd(const bf16* dy, const bf16* x, const bf16* y, bf16* dx, long n, int act, float alpha,
+                           hipStream_t st) {
+  if (n % 8) return -1;
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(blocks_for(n / 8)), dim3(NT), 0, st, dy, x, y, dx, n / 8, act, alpha);
+  return hipGetLastError();
+}

@@ -67,7 +67,8 @@ class MBConv(nn.Module):
         if self.residual:
             if self.training and self.drop_path > 0:
                 keep = 1 - self.drop_path
-                mask = torch.rand(y.shape[0], 1, 1, 1, device=y.device, dtype=y.dtype) < keep
+                # one draw per sample (rand_like of a [N, 1, 1, 1] slice: fx-traceable)
+                mask = torch.rand_like(y[:, :1, :1, :1]) < keep
                 y = y * mask / keep
             y = y + x
         return y

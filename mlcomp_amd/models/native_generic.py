@@ -1,0 +1,430 @@
+"""Generic native lowering: any ``nn.Module`` onto the HIP kernels, through torch.fx.
+
+The reference trains whatever model an experiment returns
+(`mlcomp/worker/executors/catalyst_/catalyst_.py:365-430`): its own examples' LeNet and
+CIFAR nets (`examples/digit-recognizer/model.py:8-25`, `examples/cifar_simple/model.py:8-26`),
+the contrib zoo (`mlcomp/contrib/model/pretrained.py`), segmentation encoders
+(`mlcomp/contrib/segmentation/encoders/__init__.py:12-18`).  The hand-lowered engines cover
+seven architectures; this module covers the rest:
+
+1. ``torch.fx.symbolic_trace`` the model twice (train and eval mode: ``self.training``
+   branches, dropout and drop-path are baked in at trace time).
+2. Pattern-match the graph and replace each match by one native call site
+   (:mod:`mlcomp_amd.ops.glayers`):
+
+   * ``Conv2d [-> BatchNorm2d [-> + residual]] [-> activation]`` -> ``ConvBNAct``: dense
+     convs on the implicit-GEMM MFMA kernels (BN statistics in the epilogue; without BN
+     the bias and a ReLU in the epilogue), grouped convs on the 16x16x32 MFMA block-diagonal
+     kernels, depthwise convs on the VALU kernels (``gconv.hip``); BN apply + residual +
+     any of 10 activations in one pass (``normact.hip``);
+   * ``BatchNorm2d / BatchNorm1d [-> + residual] [-> activation]`` -> ``BNAct``;
+   * ``Linear [-> ReLU]`` -> ``LinearAct`` (bias / ReLU in the dense GEMM epilogue);
+   * ``MaxPool2d`` / ``F.max_pool2d`` -> ``MaxPool``; ``AdaptiveAvgPool2d(1)`` ->
+     ``GlobalAvgPool``; ``x.view`` -> ``x.reshape`` (site outputs are channels_last views).
+
+   A fused chain needs each intermediate value to have exactly one user; every op left in
+   the graph (adds, concats, upsampling, dropout, sigmoid gates, the loss ...) is a PyTorch
+   tensor op on bf16 activations - no MIOpen / hipBLASLt / rocBLAS call remains, and a
+   module that would need one raises :class:`NativeUnsupported` (``engine: auto`` then
+   trains the stage on the torch engine and records why).
+3. Every parameter lives in the flat arena: the lowered modules' weights in kernel layout
+   (bf16 mirror for the GEMMs), any other parameter (a LayerNorm a torch op still uses, a
+   learned scale) aliased in place - its ``.data`` and ``.grad`` become arena views - so
+   one fused optimizer launch per arena and the RCCL bucketer cover the whole model.
+"""
+from __future__ import annotations
+
+import operator
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.fx as fx
+import torch.nn as nn
+import torch.nn.functional as F
+
+from mlcomp_amd.ops import functional as Fn
+from mlcomp_amd.ops.glayers import (BNAct, BNParams, ConvBNAct, ConvParams, GlobalAvgPool, LinearAct,
+                                    LinearParams, MaxPool)
+from mlcomp_amd.ops.layers import NativeContext
+from mlcomp_amd.train.native_spec import NativeUnsupported
+
+A = Fn.ACT
+_ACT_MODULES = {nn.ReLU: A['relu'], nn.ReLU6: A['relu6'], nn.SiLU: A['silu'], nn.Sigmoid: A['sigmoid'],
+                nn.Tanh: A['tanh'], nn.Hardswish: A['hardswish'], nn.LeakyReLU: A['leaky_relu'],
+                nn.GELU: A['gelu'], nn.ELU: A['elu'], nn.Hardsigmoid: A['hardsigmoid']}
+_ACT_FUNCS = {F.relu: A['relu'], torch.relu: A['relu'], torch.relu_: A['relu'], F.relu_: A['relu'],
+              F.relu6: A['relu6'], F.silu: A['silu'], torch.sigmoid: A['sigmoid'], torch.tanh: A['tanh'],
+              F.hardswish: A['hardswish'], F.leaky_relu: A['leaky_relu'], F.gelu: A['gelu'], F.elu: A['elu'],
+              F.hardsigmoid: A['hardsigmoid']}
+_ACT_METHODS = {'relu': A['relu'], 'relu_': A['relu'], 'sigmoid': A['sigmoid'], 'sigmoid_': A['sigmoid'],
+                'tanh': A['tanh'], 'tanh_': A['tanh']}
+_ADDS = {operator.add, operator.iadd, torch.add}
+
+
+def _is_module(node, modules, types):
+    return node.op == 'call_module' and isinstance(modules.get(node.target), types)
+
+
+def _act_of(node: fx.Node, modules) -> Optional[Tuple[int, float]]:
+    """(code, alpha) when ``node`` applies a supported activation to its first input."""
+    if node.op == 'call_module':
+        m = modules.get(node.target)
+        code = _ACT_MODULES.get(type(m))
+        if code is None:
+            return None
+        if isinstance(m, nn.GELU) and m.approximate != 'none':
+            return None
+        alpha = float(getattr(m, 'negative_slope', getattr(m, 'alpha', 0.0)))
+        return code, alpha
+    if node.op == 'call_function' and node.target in _ACT_FUNCS:
+        extra = [a for a in node.args[1:] if isinstance(a, fx.Node)]
+        if extra or any(isinstance(v, fx.Node) for v in node.kwargs.values()):
+            return None
+        if node.target is F.gelu and node.kwargs.get('approximate', 'none') != 'none':
+            return None
+        alpha = 0.0
+        if node.target is F.leaky_relu:
+            alpha = float(node.args[1] if len(node.args) > 1 else node.kwargs.get('negative_slope', 0.01))
+        elif node.target is F.elu:
+            alpha = float(node.args[1] if len(node.args) > 1 else node.kwargs.get('alpha', 1.0))
+        return _ACT_FUNCS[node.target], alpha
+    if node.op == 'call_method' and node.target in _ACT_METHODS and len(node.args) == 1:
+        return _ACT_METHODS[node.target], 0.0
+    return None
+
+
+def _residual_of(node: fx.Node, cur: fx.Node) -> Optional[fx.Node]:
+    """The other operand when ``node`` is ``cur + other`` (tensor + tensor, no alpha)."""
+    if node.kwargs.get('alpha', 1) != 1:
+        return None
+    if node.op == 'call_function' and node.target in _ADDS and len(node.args) == 2:
+        a, b = node.args
+    elif node.op == 'call_method' and node.target in ('add', 'add_') and len(node.args) == 2:
+        a, b = node.args
+    else:
+        return None
+    if not (isinstance(a, fx.Node) and isinstance(b, fx.Node)):
+        return None
+    if a is cur and b is not cur:
+        return b
+    if b is cur and a is not cur:
+        return a
+    return None
+
+
+def _only_user(node: fx.Node) -> Optional[fx.Node]:
+    users = list(node.users)
+    return users[0] if len(users) == 1 else None
+
+
+def _pair(v, name):
+    if isinstance(v, (tuple, list)):
+        if len(set(v)) != 1:
+            raise NativeUnsupported(f'{name}={tuple(v)}: the native kernels take square {name}s')
+        return int(v[0])
+    return int(v)
+
+
+def _check_conv(name, m: nn.Conv2d):
+    if m.padding_mode != 'zeros':
+        raise NativeUnsupported(f'{name}: padding_mode={m.padding_mode!r}')
+    if isinstance(m.padding, str):
+        raise NativeUnsupported(f'{name}: padding={m.padding!r}')
+    for attr in ('stride', 'padding', 'dilation'):
+        _pair(getattr(m, attr), f'{name}.{attr}')
+    KH, KW = m.kernel_size
+    if KH > 15 or KW > 15:
+        raise NativeUnsupported(f'{name}: kernel {KH}x{KW} (native convs take <= 15x15)')
+    Co, Cg = m.weight.shape[:2]
+    if m.groups > 1:
+        C = Cg * m.groups
+        if m.groups == C and Co == C:
+            return
+        if Co // m.groups != Cg or C % 16 or Co % 16 or not (16 % Cg == 0 or Cg % 16 == 0):
+            raise NativeUnsupported(f'{name}: grouped conv {C}->{Co} x{m.groups} groups (native: equal group '
+                                    'widths dividing or divisible by 16, channels % 16 == 0)')
+
+
+def _check_bn(name, m):
+    if m.momentum is None:
+        raise NativeUnsupported(f'{name}: BatchNorm momentum=None (cumulative average)')
+
+
+class _Lowering:
+    """One fx graph rewrite (train or eval) sharing the net's parameter sets."""
+
+    def __init__(self, net: 'GenericNet', gm: fx.GraphModule):
+        self.net, self.gm = net, gm
+        self.modules = dict(gm.named_modules())
+        self.erased = set()
+        self.nsites = 0
+
+    def _site_node(self, after: fx.Node, site, args):
+        name = f'_native_site_{self.nsites}'
+        self.nsites += 1
+        self.gm.add_submodule(name, site)
+        with self.gm.graph.inserting_after(after):
+            return self.gm.graph.call_module(name, tuple(args))
+
+    def _replace(self, chain, new):
+        chain[-1].replace_all_uses_with(new)
+        for n in reversed(chain):
+            self.gm.graph.erase_node(n)
+            self.erased.add(n)
+
+    def _tail(self, cur, chain, allow_res=True):
+        """Extend a chain with an optional residual add and activation: (res, act, alpha)."""
+        res, act, alpha = None, 0, 0.0
+        u = _only_user(cur)
+        if allow_res and u is not None and _residual_of(u, cur) is not None:
+            res = _residual_of(u, cur)
+            chain.append(u)
+            cur = u
+            u = _only_user(cur)
+        if u is not None:
+            a = _act_of(u, self.modules)
+            if a is not None:
+                act, alpha = a
+                chain.append(u)
+        return res, act, alpha
+
+    def conv(self, node):
+        m = self.modules[node.target]
+        _check_conv(node.target, m)
+        chain = [node]
+        bn_node = _only_user(node)
+        bn = None
+        if bn_node is not None and _is_module(bn_node, self.modules, nn.BatchNorm2d):
+            bm = self.modules[bn_node.target]
+            if bm.num_features == m.out_channels and bm.momentum is not None:
+                bn = bm
+        if bn is not None:
+            chain.append(bn_node)
+            res, act, alpha = self._tail(bn_node, chain)
+            cp = self.net.conv_params(node.target, m, keep_bias=False)
+            bp = self.net.bn_params(bn_node.target, bn, conv_bias=m.bias)
+        else:
+            res, act, alpha = self._tail(node, chain, allow_res=False)
+            cp = self.net.conv_params(node.target, m, keep_bias=True)
+            bp = None
+        site = ConvBNAct(self.net.ctx, cp, bp, act, alpha, residual=res is not None)
+        new = self._site_node(chain[-1], site, [node.args[0]] + ([res] if res is not None else []))
+        self._replace(chain, new)
+
+    def bn(self, node):
+        m = self.modules[node.target]
+        _check_bn(node.target, m)
+        chain = [node]
+        res, act, alpha = self._tail(node, chain)
+        site = BNAct(self.net.ctx, self.net.bn_params(node.target, m), act, alpha, residual=res is not None)
+        new = self._site_node(chain[-1], site, [node.args[0]] + ([res] if res is not None else []))
+        self._replace(chain, new)
+
+    def linear(self, node):
+        m = self.modules[node.target]
+        chain = [node]
+        u = _only_user(node)
+        act = 0
+        if u is not None and _act_of(u, self.modules) == (A['relu'], 0.0):
+            act = 3                       # the dense epilogue's ReLU code
+            chain.append(u)
+        site = LinearAct(self.net.ctx, self.net.linear_params(node.target, m), act)
+        new = self._site_node(chain[-1], site, [node.args[0]])
+        self._replace(chain, new)
+
+    def maxpool(self, node, k, s, p, d=1, ceil=False, ret=False):
+        k, s, p, d = _pair(k, 'kernel_size'), _pair(s if s is not None else k, 'stride'), _pair(p, 'padding'), \
+            _pair(d, 'dilation')
+        if d != 1 or ret or k * k > 255:
+            raise NativeUnsupported(f'max_pool2d(k={k}, dilation={d}, return_indices={ret})')
+        new = self._site_node(node, MaxPool(self.net.ctx, k, s, p, bool(ceil)), [node.args[0]])
+        self._replace([node], new)
+
+    def avgpool(self, node):
+        new = self._site_node(node, GlobalAvgPool(self.net.ctx), [node.args[0]])
+        self._replace([node], new)
+
+    def run(self):
+        g = self.gm.graph
+        for node in list(g.nodes):
+            if node in self.erased:
+                continue
+            if node.op == 'call_module':
+                m = self.modules.get(node.target)
+                if isinstance(m, nn.Conv2d):
+                    self.conv(node)
+                elif isinstance(m, (nn.BatchNorm2d, nn.BatchNorm1d)):
+                    self.bn(node)
+                elif isinstance(m, nn.Linear):
+                    self.linear(node)
+                elif isinstance(m, nn.MaxPool2d):
+                    self.maxpool(node, m.kernel_size, m.stride, m.padding, m.dilation, m.ceil_mode, m.return_indices)
+                elif isinstance(m, nn.AdaptiveAvgPool2d) and _pair(m.output_size, 'output_size') == 1:
+                    self.avgpool(node)
+                elif isinstance(m, (nn.ConvTranspose2d, nn.Conv1d, nn.Conv3d, nn.ConvTranspose1d,
+                                    nn.ConvTranspose3d, nn.BatchNorm3d, nn.LSTM, nn.GRU, nn.RNN,
+                                    nn.MultiheadAttention, nn.Bilinear, nn.InstanceNorm2d)):
+                    raise NativeUnsupported(f'{node.target}: {type(m).__name__} has no native lowering')
+            elif node.op == 'call_function':
+                t = node.target
+                if t in (F.max_pool2d, torch.max_pool2d):
+                    args = list(node.args) + [None] * 6
+                    kw = node.kwargs
+                    self.maxpool(node, kw.get('kernel_size', args[1]), kw.get('stride', args[2]),
+                                 kw.get('padding', args[3] if args[3] is not None else 0),
+                                 kw.get('dilation', args[4] if args[4] is not None else 1),
+                                 kw.get('ceil_mode', args[5] or False), kw.get('return_indices', args[6] or False))
+                elif t is F.adaptive_avg_pool2d and _pair(node.args[1] if len(node.args) > 1
+                                                          else node.kwargs['output_size'], 'output_size') == 1:
+                    self.avgpool(node)
+                elif t in (F.conv2d, torch.conv2d, F.linear, torch.matmul, torch.mm, torch.bmm, torch.addmm,
+                           F.batch_norm, torch.einsum, F.conv_transpose2d, F.scaled_dot_product_attention,
+                           operator.matmul):
+                    raise NativeUnsupported(f'{node.name}: functional {getattr(t, "__name__", t)} on module '
+                                            'parameters has no native lowering (use the nn modules)')
+            elif node.op == 'call_method':
+                if node.target == 'view':
+                    node.target = 'reshape'     # site outputs are channels_last views
+                elif node.target in ('matmul', 'mm', 'bmm'):
+                    raise NativeUnsupported(f'{node.name}: Tensor.{node.target} has no native lowering')
+        g.lint()
+        self.gm.delete_all_unused_submodules()
+        self.gm.recompile()
+        return self.gm
+
+
+class GenericNet:
+    """A model lowered onto the native kernels: ``net(x)`` runs the train or eval graph
+    (``train()`` / ``eval()``), parameters live in ``net.ctx.arena``."""
+
+    def __init__(self, model: nn.Module, device):
+        self.torch_model = model
+        self.device = torch.device(device)
+        ctx = self.ctx = NativeContext()
+        ctx.wt = None                      # generic sites read filters directly
+        ctx.grad_prezeroed = True          # the step zeroes the grad arena once
+        self._params: Dict[str, object] = {}
+        was = model.training
+        model.to(self.device)
+        try:
+            model.train()
+            self.train_gm = self._lower(model)
+            model.eval()
+            self.eval_gm = self._lower(model)
+        except NativeUnsupported:
+            raise
+        except Exception as e:             # fx cannot trace data-dependent control flow
+            raise NativeUnsupported(f'{type(model).__name__}: torch.fx tracing failed ({type(e).__name__}: '
+                                    f'{str(e).splitlines()[0] if str(e) else ""})') from e
+        finally:
+            model.train(was)
+        self._alias_residual_params(model)
+        ctx.finalize(self.device)
+        for p in self._params.values():
+            p.load_from_torch()
+        self._bind_residual()
+        ctx.arena.decay.refresh_mirror()
+        self.training = True
+
+    # ------------------------------------------------------------------ lowering
+    def _lower(self, model):
+        gm = fx.symbolic_trace(model)
+        return _Lowering(self, gm).run()
+
+    def conv_params(self, name, m, keep_bias):
+        key = f'conv:{name}:{keep_bias}'
+        if key not in self._params:
+            self._params[key] = ConvParams(self.ctx, name, m, keep_bias)
+        return self._params[key]
+
+    def bn_params(self, name, m, conv_bias=None):
+        key = f'bn:{name}'
+        if key not in self._params:
+            p = BNParams(self.ctx, name, m)
+            p.conv_bias = conv_bias        # a bias before a batch-stat BN only shifts its mean
+            self._params[key] = p
+        return self._params[key]
+
+    def linear_params(self, name, m):
+        key = f'linear:{name}'
+        if key not in self._params:
+            self._params[key] = LinearParams(self.ctx, name, m)
+        return self._params[key]
+
+    def _alias_residual_params(self, model):
+        """Parameters no site owns (read by torch ops left in the graph) get arena slots too."""
+        owned = set()
+        for p in self._params.values():
+            for attr in ('weight', 'bias'):
+                t = getattr(p.src, attr, None)
+                if isinstance(t, torch.Tensor):
+                    owned.add(id(t))
+        self._residual = []
+        for name, t in model.named_parameters():
+            if id(t) in owned or not t.requires_grad:
+                continue
+            slot = self.ctx.arena.vector(f'torch.{name}', tuple(t.shape))
+            self._residual.append((t, slot))
+
+    def _bind_residual(self):
+        arena = self.ctx.arena
+        for t, slot in self._residual:
+            slot.master.copy_(t.detach().float().reshape(slot.shape))
+            t.data = slot.master.view(t.shape)
+            t.grad = slot.grad.view(t.shape)
+            t.register_post_accumulate_grad_hook(lambda _t, s=slot: arena.mark_ready(s))
+
+    # ------------------------------------------------------------------ run
+    @property
+    def arena(self):
+        return self.ctx.arena
+
+    def train(self, mode: bool = True):
+        self.training = self.ctx.training = mode
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def __call__(self, x):
+        gm = self.train_gm if self.training else self.eval_gm
+        with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.device.type == 'cuda'):
+            return gm(x)
+
+    def logits(self, x):
+        return self(x)
+
+    def param_sets(self):
+        return list(self._params.values())
+
+    def _units(self):
+        """BatchNorm parameter sets with running statistics (flat-buffer broadcast)."""
+        return [p for p in self._params.values() if isinstance(p, BNParams) and p.track]
+
+    def export_to_torch(self):
+        for p in self._params.values():
+            p.export_to_torch()
+        return self.torch_model
+
+
+def lower_or_none(model: nn.Module) -> Optional[str]:
+    """None when ``model`` lowers (structural check on CPU, nothing allocated on a GPU),
+    else the reason it does not."""
+    try:
+        for mode in (True, False):
+            model.train(mode)
+            gm = fx.symbolic_trace(model)
+            probe = GenericNet.__new__(GenericNet)
+            probe.ctx = NativeContext()
+            probe._params = {}
+            _Lowering(probe, gm).run()
+        return None
+    except NativeUnsupported as e:
+        return str(e)
+    except Exception as e:
+        return f'torch.fx tracing failed ({type(e).__name__})'
+    finally:
+        model.train(True)
+
+
+__all__ = ['GenericNet', 'lower_or_none']

@@ -93,6 +93,22 @@ _SIGS = {
     'mlc_adam': [vp] * 6 + [i64, i64, i64, f32, f32, f32, f32, i32, vp],
     'mlc_sqnorm': [vp, i64, vp, f32, vp],
     'mlc_opt_config': [i32, i32],
+    # generic engine (gconv.hip, normact.hip, igemm.hip extras)
+    'mlc_gconv_wb_elems': [i32, i32, i32, i32],
+    'mlc_gconv_fwd': [vp] * 6 + [i32] * 13 + [vp],
+    'mlc_gconv_dgrad': [vp] * 4 + [i32] * 13 + [vp],
+    'mlc_gconv_wgrad': [vp] * 3 + [i32] * 14 + [vp],
+    'mlc_dwconv_fwd': [vp] * 5 + [i32] * 11 + [vp],
+    'mlc_dwconv_dgrad': [vp] * 3 + [i32] * 11 + [vp],
+    'mlc_dwconv_wgrad': [vp] * 4 + [i32] * 12 + [vp],
+    'mlc_bn_stats': [vp, vp, vp, i64, i32, vp],
+    'mlc_bnact_apply': [vp] * 7 + [i64, i32, i32, f32, vp],
+    'mlc_bnact_bwd_reduce': [vp] * 10 + [i64, i32, i32, f32, vp],
+    'mlc_bnact_bwd_apply': [vp] * 12 + [i64, i32, i32, f32, vp],
+    'mlc_act_fwd': [vp, vp, i64, i32, f32, vp],
+    'mlc_act_bwd': [vp] * 4 + [i64, i32, f32, vp],
+    'mlc_conv_fwd_ex': [vp] * 4 + [i32] * 13 + [vp],
+    'mlc_conv_wgrad_bias': [vp] * 4 + [i32] * 13 + [vp, i64, vp],
     'mlc_comm_unique_id_bytes': [],
     'mlc_comm_get_unique_id': [vp],
     'mlc_comm_init': [vp, i32, i32, i32, vp],
@@ -103,7 +119,7 @@ _SIGS = {
     'mlc_allgather': [vp, vp, vp, i64, i32, vp],
     'mlc_alltoall': [vp, vp, vp, i64, i32, i32, i32, vp],
 }
-_RESTYPE = {'mlc_comm_init': vp}
+_RESTYPE = {'mlc_comm_init': vp, 'mlc_gconv_wb_elems': C.c_long}
 
 
 def lib_path():

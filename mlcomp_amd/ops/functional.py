@@ -477,9 +477,23 @@ def bn_bwd(dz, z, y, mean, invstd, gamma, want_dres=False, dgamma=None, dbeta=No
 
 
 # ---------------------------------------------------------------- pooling
-def maxpool_fwd(x, k=3, s=2, p=1):
+def pool_out_hw(H, W, k, s, p, ceil_mode=False):
+    """nn.MaxPool2d's output size (ceil_mode: the last window may start in the right / bottom
+    padding as long as it starts inside the input or its left padding)."""
+    if not ceil_mode:
+        return conv_out_hw(H, W, k, k, s, p, 1)
+
+    def one(L):
+        o = -(-(L + 2 * p - k) // s) + 1
+        if (o - 1) * s >= L + p:
+            o -= 1
+        return o
+    return one(H), one(W)
+
+
+def maxpool_fwd(x, k=3, s=2, p=1, ceil_mode=False):
     N, H, W, C = x.shape
-    Ho, Wo = conv_out_hw(H, W, k, k, s, p, 1)
+    Ho, Wo = pool_out_hw(H, W, k, s, p, ceil_mode)
     if _cuda(x):
         y = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.bfloat16)
         idx = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.uint8)
@@ -487,7 +501,7 @@ def maxpool_fwd(x, k=3, s=2, p=1):
                   _lib.stream())
         return y, idx
     xf = x.permute(0, 3, 1, 2).float()
-    yf, ind = F.max_pool2d(xf, k, s, p, return_indices=True)
+    yf, ind = F.max_pool2d(xf, k, s, p, ceil_mode=ceil_mode, return_indices=True)
     return yf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous(), ind
 
 
@@ -790,3 +804,322 @@ def sqnorm(x, out, scale=1.0):
         return out
     out.add_(((x * scale) ** 2).sum())
     return out
+
+
+# ---------------------------------------------------------------- generic engine ops
+# Activation codes of csrc/kernels/normact.hip (and the dense GEMM epilogue's ReLU = 3)
+ACT = {'identity': 0, 'relu': 1, 'relu6': 2, 'silu': 3, 'sigmoid': 4, 'tanh': 5, 'hardswish': 6,
+       'leaky_relu': 7, 'gelu': 8, 'elu': 9, 'hardsigmoid': 10}
+
+
+def act_ref(a: torch.Tensor, act: int, alpha: float = 0.0) -> torch.Tensor:
+    """fp32 reference of the activation codes (the CPU path of the native ops)."""
+    if act == 1:
+        return a.clamp_min(0)
+    if act == 2:
+        return a.clamp(0, 6)
+    if act == 3:
+        return a * torch.sigmoid(a)
+    if act == 4:
+        return torch.sigmoid(a)
+    if act == 5:
+        return torch.tanh(a)
+    if act == 6:
+        return F.hardswish(a)
+    if act == 7:
+        return torch.where(a > 0, a, alpha * a)
+    if act == 8:
+        return F.gelu(a)
+    if act == 9:
+        return torch.where(a > 0, a, alpha * (torch.exp(a) - 1))
+    if act == 10:
+        return F.hardsigmoid(a)
+    return a
+
+
+def act_grad_ref(a: torch.Tensor, act: int, alpha: float = 0.0) -> torch.Tensor:
+    """d act / d a (torch's conventions at the kinks: ReLU'(0) = 0, as normact.hip)."""
+    if act == 0:
+        return torch.ones_like(a)
+    if act == 1:
+        return (a > 0).float()
+    if act == 2:
+        return ((a > 0) & (a < 6)).float()
+    if act == 7:
+        return torch.where(a > 0, torch.ones_like(a), torch.full_like(a, alpha))
+    if act == 9:
+        return torch.where(a > 0, torch.ones_like(a), alpha * torch.exp(a))
+    if act == 10:
+        return ((a > -3) & (a < 3)).float() / 6
+    if act == 6:
+        return torch.where(a < -3, torch.zeros_like(a), torch.where(a <= 3, (2 * a + 3) / 6, torch.ones_like(a)))
+    with torch.enable_grad():
+        x = a.detach().requires_grad_()
+        (g,) = torch.autograd.grad(act_ref(x, act, alpha).sum(), x)
+    return g
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2).float()
+
+
+def gconv_fwd(x, w, groups, stride=1, pad=0, dil=1, stats=None):
+    """Grouped conv (groups > 1, C/groups == Co/groups): x [N,H,W,C] bf16, w [Co,KH,KW,Cg] bf16
+    -> y [N,Ho,Wo,Co] bf16 on the 16x16x32 MFMA kernel (gconv.hip); ``stats`` as conv2d_fwd."""
+    N, H, W, C = x.shape
+    Co, KH, KW, Cg = w.shape
+    Ho, Wo = conv_out_hw(H, W, KH, KW, stride, pad, dil)
+    if _cuda(x):
+        y = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.bfloat16)
+        wb = torch.empty(int(_lib.load().mlc_gconv_wb_elems(Co, KH, KW, Cg)), device=x.device, dtype=torch.bfloat16)
+        s1, s2 = stats if stats is not None else (None, None)
+        _lib.call('mlc_gconv_fwd', _lib.ptr(x), _lib.ptr(w), _lib.ptr(wb), _lib.ptr(y), _lib.ptr(s1), _lib.ptr(s2),
+                  N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo, groups, _lib.stream())
+        return y
+    yf = F.conv2d(_nchw(x), w.permute(0, 3, 1, 2).float(), None, stride, pad, dil, groups)
+    if stats is not None:
+        stats[0][:Co].add_(yf.sum(dim=(0, 2, 3)))
+        stats[1][:Co].add_((yf * yf).sum(dim=(0, 2, 3)))
+    return yf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+
+
+def gconv_dgrad(dy, w, x_shape, groups, stride=1, pad=0, dil=1):
+    N, H, W, C = x_shape
+    Co, KH, KW, Cg = w.shape
+    _, Ho, Wo, _ = dy.shape
+    if _cuda(dy):
+        dx = torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
+        wb = torch.empty(int(_lib.load().mlc_gconv_wb_elems(C, KH, KW, Cg)), device=dy.device, dtype=torch.bfloat16)
+        _lib.call('mlc_gconv_dgrad', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(wb), _lib.ptr(dx), N, H, W, C, Co, KH, KW,
+                  stride, pad, dil, Ho, Wo, groups, _lib.stream())
+        return dx
+    dxf = torch.nn.grad.conv2d_input((N, C, H, W), w.permute(0, 3, 1, 2).float(), _nchw(dy), stride, pad, dil,
+                                     groups)
+    return dxf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+
+
+def gconv_wgrad(dy, x, w_shape, groups, stride=1, pad=0, dil=1, out=None, accumulate=False):
+    """fp32 [Co, KH, KW, Cg] weight gradient (written into / added to ``out``)."""
+    Co, KH, KW, Cg = w_shape
+    N, H, W, C = x.shape
+    _, Ho, Wo, _ = dy.shape
+    if _cuda(dy):
+        dw = out if out is not None else torch.empty(Co, KH, KW, Cg, device=dy.device, dtype=torch.float32)
+        _lib.call('mlc_gconv_wgrad', _lib.ptr(dy), _lib.ptr(x), _lib.ptr(dw), N, H, W, C, Co, KH, KW, stride, pad,
+                  dil, Ho, Wo, groups, int(accumulate), _lib.stream())
+        return dw
+    g = torch.nn.grad.conv2d_weight(_nchw(x), (Co, Cg, KH, KW), _nchw(dy), stride, pad, dil, groups)
+    g = g.permute(0, 2, 3, 1)
+    if out is None:
+        return g.contiguous()
+    if accumulate:
+        out.add_(g.reshape(out.shape))
+    else:
+        out.copy_(g.reshape(out.shape))
+    return out
+
+
+def dwconv_fwd(x, w, stride=1, pad=0, dil=1, stats=None):
+    """Depthwise conv: x [N,H,W,C] bf16, w [KH,KW,C] bf16 (tap-major) -> y [N,Ho,Wo,C]."""
+    N, H, W, C = x.shape
+    KH, KW, _ = w.shape
+    Ho, Wo = conv_out_hw(H, W, KH, KW, stride, pad, dil)
+    if _cuda(x):
+        y = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.bfloat16)
+        s1, s2 = stats if stats is not None else (None, None)
+        _lib.call('mlc_dwconv_fwd', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(s1), _lib.ptr(s2), N, H, W, C,
+                  KH, KW, stride, pad, dil, Ho, Wo, _lib.stream())
+        return y
+    yf = F.conv2d(_nchw(x), w.permute(2, 0, 1)[:, None].float(), None, stride, pad, dil, C)
+    if stats is not None:
+        stats[0][:C].add_(yf.sum(dim=(0, 2, 3)))
+        stats[1][:C].add_((yf * yf).sum(dim=(0, 2, 3)))
+    return yf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+
+
+def dwconv_dgrad(dy, w, x_shape, stride=1, pad=0, dil=1):
+    N, H, W, C = x_shape
+    KH, KW, _ = w.shape
+    _, Ho, Wo, _ = dy.shape
+    if _cuda(dy):
+        dx = torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
+        _lib.call('mlc_dwconv_dgrad', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(dx), N, H, W, C, KH, KW, stride, pad, dil,
+                  Ho, Wo, _lib.stream())
+        return dx
+    dxf = torch.nn.grad.conv2d_input((N, C, H, W), w.permute(2, 0, 1)[:, None].float(), _nchw(dy), stride, pad,
+                                     dil, C)
+    return dxf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+
+
+def dwconv_wgrad(dy, x, w_shape, stride=1, pad=0, dil=1, out=None, accumulate=False):
+    """fp32 [KH, KW, C] depthwise weight gradient."""
+    KH, KW, C = w_shape
+    N, H, W, _ = x.shape
+    _, Ho, Wo, _ = dy.shape
+    if _cuda(dy):
+        dw = out if out is not None else torch.empty(KH, KW, C, device=dy.device, dtype=torch.float32)
+        ws = slab_workspace(dy.device, 32 * KH * KW * C)
+        _lib.call('mlc_dwconv_wgrad', _lib.ptr(dy), _lib.ptr(x), _lib.ptr(dw), _lib.ptr(ws), N, H, W, C, KH, KW,
+                  stride, pad, dil, Ho, Wo, int(accumulate), _lib.stream())
+        return dw
+    g = torch.nn.grad.conv2d_weight(_nchw(x), (C, 1, KH, KW), _nchw(dy), stride, pad, dil, C)
+    g = g[:, 0].permute(1, 2, 0)
+    if out is None:
+        return g.contiguous()
+    if accumulate:
+        out.add_(g)
+    else:
+        out.copy_(g)
+    return out
+
+
+def conv2d_fwd_ex(x, w, bias=None, act=0, stride=1, pad=0, dil=1):
+    """y = act(conv(x, w) + bias) (dense epilogue; act 0 or 3 = ReLU); groups == 1."""
+    N, H, W, C = x.shape
+    Co, KH, KW, Ci = w.shape
+    assert Ci == C, (w.shape, x.shape)
+    Ho, Wo = conv_out_hw(H, W, KH, KW, stride, pad, dil)
+    if _cuda(x):
+        y = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.bfloat16)
+        _lib.call('mlc_conv_fwd_ex', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(bias), int(act), N, H, W, C, Co,
+                  KH, KW, stride, pad, dil, Ho, Wo, _lib.stream())
+        return y
+    yf = F.conv2d(_nchw(x), w.permute(0, 3, 1, 2).float(), bias, stride, pad, dil)
+    if act == 3:
+        yf = yf.clamp_min(0)
+    return yf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+
+
+def conv2d_wgrad_bias(dy, x, w_shape, dbias, stride=1, pad=0, dil=1, out=None, accumulate=False):
+    """fp32 weight gradient [Co, KH, KW, Ci] and dbias[Co] += colsum(dy), one GEMM."""
+    Co, KH, KW, Ci = w_shape
+    N, H, W, C = x.shape
+    _, Ho, Wo, _ = dy.shape
+    if _cuda(dy):
+        dw = out if out is not None else torch.empty(Co, KH, KW, Ci, device=dy.device, dtype=torch.float32)
+        ws = slab_workspace(dy.device, min(32 * Co * KH * KW * Ci, 64 << 20)) if _USE_SLAB else None
+        _lib.call('mlc_conv_wgrad_bias', _lib.ptr(dy), _lib.ptr(x), _lib.ptr(dw), _lib.ptr(dbias), N, H, W, C, Co,
+                  KH, KW, stride, pad, dil, Ho, Wo, int(accumulate), _lib.ptr(ws), ws.numel() if ws is not None else 0,
+                  _lib.stream())
+        return dw
+    dbias.add_(dy.float().sum(dim=(0, 1, 2)))
+    return conv2d_wgrad(dy, x, w_shape, stride, pad, dil, out=out, accumulate=accumulate)
+
+
+def bn_stats(x, s1, s2):
+    """Per-channel sum / sum of squares of NHWC x into (s1, s2) ([NSTAT*C] fp32 each, added)."""
+    C = x.shape[-1]
+    rows = x.numel() // C
+    if _cuda(x):
+        _lib.call('mlc_bn_stats', _lib.ptr(x), _lib.ptr(s1), _lib.ptr(s2), rows, C, _lib.stream())
+        return
+    xf = x.float().reshape(rows, C)
+    s1[:C].add_(xf.sum(0))
+    s2[:C].add_((xf * xf).sum(0))
+
+
+def bn_finalize(s1, s2, rows, gamma, beta, save_mean, save_invstd, scale, shift, run_mean=None, run_var=None,
+                eps=1e-5, momentum=0.1):
+    """Batch statistics -> mean / invstd, the fused affine (scale, shift) and running stats."""
+    C = gamma.numel()
+    ncopy = s1.numel() // C
+    if _cuda(s1):
+        _lib.call('mlc_bn_finalize', _lib.ptr(s1), _lib.ptr(s2), ncopy, _lib.ptr(gamma), _lib.ptr(beta),
+                  _lib.ptr(save_mean), _lib.ptr(save_invstd), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(run_mean),
+                  _lib.ptr(run_var), rows, C, float(eps), float(momentum), _lib.stream())
+        return
+    mean = s1.reshape(ncopy, C).sum(0) / rows
+    var = (s2.reshape(ncopy, C).sum(0) / rows - mean * mean).clamp_min(0)
+    inv = torch.rsqrt(var + eps)
+    save_mean.copy_(mean)
+    save_invstd.copy_(inv)
+    scale.copy_(inv * gamma)
+    shift.copy_(beta - mean * inv * gamma)
+    if run_mean is not None:
+        run_mean.mul_(1 - momentum).add_(momentum * mean)
+        run_var.mul_(1 - momentum).add_(momentum * var * rows / max(rows - 1, 1))
+
+
+def bnact_apply(y, res, scale, shift, act=0, alpha=0.0, res_affine=None):
+    """z = act(y*scale + shift [+ res (*rscale + rshift)]) (NHWC bf16)."""
+    C = y.shape[-1]
+    rows = y.numel() // C
+    if _cuda(y):
+        z = torch.empty_like(y)
+        rs, rh = res_affine if res_affine is not None else (None, None)
+        _lib.call('mlc_bnact_apply', _lib.ptr(y), _lib.ptr(res), _lib.ptr(z), _lib.ptr(scale), _lib.ptr(shift),
+                  _lib.ptr(rs), _lib.ptr(rh), rows, C, int(act), float(alpha), _lib.stream())
+        return z
+    a = y.float() * scale + shift
+    if res is not None:
+        r = res.float()
+        if res_affine is not None:
+            r = r * res_affine[0] + res_affine[1]
+        a = a + r
+    return act_ref(a, act, alpha).to(torch.bfloat16)
+
+
+def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0, dgamma=None, dbeta=None,
+              sums=None, coef=None, want_dres=False):
+    """Backward of z = act(BN(y) [+ res]) with the forward's (scale, shift): returns (dy, dres
+    or None) and writes dgamma / dbeta.  ``sums`` (NSTAT*2*C fp32) must be zero on entry."""
+    C = y.shape[-1]
+    rows = y.numel() // C
+    if _cuda(dz):
+        if sums is None:
+            sums = torch.zeros(NSTAT * 2 * C, device=dz.device, dtype=torch.float32)
+        if coef is None:
+            coef = torch.empty(3 * C, device=dz.device, dtype=torch.float32)
+        zz = z if act in (4, 5) else None        # sigmoid / tanh read their derivative off z
+        _lib.call('mlc_bnact_bwd_reduce', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
+                  _lib.ptr(scale), _lib.ptr(shift), None, None, _lib.ptr(sums), rows, C, int(act), float(alpha),
+                  _lib.stream())
+        _lib.call('mlc_bn_bwd_finalize', _lib.ptr(sums), _lib.ptr(invstd), _lib.ptr(gamma), _lib.ptr(coef),
+                  _lib.ptr(dgamma), _lib.ptr(dbeta), rows, C, _lib.stream())
+        dy = torch.empty_like(y)
+        dres = torch.empty_like(y) if want_dres else None
+        _lib.call('mlc_bnact_bwd_apply', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
+                  _lib.ptr(coef), _lib.ptr(scale), _lib.ptr(shift), None, None, _lib.ptr(dy), _lib.ptr(dres), rows, C,
+                  int(act), float(alpha), _lib.stream())
+        return dy, dres
+    a = y.float().reshape(rows, C) * scale + shift
+    if res is not None:
+        a = a + res.float().reshape(rows, C)
+    d = dz.float().reshape(rows, C)
+    if act:
+        if act in (4, 5):
+            zf = z.float().reshape(rows, C)
+            d = d * (zf * (1 - zf) if act == 4 else 1 - zf * zf)
+        else:
+            d = d * act_grad_ref(a, act, alpha)
+    yc = y.float().reshape(rows, C) - mean
+    S1, S2 = d.sum(0), (d * yc).sum(0)
+    if dgamma is not None:
+        dgamma.copy_(S2 * invstd)
+        dbeta.copy_(S1)
+    k1 = gamma * invstd
+    dyf = k1 * d - k1 * S1 / rows - k1 * invstd * invstd * S2 / rows * yc
+    dres = d.reshape(y.shape).to(torch.bfloat16) if want_dres else None
+    return dyf.reshape(y.shape).to(torch.bfloat16), dres
+
+
+def act_fwd(x, act, alpha=0.0):
+    if _cuda(x) and x.numel() % 8 == 0:
+        y = torch.empty_like(x)
+        _lib.call('mlc_act_fwd', _lib.ptr(x), _lib.ptr(y), x.numel(), int(act), float(alpha), _lib.stream())
+        return y
+    return act_ref(x.float(), act, alpha).to(torch.bfloat16)
+
+
+def act_bwd(dy, x, y, act, alpha=0.0):
+    if _cuda(dy) and dy.numel() % 8 == 0:
+        dx = torch.empty_like(dy)
+        _lib.call('mlc_act_bwd', _lib.ptr(dy), _lib.ptr(x), _lib.ptr(y), _lib.ptr(dx), dy.numel(), int(act),
+                  float(alpha), _lib.stream())
+        return dx
+    if act in (4, 5):
+        yf = y.float()
+        g = yf * (1 - yf) if act == 4 else 1 - yf * yf
+    else:
+        g = act_grad_ref(x.float(), act, alpha)
+    return (dy.float() * g).to(torch.bfloat16)

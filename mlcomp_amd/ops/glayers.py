@@ -1,0 +1,587 @@
+"""Native layers of the generic engine (:mod:`mlcomp_amd.models.native_generic`).
+
+The hand-lowered engines (ResNet, U-Net, BERT, ...) build their layers from
+:mod:`mlcomp_amd.ops.layers` for one architecture each.  The generic engine lowers ANY
+``nn.Module`` graph (torch.fx) onto the kernels, so its layers are written per op, not per
+architecture:
+
+* parameter sets (``ConvParams``, ``BNParams``, ``LinearParams``) - one per source module,
+  slots of the shared :class:`~mlcomp_amd.ops.arena.ParamArena` in kernel layout, loaded
+  from / exported to the torch module; a module used at several call sites shares them;
+* sites (``ConvBNAct``, ``BNAct``, ``LinearAct``, ``MaxPool``, ``GlobalAvgPool``) - one per
+  lowered call site of the fx graph (an ``nn.Module`` the graph calls), holding what a call
+  needs (activation, residual, per-call statistics scratch) and an autograd Function.
+
+Values between sites are ordinary logical-NCHW tensors, so every op the lowering leaves to
+PyTorch (views, adds, concats, dropout, the loss ...) sees what it expects.  A site's
+output is the NHWC kernel result viewed as NCHW (channels_last strides): the next site
+reads it as NHWC without a copy.  Channel counts that are not a multiple of 8 are padded
+inside a site (weights zero-padded in the arena, activations padded on the way in and
+sliced on the way out) - only small stems / toy nets pay for that copy.
+
+Gradients of weights go straight into the grad arena (the step zeroes it once, every wgrad
+accumulates) and a slot is marked ready for the bucketer after the last backward use of
+its weight in the step.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import functional as Fn
+from .layers import NativeContext
+
+
+def ceil8(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
+def to_nhwc(x: torch.Tensor, cp: Optional[int] = None) -> torch.Tensor:
+    """Logical NCHW (any strides / float dtype) -> contiguous NHWC bf16, channels padded to
+    ``cp``.  Free for a channels_last bf16 tensor with ``C == cp``."""
+    y = x.permute(0, 2, 3, 1)
+    if y.dtype != torch.bfloat16:
+        y = y.to(torch.bfloat16)
+    C = y.shape[-1]
+    if cp is not None and cp != C:
+        y = torch.nn.functional.pad(y, (0, cp - C))
+    return y.contiguous()
+
+
+def from_nhwc(y: torch.Tensor, C: int) -> torch.Tensor:
+    """NHWC kernel output -> logical NCHW view (channels_last strides), padding dropped."""
+    if y.shape[-1] != C:
+        y = y[..., :C]
+    return y.permute(0, 3, 1, 2)
+
+
+class _Uses:
+    """Counts the forward calls of a parameter set in a step; backward marks its slots ready
+    only after the last of them (weight sharing across call sites)."""
+
+    def __init__(self):
+        self.pending = 0
+
+    def fwd(self):
+        self.pending += 1
+
+    def bwd_done(self) -> bool:
+        self.pending -= 1
+        return self.pending <= 0
+
+
+# ---------------------------------------------------------------------------- parameters
+class ConvParams:
+    """nn.Conv2d -> kernel-layout slots: dense [Cop, KH, KW, Cip], grouped [Co, KH, KW, Cg],
+    depthwise [KH, KW, Cp] (tap-major); optional bias [Cop]."""
+
+    def __init__(self, ctx: NativeContext, name: str, conv: nn.Conv2d, keep_bias: bool):
+        Co, Cg, KH, KW = conv.weight.shape
+        self.ctx, self.name, self.src = ctx, name, conv
+        self.groups = conv.groups
+        self.Ci, self.Co, self.Cg = Cg * conv.groups, Co, Cg
+        self.k = (KH, KW)
+        self.stride, self.pad, self.dil = conv.stride[0], conv.padding[0], conv.dilation[0]
+        if self.groups == 1:
+            self.kind = 'dense'
+            self.Cip, self.Cop = ceil8(self.Ci), ceil8(Co)
+            self.w = ctx.arena.weight(f'{name}.weight', (self.Cop, KH, KW, self.Cip))
+        elif self.groups == self.Ci and Co == self.Ci:
+            self.kind = 'dw'
+            self.Cip = self.Cop = ceil8(Co)
+            self.w = ctx.arena.weight(f'{name}.weight', (KH, KW, self.Cop))
+        else:
+            self.kind = 'grouped'
+            self.Cip, self.Cop = self.Ci, Co
+            self.w = ctx.arena.weight(f'{name}.weight', (Co, KH, KW, Cg))
+        self.b = ctx.arena.vector(f'{name}.bias', (self.Cop,)) if (keep_bias and conv.bias is not None) else None
+        self.uses = _Uses()
+
+    def load_from_torch(self):
+        w = self.src.weight.detach().float()
+        dev = self.ctx.device
+        if self.kind == 'dense':
+            w = w.permute(0, 2, 3, 1)
+            w = torch.nn.functional.pad(w, (0, self.Cip - self.Ci, 0, 0, 0, 0, 0, self.Cop - self.Co))
+        elif self.kind == 'dw':
+            w = torch.nn.functional.pad(w[:, 0].permute(1, 2, 0), (0, self.Cop - self.Co))
+        else:
+            w = w.permute(0, 2, 3, 1)
+        self.w.master.copy_(w.to(dev))
+        if self.b is not None:
+            self.b.master.zero_()
+            self.b.master[:self.Co].copy_(self.src.bias.detach().float().to(dev))
+
+    def export_to_torch(self):
+        m = self.w.master.detach()
+        if self.kind == 'dense':
+            w = m[:self.Co, :, :, :self.Ci].permute(0, 3, 1, 2)
+        elif self.kind == 'dw':
+            w = m[..., :self.Co].permute(2, 0, 1)[:, None]
+        else:
+            w = m.permute(0, 3, 1, 2)
+        self.src.weight.data.copy_(w.to(self.src.weight.device, self.src.weight.dtype))
+        if self.b is not None:
+            self.src.bias.data.copy_(self.b.master[:self.Co].to(self.src.bias.device, self.src.bias.dtype))
+
+    def out_hw(self, H, W):
+        return Fn.conv_out_hw(H, W, self.k[0], self.k[1], self.stride, self.pad, self.dil)
+
+    # ---- the three GEMMs by kind
+    def fwd(self, x, stats=None, act=0):
+        """x: NHWC bf16 with Cip channels -> y [N, Ho, Wo, Cop] (bias and a ReLU act fused for
+        dense convs without BN: ``act`` 3)."""
+        wb = self.w.bf16
+        if self.kind == 'dense':
+            if self.b is not None or act:
+                assert stats is None
+                return Fn.conv2d_fwd_ex(x, wb, self.b.master if self.b is not None else None, act, self.stride,
+                                        self.pad, self.dil)
+            return Fn.conv2d_fwd(x, wb, self.stride, self.pad, self.dil, stats=stats)
+        if self.kind == 'dw':
+            return Fn.dwconv_fwd(x, wb, self.stride, self.pad, self.dil, stats=stats)
+        return Fn.gconv_fwd(x, wb, self.groups, self.stride, self.pad, self.dil, stats=stats)
+
+    def dgrad(self, dy, x_shape):
+        wb = self.w.bf16
+        if self.kind == 'dense':
+            return Fn.conv2d_dgrad(dy, wb, x_shape, self.stride, self.pad, self.dil)
+        if self.kind == 'dw':
+            return Fn.dwconv_dgrad(dy, wb, x_shape, self.stride, self.pad, self.dil)
+        return Fn.gconv_dgrad(dy, wb, x_shape, self.groups, self.stride, self.pad, self.dil)
+
+    def wgrad(self, dy, x):
+        acc = self.ctx.grad_prezeroed
+        if self.kind == 'dense':
+            if self.b is not None:
+                Fn.conv2d_wgrad_bias(dy, x, self.w.shape, self.b.grad, self.stride, self.pad, self.dil,
+                                     out=self.w.grad, accumulate=acc)
+            else:
+                Fn.conv2d_wgrad(dy, x, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad,
+                                accumulate=acc)
+        elif self.kind == 'dw':
+            Fn.dwconv_wgrad(dy, x, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad, accumulate=acc)
+        else:
+            Fn.gconv_wgrad(dy, x, self.w.shape, self.groups, self.stride, self.pad, self.dil, out=self.w.grad,
+                           accumulate=acc)
+
+    def mark_ready(self):
+        self.ctx.arena.mark_ready(self.w)
+        if self.b is not None:
+            self.ctx.arena.mark_ready(self.b)
+
+
+class BNParams:
+    """nn.BatchNorm2d / BatchNorm1d -> gamma / beta slots [Cp] + running statistics."""
+
+    def __init__(self, ctx: NativeContext, name: str, bn: nn.modules.batchnorm._BatchNorm):
+        self.ctx, self.name, self.src = ctx, name, bn
+        self.C = bn.num_features
+        self.Cp = ceil8(self.C)
+        self.eps = bn.eps
+        self.momentum = bn.momentum
+        self.affine = bn.affine
+        self.track = bn.track_running_stats
+        self.gamma = ctx.arena.vector(f'{name}.weight', (self.Cp,))
+        self.beta = ctx.arena.vector(f'{name}.bias', (self.Cp,))
+        self.run_mean = self.run_var = None
+        self.uses = _Uses()
+
+    def load_from_torch(self):
+        dev = self.ctx.device
+        bn = self.src
+        self.gamma.master.zero_()
+        self.beta.master.zero_()
+        self.gamma.master[:self.C].copy_(bn.weight.detach().float().to(dev) if self.affine else torch.ones(self.C))
+        self.beta.master[:self.C].copy_(bn.bias.detach().float().to(dev) if self.affine else torch.zeros(self.C))
+        if self.track:
+            self.run_mean = torch.zeros(self.Cp, device=dev)
+            self.run_var = torch.ones(self.Cp, device=dev)
+            self.run_mean[:self.C].copy_(bn.running_mean.detach().float())
+            self.run_var[:self.C].copy_(bn.running_var.detach().float())
+            cb = getattr(self, 'conv_bias', None)
+            if cb is not None:
+                # the fused conv drops its bias (a batch-statistics BN cancels it), so the
+                # running mean is kept bias-free and converted here and on export
+                self.run_mean[:self.C].sub_(cb.detach().float().to(dev))
+
+    def export_to_torch(self):
+        bn = self.src
+        if self.affine:
+            bn.weight.data.copy_(self.gamma.master[:self.C].to(bn.weight.device, bn.weight.dtype))
+            bn.bias.data.copy_(self.beta.master[:self.C].to(bn.bias.device, bn.bias.dtype))
+        if self.track:
+            rm = self.run_mean[:self.C]
+            cb = getattr(self, 'conv_bias', None)
+            if cb is not None:
+                rm = rm + cb.detach().float().to(rm.device)
+            bn.running_mean.copy_(rm.to(bn.running_mean.device))
+            bn.running_var.copy_(self.run_var[:self.C].to(bn.running_var.device))
+            if bn.num_batches_tracked is not None:
+                bn.num_batches_tracked.add_(int(getattr(self, 'batches', 0)))
+            self.batches = 0
+
+    def batch_stats(self) -> bool:
+        return self.ctx.training or not self.track
+
+    def finalize(self, s1, s2, rows):
+        """(scale, shift, mean, invstd) of this call - batch statistics (training) or the
+        running ones (inference)."""
+        dev = s1.device if s1 is not None else self.gamma.master.device
+        st = torch.empty(4, self.Cp, device=dev, dtype=torch.float32)
+        scale, shift, mean, inv = st[0], st[1], st[2], st[3]
+        if self.batch_stats():
+            upd = self.ctx.training and self.track
+            mom = self.momentum if self.momentum is not None else 0.1
+            Fn.bn_finalize(s1, s2, rows, self.gamma.master, self.beta.master, mean, inv, scale, shift,
+                           self.run_mean if upd else None, self.run_var if upd else None, self.eps, mom)
+            if upd:
+                self.batches = getattr(self, 'batches', 0) + 1
+        else:
+            torch.rsqrt(self.run_var + self.eps, out=inv)
+            torch.mul(inv, self.gamma.master, out=scale)
+            torch.sub(self.beta.master, self.run_mean * scale, out=shift)
+            mean.copy_(self.run_mean)
+        return scale, shift, mean, inv
+
+    def mark_ready(self):
+        self.ctx.arena.mark_ready(self.gamma)
+        self.ctx.arena.mark_ready(self.beta)
+
+
+class LinearParams:
+    """nn.Linear -> weight [Op, Ip] (decay arena, bf16 mirror) and bias [Op]."""
+
+    def __init__(self, ctx: NativeContext, name: str, lin: nn.Linear):
+        self.ctx, self.name, self.src = ctx, name, lin
+        self.O, self.I = lin.weight.shape
+        self.Op, self.Ip = ceil8(self.O), ceil8(self.I)
+        self.w = ctx.arena.weight(f'{name}.weight', (self.Op, self.Ip))
+        self.b = ctx.arena.vector(f'{name}.bias', (self.Op,)) if lin.bias is not None else None
+        self.uses = _Uses()
+
+    def load_from_torch(self):
+        dev = self.ctx.device
+        self.w.master.zero_()
+        self.w.master[:self.O, :self.I].copy_(self.src.weight.detach().float().to(dev))
+        if self.b is not None:
+            self.b.master.zero_()
+            self.b.master[:self.O].copy_(self.src.bias.detach().float().to(dev))
+
+    def export_to_torch(self):
+        lin = self.src
+        lin.weight.data.copy_(self.w.master[:self.O, :self.I].to(lin.weight.device, lin.weight.dtype))
+        if self.b is not None:
+            lin.bias.data.copy_(self.b.master[:self.O].to(lin.bias.device, lin.bias.dtype))
+
+    def mark_ready(self):
+        self.ctx.arena.mark_ready(self.w)
+        if self.b is not None:
+            self.ctx.arena.mark_ready(self.b)
+
+
+# ---------------------------------------------------------------------------- sites
+class Site(nn.Module):
+    """A lowered call site: forward() runs the site's autograd Function.  Holds no
+    nn.Parameters (the arena owns the weights)."""
+
+    def __init__(self, ctx: NativeContext):
+        super().__init__()
+        object.__setattr__(self, 'ctx', ctx)   # not a submodule / not in state_dict
+
+    def params(self):
+        """The parameter sets this site reads (their use counts gate mark_ready)."""
+        return [p for p in (getattr(self, 'conv', None), getattr(self, 'bn', None), getattr(self, 'lin', None))
+                if p is not None]
+
+
+class _SiteFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, site, *inputs):
+        for p in site.params():
+            p.uses.fwd()
+        out, saved, keep = site.fwd(*inputs)
+        ctx.site = site
+        ctx.keep = keep
+        ctx.n_in = len(inputs)
+        ctx.save_for_backward(*saved)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        grads = ctx.site.bwd(dout, ctx.saved_tensors, ctx.keep, [ctx.needs_input_grad[2 + i] for i in range(ctx.n_in)])
+        return (None, None) + tuple(grads)
+
+
+def _run(site, *inputs):
+    anchor = site.ctx.anchor
+    if torch.is_grad_enabled() and site.ctx.training:
+        return _SiteFn.apply(anchor, site, *inputs)
+    with torch.no_grad():
+        return site.fwd(*inputs)[0]
+
+
+class ConvBNAct(Site):
+    """conv [-> BN (batch stats in training)] [+ residual] [-> activation].  Without BN a
+    dense conv fuses its bias (and a ReLU) into the GEMM epilogue; grouped / depthwise convs
+    without BN add the bias with a torch op (rare)."""
+
+    def __init__(self, ctx, conv: ConvParams, bn: Optional[BNParams], act: int = 0, alpha: float = 0.0,
+                 residual: bool = False):
+        super().__init__(ctx)
+        object.__setattr__(self, 'conv', conv)
+        object.__setattr__(self, 'bn', bn)
+        self.act, self.alpha, self.residual = act, alpha, residual
+        if bn is not None:
+            assert bn.Cp == conv.Cop, (bn.C, conv.Co)
+        # conv epilogue fusion for BN-less dense convs: bias and ReLU
+        self.epi_act = 3 if (bn is None and conv.kind == 'dense' and act == 1 and not residual) else 0
+        self.k_st = ctx.ws.request(f'{conv.name}@{id(self)}.st', 2 * Fn.NSTAT * conv.Cop) if bn is not None else None
+        self.k_bw = ctx.ws.request(f'{conv.name}@{id(self)}.bw', 2 * Fn.NSTAT * conv.Cop) if bn is not None else None
+
+    def forward(self, x, res=None):
+        return _run(self, x, res) if res is not None else _run(self, x)
+
+    def fwd(self, x, res=None):
+        c, bn = self.conv, self.bn
+        xn = to_nhwc(x, c.Cip)
+        rn = to_nhwc(res, c.Cop) if res is not None else None
+        if bn is not None:
+            stats = None
+            if bn.batch_stats():
+                st = self.ctx.ws[self.k_st]
+                n = Fn.NSTAT * c.Cop
+                stats = (st[:n], st[n:])
+            y = c.fwd(xn, stats)
+            rows = y.numel() // y.shape[-1]
+            scale, shift, mean, inv = bn.finalize(stats[0] if stats else None, stats[1] if stats else None, rows)
+            z = Fn.bnact_apply(y, rn, scale, shift, self.act, self.alpha)
+            saved = [xn, y, z, rn if rn is not None else y, scale, shift, mean, inv]
+            return from_nhwc(z, c.Co), saved, rn is not None
+        y = c.fwd(xn, None, self.epi_act)        # dense: bias (+ ReLU) in the GEMM epilogue
+        if c.b is not None and c.kind != 'dense':
+            y = (y.float() + c.b.master).to(torch.bfloat16)
+        a = y if rn is None else (y.float() + rn.float()).to(torch.bfloat16)
+        z = Fn.act_fwd(a, self.act, self.alpha) if (self.act and not self.epi_act) else a
+        # saved: input, pre-activation (the ReLU output when the epilogue applied it), output
+        return from_nhwc(z, c.Co), [xn, a, z], rn is not None
+
+    def bwd(self, dout, saved, has_res, needs):
+        c, bn = self.conv, self.bn
+        dz = to_nhwc(dout, c.Cop)
+        dres = None
+        if bn is not None:
+            xn, y, z, rn, scale, shift, mean, inv = saved
+            ws = self.ctx.ws
+            dy, dres = Fn.bnact_bwd(dz, z, y, rn if has_res else None, mean, scale, shift, inv, bn.gamma.master,
+                                    self.act, self.alpha, dgamma=_acc_view(bn.gamma), dbeta=_acc_view(bn.beta),
+                                    sums=ws[self.k_bw], want_dres=has_res)
+            _acc_commit(bn.gamma)
+            _acc_commit(bn.beta)
+            if bn.uses.bwd_done():
+                bn.mark_ready()
+        else:
+            xn, a, z = saved
+            if self.epi_act:                     # ReLU applied by the GEMM: mask from z
+                dy = (dz.float() * (z.float() > 0)).to(torch.bfloat16)
+            elif self.act:
+                dy = Fn.act_bwd(dz, a, z, self.act, self.alpha)
+            else:
+                dy = dz
+            if has_res:
+                dres = dy
+            if c.b is not None and c.kind != 'dense':
+                c.b.grad.add_(dy.float().sum(dim=(0, 1, 2)))
+        c.wgrad(dy, xn)
+        dx = c.dgrad(dy, xn.shape) if needs[0] else None
+        if c.uses.bwd_done():
+            c.mark_ready()
+        out = [from_nhwc(dx, c.Ci) if dx is not None else None]
+        if has_res:
+            out.append(from_nhwc(dres, c.Co) if needs[1] else None)
+        return out
+
+
+def _acc_view(slot):
+    """BN dgamma / dbeta targets: the kernels overwrite, so a shared (multi-site) BN writes a
+    scratch that _acc_commit adds into the grad arena."""
+    buf = getattr(slot, '_scratch', None)
+    if buf is None or buf.device != slot.grad.device:
+        buf = torch.empty_like(slot.grad)
+        slot._scratch = buf
+    return buf
+
+
+def _acc_commit(slot):
+    slot.grad.add_(slot._scratch)
+
+
+class BNAct(Site):
+    """A BatchNorm no conv epilogue feeds (statistics pass of its own) [+ residual] [+ act]."""
+
+    def __init__(self, ctx, bn: BNParams, act: int = 0, alpha: float = 0.0, residual: bool = False):
+        super().__init__(ctx)
+        object.__setattr__(self, 'bn', bn)
+        self.act, self.alpha, self.residual = act, alpha, residual
+        self.k_st = ctx.ws.request(f'{bn.name}@{id(self)}.st', 2 * Fn.NSTAT * bn.Cp)
+        self.k_bw = ctx.ws.request(f'{bn.name}@{id(self)}.bw', 2 * Fn.NSTAT * bn.Cp)
+
+    def forward(self, x, res=None):
+        return _run(self, x, res) if res is not None else _run(self, x)
+
+    def _to(self, x):
+        if x.dim() == 2:              # BatchNorm1d over [N, C] / [N, C, L]
+            x = x[:, :, None, None]
+        elif x.dim() == 3:
+            x = x[:, :, :, None]
+        return to_nhwc(x, self.bn.Cp)
+
+    def _from(self, z, like):
+        out = from_nhwc(z, self.bn.C)
+        if like.dim() == 2:
+            return out[:, :, 0, 0]
+        return out[..., 0] if like.dim() == 3 else out
+
+    def fwd(self, x, res=None):
+        bn = self.bn
+        yn = self._to(x)
+        rn = self._to(res) if res is not None else None
+        rows = yn.numel() // yn.shape[-1]
+        stats = None
+        if bn.batch_stats():
+            st = self.ctx.ws[self.k_st]
+            n = Fn.NSTAT * bn.Cp
+            stats = (st[:n], st[n:])
+            Fn.bn_stats(yn, *stats)
+        scale, shift, mean, inv = bn.finalize(stats[0] if stats else None, stats[1] if stats else None, rows)
+        z = Fn.bnact_apply(yn, rn, scale, shift, self.act, self.alpha)
+        self._dim = x.dim()
+        return self._from(z, x), [yn, z, rn if rn is not None else yn, scale, shift, mean, inv], rn is not None
+
+    def bwd(self, dout, saved, has_res, needs):
+        bn = self.bn
+        yn, z, rn, scale, shift, mean, inv = saved
+        dz = self._to(dout)
+        dy, dres = Fn.bnact_bwd(dz, z, yn, rn if has_res else None, mean, scale, shift, inv, bn.gamma.master,
+                                self.act, self.alpha, dgamma=_acc_view(bn.gamma), dbeta=_acc_view(bn.beta),
+                                sums=self.ctx.ws[self.k_bw], want_dres=has_res)
+        _acc_commit(bn.gamma)
+        _acc_commit(bn.beta)
+        if bn.uses.bwd_done():
+            bn.mark_ready()
+        like = dout
+        out = [self._from(dy, like) if needs[0] else None]
+        if has_res:
+            out.append(self._from(dres, like) if needs[1] else None)
+        return out
+
+
+class LinearAct(Site):
+    """x [..., I] -> act(x W^T + b) on the dense GEMM (bias / ReLU in the epilogue)."""
+
+    def __init__(self, ctx, lin: LinearParams, act: int = 0):
+        super().__init__(ctx)
+        object.__setattr__(self, 'lin', lin)
+        self.act = act            # 0 or 3 (ReLU; the epilogue's code)
+
+    def forward(self, x):
+        return _run(self, x)
+
+    def fwd(self, x):
+        p = self.lin
+        lead = x.shape[:-1]
+        x2 = x.reshape(-1, x.shape[-1])
+        if x2.dtype != torch.bfloat16:
+            x2 = x2.to(torch.bfloat16)
+        if p.Ip != p.I:
+            x2 = torch.nn.functional.pad(x2, (0, p.Ip - p.I))
+        x2 = x2.contiguous()
+        B = x2.shape[0]
+        if x2.is_cuda:
+            from . import _lib
+            y = torch.empty(B, p.Op, device=x2.device, dtype=torch.bfloat16)
+            _lib.call('mlc_gemm_bf16_ex', _lib.ptr(x2), _lib.ptr(p.w.bf16), _lib.ptr(y), B, p.Op, p.Ip, p.Ip, p.Ip,
+                      p.Op, 0, 1, _lib.ptr(p.b.master if p.b is not None else None), int(self.act), None, None, None,
+                      None, 0, _lib.stream())
+        else:
+            yf = x2.float() @ p.w.bf16.float().t()
+            if p.b is not None:
+                yf = yf + p.b.master
+            if self.act == 3:
+                yf = yf.clamp_min(0)
+            y = yf.to(torch.bfloat16)
+        out = y[:, :p.O] if p.Op != p.O else y
+        return out.reshape(*lead, p.O), [x2, y], False
+
+    def bwd(self, dout, saved, has_res, needs):
+        p = self.lin
+        x2, y = saved
+        d = dout.reshape(-1, p.O)
+        if d.dtype != torch.bfloat16:
+            d = d.to(torch.bfloat16)
+        if p.Op != p.O:
+            d = torch.nn.functional.pad(d, (0, p.Op - p.O))
+        if self.act == 3:
+            d = (d.float() * (y.float() > 0)).to(torch.bfloat16)
+        d = d.contiguous()
+        if p.b is not None:
+            Fn.linear_wgrad_bias(d, x2, p.w.grad, p.b.grad)
+        else:
+            Fn.linear_wgrad(d, x2, out=p.w.grad, accumulate=True)
+        dx = Fn.linear_dgrad(d, p.w.bf16) if needs[0] else None
+        if p.uses.bwd_done():
+            p.mark_ready()
+        if dx is not None:
+            if p.Ip != p.I:
+                dx = dx[:, :p.I]
+            dx = dx.reshape(*dout.shape[:-1], p.I)
+        return [dx]
+
+
+class MaxPool(Site):
+    def __init__(self, ctx, k, s, p, ceil_mode=False):
+        super().__init__(ctx)
+        self.k, self.s, self.p, self.ceil = k, s, p, ceil_mode
+
+    def forward(self, x):
+        return _run(self, x)
+
+    def fwd(self, x):
+        C = x.shape[1]
+        xn = to_nhwc(x, ceil8(C))
+        y, idx = Fn.maxpool_fwd(xn, self.k, self.s, self.p, self.ceil)
+        return from_nhwc(y, C), [idx], tuple(xn.shape)
+
+    def bwd(self, dout, saved, xshape, needs):
+        (idx,) = saved
+        C = dout.shape[1]
+        dx = Fn.maxpool_bwd(to_nhwc(dout, xshape[-1]), idx, xshape, self.k, self.s, self.p)
+        return [from_nhwc(dx, C)]
+
+
+class GlobalAvgPool(Site):
+    """adaptive_avg_pool2d(x, 1): [N, C, H, W] -> [N, C, 1, 1]."""
+
+    def forward(self, x):
+        return _run(self, x)
+
+    def fwd(self, x):
+        C = x.shape[1]
+        xn = to_nhwc(x, ceil8(C))
+        y = Fn.avgpool_fwd(xn)              # [N, Cp]
+        return y[:, :C, None, None], [], tuple(xn.shape)
+
+    def bwd(self, dout, saved, xshape, needs):
+        N, H, W, Cp = xshape
+        C = dout.shape[1]
+        d = dout.reshape(N, C).to(torch.bfloat16)
+        if Cp != C:
+            d = torch.nn.functional.pad(d, (0, Cp - C))
+        dx = Fn.avgpool_bwd(d.contiguous(), xshape)
+        return [from_nhwc(dx, C)]
+
+
+__all__ = ['ConvParams', 'BNParams', 'LinearParams', 'ConvBNAct', 'BNAct', 'LinearAct', 'MaxPool',
+           'GlobalAvgPool', 'to_nhwc', 'from_nhwc', 'ceil8']

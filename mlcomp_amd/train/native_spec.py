@@ -31,7 +31,7 @@ _OPT_KEYS = {'SGD': {'lr', 'momentum', 'weight_decay', 'nesterov', 'dampening', 
                        'differentiable', 'fused'}}
 # the optimizers each native engine has fused kernels for
 _ENGINE_OPTS = {'resnet': ('SGD', 'Adam', 'AdamW'), 'unet': ('SGD', 'Adam', 'AdamW'),
-                'bert': ('SGD', 'Adam', 'AdamW')}
+                'bert': ('SGD', 'Adam', 'AdamW'), 'generic': ('SGD', 'Adam', 'AdamW')}
 # a criterion's own flags that only select an implementation, never the objective
 _NEUTRAL = {'reduction': 'mean'}
 
@@ -65,6 +65,8 @@ def _optimizer(spec: dict, kind: str, default_lr: float) -> Dict:
 
 
 def _criterion(spec: dict, kind: str) -> Dict:
+    if kind == 'generic':
+        return {}      # the generic engine runs the stage's own criterion (torch ops on fp32 logits)
     p = dict(spec)
     name = p.pop('criterion', 'CrossEntropyLoss')
     for k, v in _NEUTRAL.items():
@@ -121,7 +123,7 @@ def _callbacks(spec: dict) -> None:
                                     'not implemented by the native engines')
 
 
-_DEFAULT_LR = {'resnet': 0.1, 'unet': 3e-4, 'bert': 2e-5}
+_DEFAULT_LR = {'resnet': 0.1, 'unet': 3e-4, 'bert': 2e-5, 'generic': 1e-3}
 
 
 def native_plan(experiment, stage: str, kind: str) -> Dict:

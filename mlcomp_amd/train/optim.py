@@ -23,7 +23,8 @@ class _ArenaStateMixin:
         """views of one contiguous slice of an arena: (master, grad, mirror, n, ndecay, nbf)"""
         n = end - start
         mirror = a.mirror[start:end] if a.mirror is not None else None
-        return a.master[start:end], a.grad[start:end], mirror, n, n if a.decay else 0, n if mirror is not None else 0
+        decay = a.decay or getattr(self, 'decay_all', False)
+        return a.master[start:end], a.grad[start:end], mirror, n, n if decay else 0, n if mirror is not None else 0
 
     """Checkpointable optimizer state: the step counter and every arena state buffer
     (momentum / Adam moments) as CPU tensors, keyed ``<arena>.<buffer>``."""
@@ -43,8 +44,11 @@ class _ArenaStateMixin:
 
 class FusedSGD(_ArenaStateMixin):
     def __init__(self, arena: ParamArena, lr=0.1, momentum=0.9, weight_decay=0.0,
-                 nesterov=False, dampening=0.0, grad_scale=1.0):
+                 nesterov=False, dampening=0.0, grad_scale=1.0, decay_all=False):
         self.arena = arena
+        # decay_all: weight decay on every parameter (torch.optim's semantics, the generic
+        # engine); otherwise only the decay arena (matmul weights; the hand-lowered engines)
+        self.decay_all = decay_all
         self.momentum = momentum
         self.wd = weight_decay
         self.nesterov = nesterov
@@ -78,7 +82,7 @@ class FusedSGD(_ArenaStateMixin):
                     self.step_slice(a, s, e)
                 continue
             Fn.sgd_step(a.master, a.grad, a.state['momentum'], a.mirror, self.hyper,
-                        a.numel if a.decay else 0, a.numel if a.mirror is not None else 0,
+                        a.numel if (a.decay or self.decay_all) else 0, a.numel if a.mirror is not None else 0,
                         self.momentum, self.dampening, self.wd, self.nesterov, False)
 
     def step_slice(self, a, start, end):
@@ -90,8 +94,9 @@ class FusedSGD(_ArenaStateMixin):
 
 class FusedAdam(_ArenaStateMixin):
     def __init__(self, arena: ParamArena, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
-                 weight_decay=0.0, decoupled=True, grad_scale=1.0):
+                 weight_decay=0.0, decoupled=True, grad_scale=1.0, decay_all=False):
         self.arena = arena
+        self.decay_all = decay_all
         self.b1, self.b2 = betas
         self.eps = eps
         self.wd = weight_decay
@@ -127,7 +132,7 @@ class FusedAdam(_ArenaStateMixin):
                     self.step_slice(a, s, e)
                 continue
             Fn.adam_step(a.master, a.grad, a.state['exp_avg'], a.state['exp_avg_sq'], a.mirror,
-                         self.hyper, a.numel if a.decay else 0,
+                         self.hyper, a.numel if (a.decay or self.decay_all) else 0,
                          a.numel if a.mirror is not None else 0, self.b1, self.b2, self.eps,
                          self.wd, self.decoupled)
 

@@ -8,7 +8,10 @@ Two engines behind one loop:
   criterion, backward, ``torch.optim`` step; DDP through
   ``torch.nn.parallel.DistributedDataParallel`` (backend "nccl" == RCCL on ROCm) when
   ``world_size > 1``.
-* ``native`` - ResNet-family classifiers (``groups == 1``), BERT and ResNet-encoder
+* ``native`` - any model the fx lowering accepts (:mod:`mlcomp_amd.models.native_generic`:
+  the reference's example nets, the classification zoo incl. grouped / depthwise convs,
+  segmentation models) on the generic engine, and the hand-lowered engines for
+  ResNet-family classifiers (``groups == 1``), BERT and ResNet-encoder
   U-Nets (:class:`~mlcomp_amd.train.native_seg_step.NativeSegmentationStep`) on a GPU: the whole step
   runs through :class:`~mlcomp_amd.train.native_step.NativeClassifierStep` (hand-written
   HIP kernels, flat arenas, fused optimizer, RCCL bucketer, HIP-graph replay).  Loss and
@@ -140,7 +143,14 @@ def _native_kind(model: nn.Module, device: torch.device) -> Optional[str]:
                 and all(isinstance(b.att_in, nn.Identity) and isinstance(b.convs[0][1], nn.BatchNorm2d)
                         for b in dec.blocks):
             return 'unet'
-    return None
+    # everything else the fx lowering accepts runs on the generic native engine
+    from mlcomp_amd.models.native_generic import lower_or_none
+    return 'generic' if lower_or_none(model) is None else None
+
+
+def _generic_reason(model: nn.Module) -> Optional[str]:
+    from mlcomp_amd.models.native_generic import lower_or_none
+    return lower_or_none(model)
 
 
 def _native_capable(model: nn.Module, device: torch.device) -> bool:
@@ -193,7 +203,7 @@ class Runner:
         elif self.device.type != 'cuda':
             reason = 'no HIP device: the native engines run on MI355X GPUs'
         elif kind is None:
-            reason = f'{type(self.model).__name__} has no native lowering'
+            reason = f'{type(self.model).__name__} has no native lowering: {_generic_reason(self.model)}'
         if reason is None:
             from .native_spec import NativeUnsupported, native_plan
             try:
@@ -234,6 +244,13 @@ class Runner:
     def _build_native(self, stage, batch):
         plan = dict(self._native_plan or {})
         use_graph = self.experiment.args.get('graph', True)
+        if self.native_kind == 'generic':
+            from .native_generic_step import NativeGenericStep
+            self.native_step = NativeGenericStep(
+                torch_model=self.model, x=batch['features'], y=batch['targets'], device=self.device,
+                world_size=self.world_size, use_graph=use_graph, criterion=self.criterion, **plan)
+            self._apply_native_opt_state()
+            return
         if self.native_kind == 'bert':
             from .native_bert_step import NativeBertStep
             ids = batch['input_ids']
@@ -294,7 +311,7 @@ class Runner:
             kw = {k: v for k, v in dp.items() if k not in ('dataset', 'batch_size', 'on_device', 'steps', 'seed')}
             steps = int(dp.get('steps', max(1, int(dp.get('num_samples', bs)) // (bs * self.world_size))))
             out = OrderedDict(train=DeviceSyntheticLoader(bs, steps, device=self.device,
-                                                          nhwc_pad=STEM_CIN if self.state.native else None,
+                                                          nhwc_pad=STEM_CIN if self.native_kind == 'resnet' else None,
                                                           seed=self.rank, **kw))
             return out
         if dp.get('dataset') == 'records':
@@ -437,6 +454,19 @@ class Runner:
                     self._build_native(st.stage, batch)
                     self.sync_lr()
                 ns = self.native_step
+                if self.native_kind == 'generic':
+                    # any model / criterion: the stage's metric callbacks read the step's output
+                    ns.load_batch(batch['features'], batch['targets'])
+                    ns()
+                    st.batch_size = ns.batch
+                    st.input = {'features': ns.x, 'targets': ns.y}
+                    st.output = {'logits': ns.out}
+                    st.loss = ns._loss
+                    self._fire('on_batch_end')
+                    for k, v in st.batch_metrics.items():
+                        sums[k] += v * st.batch_size
+                    count += st.batch_size
+                    continue
                 if self.native_kind == 'unet':
                     ns.load_batch(batch['features'], batch['targets'])
                     ns()
@@ -493,6 +523,14 @@ class Runner:
             self.sync_lr()
         ns = self.native_step
         y = batch['targets'].to(self.device)
+        if self.native_kind == 'generic':
+            x = batch['features'].to(self.device)
+            out = ns.predict(x)
+            st.input = {'features': x, 'targets': y}
+            st.output = {'logits': out.float()}
+            st.batch_size = x.shape[0]
+            st.loss = self._eval_loss(st.output['logits'], y)
+            return
         if self.native_kind == 'bert':
             logits = ns.predict(batch['input_ids'], batch.get('token_type_ids'), batch.get('attention_mask'))
             st.input = {'input_ids': batch['input_ids'], 'targets': y}

@@ -55,6 +55,11 @@ def _bn(step):
 
 def _worker(rank, world, port, kind, out):
     import torch.distributed as dist
+    # one intra-op thread: oneDNN's multi-threaded weight-gradient reductions schedule work
+    # dynamically, so their summation order (and the last bits of every gradient) depends on
+    # timing - under a loaded host (pytest -n 8) the rank results drifted 4e-4 from the
+    # reference.  Single-threaded, both sides sum in one fixed order.
+    torch.set_num_threads(1)
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group('gloo', rank=rank, world_size=world)
     step = _make(kind, world)
@@ -67,6 +72,15 @@ def _worker(rank, world, port, kind, out):
 @pytest.mark.parametrize('kind,world', [(k, w) for k in ('resnet', 'unet', 'bert') for w in (2, 4)]
                          + [('linknet', 2), ('fpn', 2), ('pspnet', 2)])
 def test_dp_step_equals_single_process_on_the_shards(tmp_path, kind, world, monkeypatch):
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)      # the reference runs single-threaded too (see _worker)
+    try:
+        _check_dp(tmp_path, kind, world, monkeypatch)
+    finally:
+        torch.set_num_threads(threads)
+
+
+def _check_dp(tmp_path, kind, world, monkeypatch):
     mp.spawn(_worker, args=(world, _free_port(), kind, str(tmp_path)), nprocs=world)
     got = [torch.load(tmp_path / f'{kind}{r}.pt', weights_only=True) for r in range(world)]
     # single process, one shard at a time (RANK selects the shard's synthetic data and

@@ -1,0 +1,329 @@
+"""The generic native engine on CPU (the ops' reference paths, same bf16 rounding points as
+the kernels): fx lowering coverage of the reference's example nets and the zoo, per-site
+numerics against fp32 autograd, the step (fused optimizer with torch.optim semantics,
+gradient arena), gloo data parallelism, and the runner's engine choice.
+
+Reference models: `examples/digit-recognizer/model.py:8-25` (LeNet), `examples/cifar_simple/
+model.py:8-26` (CIFAR Net), `mlcomp/contrib/segmentation/encoders/__init__.py:12-18`
+(resnext / senet / dpn / densenet encoders)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+import torch.nn as nn
+import torch.nn.functional as F
+
+from mlcomp_amd.models import build_model
+from mlcomp_amd.models.native_generic import GenericNet, lower_or_none
+from mlcomp_amd.ops import functional as Fn
+
+
+class RefCifarNet(nn.Module):
+    """The reference's cifar_simple ``Net`` (conv5 6 / 16, pools, three Linear layers)."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 6, 5)
+        self.pool = nn.MaxPool2d(2, 2)
+        self.conv2 = nn.Conv2d(6, 16, 5)
+        self.fc1 = nn.Linear(16 * 5 * 5, 120)
+        self.fc2 = nn.Linear(120, 84)
+        self.fc3 = nn.Linear(84, 10)
+
+    def forward(self, x):
+        x = self.pool(F.relu(self.conv1(x)))
+        x = self.pool(F.relu(self.conv2(x)))
+        x = x.view(-1, 16 * 5 * 5)
+        x = F.relu(self.fc1(x))
+        x = F.relu(self.fc2(x))
+        return self.fc3(x)
+
+
+def _cos(a, b):
+    a, b = a.flatten().float(), b.flatten().float()
+    return (a @ b / (a.norm() * b.norm() + 1e-12)).item()
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _torch_grad(p, ref):
+    """The reference module's gradient of a parameter set, in the set's layout."""
+    m = dict(ref.named_modules())[p.name]
+    if hasattr(p, 'kind'):
+        g = m.weight.grad
+        if p.kind == 'dense':
+            return F.pad(g.permute(0, 2, 3, 1), (0, p.Cip - p.Ci, 0, 0, 0, 0, 0, p.Cop - p.Co))
+        if p.kind == 'dw':
+            return F.pad(g[:, 0].permute(1, 2, 0), (0, p.Cop - p.Co))
+        return g.permute(0, 2, 3, 1)
+    if hasattr(p, 'O'):
+        return F.pad(m.weight.grad, (0, p.Ip - p.I, 0, p.Op - p.O))
+    return F.pad(m.weight.grad, (0, p.Cp - p.C))
+
+
+def _pair(make, seed=0):
+    torch.manual_seed(seed)
+    m = make()
+    ref = make()
+    ref.load_state_dict(m.state_dict())
+    for mm in (m, ref):
+        for d in mm.modules():
+            if isinstance(d, nn.Dropout):
+                d.p = 0.0
+            if hasattr(d, 'drop_path'):
+                d.drop_path = 0.0
+    return m, ref
+
+
+@pytest.mark.parametrize('name', ['LeNet', 'resnext50_32x4d', 'se_resnext50_32x4d', 'efficientnet-b0',
+                                  'mobilenet_v2', 'densenet121', 'dpn68', 'xception', 'vgg16', 'resnet18'])
+def test_zoo_lowers_completely(name):
+    """Every conv / BN / linear / pool of these models becomes a native site: no call that
+    would reach MIOpen / hipBLASLt / rocBLAS is left in the train or eval graph."""
+    m = build_model(name, num_classes=10)
+    assert lower_or_none(m) is None
+    net = GenericNet.__new__(GenericNet)
+    from mlcomp_amd.models.native_generic import _Lowering
+    from mlcomp_amd.ops.layers import NativeContext
+    import torch.fx as fx
+    net.ctx, net._params = NativeContext(), {}
+    gm = _Lowering(net, fx.symbolic_trace(m.train())).run()
+    left = [type(mod).__name__ for mod in gm.modules()
+            if isinstance(mod, (nn.Conv2d, nn.Linear, nn.BatchNorm2d, nn.BatchNorm1d, nn.ConvTranspose2d))]
+    assert not left, left
+    for n in gm.graph.nodes:
+        assert n.target not in (F.conv2d, F.linear, F.batch_norm, torch.matmul), n
+
+
+def test_reference_example_nets_match_fp32_autograd():
+    """The reference's LeNet and CIFAR Net: outputs and every parameter gradient against
+    fp32 autograd of the same weights (bf16 activations: loose but discriminating)."""
+    for make, shape in ((RefCifarNet, (16, 3, 32, 32)), (lambda: build_model('LeNet', num_classes=10),
+                                                          (16, 1, 28, 28))):
+        m, ref = _pair(make)
+        x = torch.randn(*shape)
+        y = torch.randint(0, 10, (shape[0],))
+        net = GenericNet(m, 'cpu')
+        out = net(x)
+        F.cross_entropy(out.float(), y).backward()
+        want = ref(x)
+        F.cross_entropy(want, y).backward()
+        assert _rel(out, want) < 2e-2
+        # the gradients reach conv1 through bf16 max-pool argmaxes and ReLU masks, where a
+        # rounding can flip a window's winner: directions, not magnitudes per element
+        for p in net.param_sets():
+            g = p.w.grad if hasattr(p, 'w') else p.gamma.grad
+            assert _cos(g, _torch_grad(p, ref)) > 0.98, p.name
+            if getattr(p, 'b', None) is not None:
+                bb = dict(ref.named_modules())[p.name].bias.grad
+                assert _cos(p.b.grad[:bb.numel()], bb) > 0.98, p.name
+
+
+@pytest.mark.parametrize('act', ['relu', 'relu6', 'silu', 'sigmoid', 'tanh', 'hardswish', 'leaky_relu', 'gelu',
+                                 'elu', 'hardsigmoid'])
+@pytest.mark.parametrize('groups', [1, 2, 8, 64])
+def test_conv_bn_act_residual_site(act, groups):
+    """conv (dense / grouped Cg=32 / Cg=8 / depthwise) -> BN -> + residual -> act."""
+    mods = {'relu': nn.ReLU(), 'relu6': nn.ReLU6(), 'silu': nn.SiLU(), 'sigmoid': nn.Sigmoid(), 'tanh': nn.Tanh(),
+            'hardswish': nn.Hardswish(), 'leaky_relu': nn.LeakyReLU(0.2), 'gelu': nn.GELU(), 'elu': nn.ELU(0.7),
+            'hardsigmoid': nn.Hardsigmoid()}
+
+    class Block(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.conv = nn.Conv2d(64, 64, 3, 1, 1, groups=groups, bias=False)
+            self.bn = nn.BatchNorm2d(64)
+            self.act = mods[act]
+            self.head = nn.Conv2d(64, 16, 1)
+
+        def forward(self, x):
+            return self.head(self.act(self.bn(self.conv(x)) + x))
+
+    m, ref = _pair(Block)
+    with torch.no_grad():
+        m.bn.weight.uniform_(0.5, 1.5)
+        m.bn.bias.uniform_(-0.5, 0.5)
+        ref.load_state_dict(m.state_dict())
+    x = torch.randn(8, 64, 12, 12)
+    net = GenericNet(m, 'cpu')
+    sites = [type(s).__name__ for s in net.train_gm.modules() if hasattr(s, 'fwd')]
+    assert sites == ['ConvBNAct', 'ConvBNAct'], sites
+    xr = x.clone().requires_grad_()
+    xn = x.clone().requires_grad_()
+    out = net(xn)
+    d = torch.randn_like(out.float())
+    (out.float() * d).sum().backward()
+    want = ref(xr)
+    (want * d).sum().backward()
+    assert _rel(out, want) < 2e-2
+    assert _rel(xn.grad, xr.grad) < 5e-2
+    for p in net.param_sets():
+        g = p.w.grad if hasattr(p, 'w') else p.gamma.grad
+        assert _rel(g, _torch_grad(p, ref)) < 5e-2, (p.name, _rel(g, _torch_grad(p, ref)))
+    # running statistics moved exactly like torch's (momentum 0.1, unbiased variance)
+    bn = [p for p in net.param_sets() if hasattr(p, 'run_mean')][0]
+    assert torch.allclose(bn.run_mean[:64], ref.bn.running_mean, rtol=2e-2, atol=2e-3)
+    assert torch.allclose(bn.run_var[:64], ref.bn.running_var, rtol=2e-2, atol=2e-3)
+
+
+def test_linear_bn1d_pool_sites_and_eval_graph():
+    class Head(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.conv = nn.Conv2d(5, 24, 3, padding=1)
+            self.pool = nn.MaxPool2d(3, 2, 1, ceil_mode=True)
+            self.gap = nn.AdaptiveAvgPool2d(1)
+            self.fc = nn.Linear(24, 36)
+            self.bn1 = nn.BatchNorm1d(36)
+            self.out = nn.Linear(36, 7)
+
+        def forward(self, x):
+            x = self.gap(self.pool(F.relu(self.conv(x)))).flatten(1)
+            return self.out(F.silu(self.bn1(self.fc(x))))
+
+    m, ref = _pair(Head)
+    x = torch.randn(16, 5, 11, 13)
+    net = GenericNet(m, 'cpu')
+    kinds = sorted(type(s).__name__ for s in net.train_gm.modules() if hasattr(s, 'fwd'))
+    assert kinds == ['BNAct', 'ConvBNAct', 'GlobalAvgPool', 'LinearAct', 'LinearAct', 'MaxPool'], kinds
+    out = net(x)
+    out.float().sum().backward()
+    want = ref(x)
+    want.sum().backward()
+    assert _rel(out, want) < 4e-2          # BatchNorm1d over 16 rows amplifies bf16 rounding
+    for p in net.param_sets():           # through a bf16 max-pool: directions (see above)
+        g = p.w.grad if hasattr(p, 'w') else p.gamma.grad
+        assert _cos(g, _torch_grad(p, ref)) > 0.99, p.name
+    # inference graph: running statistics, no autograd
+    net.eval()
+    ref.eval()
+    with torch.no_grad():
+        assert _rel(net(x), ref(x)) < 5e-2
+
+
+def test_generic_step_optimizer_matches_torch_optim_semantics():
+    """One NativeGenericStep = forward + criterion + backward + fused update with torch.optim's
+    semantics (weight decay on EVERY parameter, BN and biases included): the arena after a
+    step equals torch.optim.<opt> applied to the step's own gradients."""
+    from mlcomp_amd.train.native_generic_step import NativeGenericStep
+    for opt, kw in (('SGD', dict(lr=0.1, momentum=0.9, weight_decay=1e-2)),
+                    ('AdamW', dict(lr=1e-2, weight_decay=0.1)), ('Adam', dict(lr=1e-2, weight_decay=1e-2))):
+        torch.manual_seed(0)
+        m = RefCifarNet()
+        x, y = torch.randn(8, 3, 32, 32), torch.randint(0, 10, (8,))
+        step = NativeGenericStep(m, x, y, device='cpu', use_graph=False, optimizer=opt, **kw)
+        arena = step.net.arena
+        before = [a.master.clone() for a in arena.arenas()]
+        step()                     # GraphedStep.__call__ runs opt.prepare() itself
+        grads = [a.grad.clone() for a in arena.arenas()]
+        params = [torch.nn.Parameter(b.clone()) for b in before]
+        for p, g in zip(params, grads):
+            p.grad = g
+        tkw = dict(kw)
+        o = getattr(torch.optim, opt)(params, **tkw)
+        o.step()
+        for p, a in zip(params, arena.arenas()):
+            assert torch.allclose(a.master, p.detach(), rtol=1e-5, atol=1e-6), opt
+        with torch.no_grad():            # the torch model still holds the initial weights
+            want = float(F.cross_entropy(m(x), y))
+        assert step.last_loss() == pytest.approx(want, rel=0.02)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_make(world, rank):
+    from mlcomp_amd.train.native_generic_step import NativeGenericStep
+    torch.manual_seed(0)
+    m = build_model('resnext50_32x4d', num_classes=10)
+    g = torch.Generator().manual_seed(100 + rank)
+    x, y = torch.randn(2, 3, 32, 32, generator=g), torch.randint(0, 10, (2,), generator=g)
+    return NativeGenericStep(m, x, y, device='cpu', world_size=world, use_graph=False, optimizer='SGD', lr=0.1,
+                             momentum=0.9, weight_decay=1e-4)
+
+
+def _flat(step, what):
+    return torch.cat([getattr(a, what).detach().flatten().clone() for a in step.net.arena.arenas()])
+
+
+def _dp_worker(rank, world, port, out):
+    import torch.distributed as dist
+    torch.set_num_threads(1)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    step = _dp_make(world, rank)
+    step()
+    torch.save({'g': _flat(step, 'grad'), 'w': _flat(step, 'master')}, os.path.join(out, f'r{rank}.pt'))
+    dist.destroy_process_group()
+
+
+def test_generic_data_parallel_equals_sum_of_shards(tmp_path):
+    """ResNeXt-50 (grouped convs) on the generic engine over 2 gloo ranks with different data:
+    the all-reduced gradient arena is the sum of the per-shard single-process gradients and
+    the weights are one optimizer step on their mean, identical on both ranks."""
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        mp.spawn(_dp_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2)
+        got = [torch.load(tmp_path / f'r{r}.pt', weights_only=True) for r in range(2)]
+        gsum = None
+        for r in range(2):
+            ref = _dp_make(1, r)
+            ref()
+            g = _flat(ref, 'grad')
+            gsum = g if gsum is None else gsum + g
+        scale = gsum.abs().max()
+        for r in range(2):
+            assert torch.allclose(got[r]['g'], gsum, rtol=1e-4, atol=1e-5 * scale)
+            assert torch.equal(got[r]['w'], got[0]['w'])
+    finally:
+        torch.set_num_threads(threads)
+
+
+def test_runner_picks_the_generic_engine_with_a_reason_for_the_rest(monkeypatch, tmp_path):
+    from mlcomp_amd.train.experiment import ConfigExperiment
+    from mlcomp_amd.train.runner import Runner, _native_kind
+    assert _native_kind(build_model('LeNet', num_classes=10), torch.device('cuda')) == 'generic'
+    assert _native_kind(build_model('efficientnet-b0', num_classes=10), torch.device('cuda')) == 'generic'
+
+    class Odd(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.c = nn.Conv2d(3, 8, (1, 7), padding=(0, 3))
+
+        def forward(self, x):
+            return self.c(x).mean((2, 3))
+
+    cfg = {'model_params': {'model': 'LeNet', 'num_classes': 10}, 'args': {'logdir': str(tmp_path)},
+           'stages': {'optimizer_params': {'optimizer': 'Adam', 'lr': 1e-3}, 'stage1': {}}}
+    r = Runner(ConfigExperiment(cfg), device='cpu')
+    r.model = Odd()
+    r.device = torch.device('cuda')      # selection only
+    got = r._select_engine('stage1')
+    assert got['engine'] == 'torch' and 'padding' in got['reason'], got
+    r.model = build_model('LeNet', num_classes=10)
+    got = r._select_engine('stage1')
+    assert got == {'stage': 'stage1', 'engine': 'native', 'kind': 'generic', 'precision': 'bf16', 'reason': None}
+
+
+def test_act_codes_reference_derivatives():
+    """The CPU references of the 10 activation codes and their derivatives (what the GPU
+    tests compare the kernels against) agree with torch autograd."""
+    a = torch.linspace(-7, 7, 1001)
+    for name, code in Fn.ACT.items():
+        if code == 0:
+            continue
+        x = a.clone().requires_grad_()
+        Fn.act_ref(x, code, 0.3).sum().backward()
+        g = Fn.act_grad_ref(a, code, 0.3)
+        keep = (a.abs() > 1e-3) & ((a.abs() - 3).abs() > 1e-3) & ((a - 6).abs() > 1e-3)   # kinks
+        assert torch.allclose(g[keep], x.grad[keep], atol=1e-5), name
