@@ -125,8 +125,11 @@ def embed_bwd(ds, ids, tt, word_grad, pos_grad, tok_grad):
         pt = _EMB_SCRATCH.get(key)
         if pt is None:    # [S][ntypes][H] partial sums, left zeroed by the kernel
             pt = _EMB_SCRATCH[key] = torch.zeros(S * ntypes * H, device=ds.device, dtype=torch.float32)
-        _lib.call('mlc_embed_bwd', _lib.ptr(ds.contiguous()), _lib.ptr(ids.contiguous()),
-                  _lib.ptr(tt.contiguous() if tok_grad is not None else None), _lib.ptr(word_grad),
+        # contiguous copies bound to names: a temporary freed while the argument list is
+        # still being built could hand its block to the next copy before the kernel runs
+        dsc, idc = ds.contiguous(), ids.contiguous()
+        ttc = tt.contiguous() if tok_grad is not None else None
+        _lib.call('mlc_embed_bwd', _lib.ptr(dsc), _lib.ptr(idc), _lib.ptr(ttc), _lib.ptr(word_grad),
                   _lib.ptr(pos_grad), _lib.ptr(tok_grad), _lib.ptr(pt), B, S, H, ntypes, _lib.stream())
         return
     d = ds.float().reshape(B * S, H)

@@ -11,7 +11,7 @@ torch.manual_seed(0)
 m = _no_stochastic(make())
 x, y = torch.randn(*shape), torch.randint(0, ncls, (shape[0],))
 st = NativeGenericStep(m, x, y, device='cuda', use_graph=graph, optimizer='SGD', lr=lr, momentum=0.9)
-for i in range(14):
+for i in range(int(sys.argv[4]) if len(sys.argv) > 4 else 14):
     st()
     torch.cuda.synchronize()
     bad_g = [n for n, s in st.net.arena.by_name.items() if not torch.isfinite(s.grad).all()]
