@@ -87,3 +87,17 @@ static __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int xcd = orig & 7, loc = orig >> 3;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
+
+// Zero n floats on stream st with a kernel.  Used instead of hipMemsetAsync for the
+// accumulation targets of atomics: a memset captured into a HIP graph becomes a memset
+// node that the runtime may run on a copy engine, outside the kernels' L2 ordering.
+static __global__ void __launch_bounds__(256) mlc_zero_f32_kernel(float* __restrict__ p, long n) {
+  // scalar stores: targets are arena slices with any 4-byte offset
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) p[i] = 0.f;
+}
+static inline void mlc_zero_f32(float* p, long n, hipStream_t st) {
+  if (n <= 0) return;
+  long blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(mlc_zero_f32_kernel, dim3(blocks), dim3(256), 0, st, p, n);
+}

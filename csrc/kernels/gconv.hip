@@ -541,7 +541,7 @@ MLC_EXPORT int mlc_gconv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, 
                                int KW, int S, int P, int D, int Ho, int Wo, int groups, int accumulate, hipStream_t st) {
   if (!grouped_ok(C, Co, groups)) return -1;
   const GGeom g = mkg(N, H, W, C, Ho, Wo, Co, KH, KW, S, P, D, C / groups);
-  if (!accumulate) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)Co * g.T * g.Cg, st);
+  if (!accumulate) mlc_zero_f32(dw, (long)Co * g.T * g.Cg, st);
   const int ncb = g.T * (g.KB / 16);
   const int zb = (ncb + WG_NCB - 1) / WG_NCB;
   const int base = (Co / 16) * zb;
@@ -582,7 +582,7 @@ MLC_EXPORT int mlc_dwconv_wgrad(const bf16* dy, const bf16* x, float* dw, float*
                                 int KH, int KW, int S, int P, int D, int Ho, int Wo, int accumulate, hipStream_t st) {
   if (C % 8) return -1;
   const int G = C / 8, T = KH * KW;
-  (void)hipMemsetAsync(ws, 0, sizeof(float) * (size_t)NCOPY * T * C, st);
+  mlc_zero_f32(ws, (long)NCOPY * T * C, st);
   const long work = (long)N * Ho * Wo * G;
   const int blocks = grid_groups(work, G, 1024);
   for (int t0 = 0; t0 < T; t0 += DW_TC)

@@ -1776,7 +1776,7 @@ MLC_EXPORT int mlc_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, i
                        (long)slab / 4, accumulate);
     return hipGetLastError();
   }
-  if (!accumulate) (void)hipMemsetAsync(dw, 0, slab * sizeof(float), st);
+  if (!accumulate) mlc_zero_f32(dw, (long)slab, st);
   EpiF32Atomic epi{dw, KK};
   if (in_sc) {
     if (plain) {
@@ -1858,7 +1858,7 @@ MLC_EXPORT int mlc_conv_wgrad_bias(const bf16* dy, const bf16* x, float* dw, flo
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, dw, n4, splits, n4, accumulate);
     return hipGetLastError();
   }
-  if (!accumulate) (void)hipMemsetAsync(dw, 0, slab * sizeof(float), st);
+  if (!accumulate) mlc_zero_f32(dw, (long)slab, st);
   EpiF32Atomic epi{dw, KK};
   if (plain) {
 #define MKB(R) (MatMC<R>{x, C, P, C})

@@ -23,6 +23,7 @@ MI355X-first changes:
 from __future__ import annotations
 
 import datetime
+import os
 import queue as _queue
 import threading
 import time
@@ -48,8 +49,13 @@ FATAL_RESTART_MESSAGES = (
     'hipErrorLaunchFailure', 'ncclUnhandledCudaError', 'ncclSystemError: System call',
     'unhandled system error', 'ncclRemoteError', 'MIOPEN_STATUS_INTERNAL_ERROR',
     ORPHAN_MESSAGE,
+    # a rank whose process died (SIGKILL, OOM killer): worker/daemon.PROCESS_LOST_MESSAGE
+    'task process was lost',
 )
 MAX_AUTO_RESTARTS = 3
+# a DDP rank still InProgress this long after a sibling rank succeeded is taken to hang in a
+# collective and is killed (its training finished with the others)
+STRAGGLER_SECONDS = float(os.environ.get('MLC_STRAGGLER_SECONDS', 60))
 ALIVE_SECONDS = 15
 # a Queued task whose broker message is gone (broker restarted without its journal) or
 # whose queue has been dead this long is taken back: its GPUs return to the ledger
@@ -164,7 +170,13 @@ class SupervisorBuilder:
             return
         succ, prog = counts[TaskStatus.Success], counts[TaskStatus.InProgress]
         if succ > 0 and prog > 0 and succ + prog == sum(counts.values()):
-            for c in self.provider.children(task.id):
+            kids = self.provider.children(task.id)
+            # ranks finish a few seconds apart (checkpoint, digest, process-group teardown):
+            # only a rank still running STRAGGLER_SECONDS after the first one finished hangs
+            done = [c.finished for c in kids if c.status == TaskStatus.Success.value and c.finished]
+            if done and (now() - min(done)).total_seconds() < STRAGGLER_SECONDS:
+                return
+            for c in kids:
                 if c.status == TaskStatus.InProgress.value and c.pid and c.computer_assigned:
                     q = queue_name(c.computer_assigned, c.docker_assigned or 'default', 'supervisor')
                     ok = self.broker.call(q, 'kill', c.pid, timeout=10.0)
@@ -182,12 +194,13 @@ class SupervisorBuilder:
             if c.status != TaskStatus.Failed.value:
                 continue
             logs = self.log_provider.last(1, task=c.id)
-            if logs and any(m in (logs[0].message or '') for m in FATAL_RESTART_MESSAGES):
+            hit = [m for m in FATAL_RESTART_MESSAGES if logs and m in (logs[0].message or '')]
+            if hit:
                 info['auto_restarts'] = info.get('auto_restarts', 0) + 1
                 task.additional_info = yaml_dump(info)
                 self.provider.commit()
-                self.logger.info(f'restart dag {task.dag}: fatal device error in task {c.id}',
-                                 ComponentType.Supervisor, None, task.id)
+                self.logger.info(f'restart dag {task.dag} ({info["auto_restarts"]} of {MAX_AUTO_RESTARTS}): '
+                                 f'task {c.id} failed with "{hit[0]}"', ComponentType.Supervisor, None, task.id)
                 self.start_dag(task.dag)
                 return
 

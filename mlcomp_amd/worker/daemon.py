@@ -105,6 +105,10 @@ def register_computer(session, gpu: GpuInfo, can_process: Optional[bool] = None)
 
 
 # ---------------------------------------------------------------------------- pool
+# the log line of a task whose process died (the scheduler's bounded restart matches it)
+PROCESS_LOST_MESSAGE = 'task process was lost'
+
+
 class WorkerPool:
     def __init__(self, indices: List[int], docker: Optional[str] = None, poll: float = 1.0):
         self.indices = indices
@@ -133,8 +137,10 @@ class WorkerPool:
                     p = subprocess.Popen([sys.executable, '-m', 'mlcomp_amd.worker.tasks',
                                           str(msg['args'][0])], env=env)
                     self.running[index] = p
-                    p.wait()
+                    rc = p.wait()
                     self.running.pop(index, None)
+                    if rc != 0:
+                        self._process_lost(index, int(msg['args'][0]), rc)
                 elif msg.get('task') in CONTROL_TASKS:
                     res = CONTROL_TASKS[msg['task']](*msg.get('args', []))
                     if msg.get('reply'):
@@ -144,6 +150,26 @@ class WorkerPool:
                     broker.ack(msg['id'])
                 except Exception:
                     pass  # broker gone: the lease is re-queued by the broker itself
+
+    def _process_lost(self, index: int, task_id: int, rc: int):
+        """A task process that exited abnormally while its task is still InProgress (killed:
+        OOM killer, a crashed driver, an injected fault) is failed at once - the liveness
+        scan of the worker supervisor would only see the missing pid after its grace."""
+        try:
+            session = Session.create_session(key=f'WorkerPool-{index}')
+            session.expire_all()
+            tp = TaskProvider(session)
+            t = tp.by_id(task_id)
+            if t is None or t.status != TaskStatus.InProgress.value:
+                return
+            info = yaml_load(t.additional_info) or {}
+            for pid in info.get('child_processes', []):
+                kill_pid(pid)
+            create_logger(session, 'WorkerPool', console=False).error(
+                f'{PROCESS_LOST_MESSAGE} (task {task_id}, exit code {rc})', ComponentType.Worker, hostname(), task_id)
+            tp.change_status(t, TaskStatus.Failed)
+        except Exception:
+            traceback.print_exc()
 
     def start(self):
         for i in self.indices:
@@ -191,7 +217,7 @@ class WorkerSupervisor:
             info = yaml_load(t.additional_info) or {}
             for p in info.get('child_processes', []):
                 kill_pid(p)
-            self.logger.error(f'task {t.id}: process {t.pid} is gone -> Failed',
+            self.logger.error(f'{PROCESS_LOST_MESSAGE} (task {t.id}: process {t.pid} is gone)',
                               ComponentType.WorkerSupervisor, self.name, t.id)
             tp.change_status(t, TaskStatus.Failed)
         # orphans: live task processes whose task was stopped/failed/skipped
@@ -284,4 +310,4 @@ class WorkerSupervisor:
         self._stop.set()
 
 
-__all__ = ['WorkerPool', 'WorkerSupervisor', 'GpuInfo', 'register_computer', 'usage_snapshot']
+__all__ = ['PROCESS_LOST_MESSAGE', 'WorkerPool', 'WorkerSupervisor', 'GpuInfo', 'register_computer', 'usage_snapshot']

@@ -37,6 +37,15 @@ from mlcomp_amd.utils.misc import merge_dicts_smart, set_global_seed, yaml_dump,
 from .base import Executor
 
 
+def weights_digest(model) -> str:
+    """sha1 (16 hex digits) of a model's parameters in registration order, as fp32."""
+    import hashlib
+    h = hashlib.sha1()
+    for p in model.parameters():
+        h.update(p.detach().float().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()[:16]
+
+
 class DbCallback(Callback):
     order = 200
     master_only = True
@@ -204,7 +213,6 @@ class Train(Executor):
             return 0
         fname = 'last_full.pth' if r.get('load_last') else 'best_full.pth'
         ckdir = join(experiment.logdir, 'checkpoints')
-        os.makedirs(ckdir, exist_ok=True)
         path = join(ckdir, fname)
         s = config.get()
         if r.get('master_computer') and r['master_computer'] != (os.environ.get('MLCOMP_COMPUTER')
@@ -212,6 +220,7 @@ class Train(Executor):
             from mlcomp_amd.worker.sync import copy_remote
             src = ComputerProvider(self.session).by_name(r['master_computer'])
             if src is not None:
+                os.makedirs(ckdir, exist_ok=True)
                 remote = join(src.root_folder or s.ROOT_FOLDER, 'tasks', str(r['master_task_id']),
                               experiment.logdir, 'checkpoints', fname)
                 try:
@@ -296,8 +305,13 @@ class Train(Executor):
             # first remaining stage starts
             runner.resume(self.resume_path)
         runner.run_experiment(stages, start_epoch=start_epoch)
-        if self.distr_info and torch.cuda.is_available():
-            self._log_transports(runner)
+        if self.distr_info:
+            # data parallelism keeps every rank's weights identical: one digest line per rank
+            # makes that checkable from the task logs
+            self.info(f'rank {rank} of {world}: stage {stages[-1]} weights digest '
+                      f'{weights_digest(runner.model)}', db=True)
+            if torch.cuda.is_available():
+                self._log_transports(runner)
         if self.master and self.trace:
             model = runner.model.eval().cpu().float()
             # one real input of the last stage (channels / size as the data has them)
@@ -314,4 +328,4 @@ Executor._child['Catalyst'] = Train
 Executor._child['catalyst'] = Train
 
 
-__all__ = ['Train', 'DbCallback']
+__all__ = ['Train', 'DbCallback', 'weights_digest']
