@@ -7,6 +7,7 @@ from __future__ import annotations
 import datetime
 import os
 import random
+import sys
 import re
 import signal
 from collections import defaultdict
@@ -167,11 +168,9 @@ def set_global_seed(seed: int):
         np.random.seed(seed)
     except ImportError:
         pass
-    try:
-        import torch
+    torch = sys.modules.get('torch')   # seeded if loaded; importing it costs a task ~3 s
+    if torch is not None:
         torch.manual_seed(seed)
-    except ImportError:
-        pass
 
 
 def parse_gpu_range(gpu) -> Tuple[int, int]:

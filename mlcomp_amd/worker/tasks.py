@@ -109,7 +109,7 @@ class ExecuteBuilder:
     def download(self):
         from mlcomp_amd.worker.executors import Executor, load_builtin_executors
         from mlcomp_amd.worker.storage import Storage
-        load_builtin_executors()
+        load_builtin_executors(self.executor_type)
         if self.task.debug:
             folder = os.getcwd()
         else:
@@ -126,6 +126,8 @@ class ExecuteBuilder:
 
     def create_executor(self):
         from mlcomp_amd.worker.executors import Executor
+        # again now that the executor's modules are imported (torch, if it uses it)
+        set_global_seed(self.config.get('info', {}).get('seed', 0))
         info = yaml_load(self.task.additional_info) or {}
         self.executor = Executor.from_config(executor=self.task.executor, config=self.config,
                                              additional_info=info, session=self.session,

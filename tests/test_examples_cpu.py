@@ -135,3 +135,26 @@ def test_digit_recognizer_pipeline_on_cpu(cluster):
     sub = pd.read_csv(os.path.join(data, 'submissions', 'net_test.csv'))
     assert list(sub.columns) == ['ImageId', 'Label'] and len(sub) == 300
     assert os.path.exists(os.path.join(config.get().MODEL_FOLDER, 'examples', 'net.pth'))
+
+
+def test_dispatch_to_start_latency_of_small_tasks(cluster):
+    """Scheduler dispatch -> task process running its executor, for trivial bash tasks on an
+    idle worker (the reference's budget is its 1 s scheduler tick).  A task process imports
+    only its own executor (no torch for a bash task)."""
+    import statistics
+    from mlcomp_amd.db.core import Session
+    from mlcomp_amd.db.enums import TaskStatus
+    from mlcomp_amd.db.models import Log, Task
+    lat, total = [], []
+    for _ in range(3):
+        (tid,) = _ids(_run_example(cluster['tmp'], 'bash/config.yml'))
+        res = _wait(cluster['sup'], [tid], timeout=60)
+        assert res[tid] == TaskStatus.Success
+        s = Session.create_session(key='lat')
+        t = s.get(Task, tid)
+        sent = [l.time for l in s.query(Log).filter(Log.message.like(f'sent task {tid} to %'))]
+        assert sent and t.started and t.finished
+        lat.append((t.started - sent[0]).total_seconds())
+        total.append((t.finished - sent[0]).total_seconds())
+    print(f'dispatch->start {[round(v, 2) for v in lat]} s, dispatch->finish {[round(v, 2) for v in total]} s')
+    assert statistics.median(lat) <= 1.5, lat
