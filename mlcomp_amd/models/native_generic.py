@@ -145,6 +145,16 @@ def _check_conv(name, m: nn.Conv2d):
                                     'widths dividing or divisible by 16, channels % 16 == 0)')
 
 
+def _check_convT(name, m: nn.ConvTranspose2d):
+    if m.padding_mode != 'zeros' or m.groups != 1:
+        raise NativeUnsupported(f'{name}: ConvTranspose2d with groups={m.groups}, padding_mode={m.padding_mode!r}')
+    for attr in ('stride', 'padding', 'dilation', 'output_padding'):
+        _pair(getattr(m, attr), f'{name}.{attr}')
+    KH, KW = m.kernel_size
+    if KH > 15 or KW > 15:
+        raise NativeUnsupported(f'{name}: kernel {KH}x{KW} (native convs take <= 15x15)')
+
+
 def _check_bn(name, m):
     if m.momentum is None:
         raise NativeUnsupported(f'{name}: BatchNorm momentum=None (cumulative average)')
@@ -190,7 +200,10 @@ class _Lowering:
 
     def conv(self, node):
         m = self.modules[node.target]
-        _check_conv(node.target, m)
+        if isinstance(m, nn.ConvTranspose2d):
+            _check_convT(node.target, m)
+        else:
+            _check_conv(node.target, m)
         chain = [node]
         bn_node = _only_user(node)
         bn = None
@@ -251,7 +264,7 @@ class _Lowering:
                 continue
             if node.op == 'call_module':
                 m = self.modules.get(node.target)
-                if isinstance(m, nn.Conv2d):
+                if isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)):
                     self.conv(node)
                 elif isinstance(m, (nn.BatchNorm2d, nn.BatchNorm1d)):
                     self.bn(node)
@@ -261,7 +274,7 @@ class _Lowering:
                     self.maxpool(node, m.kernel_size, m.stride, m.padding, m.dilation, m.ceil_mode, m.return_indices)
                 elif isinstance(m, nn.AdaptiveAvgPool2d) and _pair(m.output_size, 'output_size') == 1:
                     self.avgpool(node)
-                elif isinstance(m, (nn.ConvTranspose2d, nn.Conv1d, nn.Conv3d, nn.ConvTranspose1d,
+                elif isinstance(m, (nn.Conv1d, nn.Conv3d, nn.ConvTranspose1d,
                                     nn.ConvTranspose3d, nn.BatchNorm3d, nn.LSTM, nn.GRU, nn.RNN,
                                     nn.MultiheadAttention, nn.Bilinear, nn.InstanceNorm2d)):
                     raise NativeUnsupported(f'{node.target}: {type(m).__name__} has no native lowering')

@@ -75,15 +75,27 @@ class _Uses:
 # ---------------------------------------------------------------------------- parameters
 class ConvParams:
     """nn.Conv2d -> kernel-layout slots: dense [Cop, KH, KW, Cip], grouped [Co, KH, KW, Cg],
-    depthwise [KH, KW, Cp] (tap-major); optional bias [Cop]."""
+    depthwise [KH, KW, Cp] (tap-major); nn.ConvTranspose2d -> 'tr' [Cip, KH, KW, Cop] (the
+    filter of the conv whose input gradient the transposed conv is); optional bias [Cop]."""
 
-    def __init__(self, ctx: NativeContext, name: str, conv: nn.Conv2d, keep_bias: bool):
-        Co, Cg, KH, KW = conv.weight.shape
+    def __init__(self, ctx: NativeContext, name: str, conv: nn.Module, keep_bias: bool):
         self.ctx, self.name, self.src = ctx, name, conv
         self.groups = conv.groups
+        self.stride, self.pad, self.dil = conv.stride[0], conv.padding[0], conv.dilation[0]
+        if isinstance(conv, nn.ConvTranspose2d):
+            Ci, Co, KH, KW = conv.weight.shape
+            self.kind = 'tr'
+            self.Ci, self.Co, self.Cg = Ci, Co, Ci
+            self.k = (KH, KW)
+            self.out_pad = conv.output_padding[0]
+            self.Cip, self.Cop = ceil8(Ci), ceil8(Co)
+            self.w = ctx.arena.weight(f'{name}.weight', (self.Cip, KH, KW, self.Cop))
+            self.b = ctx.arena.vector(f'{name}.bias', (self.Cop,)) if (keep_bias and conv.bias is not None) else None
+            self.uses = _Uses()
+            return
+        Co, Cg, KH, KW = conv.weight.shape
         self.Ci, self.Co, self.Cg = Cg * conv.groups, Co, Cg
         self.k = (KH, KW)
-        self.stride, self.pad, self.dil = conv.stride[0], conv.padding[0], conv.dilation[0]
         if self.groups == 1:
             self.kind = 'dense'
             self.Cip, self.Cop = ceil8(self.Ci), ceil8(Co)
@@ -105,6 +117,9 @@ class ConvParams:
         if self.kind == 'dense':
             w = w.permute(0, 2, 3, 1)
             w = torch.nn.functional.pad(w, (0, self.Cip - self.Ci, 0, 0, 0, 0, 0, self.Cop - self.Co))
+        elif self.kind == 'tr':
+            w = w.permute(0, 2, 3, 1)
+            w = torch.nn.functional.pad(w, (0, self.Cop - self.Co, 0, 0, 0, 0, 0, self.Cip - self.Ci))
         elif self.kind == 'dw':
             w = torch.nn.functional.pad(w[:, 0].permute(1, 2, 0), (0, self.Cop - self.Co))
         else:
@@ -118,6 +133,8 @@ class ConvParams:
         m = self.w.master.detach()
         if self.kind == 'dense':
             w = m[:self.Co, :, :, :self.Ci].permute(0, 3, 1, 2)
+        elif self.kind == 'tr':
+            w = m[:self.Ci, :, :, :self.Co].permute(0, 3, 1, 2)
         elif self.kind == 'dw':
             w = m[..., :self.Co].permute(2, 0, 1)[:, None]
         else:
@@ -127,6 +144,10 @@ class ConvParams:
             self.src.bias.data.copy_(self.b.master[:self.Co].to(self.src.bias.device, self.src.bias.dtype))
 
     def out_hw(self, H, W):
+        if self.kind == 'tr':
+            KH, KW = self.k
+            s, p, d, op = self.stride, self.pad, self.dil, self.out_pad
+            return (H - 1) * s - 2 * p + d * (KH - 1) + op + 1, (W - 1) * s - 2 * p + d * (KW - 1) + op + 1
         return Fn.conv_out_hw(H, W, self.k[0], self.k[1], self.stride, self.pad, self.dil)
 
     # ---- the three GEMMs by kind
@@ -142,6 +163,9 @@ class ConvParams:
             return Fn.conv2d_fwd(x, wb, self.stride, self.pad, self.dil, stats=stats)
         if self.kind == 'dw':
             return Fn.dwconv_fwd(x, wb, self.stride, self.pad, self.dil, stats=stats)
+        if self.kind == 'tr':     # the dgrad parity-class GEMMs (BN statistics in the epilogue)
+            return Fn.conv_transpose2d_fwd(x, wb, self.out_hw(x.shape[1], x.shape[2]), self.stride, self.pad,
+                                           self.dil, stats=stats)
         return Fn.gconv_fwd(x, wb, self.groups, self.stride, self.pad, self.dil, stats=stats)
 
     def dgrad(self, dy, x_shape):
@@ -150,6 +174,10 @@ class ConvParams:
             return Fn.conv2d_dgrad(dy, wb, x_shape, self.stride, self.pad, self.dil)
         if self.kind == 'dw':
             return Fn.dwconv_dgrad(dy, wb, x_shape, self.stride, self.pad, self.dil)
+        if self.kind == 'tr':     # a forward conv of dy over the same filter
+            dx = Fn.conv2d_fwd(dy, wb, self.stride, self.pad, self.dil)
+            assert tuple(dx.shape) == tuple(x_shape), (dx.shape, x_shape)
+            return dx
         return Fn.gconv_dgrad(dy, wb, x_shape, self.groups, self.stride, self.pad, self.dil)
 
     def wgrad(self, dy, x):
@@ -163,6 +191,8 @@ class ConvParams:
                                 accumulate=acc)
         elif self.kind == 'dw':
             Fn.dwconv_wgrad(dy, x, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad, accumulate=acc)
+        elif self.kind == 'tr':   # the conv wgrad with the roles of x and dy swapped
+            Fn.conv2d_wgrad(x, dy, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad, accumulate=acc)
         else:
             Fn.gconv_wgrad(dy, x, self.w.shape, self.groups, self.stride, self.pad, self.dil, out=self.w.grad,
                            accumulate=acc)

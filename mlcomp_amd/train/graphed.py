@@ -97,4 +97,24 @@ class GraphedStep:
                 self.use_graph = False
                 self._body()
                 return
-        self.graph.replay()
+        self._replay()
+
+    # Replays run on a stream of their own, fenced to the caller's stream on both sides.
+    # Measured on MI355X / ROCm 7: when hundreds of eager kernels (a second model's step)
+    # are launched on the SAME stream between replays of a graph, later replays compute
+    # garbage (NaN within ~8 steps, scripts/debug/nan_test_loop.py 'eg'); a host sync after
+    # the replay, or the eager work on another stream, avoids it.  Costs two event fences.
+    _replay_stream = None
+
+    def _replay(self):
+        cur = torch.cuda.current_stream(self.device)
+        if os.environ.get('MLC_GRAPH_OWN_STREAM', '1') == '0':
+            self.graph.replay()
+            return
+        if self._replay_stream is None:
+            self._replay_stream = torch.cuda.Stream(self.device)
+        rs = self._replay_stream
+        rs.wait_stream(cur)
+        with torch.cuda.stream(rs):
+            self.graph.replay()
+        cur.wait_stream(rs)

@@ -53,6 +53,8 @@ def _rel(a, b):
 def _torch_grad(p, ref):
     """The reference module's gradient of a parameter set, in the set's layout."""
     m = dict(ref.named_modules())[p.name]
+    if getattr(p, 'kind', None) == 'tr':
+        return _torch_grad_tr(p, ref)
     if hasattr(p, 'kind'):
         g = m.weight.grad
         if p.kind == 'dense':
@@ -63,6 +65,11 @@ def _torch_grad(p, ref):
     if hasattr(p, 'O'):
         return F.pad(m.weight.grad, (0, p.Ip - p.I, 0, p.Op - p.O))
     return F.pad(m.weight.grad, (0, p.Cp - p.C))
+
+
+def _torch_grad_tr(p, ref):
+    g = dict(ref.named_modules())[p.name].weight.grad      # [Cin, Cout, KH, KW]
+    return F.pad(g.permute(0, 2, 3, 1), (0, p.Cop - p.Co, 0, 0, 0, 0, 0, p.Cip - p.Ci))
 
 
 def _pair(make, seed=0):
@@ -327,3 +334,49 @@ def test_act_codes_reference_derivatives():
         g = Fn.act_grad_ref(a, code, 0.3)
         keep = (a.abs() > 1e-3) & ((a.abs() - 3).abs() > 1e-3) & ((a - 6).abs() > 1e-3)   # kinks
         assert torch.allclose(g[keep], x.grad[keep], atol=1e-5), name
+
+
+class _UpNet(nn.Module):
+    """LinkNet-style up path: 4x4 / stride-2 transposed conv + BN + ReLU, a 3x3 stride-2
+    transposed conv with output padding and a bias (no BN), odd channel counts."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv = nn.Conv2d(3, 20, 3, 2, 1)
+        self.up1 = nn.ConvTranspose2d(20, 12, 4, 2, 1)
+        self.bn1 = nn.BatchNorm2d(12)
+        self.up2 = nn.ConvTranspose2d(12, 5, 3, 2, 1, output_padding=1)
+
+    def forward(self, x):
+        x = F.relu(self.conv(x))
+        x = F.relu(self.bn1(self.up1(x)))
+        return self.up2(x)
+
+
+def test_transposed_conv_sites_match_fp32_autograd():
+    m, ref = _pair(_UpNet)
+    x = torch.randn(4, 3, 16, 16)
+    net = GenericNet(m, 'cpu')
+    out = net(x)
+    want = ref(x)
+    assert out.shape == want.shape == (4, 5, 32, 32)
+    g = torch.randn_like(want)
+    (out.float() * g).sum().backward()
+    (want * g).sum().backward()
+    assert _rel(out, want) < 2e-2
+    kinds = {p.name: getattr(p, 'kind', None) for p in net.param_sets()}
+    assert kinds['up1'] == 'tr' and kinds['up2'] == 'tr'
+    for p in net.param_sets():
+        gg = p.w.grad if hasattr(p, 'w') else p.gamma.grad
+        assert _cos(gg, _torch_grad(p, ref)) > 0.98, p.name
+        if getattr(p, 'b', None) is not None:
+            bb = dict(ref.named_modules())[p.name].bias.grad
+            assert _cos(p.b.grad[:bb.numel()], bb) > 0.98, p.name
+    # round trip of the transposed filters through the arena layout
+    net.export_to_torch()
+    assert torch.allclose(m.up2.weight, ref.up2.weight)
+
+
+def test_linknet_lowers_completely():
+    from mlcomp_amd.contrib.segmentation.models import Linknet
+    assert lower_or_none(Linknet(encoder_name='resnet34', classes=1)) is None

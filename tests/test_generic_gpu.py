@@ -142,7 +142,7 @@ def test_maxpool_ceil_mode():
 # ------------------------------------------------------------------ whole models
 def _models():
     from mlcomp_amd.models import build_model
-    from mlcomp_amd.contrib.segmentation.models import PSPNet, Unet
+    from mlcomp_amd.contrib.segmentation.models import Linknet, PSPNet, Unet
     from test_generic_cpu import RefCifarNet
     return {
         'lenet': (lambda: build_model('LeNet', num_classes=10), (32, 1, 28, 28), 10),
@@ -152,6 +152,7 @@ def _models():
         'efficientnet-b0': (lambda: build_model('efficientnet-b0', num_classes=10), (8, 3, 96, 96), 10),
         'unet-resnext50': (lambda: Unet(encoder_name='resnext50_32x4d', classes=1), (4, 3, 64, 64), None),
         'pspnet21': (lambda: PSPNet(encoder_name='resnet34', classes=21), (4, 3, 64, 64), 21),
+        'linknet': (lambda: Linknet(encoder_name='resnet34', classes=1), (4, 3, 64, 64), None),
     }
 
 
@@ -184,70 +185,68 @@ def _to_torch_layout(p, g):
             return g[:p.Co, :, :, :p.Ci].permute(0, 3, 1, 2)
         if p.kind == 'dw':
             return g[..., :p.Co].permute(2, 0, 1)[:, None]
+        if p.kind == 'tr':
+            return g[:p.Ci, :, :, :p.Co].permute(0, 3, 1, 2)
         return g.permute(0, 3, 1, 2)
     if hasattr(p, 'O'):
         return g[:p.O, :p.I]
     return g[:p.C]
 
 
-@pytest.mark.parametrize('name', ['lenet', 'cifarnet', 'resnext50', 'efficientnet-b0', 'pspnet21'])
-def test_generic_gpu_forward_matches_cpu_native_path(name):
-    """GPU kernels vs the CPU path of the same native ops (same weights, batch and bf16
-    rounding points): the model outputs agree to 2e-2 (at a resolution where the deepest
-    BatchNorms see more than a handful of values per channel)."""
+def _native_run(m, x, y, crit, device):
+    """Forward + backward of a model on the generic native engine: (output, {parameter name:
+    gradient in the torch parameter's layout}), all on the CPU."""
     from mlcomp_amd.models.native_generic import GenericNet
-    make, shape, ncls = _models()[name]
-    if shape[-1] == 96:
-        shape = shape[:2] + (160, 160)
-    torch.manual_seed(0)
-    m_gpu = _no_stochastic(make())
-    m_cpu = _no_stochastic(make())
-    m_cpu.load_state_dict(m_gpu.state_dict())
-    x, _, _ = _data(name, shape, ncls)
-    outs = [GenericNet(m, d)(x.to(d)).detach().float().cpu() for m, d in ((m_cpu, 'cpu'), (m_gpu, DEV))]
-    assert rel(outs[1], outs[0]) < 2e-2
+    net = GenericNet(m, device)
+    out = net(x.to(device))
+    crit(out.float(), y.to(device)).backward()
+    grads = {}
+    for p in net.param_sets():
+        g = p.w.grad if hasattr(p, 'w') else p.gamma.grad
+        if g is not None:
+            grads[p.name] = _to_torch_layout(p, g).detach().float().cpu()
+    return out.detach().float().cpu(), grads
+
+
+def _rel_map(a, b):
+    return {n: rel(a[n], b[n]) for n in b if n in a and float(b[n].norm()) > 0}
 
 
 @pytest.mark.parametrize('name', list(_models()))
-def test_generic_gradients_as_accurate_as_stock_bf16_autocast(name):
-    """Against fp32 autograd, the native engine's parameter gradients are as accurate as the
-    stock PyTorch-ROCm bf16 path (autocast, MIOpen / hipBLASLt) on the same weights and batch.
+def test_generic_gpu_step_matches_cpu_native_within_bf16_noise(name):
+    """The GPU kernels against the CPU path of the same native ops (same weights and batch,
+    same bf16 rounding points, fp32 accumulation in both) - forward output and every
+    parameter gradient.
 
-    Both are bf16 computations: at these small test shapes a deep net's gradients are far
-    from fp32 in BOTH (measured on the MI355X, scripts/debug/bisect_generic.py: SE-ResNeXt-50
-    at 96x96 mean direction cosine 0.65 native vs 0.63 autocast, U-Net-ResNeXt-50 0.35 vs
-    0.39; ReLU masks / max-pool winners flip on one-ulp differences), so the anchor is the
-    stock path's own error, per model: mean cosine within 0.03 of autocast's, and the
-    forward output no further from fp32 than autocast's plus 1e-2."""
-    from mlcomp_amd.models.native_generic import GenericNet
+    Bitwise agreement is impossible (fp32 summation order differs), and in a deep ReLU /
+    max-pool net one-ulp differences flip masks and winners that then move whole gradients.
+    The anchor is therefore measured, per model: the CPU path run again on the input
+    perturbed by ~one bf16 ulp (x * (1 + 2^-8 n)).  The GPU must be no further from the CPU
+    result than that perturbation moves it: output rel error <= max(2e-2, 2 x noise); mean
+    gradient direction cosine >= the perturbed run's - 0.02; and no parameter whose gradient
+    error exceeds 3 x its perturbation error + 5e-2 (a wrong kernel for one layer shows up
+    there even when the mean is fine)."""
     make, shape, ncls = _models()[name]
     torch.manual_seed(0)
     ms = [_no_stochastic(make()) for _ in range(3)]
     for m in ms[1:]:
         m.load_state_dict(ms[0].state_dict())
     x, y, crit = _data(name, shape, ncls)
-    ref = ms[0].train()                                   # fp32 autograd on the CPU
-    out_ref = ref(x)
-    crit(out_ref, y).backward()
-    g_ref = {n: p.grad.clone() for n, p in ref.named_parameters() if p.grad is not None}
-    auto = ms[1].to(DEV).train()          # NCHW: the reference Net's x.view() needs it
-    with torch.autocast('cuda', dtype=torch.bfloat16):
-        out_auto = auto(x.to(DEV))
-    crit(out_auto.float(), y.to(DEV)).backward()
-    cos_auto = [_cos(p.grad, g_ref[n]) for n, p in auto.named_parameters() if n in g_ref]
-    net = GenericNet(ms[2], DEV)
-    out_nat = net(x.to(DEV))
-    crit(out_nat.float(), y.to(DEV)).backward()
-    cos_nat = []
-    for p in net.param_sets():
-        n = p.name + ('.weight' if f'{p.name}.weight' in g_ref else '')
-        if n in g_ref:
-            g = p.w.grad if hasattr(p, 'w') else p.gamma.grad
-            cos_nat.append(_cos(_to_torch_layout(p, g), g_ref[n]))
-    torch.cuda.synchronize()
-    ca, cn = sum(cos_auto) / len(cos_auto), sum(cos_nat) / len(cos_nat)
-    assert cn >= ca - 0.03, (name, cn, ca)
-    assert rel(out_nat, out_ref) <= rel(out_auto, out_ref) + 1e-2, (rel(out_nat, out_ref), rel(out_auto, out_ref))
+    xp = x * (1 + 2 ** -8 * torch.randn_like(x))
+    out_c, g_c = _native_run(ms[0], x, y, crit, 'cpu')
+    out_p, g_p = _native_run(ms[1], xp, y, crit, 'cpu')
+    out_g, g_g = _native_run(ms[2], x, y, crit, DEV)
+    noise_out, err_out = rel(out_p, out_c), rel(out_g, out_c)
+    assert err_out <= max(2e-2, 2 * noise_out), (name, err_out, noise_out)
+    assert set(g_g) == set(g_c) and len(g_c) > 0
+    cos_n = sum(_cos(g_p[n], g_c[n]) for n in g_c) / len(g_c)
+    cos_g = sum(_cos(g_g[n], g_c[n]) for n in g_c) / len(g_c)
+    assert cos_g >= cos_n - 0.02, (name, cos_g, cos_n)
+    rn, rg = _rel_map(g_p, g_c), _rel_map(g_g, g_c)
+    bad = {n: (round(rg[n], 4), round(rn[n], 4)) for n in rg if rg[n] > 3 * rn[n] + 5e-2}
+    assert not bad, (name, bad)
+    print(f'{name}: out err {err_out:.4f} (noise {noise_out:.4f}), grad cos {cos_g:.4f} (noise {cos_n:.4f}), '
+          f'median grad rel {sorted(rg.values())[len(rg) // 2]:.4f} (noise {sorted(rn.values())[len(rn) // 2]:.4f})')
 
 
 @pytest.mark.parametrize('name,lr', [('cifarnet', 0.05), ('resnext50', 0.05), ('efficientnet-b0', 0.02)])
