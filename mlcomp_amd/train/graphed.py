@@ -19,10 +19,44 @@ step protocol from :class:`GraphedStep`:
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import warnings
 
 import torch
+
+
+_WORK_STREAMS = {}
+
+
+@contextlib.contextmanager
+def work_stream(device):
+    """Run the enclosed GPU work on a stream of the framework's own instead of the NULL
+    (default) stream, fenced to it on both sides; a no-op off the GPU or when the caller is
+    already on a non-default stream.
+
+    Measured on MI355X / ROCm 7 (scripts/debug/nan_test_loop.py): hundreds of eager native
+    kernels launched on the NULL stream between replays of a captured step graph make later
+    replays compute garbage (NaN within ~10 steps: a second model trained eagerly next to a
+    graphed one, an eager validation pass between graphed epochs); the same work on a
+    created stream does not.  The runner and every native step therefore keep their
+    kernels off the NULL stream."""
+    device = torch.device(device)
+    if device.type != 'cuda' or os.environ.get('MLC_WORK_STREAM', '1') == '0':
+        yield
+        return
+    cur = torch.cuda.current_stream(device)
+    if cur.cuda_stream != 0:
+        yield
+        return
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    st = _WORK_STREAMS.get(key)
+    if st is None:
+        st = _WORK_STREAMS[key] = torch.cuda.Stream(device)
+    st.wait_stream(cur)
+    with torch.cuda.stream(st):
+        yield
+    cur.wait_stream(st)
 
 
 class GraphedStep:
@@ -81,6 +115,10 @@ class GraphedStep:
     def __call__(self):
         self.calls += 1
         self.opt.prepare()
+        with work_stream(self.device):
+            self._call()
+
+    def _call(self):
         if not self.use_graph:
             self._body()
             return
@@ -97,24 +135,4 @@ class GraphedStep:
                 self.use_graph = False
                 self._body()
                 return
-        self._replay()
-
-    # Replays run on a stream of their own, fenced to the caller's stream on both sides.
-    # Measured on MI355X / ROCm 7: when hundreds of eager kernels (a second model's step)
-    # are launched on the SAME stream between replays of a graph, later replays compute
-    # garbage (NaN within ~8 steps, scripts/debug/nan_test_loop.py 'eg'); a host sync after
-    # the replay, or the eager work on another stream, avoids it.  Costs two event fences.
-    _replay_stream = None
-
-    def _replay(self):
-        cur = torch.cuda.current_stream(self.device)
-        if os.environ.get('MLC_GRAPH_OWN_STREAM', '1') == '0':
-            self.graph.replay()
-            return
-        if self._replay_stream is None:
-            self._replay_stream = torch.cuda.Stream(self.device)
-        rs = self._replay_stream
-        rs.wait_stream(cur)
-        with torch.cuda.stream(rs):
-            self.graph.replay()
-        cur.wait_stream(rs)
+        self.graph.replay()

@@ -18,7 +18,7 @@ from mlcomp_amd.models.native_generic import GenericNet
 from mlcomp_amd.ops.layers import flatten_bn_buffers
 from mlcomp_amd.parallel.comm import make_comm
 from mlcomp_amd.parallel.ddp import GradBucketer
-from mlcomp_amd.train.graphed import GraphedStep
+from mlcomp_amd.train.graphed import GraphedStep, work_stream
 from mlcomp_amd.train.optim import FusedAdam, FusedSGD
 
 
@@ -74,7 +74,7 @@ class NativeGenericStep(GraphedStep):
     def predict(self, x):
         self.net.eval()
         try:
-            with torch.no_grad():
+            with torch.no_grad(), work_stream(self.device):
                 return self.net(x.to(self.device))
         finally:
             self.net.train()

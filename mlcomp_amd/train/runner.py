@@ -624,9 +624,11 @@ class Runner:
             json.dump(self.experiment._config, f, indent=2, default=str)
 
     def run_experiment(self, stages: Optional[List[str]] = None, start_epoch: int = 0):
+        from mlcomp_amd.train.graphed import work_stream
         self.save_config()
-        for i, s in enumerate(stages or self.experiment.stages):
-            self.run_stage(s, start_epoch if i == 0 else 0)
+        with work_stream(self.device):       # no native kernel on the NULL stream (graphed.py)
+            for i, s in enumerate(stages or self.experiment.stages):
+                self.run_stage(s, start_epoch if i == 0 else 0)
         return self.state
 
 
