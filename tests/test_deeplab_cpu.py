@@ -97,4 +97,4 @@ def test_native_deeplab_predict_matches_torch_eval():
 def test_runner_picks_native_engine_for_deeplab():
     from mlcomp_amd.train.runner import _native_kind
     assert _native_kind(DeepLab(num_classes=1), torch.device('cuda')) == 'unet'
-    assert _native_kind(DeepLab(), torch.device('cuda')) is None          # 21-class softmax default
+    assert _native_kind(DeepLab(), torch.device('cuda')) == 'generic'     # 21-class softmax default

@@ -117,4 +117,5 @@ def test_native_linknet_predict_and_export_running_stats():
 def test_runner_picks_native_engine_for_linknet():
     from mlcomp_amd.train.runner import _native_kind
     assert _native_kind(Linknet(encoder_name='resnet18'), torch.device('cuda')) == 'unet'
-    assert _native_kind(Linknet(encoder_name='resnet18', decoder_use_batchnorm=False), torch.device('cuda')) is None
+    # BN-less decoder: not the hand engine, the generic one
+    assert _native_kind(Linknet(encoder_name='resnet18', decoder_use_batchnorm=False), torch.device('cuda')) == 'generic'

@@ -89,7 +89,7 @@ def test_native_pspnet_predict_matches_torch_eval():
 def test_runner_picks_native_engine_for_pspnet():
     from mlcomp_amd.train.runner import _native_kind
     assert _native_kind(PSPNet(encoder_name='resnet18', classes=1), torch.device('cuda')) == 'unet'
-    assert _native_kind(PSPNet(encoder_name='resnet18'), torch.device('cuda')) is None   # 21-class softmax
+    assert _native_kind(PSPNet(encoder_name='resnet18'), torch.device('cuda')) == 'generic'   # 21-class softmax
 
 
 def test_native_pspnet_unused_stages_frozen_under_weight_decay():
