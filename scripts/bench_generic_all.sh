@@ -3,6 +3,7 @@
 # Usage (on the GPU box): bash scripts/bench_generic_all.sh OUT_FILE [impl...]
 set -o pipefail
 OUT=${1:-gpurun_out/generic_bench.jsonl}; shift
+mkdir -p "$(dirname "$OUT")"
 IMPLS=${@:-native torch}
 T=${STEP_TIMEOUT:-240}
 run() {
