@@ -450,6 +450,154 @@ dw_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* 
   }
 }
 
+// ---- strip kernels (KW in {3, 5, 7}, stride 1 / 2, dilation 1): a thread owns one 8-channel
+// group and a strip of DW_SW consecutive output columns of one output row.  The x row
+// segment a strip needs for one filter row is loaded ONCE ((DW_SW-1)*S + KW vectors instead
+// of DW_SW*KW), every load is straight-line (out-of-range taps load a clamped address and are
+// zeroed), so a thread has ~20 16-byte loads in flight instead of one.
+constexpr int DW_SW = 8;
+
+__device__ __forceinline__ uint4 ld_or_zero(const bf16* base, long off, bool ok) {
+  const uint4 v = ldg16(base + (ok ? off : 0));
+  return ok ? v : make_uint4(0u, 0u, 0u, 0u);
+}
+
+// forward: acc[o] = sum_{r,s} x[ho*S-P+r][(wo0+o)*S-P+s] * w[r][s]
+template <int KW, int S>
+__global__ void __launch_bounds__(NT)
+dw_fwd_strip_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, bf16* __restrict__ y,
+                    float* __restrict__ sum, float* __restrict__ sumsq, int N, int H, int W, int C, int Ho, int Wo,
+                    int KH, int P) {
+  constexpr int XS = (DW_SW - 1) * S + KW;
+  const int G = C >> 3;
+  const int Wq = (Wo + DW_SW - 1) / DW_SW;
+  const long total = (long)N * Ho * Wq * G;
+  const long gtid = (long)blockIdx.x * NT + threadIdx.x;
+  const int cg = (int)(gtid % G);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  for (long i = gtid; i < total; i += (long)gridDim.x * NT) {
+    long t = i / G;
+    const int wq = (int)(t % Wq); t /= Wq;
+    const int ho = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    const int wo0 = wq * DW_SW;
+    const int wi0 = wo0 * S - P;
+    float acc[DW_SW][8];
+#pragma unroll
+    for (int o = 0; o < DW_SW; ++o)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[o][e] = 0.f;
+    for (int r = 0; r < KH; ++r) {
+      const int hi = ho * S - P + r;
+      if ((unsigned)hi >= (unsigned)H) continue;
+      const bf16* xr = x + ((long)n * H + hi) * W * C + cg * 8;
+      uint4 xv[XS], wv[KW];
+#pragma unroll
+      for (int j = 0; j < XS; ++j) {
+        const int wi = wi0 + j;
+        xv[j] = ld_or_zero(xr, (long)wi * C, (unsigned)wi < (unsigned)W);
+      }
+#pragma unroll
+      for (int q = 0; q < KW; ++q) wv[q] = ldg16(w + (long)(r * KW + q) * C + cg * 8);
+#pragma unroll
+      for (int q = 0; q < KW; ++q) {
+        float wf[8];
+        unpack8(wv[q], wf);
+#pragma unroll
+        for (int o = 0; o < DW_SW; ++o) {
+          float xf[8];
+          unpack8(xv[o * S + q], xf);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[o][e] += xf[e] * wf[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < DW_SW; ++o) {
+      if (wo0 + o < Wo) {
+        *reinterpret_cast<uint4*>(y + (((long)n * Ho + ho) * Wo + wo0 + o) * C + cg * 8) = pack8(acc[o]);
+        if (sum) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { s1[e] += acc[o][e]; s2[e] += acc[o][e] * acc[o][e]; }
+        }
+      }
+    }
+  }
+  if (sum) red_stats(s1, s2, sum, sumsq, C, G);
+}
+
+// weight gradient of filter row r = blockIdx.y: acc[q] = sum over pixels dy[p] * x[p@(r,q)],
+// reduced per block (LDS) and added into copy (block % NCOPY) of ws[NCOPY][KH*KW][C]
+template <int KW, int S>
+__global__ void __launch_bounds__(NT)
+dw_wgrad_strip_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* __restrict__ ws, int N,
+                      int H, int W, int C, int Ho, int Wo, int KH, int P) {
+  constexpr int XS = (DW_SW - 1) * S + KW;
+  __shared__ float rb[NT][KW * 8 + 1];
+  const int G = C >> 3;
+  const int r = blockIdx.y;
+  const int Wq = (Wo + DW_SW - 1) / DW_SW;
+  const long total = (long)N * Ho * Wq * G;
+  const long gtid = (long)blockIdx.x * NT + threadIdx.x;
+  const int cg = (int)(gtid % G);
+  float acc[KW][8];
+#pragma unroll
+  for (int q = 0; q < KW; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[q][e] = 0.f;
+  for (long i = gtid; i < total; i += (long)gridDim.x * NT) {
+    long t = i / G;
+    const int wq = (int)(t % Wq); t /= Wq;
+    const int ho = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    const int hi = ho * S - P + r;
+    if ((unsigned)hi >= (unsigned)H) continue;
+    const int wo0 = wq * DW_SW;
+    const int wi0 = wo0 * S - P;
+    const bf16* dyr = dy + ((long)n * Ho + ho) * Wo * C + cg * 8;
+    const bf16* xr = x + ((long)n * H + hi) * W * C + cg * 8;
+    uint4 gv[DW_SW], xv[XS];
+#pragma unroll
+    for (int o = 0; o < DW_SW; ++o) gv[o] = ld_or_zero(dyr, (long)(wo0 + o) * C, wo0 + o < Wo);
+#pragma unroll
+    for (int j = 0; j < XS; ++j) {
+      const int wi = wi0 + j;
+      xv[j] = ld_or_zero(xr, (long)wi * C, (unsigned)wi < (unsigned)W);
+    }
+#pragma unroll
+    for (int o = 0; o < DW_SW; ++o) {
+      float gf[8];
+      unpack8(gv[o], gf);
+#pragma unroll
+      for (int q = 0; q < KW; ++q) {
+        float xf[8];
+        unpack8(xv[o * S + q], xf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[q][e] += gf[e] * xf[e];
+      }
+    }
+  }
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < KW; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) rb[tid][q * 8 + e] = acc[q][e];
+  __syncthreads();
+  const int lanes = NT < G ? NT : G;
+  const int base_cg = (int)(((long)blockIdx.x * NT) % G);
+  float* dst = ws + (long)(blockIdx.x % NCOPY) * KH * KW * C;
+  for (int qq = tid; qq < lanes * KW * 8; qq += NT) {
+    const int l = qq % lanes, ke = qq / lanes;
+    const int q = ke >> 3, e = ke & 7;
+    float a = 0.f;
+    for (int u = l; u < NT; u += G) a += rb[u][q * 8 + e];
+    const int c = ((base_cg + l) % G) * 8 + e;
+    atomicAdd(dst + (long)(r * KW + q) * C + c, a);
+  }
+}
+
 // dw[t][c] (+)= sum over the NCOPY copies
 __global__ void __launch_bounds__(NT)
 copies_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n, int accumulate) {
@@ -481,6 +629,16 @@ inline int grid_groups(long work, int G, int cap) {
 inline int blocks_for(long work) {
   long b = (work + NT - 1) / NT;
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
+}
+
+// MLC_DW_STRIPS=0 selects the per-pixel depthwise kernels (A/B)
+inline bool dw_strips() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MLC_DW_STRIPS");
+    v = e ? atoi(e) : 1;
+  }
+  return v != 0;
 }
 
 inline bool grouped_ok(int C, int Co, int groups) {
@@ -563,6 +721,16 @@ MLC_EXPORT int mlc_dwconv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum,
                               int C, int KH, int KW, int S, int P, int D, int Ho, int Wo, hipStream_t st) {
   if (C % 8 || ((sum == nullptr) != (sumsq == nullptr))) return -1;
   const int G = C / 8;
+  if (D == 1 && (S == 1 || S == 2) && (KW == 3 || KW == 5 || KW == 7) && dw_strips()) {
+    const long work = (long)N * Ho * ((Wo + DW_SW - 1) / DW_SW) * G;
+    const dim3 grid(grid_groups(work, G, 2048));
+#define DWF(K, SS) hipLaunchKernelGGL((dw_fwd_strip_kernel<K, SS>), grid, dim3(NT), 0, st, x, w, y, sum, sumsq, N, H, \
+                                      W, C, Ho, Wo, KH, P)
+    if (S == 1) { if (KW == 3) DWF(3, 1); else if (KW == 5) DWF(5, 1); else DWF(7, 1); }
+    else { if (KW == 3) DWF(3, 2); else if (KW == 5) DWF(5, 2); else DWF(7, 2); }
+#undef DWF
+    return hipGetLastError();
+  }
   const long work = (long)N * Ho * ((Wo + DW_OW - 1) / DW_OW) * G;
   hipLaunchKernelGGL(dw_fwd_kernel, dim3(grid_groups(work, G, 2048)), dim3(NT), 0, st, x, w, y, sum, sumsq, N, H, W,
                      C, Ho, Wo, KH, KW, S, P, D);
@@ -583,6 +751,18 @@ MLC_EXPORT int mlc_dwconv_wgrad(const bf16* dy, const bf16* x, float* dw, float*
   if (C % 8) return -1;
   const int G = C / 8, T = KH * KW;
   mlc_zero_f32(ws, (long)NCOPY * T * C, st);
+  if (D == 1 && (S == 1 || S == 2) && (KW == 3 || KW == 5 || KW == 7) && dw_strips()) {
+    const long work = (long)N * Ho * ((Wo + DW_SW - 1) / DW_SW) * G;
+    const dim3 grid(grid_groups(work, G, 512), KH);
+#define DWW(K, SS) hipLaunchKernelGGL((dw_wgrad_strip_kernel<K, SS>), grid, dim3(NT), 0, st, dy, x, ws, N, H, W, C, \
+                                      Ho, Wo, KH, P)
+    if (S == 1) { if (KW == 3) DWW(3, 1); else if (KW == 5) DWW(5, 1); else DWW(7, 1); }
+    else { if (KW == 3) DWW(3, 2); else if (KW == 5) DWW(5, 2); else DWW(7, 2); }
+#undef DWW
+    hipLaunchKernelGGL(copies_reduce_kernel, dim3(blocks_for((long)T * C)), dim3(NT), 0, st, ws, dw, (long)T * C,
+                       accumulate);
+    return hipGetLastError();
+  }
   const long work = (long)N * Ho * Wo * G;
   const int blocks = grid_groups(work, G, 1024);
   for (int t0 = 0; t0 < T; t0 += DW_TC)

@@ -83,7 +83,16 @@ stats_kernel(const bf16* __restrict__ x, float* __restrict__ sum, float* __restr
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
   const long total = rows * G;
-  for (long i = gtid; i < total; i += stride) {
+  long i = gtid;
+  for (; i + stride < total; i += 2 * stride) {
+    float f[8], g[8];
+    const uint4 a = ldg16(x + i * 8), b = ldg16(x + (i + stride) * 8);
+    unpack8(a, f);
+    unpack8(b, g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s1[e] += f[e] + g[e]; s2[e] += f[e] * f[e] + g[e] * g[e]; }
+  }
+  if (i < total) {
     float f[8];
     unpack8(ldg16(x + i * 8), f);
 #pragma unroll
@@ -176,15 +185,24 @@ bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const
   for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; s1[j] = 0.f; s2[j] = 0.f; }
   const long total = rows * G;
   const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
-  for (long i = gtid; i < total; i += stride) {
-    const uint4 dv = ldg16(dz + i * 8), yv = ldg16(y + i * 8);
-    const uint4 zv = z ? ldg16(z + i * 8) : z4, rv = res ? ldg16(res + i * 8) : z4;
-    float d[8], yy[8];
-    unpack8(dv, d);
-    unpack8(yv, yy);
-    dU8(d, zv, yv, rv, res != nullptr, c, act, alpha);
+  for (long i0 = gtid; i0 < total; i0 += 2 * stride) {
+    const bool two = i0 + stride < total;
+    const long i1 = two ? i0 + stride : i0;
+    uint4 dv[2], yv[2], zv[2], rv[2];
+    dv[0] = ldg16(dz + i0 * 8); dv[1] = ldg16(dz + i1 * 8);
+    yv[0] = ldg16(y + i0 * 8); yv[1] = ldg16(y + i1 * 8);
+    zv[0] = z ? ldg16(z + i0 * 8) : z4; zv[1] = z ? ldg16(z + i1 * 8) : z4;
+    rv[0] = res ? ldg16(res + i0 * 8) : z4; rv[1] = res ? ldg16(res + i1 * 8) : z4;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { s1[j] += d[j]; s2[j] += d[j] * (yy[j] - mu[j]); }
+    for (int k = 0; k < 2; ++k) {
+      if (k == 1 && !two) break;
+      float d[8], yy[8];
+      unpack8(dv[k], d);
+      unpack8(yv[k], yy);
+      dU8(d, zv[k], yv[k], rv[k], res != nullptr, c, act, alpha);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s1[j] += d[j]; s2[j] += d[j] * (yy[j] - mu[j]); }
+    }
   }
   const int t = threadIdx.x;
 #pragma unroll
@@ -288,6 +306,19 @@ inline int grid_for(long rows, int C, int cap = 1024) {
   return (int)(((blocks + m - 1) / m) * m);
 }
 
+// block cap of the reducing passes: every block ends in C*2 float atomics onto one of 32
+// partial copies, so the per-address atomic chains grow with the block count (A/B knob
+// MLC_NORMACT_CAP; the streaming loop is unrolled by two to keep enough loads in flight)
+inline int reduce_cap() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MLC_NORMACT_CAP");
+    v = e ? atoi(e) : 512;
+    if (v < 32) v = 32;
+  }
+  return v;
+}
+
 inline int blocks_for(long work) {
   long b = (work + NT - 1) / NT;
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
@@ -300,7 +331,7 @@ using namespace normact;
 // sum/sumsq: 32*C fp32 each, zeroed by the caller; C % 8 == 0
 MLC_EXPORT int mlc_bn_stats(const bf16* x, float* sum, float* sumsq, long rows, int C, hipStream_t st) {
   if (C % 8) return -1;
-  hipLaunchKernelGGL(stats_kernel, dim3(grid_for(rows, C)), dim3(NT), 0, st, x, sum, sumsq, rows, C);
+  hipLaunchKernelGGL(stats_kernel, dim3(grid_for(rows, C, reduce_cap())), dim3(NT), 0, st, x, sum, sumsq, rows, C);
   return hipGetLastError();
 }
 
@@ -318,7 +349,8 @@ MLC_EXPORT int mlc_bnact_bwd_reduce(const bf16* dz, const bf16* z, const bf16* y
                                     const float* scale, const float* shift, const float* rscale, const float* rshift,
                                     float* sums, long rows, int C, int act, float alpha, hipStream_t st) {
   if (C % 8) return -1;
-  hipLaunchKernelGGL(bwd_reduce_kernel, dim3(grid_for(rows, C)), dim3(NT), 0, st, dz, z, y, res, mean, scale, shift,
+  hipLaunchKernelGGL(bwd_reduce_kernel, dim3(grid_for(rows, C, reduce_cap())), dim3(NT), 0, st, dz, z, y, res, mean,
+                     scale, shift,
                      rscale, rshift, sums, rows, C, act, alpha);
   return hipGetLastError();
 }

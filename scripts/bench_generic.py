@@ -63,9 +63,15 @@ def main():
         step = NativeGenericStep(model, x, y, device=dev, criterion=crit, optimizer=a.optimizer, **okw)
         run = step
     else:
-        model = model.to(dev).to(memory_format=torch.channels_last)
+        model = model.to(dev)
+        xc = x
+        try:                      # channels_last (MIOpen's NHWC kernels) unless the model's
+            with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16):   # views need NCHW
+                model.to(memory_format=torch.channels_last)(x.contiguous(memory_format=torch.channels_last))
+            xc = x.contiguous(memory_format=torch.channels_last)
+        except RuntimeError:
+            model = model.to(memory_format=torch.contiguous_format)
         opt = getattr(torch.optim, a.optimizer)(model.parameters(), **okw)
-        xc = x.contiguous(memory_format=torch.channels_last)
 
         def run():
             with torch.autocast('cuda', dtype=torch.bfloat16):

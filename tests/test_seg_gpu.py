@@ -371,3 +371,62 @@ def test_gn_relu_native_vs_fp32(N, H, W, C, G):
     assert rel(z.permute(0, 3, 1, 2), ref.detach()) < 1e-2
     assert rel(xn.grad.permute(0, 3, 1, 2), xr.grad) < 2e-2
     assert rel(u.g.grad, gn.weight.grad) < 1e-2 and rel(u.b.grad, gn.bias.grad) < 1e-2
+
+
+@pytest.mark.parametrize('arch', ['linknet', 'fpn', 'pspnet', 'deeplab'])
+def test_seg_engine_20_step_loss_trajectory_tracks_fp32(arch):
+    """20 Adam steps of the native engine (bf16, HIP graph) against fp32 PyTorch training the
+    same weights on the same batch: the loss trajectories agree step by step (mean relative
+    gap <= 5 %, every step within 12 %).  With MLC_TRAJ_OUT set the two trajectories are
+    appended there as a JSON line (the kept record, profiles/round4/trajectories.jsonl)."""
+    import json
+    import os
+    from mlcomp_amd.contrib.criterion import BCEDiceLoss
+    from mlcomp_amd.contrib.segmentation.deeplab import DeepLab
+    from mlcomp_amd.contrib.segmentation.models import FPN, Linknet, PSPNet
+    from mlcomp_amd.ops import functional as Fn
+    from mlcomp_amd.train.native_seg_step import NativeSegmentationStep
+
+    def make():
+        if arch == 'deeplab':
+            m = DeepLab(backbone='resnet', num_classes=1)
+        elif arch == 'fpn':
+            m = FPN(encoder_name='resnet34', classes=1, dropout=0.0)
+        elif arch == 'pspnet':
+            m = PSPNet(encoder_name='resnet34', classes=1, dropout=0.0)
+        else:
+            m = Linknet(encoder_name='resnet34', classes=1)
+        for mod in m.modules():
+            if isinstance(mod, (torch.nn.Dropout, torch.nn.Dropout2d)):
+                mod.p = 0.0
+        return m
+    torch.manual_seed(3)
+    tm = make()
+    ref = make()
+    ref.load_state_dict(tm.state_dict())
+    lr = 1e-4
+    st = NativeSegmentationStep(torch_model=tm, batch=4, image_size=128, device=DEV, use_graph=True, seed=3,
+                                warmup_eager=1, lr=lr)
+    x = Fn.stem_s2d_to_nhwc(st.x).permute(0, 3, 1, 2).float().contiguous()
+    t = st.t.view(4, 1, 128, 128).float()
+    ref = ref.to(DEV).train()
+    opt = torch.optim.Adam(ref.parameters(), lr=lr)
+    crit = BCEDiceLoss()
+    lf, ln = [], []
+    for _ in range(20):
+        opt.zero_grad(set_to_none=True)
+        loss = crit(ref(x), t)
+        loss.backward()
+        opt.step()
+        lf.append(float(loss.item()))
+        st()
+        ln.append(st.last_loss())
+    gaps = [abs(a - b) / abs(b) for a, b in zip(ln, lf)]
+    if os.environ.get('MLC_TRAJ_OUT'):
+        with open(os.environ['MLC_TRAJ_OUT'], 'a') as f:
+            f.write(json.dumps({'arch': arch, 'lr': lr, 'batch': 4, 'size': 128, 'native_bf16': ln,
+                                'torch_fp32': lf, 'mean_rel_gap': sum(gaps) / len(gaps),
+                                'max_rel_gap': max(gaps)}) + '\n')
+    assert st.graph is not None
+    assert sum(gaps) / len(gaps) <= 0.05 and max(gaps) <= 0.12, (arch, ln, lf)
+    assert ln[-1] < ln[0], ln
