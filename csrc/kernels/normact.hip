@@ -172,7 +172,7 @@ __global__ void __launch_bounds__(NT)
 bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const bf16* __restrict__ y,
                   const bf16* __restrict__ res, const float* __restrict__ mean, const float* __restrict__ scale,
                   const float* __restrict__ shift, const float* __restrict__ rscale, const float* __restrict__ rshift,
-                  float* __restrict__ sums, long rows, int C, int act, float alpha) {
+                  float* __restrict__ sums, long rows, int C, int act, float alpha, int direct) {
   __shared__ float rb[NT][17];
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
@@ -218,11 +218,20 @@ bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const
 #pragma unroll
       for (int e = 0; e < 8; ++e) { a[e] += rb[u][e]; b[e] += rb[u][8 + e]; }
     const int cg = (base_cg + t) % G;
-    float* dst = sums + (long)(blockIdx.x % NCOPY) * 2 * C;
+    if (direct) {   // one row of partial sums per block (every channel group covered): no atomics
+      float* dst = sums + (long)blockIdx.x * 2 * C;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      atomicAdd(dst + cg * 8 + e, a[e]);
-      atomicAdd(dst + C + cg * 8 + e, b[e]);
+      for (int e = 0; e < 8; ++e) {
+        dst[cg * 8 + e] = a[e];
+        dst[C + cg * 8 + e] = b[e];
+      }
+    } else {
+      float* dst = sums + (long)(blockIdx.x % NCOPY) * 2 * C;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        atomicAdd(dst + cg * 8 + e, a[e]);
+        atomicAdd(dst + C + cg * 8 + e, b[e]);
+      }
     }
   }
 }
@@ -262,6 +271,34 @@ bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const 
     for (int j = 0; j < 8; ++j) o[j] = k1[j] * d[j] + k2[j] + k3[j] * (yy[j] - mu[j]);
     *reinterpret_cast<uint4*>(dy + i * 8) = pack8(o);
   }
+}
+
+// S1 / S2 of channel c summed over the nrow partial rows [nrow][2][C], then the backward
+// coefficients (dy = k1*dU + k2 + k3*(y - mean)) and dgamma / dbeta (batchnorm.hip's math)
+__global__ void __launch_bounds__(NT)
+bwd_finalize_rows_kernel(const float* __restrict__ part, int nrow, const float* __restrict__ invstd,
+                         const float* __restrict__ gamma, float* __restrict__ coef, float* __restrict__ dgamma,
+                         float* __restrict__ dbeta, long rows, int C) {
+  // one wave per channel, its 64 lanes over the rows (a handful of independent loads each,
+  // the finalize must not run on a few CUs: C/4 blocks)
+  const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6), q = threadIdx.x & 63;
+  float S1 = 0.f, S2 = 0.f;
+  if (c < C) {
+    for (int k = q; k < nrow; k += 64) {
+      S1 += part[(size_t)k * 2 * C + c];
+      S2 += part[(size_t)k * 2 * C + C + c];
+    }
+  }
+  S1 = wave_sum(S1);
+  S2 = wave_sum(S2);
+  if (c >= C || q != 0) return;
+  const float invM = 1.f / (float)rows;
+  const float is = invstd[c];
+  const float k1 = gamma[c] * is;
+  coef[c] = k1;
+  coef[C + c] = -k1 * S1 * invM;
+  coef[2 * C + c] = -k1 * is * is * S2 * invM;
+  if (dgamma) { dgamma[c] = S2 * is; dbeta[c] = S1; }
 }
 
 // y = act(x) and dx = dy * act'(x) for a torch-free activation between native ops
@@ -351,7 +388,30 @@ MLC_EXPORT int mlc_bnact_bwd_reduce(const bf16* dz, const bf16* z, const bf16* y
   if (C % 8) return -1;
   hipLaunchKernelGGL(bwd_reduce_kernel, dim3(grid_for(rows, C, reduce_cap())), dim3(NT), 0, st, dz, z, y, res, mean,
                      scale, shift,
-                     rscale, rshift, sums, rows, C, act, alpha);
+                     rscale, rshift, sums, rows, C, act, alpha, 0);
+  return hipGetLastError();
+}
+
+// The whole BN(+act) backward in one call, with the reduction written as one row of partial
+// sums per block (plain stores; `part` holds part_floats >= blocks*2*C floats, C <= 2048)
+// instead of float atomics onto 32 copies: reduce -> finalize over the rows -> apply.
+MLC_EXPORT int mlc_bnact_bwd(const bf16* dz, const bf16* z, const bf16* y, const bf16* res, const float* mean,
+                             const float* scale, const float* shift, const float* invstd, const float* gamma,
+                             float* part, long part_floats, float* coef, float* dgamma, float* dbeta, bf16* dy,
+                             bf16* dres, long rows, int C, int act, float alpha, hipStream_t st) {
+  const int G = C >> 3;
+  if (C % 8 || G > NT || part_floats < 2L * C) return -1;
+  long cap = part_floats / (2L * C);
+  if (cap > reduce_cap()) cap = reduce_cap();
+  int blocks = grid_for(rows, C, (int)cap);
+  while (blocks > cap && blocks > 1) blocks = grid_for(rows, C, blocks / 2);   // rounding to C/8 multiples
+  if ((long)blocks * 2 * C > part_floats) return -1;
+  hipLaunchKernelGGL(bwd_reduce_kernel, dim3(blocks), dim3(NT), 0, st, dz, z, y, res, mean, scale, shift,
+                     (const float*)nullptr, (const float*)nullptr, part, rows, C, act, alpha, 1);
+  hipLaunchKernelGGL(bwd_finalize_rows_kernel, dim3((C + NT / 64 - 1) / (NT / 64)), dim3(NT), 0, st, part, blocks,
+                     invstd, gamma, coef, dgamma, dbeta, rows, C);
+  hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_for(rows, C, 768)), dim3(NT), 0, st, dz, z, y, res, mean, coef,
+                     scale, shift, (const float*)nullptr, (const float*)nullptr, dy, dres, rows, C, act, alpha);
   return hipGetLastError();
 }
 

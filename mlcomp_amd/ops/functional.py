@@ -1066,11 +1066,21 @@ def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0
     C = y.shape[-1]
     rows = y.numel() // C
     if _cuda(dz):
-        if sums is None:
-            sums = torch.zeros(NSTAT * 2 * C, device=dz.device, dtype=torch.float32)
         if coef is None:
             coef = torch.empty(3 * C, device=dz.device, dtype=torch.float32)
         zz = z if act in (4, 5) else None        # sigmoid / tanh read their derivative off z
+        if C <= 2048:          # (fixed summation order: deterministic as well)
+            # one call: reduce to per-block partial rows (no float atomics), finalize, apply
+            part = slab_workspace(dz.device, 512 * 2 * C)
+            dy = torch.empty_like(y)
+            dres = torch.empty_like(y) if want_dres else None
+            _lib.call('mlc_bnact_bwd', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
+                      _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(invstd), _lib.ptr(gamma), _lib.ptr(part), part.numel(),
+                      _lib.ptr(coef), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(dy), _lib.ptr(dres), rows, C,
+                      int(act), float(alpha), _lib.stream())
+            return dy, dres
+        if sums is None:
+            sums = torch.zeros(NSTAT * 2 * C, device=dz.device, dtype=torch.float32)
         _lib.call('mlc_bnact_bwd_reduce', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
                   _lib.ptr(scale), _lib.ptr(shift), None, None, _lib.ptr(sums), rows, C, int(act), float(alpha),
                   _lib.stream())
