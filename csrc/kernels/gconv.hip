@@ -598,6 +598,68 @@ dw_wgrad_strip_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, f
   }
 }
 
+// input gradient: dx[hi][wi0+o] = sum_{r,s} dy[(hi+P-r)/S][(wi0+o+P-s)/S] * w[r][s] over the
+// taps whose offsets divide by S.  wi0 is a multiple of 8, so with P = 2*ph + PP the dy
+// column a (o, s) pair reads is a compile-time offset from the strip's first column.
+constexpr int fdiv2(int a) { return a >= 0 ? a / 2 : -((-a + 1) / 2); }
+
+template <int KW, int S, int PP>
+__global__ void __launch_bounds__(NT)
+dw_dgrad_strip_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ w, bf16* __restrict__ dx, int N, int H,
+                      int W, int C, int Ho, int Wo, int KH, int P) {
+  constexpr int FB = S == 1 ? -(KW - 1) : fdiv2(PP - (KW - 1));
+  constexpr int NW = S == 1 ? DW_SW + KW - 1 : (DW_SW - 1 + PP) / 2 - FB + 1;
+  const int G = C >> 3;
+  const int Wq = (W + DW_SW - 1) / DW_SW;
+  const long total = (long)N * H * Wq * G;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int cg = (int)(i % G);
+    long t = i / G;
+    const int wq = (int)(t % Wq); t /= Wq;
+    const int hi = (int)(t % H);
+    const int n = (int)(t / H);
+    const int wi0 = wq * DW_SW;
+    const int col0 = S == 1 ? wi0 + P + FB : wi0 / 2 + (P - PP) / 2 + FB;
+    float acc[DW_SW][8];
+#pragma unroll
+    for (int o = 0; o < DW_SW; ++o)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[o][e] = 0.f;
+    for (int r = 0; r < KH; ++r) {
+      const int nh = hi + P - r;
+      if (nh < 0 || (S == 2 && (nh & 1))) continue;
+      const int ho = S == 1 ? nh : nh >> 1;
+      if (ho >= Ho) continue;
+      const bf16* dr = dy + ((long)n * Ho + ho) * Wo * C + cg * 8;
+      uint4 gv[NW], wv[KW];
+#pragma unroll
+      for (int j = 0; j < NW; ++j) {
+        const int wo = col0 + j;
+        gv[j] = ld_or_zero(dr, (long)wo * C, (unsigned)wo < (unsigned)Wo);
+      }
+#pragma unroll
+      for (int q = 0; q < KW; ++q) wv[q] = ldg16(w + (long)(r * KW + q) * C + cg * 8);
+#pragma unroll
+      for (int q = 0; q < KW; ++q) {
+        float wf[8];
+        unpack8(wv[q], wf);
+#pragma unroll
+        for (int o = 0; o < DW_SW; ++o) {
+          if (S == 2 && ((o + PP - q) & 1)) continue;             // compile-time
+          const int j = S == 1 ? o - q - FB : (o + PP - q) / 2 - FB;
+          float gf[8];
+          unpack8(gv[j], gf);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[o][e] += gf[e] * wf[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < DW_SW; ++o)
+      if (wi0 + o < W) *reinterpret_cast<uint4*>(dx + (((long)n * H + hi) * W + wi0 + o) * C + cg * 8) = pack8(acc[o]);
+  }
+}
+
 // dw[t][c] (+)= sum over the NCOPY copies
 __global__ void __launch_bounds__(NT)
 copies_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n, int accumulate) {
@@ -740,6 +802,17 @@ MLC_EXPORT int mlc_dwconv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum,
 MLC_EXPORT int mlc_dwconv_dgrad(const bf16* dy, const bf16* w, bf16* dx, int N, int H, int W, int C, int KH, int KW,
                                 int S, int P, int D, int Ho, int Wo, hipStream_t st) {
   if (C % 8) return -1;
+  if (D == 1 && (S == 1 || S == 2) && (KW == 3 || KW == 5 || KW == 7) && dw_strips()) {
+    const long work = (long)N * H * ((W + DW_SW - 1) / DW_SW) * (C / 8);
+    const dim3 grid(blocks_for(work));
+#define DWD(K, SS, PP) hipLaunchKernelGGL((dw_dgrad_strip_kernel<K, SS, PP>), grid, dim3(NT), 0, st, dy, w, dx, N, H, \
+                                          W, C, Ho, Wo, KH, P)
+    if (S == 1) { if (KW == 3) DWD(3, 1, 0); else if (KW == 5) DWD(5, 1, 0); else DWD(7, 1, 0); }
+    else if (P & 1) { if (KW == 3) DWD(3, 2, 1); else if (KW == 5) DWD(5, 2, 1); else DWD(7, 2, 1); }
+    else { if (KW == 3) DWD(3, 2, 0); else if (KW == 5) DWD(5, 2, 0); else DWD(7, 2, 0); }
+#undef DWD
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(dw_dgrad_kernel, dim3(blocks_for((long)N * H * W * (C / 8))), dim3(NT), 0, st, dy, w, dx, N, H,
                      W, C, Ho, Wo, KH, KW, S, P, D);
   return hipGetLastError();

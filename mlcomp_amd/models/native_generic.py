@@ -332,6 +332,16 @@ class GenericNet:
         finally:
             model.train(was)
         self._alias_residual_params(model)
+        # a BatchNorm called from one site of the training graph writes dgamma / dbeta straight
+        # into the (per-step zeroed) grad arena; a shared one accumulates through a scratch
+        uses = {}
+        for site in self.train_gm.modules():
+            bn = getattr(site, 'bn', None)
+            if isinstance(bn, BNParams):
+                uses[id(bn)] = uses.get(id(bn), 0) + 1
+        for p in self._params.values():
+            if isinstance(p, BNParams):
+                p.single_site = uses.get(id(p), 0) == 1
         ctx.finalize(self.device)
         for p in self._params.values():
             p.load_from_torch()

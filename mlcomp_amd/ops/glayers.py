@@ -321,6 +321,9 @@ class Site(nn.Module):
         super().__init__()
         object.__setattr__(self, 'ctx', ctx)   # not a submodule / not in state_dict
 
+    def _direct_bn_grads(self) -> bool:
+        return bool(getattr(self.bn, 'single_site', False)) and bool(getattr(self.ctx, 'grad_prezeroed', False))
+
     def params(self):
         """The parameter sets this site reads (their use counts gate mark_ready)."""
         return [p for p in (getattr(self, 'conv', None), getattr(self, 'bn', None), getattr(self, 'lin', None))
@@ -405,11 +408,12 @@ class ConvBNAct(Site):
         if bn is not None:
             xn, y, z, rn, scale, shift, mean, inv = saved
             ws = self.ctx.ws
+            d = self._direct_bn_grads()
             dy, dres = Fn.bnact_bwd(dz, z, y, rn if has_res else None, mean, scale, shift, inv, bn.gamma.master,
-                                    self.act, self.alpha, dgamma=_acc_view(bn.gamma), dbeta=_acc_view(bn.beta),
+                                    self.act, self.alpha, dgamma=_acc_view(bn.gamma, d), dbeta=_acc_view(bn.beta, d),
                                     sums=ws[self.k_bw], want_dres=has_res)
-            _acc_commit(bn.gamma)
-            _acc_commit(bn.beta)
+            _acc_commit(bn.gamma, d)
+            _acc_commit(bn.beta, d)
             if bn.uses.bwd_done():
                 bn.mark_ready()
         else:
@@ -434,9 +438,12 @@ class ConvBNAct(Site):
         return out
 
 
-def _acc_view(slot):
+def _acc_view(slot, direct=False):
     """BN dgamma / dbeta targets: the kernels overwrite, so a shared (multi-site) BN writes a
-    scratch that _acc_commit adds into the grad arena."""
+    scratch that _acc_commit adds into the grad arena; a single-site BN (``direct``) writes
+    the grad arena itself (zeroed once per step, so overwrite == accumulate)."""
+    if direct and slot.grad is not None:
+        return slot.grad
     buf = getattr(slot, '_scratch', None)
     if buf is None or buf.device != slot.grad.device:
         buf = torch.empty_like(slot.grad)
@@ -444,8 +451,9 @@ def _acc_view(slot):
     return buf
 
 
-def _acc_commit(slot):
-    slot.grad.add_(slot._scratch)
+def _acc_commit(slot, direct=False):
+    if not direct:
+        slot.grad.add_(slot._scratch)
 
 
 class BNAct(Site):
@@ -494,11 +502,12 @@ class BNAct(Site):
         bn = self.bn
         yn, z, rn, scale, shift, mean, inv = saved
         dz = self._to(dout)
+        d = self._direct_bn_grads()
         dy, dres = Fn.bnact_bwd(dz, z, yn, rn if has_res else None, mean, scale, shift, inv, bn.gamma.master,
-                                self.act, self.alpha, dgamma=_acc_view(bn.gamma), dbeta=_acc_view(bn.beta),
+                                self.act, self.alpha, dgamma=_acc_view(bn.gamma, d), dbeta=_acc_view(bn.beta, d),
                                 sums=self.ctx.ws[self.k_bw], want_dres=has_res)
-        _acc_commit(bn.gamma)
-        _acc_commit(bn.beta)
+        _acc_commit(bn.gamma, d)
+        _acc_commit(bn.beta, d)
         if bn.uses.bwd_done():
             bn.mark_ready()
         like = dout
