@@ -649,6 +649,13 @@ def linear_wgrad(dout, x, out=None, accumulate=False):
     spread the long token reduction over the whole chip."""
     B, O = dout.shape
     I = x.shape[1]
+    if _cuda(dout) and B % 8:
+        # the GEMM reduces over the rows in 8-row chunks: zero rows add nothing (a batch of
+        # 4 sequences in BERT's classifier head)
+        pad = 8 - B % 8
+        dout = torch.nn.functional.pad(dout, (0, 0, 0, pad))
+        x = torch.nn.functional.pad(x, (0, 0, 0, pad))
+        B += pad
     if _cuda(dout):
         dw = out if out is not None else torch.empty(O, I, device=dout.device, dtype=torch.float32)
         if accumulate:
