@@ -31,9 +31,15 @@ struct GGeom {
   int N, Hi, Wi, Ci;        // operand image (x; dy for the transposed map)
   int Ho, Wo, Co;           // output image (y; dx for the transposed map)
   int KH, KW, S, P, D;
-  int Cg, KB, T, Kp;        // group width, K channels per tap, taps, padded K (mult. of 32)
+  int Cg, KB, T, Kp;        // K-side channels per group, K channels per tap (mult. of 16), taps,
+                            // padded K (mult. of 32)
+  int Cog;                  // output channels per group
   long M;                   // output pixels
 };
+
+// first K-side channel (8-aligned) of the 16-channel output block starting at oc0: the block
+// spans the groups oc0/Cog .. (oc0+15)/Cog, whose K-side channels start at (oc0/Cog)*Cg
+__device__ __host__ __forceinline__ int blk_cbase(int oc0, int Cog, int Cg) { return (oc0 / Cog) * Cg & ~7; }
 
 __device__ __forceinline__ bf16x8 ldfrag(const bf16* p) {
   return *reinterpret_cast<const bf16x8*>(p);
@@ -43,22 +49,24 @@ __device__ __forceinline__ bf16x8 ldfrag(const bf16* p) {
 // WB[ob][j][k] (k < Kp): the B operand of the 16-column output block ob.  tr = 0: the
 // forward filter w[Co][T][Cg]; tr = 1: the dgrad filter (output channel = the conv's
 // input channel, K over the conv's output channels of the group).
+// Cout: output channels (rows of wb: Cout rounded up to 16), Cin: K-side channels; Cg / Cog:
+// K-side / output channels per group
 __global__ void __launch_bounds__(NT)
-expand_kernel(const bf16* __restrict__ w, bf16* __restrict__ wb, int Cout, int T, int Cg, int KB, int Kp,
-              int tr) {
-  const long total = (long)Cout * Kp;
+expand_kernel(const bf16* __restrict__ w, bf16* __restrict__ wb, int Cout, int Cin, int T, int Cg, int Cog,
+              int KB, int Kp, int tr) {
+  const long total = (long)((Cout + 15) / 16 * 16) * Kp;
   for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
     const int k = (int)(i % Kp);
     const int oc = (int)(i / Kp);           // = ob*16 + j
     float v = 0.f;
-    if (k < T * KB) {
+    if (k < T * KB && oc < Cout) {
       const int t = k / KB, kb = k % KB;
-      const int g = oc / Cg;
-      const int cbase = Cg >= 16 ? g * Cg : (oc / 16) * 16;
-      const int ci = cbase + kb;            // the K-side channel
-      if (ci / Cg == g) {
-        // forward: w[oc][t][ci - g*Cg]; transposed: the conv's output channel is ci
-        v = tr ? (float)w[((long)ci * T + t) * Cg + (oc - g * Cg)] : (float)w[((long)oc * T + t) * Cg + (ci - g * Cg)];
+      const int g = oc / Cog;
+      const int ci = blk_cbase(oc & ~15, Cog, Cg) + kb;   // the K-side channel
+      if (ci < Cin && ci / Cg == g) {
+        // forward: w[oc][t][ci - g*Cg]; transposed: the conv's output channel is ci and its
+        // filter rows hold Cog (= the conv's input width per group) values
+        v = tr ? (float)w[((long)ci * T + t) * Cog + (oc - g * Cog)] : (float)w[((long)oc * T + t) * Cg + (ci - g * Cg)];
       }
     }
     wb[i] = (bf16)v;
@@ -76,8 +84,7 @@ gconv_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wb, bf16* __r
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ob = blockIdx.y;
   const int oc0 = ob * 16;
-  const int grp = oc0 / g.Cg;
-  const int cbase = g.Cg >= 16 ? grp * g.Cg : oc0;   // first K-side channel of the block
+  const int cbase = blk_cbase(oc0, g.Cog, g.Cg);     // first K-side channel of the block
   const long m0 = (long)blockIdx.x * 128 + wave * 32;
   const int hl = lane >> 4;                          // k-chunk (8 channels) of the lane
   // the two sub-tiles' rows of this lane
@@ -118,7 +125,7 @@ gconv_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wb, bf16* __r
         hi = nh / g.S;
         wi = nw / g.S;
       }
-      v = v && (unsigned)hi < (unsigned)g.Hi && (unsigned)wi < (unsigned)g.Wi;
+      v = v && (unsigned)hi < (unsigned)g.Hi && (unsigned)wi < (unsigned)g.Wi && cbase + kb < g.Ci;
       a[s] = v ? ldfrag(in + (((long)n[s] * g.Hi + hi) * g.Wi + wi) * g.Ci + cbase + kb) : zero;
     }
 #pragma unroll
@@ -139,7 +146,7 @@ gconv_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wb, bf16* __r
       }
     s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
     s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
-    if (lane < 16) {
+    if (lane < 16 && oc0 + j < g.Co) {
       const int slot = (int)((blockIdx.x * 4 + wave) % NCOPY);
       atomicAdd(sum + (long)slot * g.Co + oc0 + j, s1);
       atomicAdd(sumsq + (long)slot * g.Co + oc0 + j, s2);
@@ -155,7 +162,7 @@ gconv_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wb, bf16* __r
   __builtin_amdgcn_wave_barrier();
   {
     const long m = m0 + (lane >> 1);
-    if (m < g.M)
+    if (m < g.M && oc0 + 8 * (lane & 1) < g.Co)      // Co % 8 == 0: whole 8-channel chunks
       *reinterpret_cast<uint4*>(out + m * g.Co + oc0 + 8 * (lane & 1)) =
           *reinterpret_cast<const uint4*>(st + (lane >> 1) * 16 + 8 * (lane & 1));
   }
@@ -192,8 +199,7 @@ gconv_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, floa
   __shared__ float red[4][WG_NCB][16][17];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ob = blockIdx.y, oc0 = ob * 16;
-  const int grp = oc0 / g.Cg;
-  const int cbase = g.Cg >= 16 ? grp * g.Cg : oc0;
+  const int cbase = blk_cbase(oc0, g.Cog, g.Cg);
   const int nsub = g.KB / 16;                       // 16-channel input blocks per tap
   const int cb0 = blockIdx.z * WG_NCB;
   const int ncb = min(WG_NCB, ncb_total - cb0);
@@ -225,12 +231,13 @@ gconv_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, floa
       ho = (int)(t % g.Ho);
       n = (int)(t / g.Ho);
     }
-    uint4 va = pv ? ldg16(dy + p * g.Co + oc0 + 8 * half) : z4;
+    uint4 va = pv && oc0 + 8 * half < g.Co ? ldg16(dy + p * g.Co + oc0 + 8 * half) : z4;
     uint4 vb[WG_NCB];
 #pragma unroll
     for (int c = 0; c < WG_NCB; ++c) {
       const int hi = ho * g.S - g.P + tr_[c] * g.D, wi = wo * g.S - g.P + ts_[c] * g.D;
-      const bool v = pv && c < ncb && (unsigned)hi < (unsigned)g.Hi && (unsigned)wi < (unsigned)g.Wi;
+      const bool v = pv && c < ncb && (unsigned)hi < (unsigned)g.Hi && (unsigned)wi < (unsigned)g.Wi &&
+                     tc_[c] < g.Ci;
       vb[c] = v ? ldg16(x + (((long)n * g.Hi + hi) * g.Wi + wi) * g.Ci + tc_[c]) : z4;
     }
     __builtin_amdgcn_wave_barrier();   // the previous iteration's reads are done (same wave)
@@ -262,8 +269,8 @@ gconv_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, floa
     const float v = red[0][c][row][cl] + red[1][c][row][cl] + red[2][c][row][cl] + red[3][c][row][cl];
     const int cb = cb0 + c, t = cb / nsub, sb = cb - t * nsub;
     const int oc = oc0 + row, ci = cbase + 16 * sb + cl;
-    if (ci / g.Cg != oc / g.Cg) continue;              // off the block diagonal
-    atomicAdd(dw + ((long)oc * g.T + t) * g.Cg + (ci - (oc / g.Cg) * g.Cg), v);
+    if (oc >= g.Co || ci >= g.Ci || ci / g.Cg != oc / g.Cog) continue;   // off the block diagonal
+    atomicAdd(dw + ((long)oc * g.T + t) * g.Cg + (ci - (oc / g.Cog) * g.Cg), v);
   }
 }
 
@@ -703,18 +710,32 @@ inline bool dw_strips() {
   return v != 0;
 }
 
+// K-side channels per tap that every 16-channel output block needs (its groups' K-side
+// channel span, 8-aligned), rounded up to 16
+inline int block_kb(int Cout, int Cog, int Cg) {
+  int kb = 16;
+  for (int oc0 = 0; oc0 < Cout; oc0 += 16) {
+    const int last = (oc0 + 15 < Cout ? oc0 + 15 : Cout - 1) / Cog;
+    const int hi = ((last + 1) * Cg + 7) & ~7;
+    const int w = hi - blk_cbase(oc0, Cog, Cg);
+    if (w > kb) kb = w;
+  }
+  return (kb + 15) / 16 * 16;
+}
+
+// any group widths (C/groups may differ from Co/groups), channel counts multiple of 8; the
+// K-side span of a 16-channel output block is bounded so the block-diagonal waste stays small
 inline bool grouped_ok(int C, int Co, int groups) {
-  if (groups < 2 || C % groups || Co % groups || C / groups != Co / groups) return false;
-  const int Cg = C / groups;
-  return (16 % Cg == 0 || Cg % 16 == 0) && C % 16 == 0 && Co % 16 == 0;
+  if (groups < 2 || C % groups || Co % groups || C % 8 || Co % 8) return false;
+  return block_kb(Co, Co / groups, C / groups) <= 256 && block_kb(C, C / groups, Co / groups) <= 256;
 }
 
 inline GGeom mkg(int N, int Hi, int Wi, int Ci, int Ho, int Wo, int Co, int KH, int KW, int S, int P, int D,
-                 int Cg) {
+                 int Cg, int Cog) {
   GGeom g;
   g.N = N; g.Hi = Hi; g.Wi = Wi; g.Ci = Ci; g.Ho = Ho; g.Wo = Wo; g.Co = Co;
   g.KH = KH; g.KW = KW; g.S = S; g.P = P; g.D = D;
-  g.Cg = Cg; g.KB = Cg > 16 ? Cg : 16; g.T = KH * KW; g.Kp = (g.T * g.KB + 31) / 32 * 32;
+  g.Cg = Cg; g.Cog = Cog; g.KB = block_kb(Co, Cog, Cg); g.T = KH * KW; g.Kp = (g.T * g.KB + 31) / 32 * 32;
   g.M = (long)N * Ho * Wo;
   return g;
 }
@@ -723,10 +744,13 @@ inline GGeom mkg(int N, int Hi, int Wi, int Ci, int Ho, int Wo, int Co, int KH, 
 
 using namespace gconv;
 
-// bytes of the expanded filter (bf16) that mlc_gconv_fwd / _dgrad need in `wb`
-MLC_EXPORT long mlc_gconv_wb_elems(int Cout, int KH, int KW, int Cg) {
-  const int KB = Cg > 16 ? Cg : 16;
-  return (long)Cout * ((KH * KW * KB + 31) / 32 * 32);
+// elements of the expanded filter (bf16) that mlc_gconv_fwd (tr 0) / _dgrad (tr 1) need in
+// `wb`, for a conv with C input and Co output channels
+MLC_EXPORT long mlc_gconv_wb_elems(int C, int Co, int KH, int KW, int groups, int tr) {
+  if (groups < 1 || C % groups || Co % groups) return -1;
+  const int Cout = tr ? C : Co, Cog = Cout / groups, Cg = (tr ? Co : C) / groups;
+  const int KB = block_kb(Cout, Cog, Cg);
+  return (long)((Cout + 15) / 16 * 16) * ((KH * KW * KB + 31) / 32 * 32);
 }
 
 // y[N,Ho,Wo,Co] = grouped conv of x[N,H,W,C] with w[Co][KH][KW][C/groups]; wb: scratch of
@@ -735,10 +759,10 @@ MLC_EXPORT int mlc_gconv_fwd(const bf16* x, const bf16* w, bf16* wb, bf16* y, fl
                              int W, int C, int Co, int KH, int KW, int S, int P, int D, int Ho, int Wo, int groups,
                              hipStream_t st) {
   if (!grouped_ok(C, Co, groups) || ((sum == nullptr) != (sumsq == nullptr))) return -1;
-  const GGeom g = mkg(N, H, W, C, Ho, Wo, Co, KH, KW, S, P, D, C / groups);
-  hipLaunchKernelGGL(expand_kernel, dim3(blocks_for((long)Co * g.Kp)), dim3(NT), 0, st, w, wb, Co, g.T, g.Cg, g.KB,
-                     g.Kp, 0);
-  const dim3 grid((unsigned)((g.M + 127) / 128), Co / 16);
+  const GGeom g = mkg(N, H, W, C, Ho, Wo, Co, KH, KW, S, P, D, C / groups, Co / groups);
+  hipLaunchKernelGGL(expand_kernel, dim3(blocks_for((long)(Co + 15) / 16 * 16 * g.Kp)), dim3(NT), 0, st, w, wb, Co,
+                     C, g.T, g.Cg, g.Cog, g.KB, g.Kp, 0);
+  const dim3 grid((unsigned)((g.M + 127) / 128), (Co + 15) / 16);
   hipLaunchKernelGGL(gconv_kernel<false>, grid, dim3(NT), 0, st, x, wb, y, sum, sumsq, g);
   return hipGetLastError();
 }
@@ -748,10 +772,10 @@ MLC_EXPORT int mlc_gconv_dgrad(const bf16* dy, const bf16* w, bf16* wb, bf16* dx
                                int KH, int KW, int S, int P, int D, int Ho, int Wo, int groups, hipStream_t st) {
   if (!grouped_ok(C, Co, groups)) return -1;
   // the roles swap: operand image dy (Co channels), output dx (C channels)
-  const GGeom g = mkg(N, Ho, Wo, Co, H, W, C, KH, KW, S, P, D, C / groups);
-  hipLaunchKernelGGL(expand_kernel, dim3(blocks_for((long)C * g.Kp)), dim3(NT), 0, st, w, wb, C, g.T, g.Cg, g.KB,
-                     g.Kp, 1);
-  const dim3 grid((unsigned)((g.M + 127) / 128), C / 16);
+  const GGeom g = mkg(N, Ho, Wo, Co, H, W, C, KH, KW, S, P, D, Co / groups, C / groups);
+  hipLaunchKernelGGL(expand_kernel, dim3(blocks_for((long)(C + 15) / 16 * 16 * g.Kp)), dim3(NT), 0, st, w, wb, C,
+                     Co, g.T, g.Cg, g.Cog, g.KB, g.Kp, 1);
+  const dim3 grid((unsigned)((g.M + 127) / 128), (C + 15) / 16);
   hipLaunchKernelGGL(gconv_kernel<true>, grid, dim3(NT), 0, st, dy, wb, dx, nullptr, nullptr, g);
   return hipGetLastError();
 }
@@ -760,11 +784,11 @@ MLC_EXPORT int mlc_gconv_dgrad(const bf16* dy, const bf16* w, bf16* wb, bf16* dx
 MLC_EXPORT int mlc_gconv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int Co, int KH,
                                int KW, int S, int P, int D, int Ho, int Wo, int groups, int accumulate, hipStream_t st) {
   if (!grouped_ok(C, Co, groups)) return -1;
-  const GGeom g = mkg(N, H, W, C, Ho, Wo, Co, KH, KW, S, P, D, C / groups);
+  const GGeom g = mkg(N, H, W, C, Ho, Wo, Co, KH, KW, S, P, D, C / groups, Co / groups);
   if (!accumulate) mlc_zero_f32(dw, (long)Co * g.T * g.Cg, st);
   const int ncb = g.T * (g.KB / 16);
   const int zb = (ncb + WG_NCB - 1) / WG_NCB;
-  const int base = (Co / 16) * zb;
+  const int base = ((Co + 15) / 16) * zb;
   // enough pixel chunks to give the chip ~2048 blocks, at least 128 pixels each
   long chunks = (2048 + base - 1) / base;
   const long maxc = (g.M + 127) / 128;
@@ -773,7 +797,7 @@ MLC_EXPORT int mlc_gconv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, 
   long chunk = (g.M + chunks - 1) / chunks;
   chunk = (chunk + 127) / 128 * 128;
   chunks = (g.M + chunk - 1) / chunk;
-  const dim3 grid((unsigned)chunks, Co / 16, zb);
+  const dim3 grid((unsigned)chunks, (Co + 15) / 16, zb);
   hipLaunchKernelGGL(gconv_wgrad_kernel, grid, dim3(NT), 0, st, dy, x, dw, g, ncb, chunk);
   return hipGetLastError();
 }

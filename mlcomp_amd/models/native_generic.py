@@ -140,9 +140,9 @@ def _check_conv(name, m: nn.Conv2d):
         C = Cg * m.groups
         if m.groups == C and Co == C:
             return
-        if Co // m.groups != Cg or C % 16 or Co % 16 or not (16 % Cg == 0 or Cg % 16 == 0):
-            raise NativeUnsupported(f'{name}: grouped conv {C}->{Co} x{m.groups} groups (native: equal group '
-                                    'widths dividing or divisible by 16, channels % 16 == 0)')
+        if not Fn.gconv_ok(C, Co, m.groups):
+            raise NativeUnsupported(f'{name}: grouped conv {C}->{Co} x{m.groups} groups (native: channels % 8 == 0 '
+                                    'and a bounded block-diagonal span)')
 
 
 def _check_convT(name, m: nn.ConvTranspose2d):

@@ -870,6 +870,24 @@ def _nchw(x):
     return x.permute(0, 3, 1, 2).float()
 
 
+def gconv_block_kb(Cout: int, Cog: int, Cg: int) -> int:
+    """K-side channels per tap of the grouped-conv kernels (csrc/kernels/gconv.hip block_kb):
+    the widest 8-aligned K-side span of a 16-channel output block, rounded up to 16."""
+    kb = 16
+    for oc0 in range(0, Cout, 16):
+        last = min(oc0 + 15, Cout - 1) // Cog
+        lo = (oc0 // Cog) * Cg & ~7
+        kb = max(kb, (((last + 1) * Cg + 7) & ~7) - lo)
+    return (kb + 15) // 16 * 16
+
+
+def gconv_ok(C: int, Co: int, groups: int) -> bool:
+    """Shapes the grouped-conv kernels take (any group widths; channels % 8; bounded waste)."""
+    if groups < 2 or C % groups or Co % groups or C % 8 or Co % 8:
+        return False
+    return gconv_block_kb(Co, Co // groups, C // groups) <= 256 and gconv_block_kb(C, C // groups, Co // groups) <= 256
+
+
 def gconv_fwd(x, w, groups, stride=1, pad=0, dil=1, stats=None):
     """Grouped conv (groups > 1, C/groups == Co/groups): x [N,H,W,C] bf16, w [Co,KH,KW,Cg] bf16
     -> y [N,Ho,Wo,Co] bf16 on the 16x16x32 MFMA kernel (gconv.hip); ``stats`` as conv2d_fwd."""
@@ -878,7 +896,8 @@ def gconv_fwd(x, w, groups, stride=1, pad=0, dil=1, stats=None):
     Ho, Wo = conv_out_hw(H, W, KH, KW, stride, pad, dil)
     if _cuda(x):
         y = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.bfloat16)
-        wb = torch.empty(int(_lib.load().mlc_gconv_wb_elems(Co, KH, KW, Cg)), device=x.device, dtype=torch.bfloat16)
+        wb = torch.empty(int(_lib.load().mlc_gconv_wb_elems(C, Co, KH, KW, groups, 0)), device=x.device,
+                         dtype=torch.bfloat16)
         s1, s2 = stats if stats is not None else (None, None)
         _lib.call('mlc_gconv_fwd', _lib.ptr(x), _lib.ptr(w), _lib.ptr(wb), _lib.ptr(y), _lib.ptr(s1), _lib.ptr(s2),
                   N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo, groups, _lib.stream())
@@ -896,7 +915,8 @@ def gconv_dgrad(dy, w, x_shape, groups, stride=1, pad=0, dil=1):
     _, Ho, Wo, _ = dy.shape
     if _cuda(dy):
         dx = torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
-        wb = torch.empty(int(_lib.load().mlc_gconv_wb_elems(C, KH, KW, Cg)), device=dy.device, dtype=torch.bfloat16)
+        wb = torch.empty(int(_lib.load().mlc_gconv_wb_elems(C, Co, KH, KW, groups, 1)), device=dy.device,
+                         dtype=torch.bfloat16)
         _lib.call('mlc_gconv_dgrad', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(wb), _lib.ptr(dx), N, H, W, C, Co, KH, KW,
                   stride, pad, dil, Ho, Wo, groups, _lib.stream())
         return dx

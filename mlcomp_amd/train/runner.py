@@ -194,22 +194,23 @@ class Runner:
         natively; ``engine: auto`` falls back to the torch engine and the reason is kept
         (``engine_log``, reported to the task by the train executor)."""
         forced = self.engine == 'native'
-        kind = _native_kind(self.model, self.device) if self.device.type == 'cuda' else None
+        kind = _native_kind(self.model, self.device)
         reason = None
         if self.engine == 'torch':
             reason = 'engine: torch requested'
         elif self.precision != 'bf16':
             reason = f'precision {self.precision}: the native engines compute in bf16 (fp32 master weights)'
-        elif self.device.type != 'cuda':
-            reason = 'no HIP device: the native engines run on MI355X GPUs'
         elif kind is None:
-            reason = f'{type(self.model).__name__} has no native lowering: {_generic_reason(self.model)}'
+            reason = ('no HIP device: the native engines run on MI355X GPUs' if self.device.type != 'cuda' else
+                      f'{type(self.model).__name__} has no native lowering: {_generic_reason(self.model)}')
         if reason is None:
             from .native_spec import NativeUnsupported, native_plan
             try:
                 self._native_plan = native_plan(self.experiment, stage, kind)
             except NativeUnsupported as e:
                 reason = str(e)
+        if reason is None and self.device.type != 'cuda':
+            reason = 'no HIP device: the native engines run on MI355X GPUs'
         if reason is not None and forced:
             raise RuntimeError(f'engine: native cannot run stage {stage!r}: {reason}')
         if reason is not None:

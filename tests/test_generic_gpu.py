@@ -26,22 +26,26 @@ def _bf(*shape, scale=1.0):
 
 
 # ------------------------------------------------------------------ grouped / depthwise
-@pytest.mark.parametrize('N,H,W,C,Cg,k,s,p,d', [
-    (4, 14, 14, 128, 4, 3, 1, 1, 1), (2, 15, 13, 256, 8, 3, 2, 1, 1), (2, 9, 9, 256, 16, 3, 1, 1, 1),
-    (2, 7, 7, 512, 32, 3, 1, 1, 1), (2, 8, 8, 128, 64, 3, 2, 1, 1), (3, 10, 11, 64, 2, 3, 1, 2, 2),
-    (2, 6, 6, 64, 16, 1, 1, 0, 1), (1, 17, 19, 96, 32, 5, 2, 2, 1)])
-def test_grouped_conv_kernels_vs_fp32(N, H, W, C, Cg, k, s, p, d):
+@pytest.mark.parametrize('N,H,W,C,Cg,k,s,p,d,Co', [
+    (4, 14, 14, 128, 4, 3, 1, 1, 1, 128), (2, 15, 13, 256, 8, 3, 2, 1, 1, 256), (2, 9, 9, 256, 16, 3, 1, 1, 1, 256),
+    (2, 7, 7, 512, 32, 3, 1, 1, 1, 512), (2, 8, 8, 128, 64, 3, 2, 1, 1, 128), (3, 10, 11, 64, 2, 3, 1, 2, 2, 64),
+    (2, 6, 6, 64, 16, 1, 1, 0, 1, 64), (1, 17, 19, 96, 32, 5, 2, 2, 1, 96),
+    # dpn92 (3 channels per group), dpn107 (200 channels, x50), senet154 (2 in / 4 out per group),
+    # a depthwise conv with channel multiplier 2, and 24-wide groups
+    (2, 9, 10, 96, 3, 3, 1, 1, 1, 96), (2, 8, 8, 200, 4, 3, 2, 1, 1, 200), (2, 7, 9, 128, 2, 3, 1, 1, 1, 256),
+    (2, 8, 8, 32, 1, 3, 1, 1, 1, 64), (2, 6, 7, 96, 24, 3, 1, 1, 1, 96)])
+def test_grouped_conv_kernels_vs_fp32(N, H, W, C, Cg, k, s, p, d, Co):
     torch.manual_seed(0)
     groups = C // Cg
     x = _bf(N, H, W, C)
-    w = _bf(C, k, k, Cg, scale=0.2)
+    w = _bf(Co, k, k, Cg, scale=0.2)
     Ho, Wo = Fn.conv_out_hw(H, W, k, k, s, p, d)
-    dy = _bf(N, Ho, Wo, C)
-    s_cpu = torch.zeros(2, 32 * C)
+    dy = _bf(N, Ho, Wo, Co)
+    s_cpu = torch.zeros(2, 32 * Co)
     y_ref = Fn.gconv_fwd(x, w, groups, s, p, d, stats=(s_cpu[0], s_cpu[1]))
     dx_ref = Fn.gconv_dgrad(dy, w, x.shape, groups, s, p, d)
     dw_ref = Fn.gconv_wgrad(dy, x, w.shape, groups, s, p, d)
-    s_gpu = torch.zeros(2, 32 * C, device=DEV)
+    s_gpu = torch.zeros(2, 32 * Co, device=DEV)
     y = Fn.gconv_fwd(x.to(DEV), w.to(DEV), groups, s, p, d, stats=(s_gpu[0], s_gpu[1]))
     dx = Fn.gconv_dgrad(dy.to(DEV), w.to(DEV), x.shape, groups, s, p, d)
     dw = Fn.gconv_wgrad(dy.to(DEV), x.to(DEV), w.shape, groups, s, p, d)
@@ -49,8 +53,8 @@ def test_grouped_conv_kernels_vs_fp32(N, H, W, C, Cg, k, s, p, d):
     assert rel(y, y_ref) < 8e-3
     assert rel(dx, dx_ref) < 8e-3
     assert rel(dw, dw_ref) < 1e-3
-    s1 = s_gpu[0].view(32, C).sum(0).cpu()
-    assert rel(s1, s_cpu[0][:C]) < 1e-3 and rel(s_gpu[1].view(32, C).sum(0), s_cpu[1][:C]) < 1e-3
+    s1 = s_gpu[0].view(32, Co).sum(0).cpu()
+    assert rel(s1, s_cpu[0][:Co]) < 1e-3 and rel(s_gpu[1].view(32, Co).sum(0), s_cpu[1][:Co]) < 1e-3
     # accumulate mode adds onto the existing gradient
     dw2 = dw.clone()
     Fn.gconv_wgrad(dy.to(DEV), x.to(DEV), w.shape, groups, s, p, d, out=dw2, accumulate=True)
