@@ -30,6 +30,7 @@ struct ConvGeom {
   int N, H, W, C;      // input NHWC
   int Ho, Wo, Co;      // output
   int KH, KW, stride, pad, dil;
+  int padw;            // W-axis padding (pad is the H-axis one; equal unless packed, see unpack_pad)
   FastDiv fWo, fHo, fW, fH, fC, fCo, fKW;
 };
 
@@ -72,11 +73,22 @@ using igemm::ConvGeom;
 using igemm::DgradClass;
 using igemm::FastDiv;
 
+// The conv exports take one int `pad`: a plain value pads both axes; (1 << 30) | (pad_w << 15)
+// | pad_h packs per-axis paddings (a 1x7 / 7x1 conv with padding (0, 3) / (3, 0)).
+constexpr int PAD_PACKED = 1 << 30;
+static inline void unpack_pad(int pad, int& ph, int& pw) {
+  if (pad & PAD_PACKED) { ph = pad & 0x7fff; pw = (pad >> 15) & 0x7fff; }
+  else { ph = pad; pw = pad; }
+}
+static inline int pack_pad(int ph, int pw) { return ph == pw ? ph : (PAD_PACKED | (pw << 15) | ph); }
+
 static inline ConvGeom mkgeom(int N, int H, int W, int C, int Co, int KH, int KW, int stride, int pad,
                        int dil, int Ho, int Wo) {
   ConvGeom g;
   g.N = N; g.H = H; g.W = W; g.C = C; g.Co = Co; g.KH = KH; g.KW = KW;
-  g.stride = stride; g.pad = pad; g.dil = dil; g.Ho = Ho; g.Wo = Wo;
+  int ph, pw;
+  unpack_pad(pad, ph, pw);
+  g.stride = stride; g.pad = ph; g.padw = pw; g.dil = dil; g.Ho = Ho; g.Wo = Wo;
   g.fWo = FastDiv(Wo); g.fHo = FastDiv(Ho); g.fW = FastDiv(W); g.fH = FastDiv(H);
   g.fC = FastDiv(C); g.fCo = FastDiv(Co); g.fKW = FastDiv(KW);
   return g;
@@ -93,17 +105,19 @@ static inline DgradClass mkclass(int S, int ph, int pw, int H, int W, int Ho, in
   c.S = S; c.ph = ph; c.pw = pw;
   c.Hc = (H - ph + S - 1) / S; c.Wc = (W - pw + S - 1) / S;
   c.fWc = FastDiv(c.Wc > 0 ? c.Wc : 1); c.fHc = FastDiv(c.Hc > 0 ? c.Hc : 1);
-  auto axis = [&](int p, int KK, int& r0, int& step, int& n, int& d0, int& ds) {
+  int pad_h, pad_w;
+  unpack_pad(pad, pad_h, pad_w);
+  auto axis = [&](int p, int KK, int pd, int& r0, int& step, int& n, int& d0, int& ds) {
     r0 = -1; n = 0;
     for (int r = 0; r < KK; ++r)
-      if ((((p + pad - r * dil) % S) + S) % S == 0) { if (r0 < 0) r0 = r; ++n; }
+      if ((((p + pd - r * dil) % S) + S) % S == 0) { if (r0 < 0) r0 = r; ++n; }
     step = S / gcd_i(S, dil);
     if (n == 0) { r0 = 0; d0 = 0; ds = 0; return; }
-    d0 = (p + pad - r0 * dil) / S;
+    d0 = (p + pd - r0 * dil) / S;
     ds = step * dil / S;
   };
-  axis(ph, KH, c.r0, c.rstep, c.nr, c.dh0, c.dhs);
-  axis(pw, KW, c.s0, c.sstep, c.ns, c.dw0, c.dws);
+  axis(ph, KH, pad_h, c.r0, c.rstep, c.nr, c.dh0, c.dhs);
+  axis(pw, KW, pad_w, c.s0, c.sstep, c.ns, c.dw0, c.dws);
   c.ncb = (Co + 63) / 64;
   c.fns = FastDiv(c.ns > 0 ? c.ns : 1); c.fncb = FastDiv(c.ncb);
   c.tmin = (c.nr > 0 && c.ns > 0)

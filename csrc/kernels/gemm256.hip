@@ -174,7 +174,7 @@ struct ConvFwdA {
     g.fWo.divmod((unsigned)m, t, wo);
     g.fHo.divmod(t, n, ho);
     hb = (int)ho * g.stride - g.pad;
-    wb = (int)wo * g.stride - g.pad;
+    wb = (int)wo * g.stride - g.padw;
     return (((long long)n * g.H + hb) * g.W + wb) * g.C;
   }
   __device__ void init(St& st, int r0, int tid) const {

@@ -257,7 +257,7 @@ struct ConvFwdA {
     g.fWo.divmod((unsigned)m, t, wo);
     g.fHo.divmod(t, n, ho);
     hb = (int)ho * g.stride - g.pad;
-    wb = (int)wo * g.stride - g.pad;
+    wb = (int)wo * g.stride - g.padw;
     return (((long long)n * g.H + hb) * g.W + wb) * g.C;
   }
   __device__ void init(St& st, int m0, int tid) const {
@@ -465,7 +465,7 @@ struct ConvWgradB {
     unsigned t, w0, n0, h0;
     g.fWo.divmod((unsigned)p0, t, w0);
     g.fHo.divmod(t, n0, h0);
-    const long long b0 = (((long long)n0 * g.H + (int)h0 * g.stride - g.pad) * g.W + (int)w0 * g.stride - g.pad) * g.C;
+    const long long b0 = (((long long)n0 * g.H + (int)h0 * g.stride - g.pad) * g.W + (int)w0 * g.stride - g.padw) * g.C;
     const Rsrc rsr = rsrc(x + b0);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -474,7 +474,7 @@ struct ConvWgradB {
       g.fWo.divmod(w0 + (unsigned)kr, cw, wo);
       g.fHo.divmod(h0 + cw, ch, ho);
       const int hb = p0 + kr < P ? (int)ho * g.stride - g.pad : -(1 << 29);
-      const int wb = (int)wo * g.stride - g.pad;
+      const int wb = (int)wo * g.stride - g.padw;
       const unsigned rel = (unsigned)((((int)ch * g.H + ((int)ho - (int)h0) * g.stride) * g.W +
                                        ((int)wo - (int)w0) * g.stride) * g.C) * 2u;
 #pragma unroll
@@ -590,7 +590,7 @@ struct ConvWgradBBn : ConvWgradB<R> {
       g.fWo.divmod(w0 + (unsigned)kr, cw, wo);
       g.fHo.divmod(h0 + cw, ch, ho);
       hb[j] = p0 + kr < this->P ? (int)ho * g.stride - g.pad : -(1 << 29);
-      wb[j] = (int)wo * g.stride - g.pad;
+      wb[j] = (int)wo * g.stride - g.padw;
     }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -1600,7 +1600,9 @@ MLC_EXPORT int mlc_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, const bf1
 MLC_EXPORT int mlc_conv_tr_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, float* sumsq, int N, int Hi,
                                int Wi, int Cin, int Cout, int KH, int KW, int stride, int pad, int dil, int Ho,
                                int Wo, hipStream_t st) {
-  if (Hi != (Ho + 2 * pad - dil * (KH - 1) - 1) / stride + 1 || Wi != (Wo + 2 * pad - dil * (KW - 1) - 1) / stride + 1)
+  int pad_h, pad_w;
+  unpack_pad(pad, pad_h, pad_w);
+  if (Hi != (Ho + 2 * pad_h - dil * (KH - 1) - 1) / stride + 1 || Wi != (Wo + 2 * pad_w - dil * (KW - 1) - 1) / stride + 1)
     return -1;
   return conv_dgrad_impl(x, w, y, nullptr, N, Ho, Wo, Cout, Cin, KH, KW, stride, pad, dil, Hi, Wi, nullptr,
                          nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
@@ -1626,9 +1628,11 @@ MLC_EXPORT int mlc_conv_dgrad_t(const bf16* dy, const bf16* wt, bf16* dx, const 
   BnBwdEpi bn{bn_mask, bn_y0, bn_mean0, bn_sums0, bn_y1, bn_mean1, bn_sums1,
               bn_msc0, bn_msh0, bn_msc1, bn_msh1, g_mlc_ncopy};
   if (bn_y0 && g_mlc_det && ((long)N * H * W + 63) / 64 > g_mlc_ncopy) return -2;
-  const int ph = dil * (KH - 1) - pad, pw = dil * (KW - 1) - pad;
-  if (stride == 1 && ph >= 0 && ph == pw) {
-    if (Ho != H + 2 * pad - dil * (KH - 1) || Wo != W + 2 * pad - dil * (KW - 1)) return -1;
+  int pad_h, pad_w;
+  unpack_pad(pad, pad_h, pad_w);
+  const int ph = dil * (KH - 1) - pad_h, pw = dil * (KW - 1) - pad_w;
+  if (stride == 1 && ph >= 0 && pw >= 0) {
+    if (Ho != H + 2 * pad_h - dil * (KH - 1) || Wo != W + 2 * pad_w - dil * (KW - 1)) return -1;
     const int M = N * H * W, K = KH * KW * Co;
     const int tile = pick_tile(M, C);
     EpiBF16<> epi{dx, C, nullptr, nullptr, IdentityRows{}, addend, bn};
@@ -1639,7 +1643,7 @@ MLC_EXPORT int mlc_conv_dgrad_t(const bf16* dy, const bf16* wt, bf16* dx, const 
 #undef MKA
     }
     // geometry of the equivalent forward conv: input dy [N, Ho, Wo, Co], output [N, H, W, C]
-    const ConvGeom gf = mkgeom(N, Ho, Wo, Co, C, KH, KW, 1, ph, dil, H, W);
+    const ConvGeom gf = mkgeom(N, Ho, Wo, Co, C, KH, KW, 1, pack_pad(ph, pw), dil, H, W);
 #define MKA(R) (ConvFwdA<R>{dy, gf, M, K})
     MLC_TILE_DISPATCH(tile, M, C, K, 1, st, epi, MKA, MKB);
 #undef MKA

@@ -130,8 +130,10 @@ def _check_conv(name, m: nn.Conv2d):
         raise NativeUnsupported(f'{name}: padding_mode={m.padding_mode!r}')
     if isinstance(m.padding, str):
         raise NativeUnsupported(f'{name}: padding={m.padding!r}')
-    for attr in ('stride', 'padding', 'dilation'):
+    for attr in ('stride', 'dilation'):
         _pair(getattr(m, attr), f'{name}.{attr}')
+    if m.groups != 1:
+        _pair(m.padding, f'{name}.padding')        # grouped / depthwise kernels: one pad
     KH, KW = m.kernel_size
     if KH > 15 or KW > 15:
         raise NativeUnsupported(f'{name}: kernel {KH}x{KW} (native convs take <= 15x15)')

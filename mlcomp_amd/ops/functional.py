@@ -30,9 +30,19 @@ def _cuda(t):
 
 
 def conv_out_hw(H, W, KH, KW, stride, pad, dil):
-    Ho = (H + 2 * pad - dil * (KH - 1) - 1) // stride + 1
-    Wo = (W + 2 * pad - dil * (KW - 1) - 1) // stride + 1
+    ph, pw = (pad, pad) if isinstance(pad, int) else tuple(pad)
+    Ho = (H + 2 * ph - dil * (KH - 1) - 1) // stride + 1
+    Wo = (W + 2 * pw - dil * (KW - 1) - 1) // stride + 1
     return Ho, Wo
+
+
+def pack_pad(pad) -> int:
+    """The ``pad`` argument of the dense conv kernels: an int pads both axes, (pad_h, pad_w)
+    with different values is packed as (1 << 30) | (pad_w << 15) | pad_h (convgeom.h)."""
+    if isinstance(pad, int):
+        return pad
+    ph, pw = (int(v) for v in pad)
+    return ph if ph == pw else (1 << 30) | (pw << 15) | ph
 
 
 # ---------------------------------------------------------------- conv
@@ -59,7 +69,7 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, stride=1, pad=0, dil=1,
         s1, s2 = (stats if stats is not None else (None, None))
         sc, sh = in_affine if in_affine is not None else (None, None)
         _lib.call('mlc_conv_fwd', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(s1), _lib.ptr(s2),
-                  N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo, _lib.ptr(sc), _lib.ptr(sh), _lib.stream())
+                  N, H, W, C, Co, KH, KW, stride, pack_pad(pad), dil, Ho, Wo, _lib.ptr(sc), _lib.ptr(sh), _lib.stream())
         return y
     if in_affine is not None:
         x = bn_relu_input(x, in_affine)
@@ -91,7 +101,7 @@ def conv_transpose2d_fwd(x: torch.Tensor, w: torch.Tensor, out_hw, stride=2, pad
         y = torch.empty(N, Ho, Wo, Cout, device=x.device, dtype=torch.bfloat16)
         s1, s2 = (stats if stats is not None else (None, None))
         _lib.call('mlc_conv_tr_fwd', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(s1), _lib.ptr(s2),
-                  N, Hi, Wi, Cin, Cout, KH, KW, stride, pad, dil, Ho, Wo, _lib.stream())
+                  N, Hi, Wi, Cin, Cout, KH, KW, stride, pack_pad(pad), dil, Ho, Wo, _lib.stream())
         return y
     oph = Ho - ((Hi - 1) * stride - 2 * pad + dil * (KH - 1) + 1)
     opw = Wo - ((Wi - 1) * stride - 2 * pad + dil * (KW - 1) + 1)
@@ -216,10 +226,10 @@ def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=1, pad=0, di
         if wt is not None:
             assert tuple(wt.shape) == (Ci, KH, KW, Co), (wt.shape, w.shape)
             _lib.call('mlc_conv_dgrad_t', _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(addend), N, H, W,
-                      C, Co, KH, KW, stride, pad, dil, Ho, Wo, *[_lib.ptr(t) for t in b], _lib.stream())
+                      C, Co, KH, KW, stride, pack_pad(pad), dil, Ho, Wo, *[_lib.ptr(t) for t in b], _lib.stream())
             return dx
         _lib.call('mlc_conv_dgrad', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(dx), _lib.ptr(addend), N, H, W, C,
-                  Co, KH, KW, stride, pad, dil, Ho, Wo, *[_lib.ptr(t) for t in b], _lib.stream())
+                  Co, KH, KW, stride, pack_pad(pad), dil, Ho, Wo, *[_lib.ptr(t) for t in b], _lib.stream())
         return dx
     if wt is not None and dgrad_as_fwd_conv(KH, KW, stride, pad, dil):   # forward conv over wt
         dxf = F.conv2d(dy.permute(0, 3, 1, 2).float(), wt.permute(0, 3, 1, 2).float(), None, 1,
@@ -312,7 +322,7 @@ def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride=1, pad=0, di
         ws = slab_workspace(dy.device, min(32 * Co * KH * KW * Ci, 64 << 20)) if _USE_SLAB else None
         sc, sh = in_affine if in_affine is not None else (None, None)
         _lib.call('mlc_conv_wgrad', _lib.ptr(dy), _lib.ptr(x), _lib.ptr(dw), N, H, W, C, Co, KH, KW,
-                  stride, pad, dil, Ho, Wo, 0, int(accumulate), _lib.ptr(ws),
+                  stride, pack_pad(pad), dil, Ho, Wo, 0, int(accumulate), _lib.ptr(ws),
                   ws.numel() if ws is not None else 0, _lib.ptr(sc), _lib.ptr(sh), _lib.stream())
         return dw
     if in_affine is not None:
@@ -1009,7 +1019,7 @@ def conv2d_fwd_ex(x, w, bias=None, act=0, stride=1, pad=0, dil=1):
     if _cuda(x):
         y = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.bfloat16)
         _lib.call('mlc_conv_fwd_ex', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(bias), int(act), N, H, W, C, Co,
-                  KH, KW, stride, pad, dil, Ho, Wo, _lib.stream())
+                  KH, KW, stride, pack_pad(pad), dil, Ho, Wo, _lib.stream())
         return y
     yf = F.conv2d(_nchw(x), w.permute(0, 3, 1, 2).float(), bias, stride, pad, dil)
     if act == 3:
@@ -1026,7 +1036,7 @@ def conv2d_wgrad_bias(dy, x, w_shape, dbias, stride=1, pad=0, dil=1, out=None, a
         dw = out if out is not None else torch.empty(Co, KH, KW, Ci, device=dy.device, dtype=torch.float32)
         ws = slab_workspace(dy.device, min(32 * Co * KH * KW * Ci, 64 << 20)) if _USE_SLAB else None
         _lib.call('mlc_conv_wgrad_bias', _lib.ptr(dy), _lib.ptr(x), _lib.ptr(dw), _lib.ptr(dbias), N, H, W, C, Co,
-                  KH, KW, stride, pad, dil, Ho, Wo, int(accumulate), _lib.ptr(ws), ws.numel() if ws is not None else 0,
+                  KH, KW, stride, pack_pad(pad), dil, Ho, Wo, int(accumulate), _lib.ptr(ws), ws.numel() if ws is not None else 0,
                   _lib.stream())
         return dw
     dbias.add_(dy.float().sum(dim=(0, 1, 2)))

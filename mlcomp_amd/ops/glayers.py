@@ -82,6 +82,8 @@ class ConvParams:
         self.ctx, self.name, self.src = ctx, name, conv
         self.groups = conv.groups
         self.stride, self.pad, self.dil = conv.stride[0], conv.padding[0], conv.dilation[0]
+        if not isinstance(conv, nn.ConvTranspose2d) and conv.groups == 1 and conv.padding[0] != conv.padding[1]:
+            self.pad = (conv.padding[0], conv.padding[1])   # per-axis (dense convs: Inception's 1x7 / 7x1)
         if isinstance(conv, nn.ConvTranspose2d):
             Ci, Co, KH, KW = conv.weight.shape
             self.kind = 'tr'

@@ -301,3 +301,27 @@ def test_runner_trains_reference_lenet_natively(tmp_path):
     st = r.run_experiment()
     assert r.engine_log[0]['kind'] == 'generic' and r.engine_log[0]['engine'] == 'native'
     assert st.epoch_metrics['train_loss'] < 2.31 and 'valid_accuracy01' in st.epoch_metrics
+
+
+@pytest.mark.parametrize('N,H,W,C,Co,kh,kw,s,ph,pw', [(2, 17, 17, 64, 96, 1, 7, 1, 0, 3), (2, 17, 17, 64, 96, 7, 1, 1, 3, 0),
+                                                     (2, 15, 13, 32, 48, 7, 1, 2, 3, 0), (2, 9, 11, 16, 24, 1, 3, 2, 0, 1),
+                                                     (1, 8, 8, 8, 16, 3, 3, 1, 0, 2)])
+def test_dense_conv_per_axis_padding_vs_fp32(N, H, W, C, Co, kh, kw, s, ph, pw):
+    """Inception-style 1x7 / 7x1 convs with padding (0, 3) / (3, 0): the packed per-axis pad
+    through the implicit-GEMM forward, the parity-class input gradient and the weight
+    gradient, against the CPU path (F.conv2d with the same padding)."""
+    torch.manual_seed(0)
+    x = _bf(N, H, W, C)
+    w = _bf(Co, kh, kw, C, scale=0.2)
+    pad = (ph, pw)
+    Ho, Wo = Fn.conv_out_hw(H, W, kh, kw, s, pad, 1)
+    dy = _bf(N, Ho, Wo, Co)
+    y_ref = Fn.conv2d_fwd(x, w, s, pad, 1)
+    dx_ref = Fn.conv2d_dgrad(dy, w, x.shape, s, pad, 1)
+    dw_ref = Fn.conv2d_wgrad(dy, x, w.shape, s, pad, 1)
+    y = Fn.conv2d_fwd(x.to(DEV), w.to(DEV), s, pad, 1)
+    dx = Fn.conv2d_dgrad(dy.to(DEV), w.to(DEV), x.shape, s, pad, 1)
+    dw = Fn.conv2d_wgrad(dy.to(DEV), x.to(DEV), w.shape, s, pad, 1)
+    torch.cuda.synchronize()
+    assert y.shape == y_ref.shape == (N, Ho, Wo, Co)
+    assert rel(y, y_ref) < 8e-3 and rel(dx, dx_ref) < 8e-3 and rel(dw, dw_ref) < 1e-3
