@@ -86,7 +86,7 @@ def _pair(make, seed=0):
     return m, ref
 
 
-@pytest.mark.parametrize('name', ['LeNet', 'resnext50_32x4d', 'se_resnext50_32x4d', 'efficientnet-b0', 'dpn92', 'senet154',
+@pytest.mark.parametrize('name', ['LeNet', 'resnext50_32x4d', 'se_resnext50_32x4d', 'efficientnet-b0', 'dpn92', 'senet154', 'inceptionresnetv2',
                                   'mobilenet_v2', 'densenet121', 'dpn68', 'xception', 'vgg16', 'resnet18'])
 def test_zoo_lowers_completely(name):
     """Every conv / BN / linear / pool of these models becomes a native site: no call that
