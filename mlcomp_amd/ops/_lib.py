@@ -94,7 +94,7 @@ _SIGS = {
     'mlc_sqnorm': [vp, i64, vp, f32, vp],
     'mlc_opt_config': [i32, i32],
     # generic engine (gconv.hip, normact.hip, igemm.hip extras)
-    'mlc_gconv_wb_elems': [i32, i32, i32, i32],
+    'mlc_gconv_wb_elems': [i32] * 6,
     'mlc_gconv_fwd': [vp] * 6 + [i32] * 13 + [vp],
     'mlc_gconv_dgrad': [vp] * 4 + [i32] * 13 + [vp],
     'mlc_gconv_wgrad': [vp] * 3 + [i32] * 14 + [vp],

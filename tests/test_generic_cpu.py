@@ -305,7 +305,7 @@ def test_runner_picks_the_generic_engine_with_a_reason_for_the_rest(monkeypatch,
     class Odd(nn.Module):
         def __init__(self):
             super().__init__()
-            self.c = nn.Conv2d(3, 8, (1, 7), padding=(0, 3))
+            self.c = nn.Conv2d(3, 8, 3, padding=1, padding_mode='reflect')
 
         def forward(self, x):
             return self.c(x).mean((2, 3))
@@ -316,7 +316,7 @@ def test_runner_picks_the_generic_engine_with_a_reason_for_the_rest(monkeypatch,
     r.model = Odd()
     r.device = torch.device('cuda')      # selection only
     got = r._select_engine('stage1')
-    assert got['engine'] == 'torch' and 'padding' in got['reason'], got
+    assert got['engine'] == 'torch' and 'padding_mode' in got['reason'], got
     r.model = build_model('LeNet', num_classes=10)
     got = r._select_engine('stage1')
     assert got == {'stage': 'stage1', 'engine': 'native', 'kind': 'generic', 'precision': 'bf16', 'reason': None}
