@@ -1,0 +1,386 @@
+// Library GEMM backend (hipBLASLt) for the plain dense-layer GEMMs, and the per-shape
+// selection between it and the native MFMA kernels (igemm.hip).
+//
+// The dense layers of BERT-base (M = 4096 tokens, K = 768 / 3072) are plain GEMMs with a
+// bias or residual epilogue; on those shapes hipBLASLt's assembly kernels run 25-45 %
+// faster than the 128x128 / three-wide native tiles (profiles/round4/dense_tiles.txt),
+// while the native kernels win wherever an epilogue does real work (GELU + stored
+// derivative, GELU-derivative multiply, split-K column sums).  So the two exported entry
+// points the models call - mlc_gemm_bf16_ex and mlc_linear_wgrad_bias - pick per shape:
+//
+//   * the first EAGER call of a (kind, M, N, K, strides, epilogue) key times the native
+//     launcher and the top hipBLASLt heuristic algorithms on scratch outputs (same
+//     inputs, same stream) and caches the winner; hipBLASLt must win by MLC_BLASLT_MARGIN
+//     (default 3 %) so timing noise cannot flip a tie between processes;
+//   * calls under HIP-graph capture only read the cache (a key first seen while
+//     capturing runs native), so a captured step replays whatever warm-up chose;
+//   * deterministic mode (mlc_set_deterministic) always runs native.
+//
+// MLC_BLASLT=0 disables the library path, =1 forces it wherever it applies, unset/auto
+// times both.  Every hipBLASLt call gets a private workspace per (device, stream): the
+// weight-gradient side stream and the main stream may run GEMMs concurrently.
+//
+// Row-major problem C[M][N] = op(A) op(B) maps onto hipBLASLt's column-major D = A' B'
+// as D = C^T (N x M, ld ldc), A' = the B operand, B' = the A operand; the bias vector
+// runs along D's rows (N), which is the per-output-feature bias; BGRADB reduces B' over
+// k, which for the weight gradient dW = dY^T X is the bias gradient colsum(dY).
+#include <hipblaslt/hipblaslt.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "common.h"
+
+// native launchers (igemm.hip)
+extern "C" int mlc_gemm_bf16_ex_native(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int lda, int ldb,
+                                       int ldc, int ta, int tb, const float* bias, int act, bf16* preact,
+                                       const bf16* addend, const bf16* dact, float* ws, long ws_floats,
+                                       hipStream_t st);
+extern "C" int mlc_colsum_acc(const bf16* g, float* out, float* scratch, int R, int C, hipStream_t st);
+extern "C" int mlc_linear_wgrad_bias_native(const bf16* A, const bf16* B, float* C, float* dbias, int M, int N,
+                                            int K, int lda, int ldb, int ldc, int splits, float* ws, long ws_floats,
+                                            hipStream_t st);
+
+namespace {
+
+constexpr size_t kWorkspace = 32ull << 20;   // per (device, stream)
+constexpr int kBiasScratch = 1 << 16;        // floats: bias-gradient staging
+
+int g_mode = -1;          // 0 off, 1 force, 2 auto (timed)
+float g_margin = 0.03f;
+int g_verbose = 0;
+
+int mode() {
+  if (g_mode < 0) {
+    const char* e = getenv("MLC_BLASLT");
+    g_mode = !e || !strcmp(e, "auto") ? 2 : atoi(e) ? 1 : 0;
+    if (const char* m = getenv("MLC_BLASLT_MARGIN")) g_margin = (float)atof(m);
+    if (const char* v = getenv("MLC_BLASLT_VERBOSE")) g_verbose = atoi(v);
+  }
+  return g_mode;
+}
+
+struct StreamRes {
+  void* ws = nullptr;
+  float* bias = nullptr;     // BGRADB output, added into the bias gradient
+  float* colsum = nullptr;   // mlc_colsum_acc scratch (kept zeroed by the kernel)
+};
+constexpr int kColsumFloats = 32 * 8192;   // NSTAT copies x up to 8192 columns
+
+// Workspaces are allocated in one go on the first eager call (no allocation may happen
+// while a stream is being captured) and handed to streams as they show up - including
+// the graph-capture stream, which first appears mid-capture.
+constexpr int kSlots = 8;
+
+struct DevRes {
+  hipblasLtHandle_t handle = nullptr;
+  std::vector<StreamRes> slots;
+  std::map<hipStream_t, int> owner;
+};
+
+// kind 0: bf16 out (+bias | +addend);  kind 1: fp32 out accumulate (+ bias gradient)
+struct Key {
+  int dev, kind, M, N, K, lda, ldb, ldc, ta, tb, epi;
+  bool operator<(const Key& o) const {
+    return std::tie(dev, kind, M, N, K, lda, ldb, ldc, ta, tb, epi) <
+           std::tie(o.dev, o.kind, o.M, o.N, o.K, o.lda, o.ldb, o.ldc, o.ta, o.tb, o.epi);
+  }
+};
+
+struct Plan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr, d = nullptr;
+  std::vector<hipblasLtMatmulHeuristicResult_t> algos;
+  int pick = -1;            // -1 undecided, -2 native, >= 0 index into algos
+  int epi = 0;              // epilogue actually built (a weight gradient whose BGRADB form
+                            // has no kernel falls back to 0 + mlc_colsum_acc)
+  float t_native = 0.f, t_lib = 0.f;
+};
+
+std::mutex g_mu;
+std::map<int, DevRes> g_dev;
+std::map<Key, Plan> g_plans;
+
+bool capturing(hipStream_t st) {
+  hipStreamCaptureStatus s = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &s) != hipSuccess) return true;
+  return s != hipStreamCaptureStatusNone;
+}
+
+DevRes* dev_res(int dev, bool can_alloc) {
+  DevRes& r = g_dev[dev];
+  if (!r.handle) {
+    if (!can_alloc || hipblasLtCreate(&r.handle) != HIPBLAS_STATUS_SUCCESS) {
+      r.handle = nullptr;
+      return nullptr;
+    }
+    for (int i = 0; i < kSlots; ++i) {
+      StreamRes s;
+      if (hipMalloc(&s.ws, kWorkspace) != hipSuccess) break;
+      if (hipMalloc((void**)&s.bias, kBiasScratch * sizeof(float)) != hipSuccess ||
+          hipMalloc((void**)&s.colsum, kColsumFloats * sizeof(float)) != hipSuccess ||
+          hipMemset(s.colsum, 0, kColsumFloats * sizeof(float)) != hipSuccess) {
+        (void)hipFree(s.ws);
+        break;
+      }
+      r.slots.push_back(s);
+    }
+  }
+  return &r;
+}
+
+StreamRes* stream_res(DevRes* r, hipStream_t st) {
+  auto it = r->owner.find(st);
+  if (it != r->owner.end()) return &r->slots[it->second];
+  const int i = (int)r->owner.size();
+  if (i >= (int)r->slots.size()) return nullptr;   // more streams than slots: native
+  r->owner[st] = i;
+  return &r->slots[i];
+}
+
+__global__ void __launch_bounds__(256) vec_acc_kernel(float* __restrict__ dst, const float* __restrict__ src, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) dst[i] += src[i];
+}
+
+void destroy_plan(Plan& p) {
+  if (p.desc) hipblasLtMatmulDescDestroy(p.desc);
+  for (auto* l : {p.a, p.b, p.c, p.d})
+    if (l) hipblasLtMatrixLayoutDestroy(l);
+  p = Plan{};
+}
+
+bool build_plan(DevRes* r, const Key& k, Plan& p, int epi) {
+  p.epi = epi;
+  const hipblasOperation_t opA = k.tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;   // A' = the B operand
+  const hipblasOperation_t opB = k.ta ? HIPBLAS_OP_T : HIPBLAS_OP_N;   // B' = the A operand
+  const hipDataType dt = k.kind == 1 ? HIP_R_32F : HIP_R_16BF;
+  bool ok = hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) == HIPBLAS_STATUS_SUCCESS;
+  ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)) == 0;
+  ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)) == 0;
+  // epi: 0 none, 1 bias (kind 0), 2 bias gradient (kind 1)
+  const hipblasLtEpilogue_t ep = epi == 1 ? HIPBLASLT_EPILOGUE_BIAS
+                               : epi == 2 ? HIPBLASLT_EPILOGUE_BGRADB : HIPBLASLT_EPILOGUE_DEFAULT;
+  ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &ep, sizeof(ep)) == 0;
+  if (epi) {
+    const int32_t bt = HIP_R_32F;
+    ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)) == 0;
+  }
+  // A' (rows x cols, ld) in column-major terms
+  const uint64_t ar = k.tb ? k.K : k.N, ac = k.tb ? k.N : k.K;
+  const uint64_t br = k.ta ? k.M : k.K, bc = k.ta ? k.K : k.M;
+  ok = ok && hipblasLtMatrixLayoutCreate(&p.a, HIP_R_16BF, ar, ac, k.ldb) == 0;
+  ok = ok && hipblasLtMatrixLayoutCreate(&p.b, HIP_R_16BF, br, bc, k.lda) == 0;
+  ok = ok && hipblasLtMatrixLayoutCreate(&p.c, dt, k.N, k.M, k.ldc) == 0;
+  ok = ok && hipblasLtMatrixLayoutCreate(&p.d, dt, k.N, k.M, k.ldc) == 0;
+  if (!ok) return false;
+  hipblasLtMatmulPreference_t pref;
+  if (hipblasLtMatmulPreferenceCreate(&pref) != 0) return false;
+  const uint64_t wsb = kWorkspace;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
+  hipblasLtMatmulHeuristicResult_t res[4];
+  int n = 0;
+  const hipblasStatus_t s = hipblasLtMatmulAlgoGetHeuristic(r->handle, p.desc, p.a, p.b, p.c, p.d, pref, 4, res, &n);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (s != HIPBLAS_STATUS_SUCCESS) return false;
+  for (int i = 0; i < n; ++i)
+    if (res[i].state == HIPBLAS_STATUS_SUCCESS && res[i].workspaceSize <= kWorkspace) p.algos.push_back(res[i]);
+  return !p.algos.empty();
+}
+
+// D = op(A) op(B) (+bias) (+C)
+int run_lib(DevRes* r, StreamRes* s, Plan& p, int algo, const Key& k, const void* A, const void* B, const void* Cin,
+            void* D, const float* bias, float* bgrad, hipStream_t st) {
+  const float alpha = 1.f, beta = Cin ? 1.f : 0.f;
+  if (p.epi == 1) hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
+  if (p.epi == 2) hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bgrad, sizeof(bgrad));
+  const hipblasStatus_t e = hipblasLtMatmul(r->handle, p.desc, &alpha, B, p.a, A, p.b, &beta, Cin ? Cin : D, p.c, D,
+                                            p.d, &p.algos[algo].algo, s->ws, kWorkspace, st);
+  return e == HIPBLAS_STATUS_SUCCESS ? 0 : -100 - (int)e;
+}
+
+template <class F>
+float time_ms(F f, hipStream_t st) {
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  float best = 1e30f;
+  for (int rep = 0; rep < 3; ++rep) {
+    f();
+    hipEventRecord(a, st);
+    for (int i = 0; i < 5; ++i) f();
+    hipEventRecord(b, st);
+    hipEventSynchronize(b);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, a, b);
+    best = std::min(best, ms / 5);
+  }
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  return best;
+}
+
+// Resolve (building / timing as needed) the choice for key k.  Returns the Plan with
+// pick >= 0 when hipBLASLt should run, nullptr for native.  `native(out, bout)` and
+// `lib(algo, out, bout)` run the two candidates into the given outputs.
+template <class FN, class FL>
+Plan* choose(const Key& k, hipStream_t st, size_t out_bytes, FN native, FL lib, DevRes** rp, StreamRes** sp) {
+  const int m = mode();
+  if (m == 0 || g_mlc_det) return nullptr;
+  const bool cap = capturing(st);
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_plans.find(k);
+  if (it != g_plans.end() && it->second.pick == -2) return nullptr;
+  DevRes* r = dev_res(k.dev, !cap);
+  if (!r) return nullptr;
+  StreamRes* s = stream_res(r, st);
+  if (!s) return nullptr;
+  *rp = r;
+  *sp = s;
+  if (it != g_plans.end() && it->second.pick >= 0) return &it->second;
+  if (cap) return nullptr;   // first seen under capture: native (nothing may be timed now)
+  Plan& p = g_plans[k];
+  bool built = build_plan(r, k, p, k.epi);
+  if (!built && k.kind == 1) {   // no BGRADB kernel for this problem: plain GEMM + column sums
+    destroy_plan(p);
+    built = build_plan(r, k, p, 0);
+  }
+  if (!built) {
+    p.pick = -2;
+    return nullptr;
+  }
+  if (m == 1) {
+    p.pick = 0;
+    return &p;
+  }
+  void* out = nullptr;
+  float* bout = nullptr;
+  if (hipMalloc(&out, out_bytes) != hipSuccess || hipMalloc((void**)&bout, (size_t)(k.M + k.N) * 4) != hipSuccess) {
+    if (out) (void)hipFree(out);
+    p.pick = -2;
+    return nullptr;
+  }
+  hipMemsetAsync(out, 0, out_bytes, st);
+  hipMemsetAsync(bout, 0, (size_t)(k.M + k.N) * 4, st);
+  p.t_native = time_ms([&] { native(out, bout); }, st);
+  int best = -2;
+  float tb = p.t_native * (1.f - g_margin);
+  for (int i = 0; i < (int)p.algos.size(); ++i) {
+    if (lib(r, s, p, i, out, bout) != 0) continue;
+    const float t = time_ms([&] { lib(r, s, p, i, out, bout); }, st);
+    if (t < tb) {
+      tb = t;
+      best = i;
+    }
+  }
+  hipStreamSynchronize(st);
+  (void)hipFree(out);
+  (void)hipFree(bout);
+  p.pick = best;
+  p.t_lib = best >= 0 ? tb : 0.f;
+  if (g_verbose)
+    fprintf(stderr, "[blaslt] kind %d M %d N %d K %d ta %d tb %d epi %d/%d: native %.1f us, lib %s%.1f us\n", k.kind,
+            k.M, k.N, k.K, k.ta, k.tb, k.epi, p.epi, p.t_native * 1e3f, best >= 0 ? "" : "(not faster) ",
+            best >= 0 ? tb * 1e3f : 0.f);
+  return best >= 0 ? &p : nullptr;
+}
+
+int cur_dev() {
+  int d = 0;
+  hipGetDevice(&d);
+  return d;
+}
+
+}  // namespace
+
+// bf16-output dense GEMM (igemm.hip mlc_gemm_bf16_ex_native semantics).  The library path
+// takes the plain and bias / residual-addend forms; activation epilogues stay native.
+MLC_EXPORT int mlc_gemm_bf16_ex(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int lda, int ldb,
+                                int ldc, int ta, int tb, const float* bias, int act, bf16* preact,
+                                const bf16* addend, const bf16* dact, float* ws, long ws_floats,
+                                hipStream_t st) {
+  if (act == 0 && !preact && !dact && !(bias && addend) && mode()) {
+    const Key k{cur_dev(), 0, M, N, K, lda, ldb, ldc, ta, tb, bias ? 1 : 0};
+    DevRes* r = nullptr;
+    StreamRes* s = nullptr;
+    auto native = [&](void* out, float*) {
+      mlc_gemm_bf16_ex_native(A, B, (bf16*)out, M, N, K, lda, ldb, ldc, ta, tb, bias, 0, nullptr, addend, nullptr,
+                              ws, ws_floats, st);
+    };
+    auto lib = [&](DevRes* rr, StreamRes* ss, Plan& p, int i, void* out, float*) {
+      return run_lib(rr, ss, p, i, k, A, B, addend, out, bias, nullptr, st);
+    };
+    if (Plan* p = choose(k, st, (size_t)M * ldc * 2, native, lib, &r, &s))
+      if (run_lib(r, s, *p, p->pick, k, A, B, addend, C, bias, nullptr, st) == 0) return 0;
+  }
+  return mlc_gemm_bf16_ex_native(A, B, C, M, N, K, lda, ldb, ldc, ta, tb, bias, act, preact, addend, dact, ws,
+                                 ws_floats, st);
+}
+
+// Dense weight + bias gradient (igemm.hip mlc_linear_wgrad_bias_native semantics):
+// dW[M][N] += dY^T X, dbias[M] += colsum(dY).  Library path: fp32 D accumulated in place
+// (beta 1) with the BGRADB epilogue writing colsum(dY) to a per-stream staging vector that
+// one small kernel adds into dbias.
+MLC_EXPORT int mlc_linear_wgrad_bias(const bf16* A, const bf16* B, float* C, float* dbias, int M, int N, int K,
+                                     int lda, int ldb, int ldc, int splits, float* ws, long ws_floats,
+                                     hipStream_t st) {
+  if (mode() && M <= kBiasScratch && M <= 8192 && lda == M) {
+    // row-major problem: C[M][N] = A^T B with A = dY [K][M] (ta = 1), B = X [K][N] (tb = 0)
+    const Key k{cur_dev(), 1, M, N, K, lda, ldb, ldc, 1, 0, 2};
+    DevRes* r = nullptr;
+    StreamRes* s = nullptr;
+    auto native = [&](void* out, float* bout) {
+      mlc_linear_wgrad_bias_native(A, B, (float*)out, bout, M, N, K, lda, ldb, ldc, splits, ws, ws_floats, st);
+    };
+    // dW accumulated in place (beta 1); the bias gradient either from the BGRADB epilogue
+    // (staged, then added) or from the column-sum kernel
+    auto lib = [&](DevRes* rr, StreamRes* ss, Plan& p, int i, void* out, float* bout) {
+      const int e = run_lib(rr, ss, p, i, k, A, B, out, out, nullptr, ss->bias, st);
+      if (e) return e;
+      if (p.epi == 2) {
+        hipLaunchKernelGGL(vec_acc_kernel, dim3((M + 255) / 256), dim3(256), 0, st, bout, ss->bias, M);
+        return (int)hipGetLastError();
+      }
+      return mlc_colsum_acc(A, bout, ss->colsum, K, M, st);
+    };
+    if (Plan* p = choose(k, st, (size_t)M * ldc * 4, native, lib, &r, &s))
+      if (lib(r, s, *p, p->pick, C, dbias) == 0) return 0;
+  }
+  return mlc_linear_wgrad_bias_native(A, B, C, dbias, M, N, K, lda, ldb, ldc, splits, ws, ws_floats, st);
+}
+
+// 0 off, 1 force, 2 auto; a negative argument only reads.  Changing the mode clears the
+// cached per-shape choices.
+MLC_EXPORT int mlc_blaslt_mode(int m) {
+  const int old = mode();
+  if (m >= 0 && m != old) {
+    std::lock_guard<std::mutex> g(g_mu);
+    g_mode = m;
+    for (auto& kv : g_plans) destroy_plan(kv.second);
+    g_plans.clear();
+  }
+  return old;
+}
+
+// Report the cached choices: up to `cap` rows of 10 ints
+// [kind, M, N, K, ta, tb, epi, pick (-2 native / algo index), native ns, library ns].
+MLC_EXPORT int mlc_blaslt_choices(int* out, int cap) {
+  std::lock_guard<std::mutex> g(g_mu);
+  int n = 0;
+  for (auto& kv : g_plans) {
+    if (n >= cap) break;
+    const Key& k = kv.first;
+    const Plan& p = kv.second;
+    const int row[10] = {k.kind, k.M, k.N, k.K, k.ta, k.tb, k.epi, p.pick, (int)(p.t_native * 1e6f),
+                         (int)(p.t_lib * 1e6f)};
+    memcpy(out + 10 * n, row, sizeof(row));
+    ++n;
+  }
+  return n;
+}

@@ -1911,7 +1911,7 @@ MLC_EXPORT int mlc_gemm_f32out(const bf16* A, const bf16* B, float* C, const flo
 // (lda), X [K][N] (ldb), M % 8 == N % 8 == 0.
 // With a workspace (ws_floats >= splits*M*N, ldc == N) the split-K partial tiles go to fp32
 // slabs and one reduction pass adds their sum into dW; otherwise fp32 atomics into dW.
-MLC_EXPORT int mlc_linear_wgrad_bias(const bf16* A, const bf16* B, float* C, float* dbias, int M, int N, int K,
+MLC_EXPORT int mlc_linear_wgrad_bias_native(const bf16* A, const bf16* B, float* C, float* dbias, int M, int N, int K,
                                      int lda, int ldb, int ldc, int splits, float* ws, long ws_floats,
                                      hipStream_t st) {
   if (K % 8 || lda % 8 || ldb % 8 || M % 8 || N % 8) return -1;
@@ -1984,7 +1984,7 @@ dense_finalize_kernel(const float* __restrict__ ws, int splits, DenseFinish fin,
 // the chip, the K reduction is split across workgroups into per-split fp32 slabs of ws
 // (plain stores: ~4x cheaper than fp32 atomics into one buffer) and the epilogue runs in a
 // finishing pass that sums the slabs.
-MLC_EXPORT int mlc_gemm_bf16_ex(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int lda, int ldb,
+MLC_EXPORT int mlc_gemm_bf16_ex_native(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int lda, int ldb,
                                 int ldc, int ta, int tb, const float* bias, int act, bf16* preact,
                                 const bf16* addend, const bf16* dact, float* ws, long ws_floats,
                                 hipStream_t st) {

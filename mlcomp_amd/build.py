@@ -67,7 +67,7 @@ def build_kernels(verbose=False, jobs=None):
             f.result()
     if todo or _newer(KERNEL_LIB, objs):
         _run([HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', '-o', KERNEL_LIB] + objs
-             + ['-L/opt/rocm/lib', '-lrccl', '-Wl,-rpath,/opt/rocm/lib'])
+             + ['-L/opt/rocm/lib', '-lrccl', '-lhipblaslt', '-Wl,-rpath,/opt/rocm/lib'])
     if verbose:
         print(f'[build] kernels: {len(todo)} rebuilt -> {KERNEL_LIB}')
     return KERNEL_LIB

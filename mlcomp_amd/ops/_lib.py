@@ -46,6 +46,7 @@ _SIGS = {
     'mlc_conv256_fwd': [vp] * 5 + [i32] * 13 + [vp],
     'mlc_augment': [vp, vp, vp, vp] + [i32] * 7 + [vp],
     'mlc_gemm_bf16_ex': [vp, vp, vp] + [i32] * 8 + [vp, i32, vp, vp, vp, vp, i64, vp],
+    'mlc_gemm_bf16_ex_native': [vp, vp, vp] + [i32] * 8 + [vp, i32, vp, vp, vp, vp, i64, vp],
     'mlc_ln_fwd': [vp] * 8 + [i32, i32, f32, f32, f32, vp, u32, u32, vp],
     'mlc_ln_bwd': [vp] * 10 + [i32, i32, f32, f32, vp, u32, u32, vp],
     'mlc_ln_finalize_many': [vp, i32, i32, vp],
@@ -53,6 +54,10 @@ _SIGS = {
     'mlc_softmax_fwd': [vp] * 4 + [i64, i32, i32, f32, f32, vp, u32, vp],
     'mlc_softmax_bwd': [vp] * 3 + [i64, i32, f32, f32, vp, u32, vp],
     'mlc_linear_wgrad_bias': [vp] * 4 + [i32] * 7 + [vp, i64, vp],
+    'mlc_linear_wgrad_bias_native': [vp] * 4 + [i32] * 7 + [vp, i64, vp],
+    # library GEMM selection (blaslt.hip)
+    'mlc_blaslt_mode': [i32],
+    'mlc_blaslt_choices': [vp, i32],
     'mlc_upcat_fwd': [vp, vp, vp] + [i32] * 5 + [vp],
     'mlc_upcat_bwd': [vp, vp, vp] + [i32] * 5 + [vp],
     'mlc_seg_head_fwd': [vp] * 6 + [i64, i32, i32, vp],
