@@ -42,6 +42,10 @@ extern "C" int mlc_gemm_bf16_ex_native(const bf16* A, const bf16* B, bf16* C, in
                                        int ldc, int ta, int tb, const float* bias, int act, bf16* preact,
                                        const bf16* addend, const bf16* dact, float* ws, long ws_floats,
                                        hipStream_t st);
+extern "C" int mlc_conv_wgrad_native(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int Co,
+                                      int KH, int KW, int stride, int pad, int dil, int Ho, int Wo, int splits,
+                                      int accumulate, float* ws, long ws_floats, const float* in_sc,
+                                      const float* in_sh, hipStream_t st);
 extern "C" int mlc_colsum_acc(const bf16* g, float* out, float* scratch, int R, int C, hipStream_t st);
 extern "C" int mlc_linear_wgrad_bias_native(const bf16* A, const bf16* B, float* C, float* dbias, int M, int N,
                                             int K, int lda, int ldb, int ldc, int splits, float* ws, long ws_floats,
@@ -84,7 +88,8 @@ struct DevRes {
   std::map<hipStream_t, int> owner;
 };
 
-// kind 0: bf16 out (+bias | +addend);  kind 1: fp32 out accumulate (+ bias gradient)
+// kind 0: bf16 out (+bias | +addend);  kind 1: fp32 out accumulate (+ bias gradient);
+// kind 2: fp32 out, written (epi 0) or accumulated (epi 1) - the 1x1 conv weight gradient
 struct Key {
   int dev, kind, M, N, K, lda, ldb, ldc, ta, tb, epi;
   bool operator<(const Key& o) const {
@@ -157,14 +162,15 @@ void destroy_plan(Plan& p) {
 }
 
 bool build_plan(DevRes* r, const Key& k, Plan& p, int epi) {
-  p.epi = epi;
   const hipblasOperation_t opA = k.tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;   // A' = the B operand
   const hipblasOperation_t opB = k.ta ? HIPBLAS_OP_T : HIPBLAS_OP_N;   // B' = the A operand
-  const hipDataType dt = k.kind == 1 ? HIP_R_32F : HIP_R_16BF;
+  const hipDataType dt = k.kind >= 1 ? HIP_R_32F : HIP_R_16BF;
   bool ok = hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) == HIPBLAS_STATUS_SUCCESS;
   ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)) == 0;
   ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)) == 0;
   // epi: 0 none, 1 bias (kind 0), 2 bias gradient (kind 1)
+  if (k.kind == 2) epi = 0;   // kind 2's epi is the accumulate flag (beta), not an epilogue
+  p.epi = epi;
   const hipblasLtEpilogue_t ep = epi == 1 ? HIPBLASLT_EPILOGUE_BIAS
                                : epi == 2 ? HIPBLASLT_EPILOGUE_BGRADB : HIPBLASLT_EPILOGUE_DEFAULT;
   ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &ep, sizeof(ep)) == 0;
@@ -353,6 +359,31 @@ MLC_EXPORT int mlc_linear_wgrad_bias(const bf16* A, const bf16* B, float* C, flo
       if (lib(r, s, *p, p->pick, C, dbias) == 0) return 0;
   }
   return mlc_linear_wgrad_bias_native(A, B, C, dbias, M, N, K, lda, ldb, ldc, splits, ws, ws_floats, st);
+}
+
+// Conv weight gradient (igemm.hip mlc_conv_wgrad_native semantics).  A 1x1 / stride-1 /
+// unpadded conv without an input BN transform is the plain GEMM dw[Co][C] (+)= dy^T x
+// (A = dy [P][Co], B = x [P][C]), which goes through the same per-shape selection.
+MLC_EXPORT int mlc_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int Co, int KH,
+                              int KW, int stride, int pad, int dil, int Ho, int Wo, int splits, int accumulate,
+                              float* ws, long ws_floats, const float* in_sc, const float* in_sh, hipStream_t st) {
+  if (KH == 1 && KW == 1 && stride == 1 && pad == 0 && !in_sc && !in_sh && C % 8 == 0 && Co % 8 == 0 && mode()) {
+    const int P = N * Ho * Wo;
+    const Key k{cur_dev(), 2, Co, C, P, Co, C, C, 1, 0, accumulate ? 1 : 0};
+    DevRes* r = nullptr;
+    StreamRes* s = nullptr;
+    auto native = [&](void* out, float*) {
+      mlc_conv_wgrad_native(dy, x, (float*)out, N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo, splits,
+                            accumulate, ws, ws_floats, in_sc, in_sh, st);
+    };
+    auto lib = [&](DevRes* rr, StreamRes* ss, Plan& p, int i, void* out, float*) {
+      return run_lib(rr, ss, p, i, k, dy, x, accumulate ? out : nullptr, out, nullptr, nullptr, st);
+    };
+    if (Plan* p = choose(k, st, (size_t)Co * C * 4, native, lib, &r, &s))
+      if (lib(r, s, *p, p->pick, dw, nullptr) == 0) return 0;
+  }
+  return mlc_conv_wgrad_native(dy, x, dw, N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo, splits, accumulate, ws,
+                               ws_floats, in_sc, in_sh, st);
 }
 
 // 0 off, 1 force, 2 auto; a negative argument only reads.  Changing the mode clears the

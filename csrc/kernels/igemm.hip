@@ -1707,7 +1707,7 @@ splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long
 // plain stores and one reduction pass sums them into dw; without, they are added into dw
 // with fp32 atomics (memory-side, ~1.3 TB/s: the slab round trip is ~4x cheaper).
 // in_sc/in_sh: as in mlc_conv_fwd - x is pre-BN and the conv's input is relu(x*sc + sh).
-MLC_EXPORT int mlc_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, int H, int W,
+MLC_EXPORT int mlc_conv_wgrad_native(const bf16* dy, const bf16* x, float* dw, int N, int H, int W,
                               int C, int Co, int KH, int KW, int stride, int pad, int dil,
                               int Ho, int Wo, int splits, int accumulate, float* ws, long ws_floats,
                               const float* in_sc, const float* in_sh, hipStream_t st) {

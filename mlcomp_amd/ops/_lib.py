@@ -39,6 +39,7 @@ _SIGS = {
     'mlc_conv_tr_fwd': [vp] * 5 + [i32] * 12 + [vp],
     'mlc_wt_transpose': [vp, i32, i64, vp],
     'mlc_conv_wgrad': [vp, vp, vp] + [i32] * 14 + [vp, i64, vp, vp, vp],
+    'mlc_conv_wgrad_native': [vp, vp, vp] + [i32] * 14 + [vp, i64, vp, vp, vp],
     'mlc_gemm_f32out': [vp, vp, vp, vp] + [i32] * 11 + [vp],
     'mlc_gemm_bf16out': [vp, vp, vp] + [i32] * 8 + [vp],
     'mlc_gemm256_nt': [vp, vp, vp, vp] + [i32] * 6 + [vp, i32, vp, vp, i32, i32, vp],
