@@ -77,15 +77,17 @@ struct StreamRes {
 };
 constexpr int kColsumFloats = 32 * 8192;   // NSTAT copies x up to 8192 columns
 
-// Workspaces are allocated in one go on the first eager call (no allocation may happen
-// while a stream is being captured) and handed to streams as they show up - including
-// the graph-capture stream, which first appears mid-capture.
-constexpr int kSlots = 8;
+// Every stream that runs a library GEMM gets its own workspace (a weight-gradient side
+// stream and the main stream may run GEMMs concurrently).  Eager streams allocate theirs on
+// first use; nothing may be allocated while a stream is being captured, so streams first
+// seen mid-capture (the graph-capture stream) take one from a small reserve allocated with
+// the handle.  No reserve left: that call runs native.
+constexpr int kReserve = 4;
 
 struct DevRes {
   hipblasLtHandle_t handle = nullptr;
-  std::vector<StreamRes> slots;
-  std::map<hipStream_t, int> owner;
+  std::map<hipStream_t, StreamRes> res;
+  std::vector<StreamRes> reserve;
 };
 
 // kind 0: bf16 out (+bias | +addend);  kind 1: fp32 out accumulate (+ bias gradient);
@@ -118,6 +120,19 @@ bool capturing(hipStream_t st) {
   return s != hipStreamCaptureStatusNone;
 }
 
+bool alloc_res(StreamRes& s) {
+  s = StreamRes{};
+  if (hipMalloc(&s.ws, kWorkspace) == hipSuccess &&
+      hipMalloc((void**)&s.bias, kBiasScratch * sizeof(float)) == hipSuccess &&
+      hipMalloc((void**)&s.colsum, kColsumFloats * sizeof(float)) == hipSuccess &&
+      hipMemset(s.colsum, 0, kColsumFloats * sizeof(float)) == hipSuccess)
+    return true;
+  for (void* q : {s.ws, (void*)s.bias, (void*)s.colsum})
+    if (q) (void)hipFree(q);
+  s = StreamRes{};
+  return false;
+}
+
 DevRes* dev_res(int dev, bool can_alloc) {
   DevRes& r = g_dev[dev];
   if (!r.handle) {
@@ -125,28 +140,27 @@ DevRes* dev_res(int dev, bool can_alloc) {
       r.handle = nullptr;
       return nullptr;
     }
-    for (int i = 0; i < kSlots; ++i) {
+    for (int i = 0; i < kReserve; ++i) {
       StreamRes s;
-      if (hipMalloc(&s.ws, kWorkspace) != hipSuccess) break;
-      if (hipMalloc((void**)&s.bias, kBiasScratch * sizeof(float)) != hipSuccess ||
-          hipMalloc((void**)&s.colsum, kColsumFloats * sizeof(float)) != hipSuccess ||
-          hipMemset(s.colsum, 0, kColsumFloats * sizeof(float)) != hipSuccess) {
-        (void)hipFree(s.ws);
-        break;
-      }
-      r.slots.push_back(s);
+      if (!alloc_res(s)) break;
+      r.reserve.push_back(s);
     }
   }
   return &r;
 }
 
-StreamRes* stream_res(DevRes* r, hipStream_t st) {
-  auto it = r->owner.find(st);
-  if (it != r->owner.end()) return &r->slots[it->second];
-  const int i = (int)r->owner.size();
-  if (i >= (int)r->slots.size()) return nullptr;   // more streams than slots: native
-  r->owner[st] = i;
-  return &r->slots[i];
+StreamRes* stream_res(DevRes* r, hipStream_t st, bool cap) {
+  auto it = r->res.find(st);
+  if (it != r->res.end()) return &it->second;
+  StreamRes s;
+  if (cap) {
+    if (r->reserve.empty()) return nullptr;
+    s = r->reserve.back();
+    r->reserve.pop_back();
+  } else if (!alloc_res(s)) {
+    return nullptr;
+  }
+  return &(r->res[st] = s);
 }
 
 __global__ void __launch_bounds__(256) vec_acc_kernel(float* __restrict__ dst, const float* __restrict__ src, int n) {
@@ -243,14 +257,14 @@ Plan* choose(const Key& k, hipStream_t st, size_t out_bytes, FN native, FL lib, 
   std::lock_guard<std::mutex> g(g_mu);
   auto it = g_plans.find(k);
   if (it != g_plans.end() && it->second.pick == -2) return nullptr;
+  if (it == g_plans.end() && cap) return nullptr;   // first seen under capture: native (nothing may be timed now)
   DevRes* r = dev_res(k.dev, !cap);
   if (!r) return nullptr;
-  StreamRes* s = stream_res(r, st);
+  StreamRes* s = stream_res(r, st, cap);
   if (!s) return nullptr;
   *rp = r;
   *sp = s;
   if (it != g_plans.end() && it->second.pick >= 0) return &it->second;
-  if (cap) return nullptr;   // first seen under capture: native (nothing may be timed now)
   Plan& p = g_plans[k];
   bool built = build_plan(r, k, p, k.epi);
   if (!built && k.kind == 1) {   // no BGRADB kernel for this problem: plain GEMM + column sums
@@ -275,8 +289,8 @@ Plan* choose(const Key& k, hipStream_t st, size_t out_bytes, FN native, FL lib, 
   hipMemsetAsync(out, 0, out_bytes, st);
   hipMemsetAsync(bout, 0, (size_t)(k.M + k.N) * 4, st);
   p.t_native = time_ms([&] { native(out, bout); }, st);
-  int best = -2;
-  float tb = p.t_native * (1.f - g_margin);
+  int best = -1;
+  float tb = 1e30f;
   for (int i = 0; i < (int)p.algos.size(); ++i) {
     if (lib(r, s, p, i, out, bout) != 0) continue;
     const float t = time_ms([&] { lib(r, s, p, i, out, bout); }, st);
@@ -288,13 +302,14 @@ Plan* choose(const Key& k, hipStream_t st, size_t out_bytes, FN native, FL lib, 
   hipStreamSynchronize(st);
   (void)hipFree(out);
   (void)hipFree(bout);
-  p.pick = best;
-  p.t_lib = best >= 0 ? tb : 0.f;
+  const bool win = best >= 0 && tb < p.t_native * (1.f - g_margin);
+  p.pick = win ? best : -2;
+  p.t_lib = best >= 0 ? tb : 0.f;   // the fastest library time, kept for the report either way
   if (g_verbose)
-    fprintf(stderr, "[blaslt] kind %d M %d N %d K %d ta %d tb %d epi %d/%d: native %.1f us, lib %s%.1f us\n", k.kind,
-            k.M, k.N, k.K, k.ta, k.tb, k.epi, p.epi, p.t_native * 1e3f, best >= 0 ? "" : "(not faster) ",
-            best >= 0 ? tb * 1e3f : 0.f);
-  return best >= 0 ? &p : nullptr;
+    fprintf(stderr, "[blaslt] kind %d M %d N %d K %d ta %d tb %d epi %d/%d: native %.1f us, lib %.1f us -> %s\n",
+            k.kind, k.M, k.N, k.K, k.ta, k.tb, k.epi, p.epi, p.t_native * 1e3f, p.t_lib * 1e3f,
+            win ? "hipblaslt" : "native");
+  return win ? &p : nullptr;
 }
 
 int cur_dev() {

@@ -58,6 +58,15 @@ ln_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ r, bf16* __re
   const uint32_t seed = seedp ? *seedp : 0u;
   const size_t base = (size_t)row * H;
   float v[MAXC][4];
+  // gamma / beta are issued with the row loads: fetched after the two reductions they
+  // were a second dependent memory round trip at the end of every (short-lived) wave
+  float ga[MAXC][4], be[MAXC][4];
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int c = lane + 64 * k;
+    load4f(gamma + 4 * (c < nch ? c : 0), ga[k]);
+    load4f(beta + 4 * (c < nch ? c : 0), be[k]);
+  }
   float sum = 0.f;
 #pragma unroll
   for (int k = 0; k < MAXC; ++k) {
@@ -99,15 +108,12 @@ ln_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ r, bf16* __re
 #pragma unroll
   for (int k = 0; k < MAXC; ++k) {
     const int c = lane + 64 * k;
-    float ga[4], be[4];
-    load4f(gamma + 4 * (c < nch ? c : 0), ga);
-    load4f(beta + 4 * (c < nch ? c : 0), be);
     if (c < nch) {
       float o[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int col = 4 * c + e;
-        o[e] = (v[k][e] - mean) * rstd * ga[e] + be[e];
+        o[e] = (v[k][e] - mean) * rstd * ga[k][e] + be[k][e];
         if (thr_out)
           o[e] = keep(seed, salt_out, (uint32_t)(base + col), thr_out) ? o[e] * inv_keep_out : 0.f;
       }
