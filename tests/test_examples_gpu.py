@@ -39,3 +39,27 @@ def test_digit_recognizer_lenet_trains_natively_through_the_dag(cluster):
     assert all(v == TaskStatus.Success for v in res.values()), res
     _, eng = _engine_info(ids[0])
     assert eng['stage1']['engine'] == 'native' and eng['stage1']['kind'] == 'generic', eng
+
+
+@pytest.mark.timeout(400)
+def test_multi_branch_resnet50_and_bert_dag_on_one_gpu(cluster):
+    """BASELINE config 5 (ResNet-50 + BERT-base train tasks in one DAG) through the whole
+    stack on the box's one GPU: with one GPU per task the scheduler runs the two branches one
+    after the other, both full-size models on their native engines (short epochs)."""
+    from mlcomp_amd.db.enums import TaskStatus
+    ids = _ids(_run_example(cluster['tmp'], 'multi_branch/config.yml', params={
+        'executors/resnet50/gpu': 1, 'executors/bert/gpu': 1,
+        'executors/resnet50/params/stages/data_params/steps': 20,
+        'executors/resnet50/params/stages/state_params/num_epochs': 1,
+        'executors/bert/params/stages/data_params/num_samples': 2048,
+        'executors/bert/params/stages/data_params/valid_samples': 256,
+        'executors/bert/params/stages/state_params/num_epochs': 1}))
+    res = _wait_live(cluster, ids, timeout=360)
+    assert all(v == TaskStatus.Success for v in res.values()), res
+    engines = {}
+    for tid in ids:
+        t, eng = _engine_info(tid)
+        if eng:
+            engines[t.executor] = eng['stage1']
+    assert set(engines) == {'resnet50', 'bert'}, engines
+    assert all(e['engine'] == 'native' for e in engines.values()), engines
