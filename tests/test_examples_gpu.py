@@ -63,3 +63,20 @@ def test_multi_branch_resnet50_and_bert_dag_on_one_gpu(cluster):
             engines[t.executor] = eng['stage1']
     assert set(engines) == {'resnet50', 'bert'}, engines
     assert all(e['engine'] == 'native' for e in engines.values()), engines
+
+
+@pytest.mark.timeout(400)
+def test_unet_segmentation_train_then_valid_dag_on_gpu(cluster):
+    """BASELINE config 3 (U-Net segmentation DAG: train node -> traced model -> valid node)
+    on the box's one GPU: the train task runs the native U-Net engine, traces the model, and
+    the valid_segmentation task scores it."""
+    from mlcomp_amd.db.enums import TaskStatus
+    ids = _ids(_run_example(cluster['tmp'], 'unet_segmentation/config.yml', params={
+        'executors/train/gpu': 1,
+        'executors/train/params/stages/data_params/num_samples': 256,
+        'executors/train/params/stages/data_params/valid_samples': 64,
+        'executors/train/params/stages/state_params/num_epochs': 1}))
+    res = _wait_live(cluster, ids, timeout=360)
+    assert all(v == TaskStatus.Success for v in res.values()), res
+    t, eng = _engine_info(ids[0])
+    assert t.executor == 'train' and eng['stage1']['engine'] == 'native', eng
