@@ -106,6 +106,11 @@ class _Dense:
             side.wait_event(fork)
         with Fn.side_stream(side):
             self.bwd_params(dy, x)
+        if self.ctx.wgrad_defer:
+            # no per-layer join: the chain joins in flush_wgrad; keep dy / x alive for it
+            dy.record_stream(side)
+            x.record_stream(side)
+            return lambda: None
         return lambda: main.wait_stream(side)
 
     def backward(self, dy, x, **dgrad_kw):
@@ -353,6 +358,7 @@ class NativeBert:
         self.k_loss = ctx.ws.request('loss', 1)
         self.k_correct = ctx.ws.request('correct', 1)
         ctx.finalize(device)
+        ctx.default_wgrad_defer(False)
         self.device = ctx.device
         self.seed = torch.zeros(1, device=self.device, dtype=torch.int32)
         self.ln_fin = Tx.LnFinalizer()

@@ -121,6 +121,9 @@ class ParamArena:
         self.device = None
         self.ready_hook = None  # callable(slot) set by the gradient bucketer
         self.flush = None       # callable() joining gradient work still in flight (native layers)
+        # streams other than the current one that write gradients without joining per
+        # layer (NativeContext.wgrad_defer): a bucket's all-reduce / update waits on them too
+        self.grad_streams = []
 
     def weight(self, name, shape) -> Slot:
         s = self.decay.add(name, shape)

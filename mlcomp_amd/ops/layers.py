@@ -86,6 +86,12 @@ class NativeContext:
         # NEXT layer's backward (event per layer) instead of its own, so the main stream does
         # not stall on a just-finished wgrad; flush_wgrad joins the last one
         self.wgrad_lag = os.environ.get('MLC_WGRAD_LAG', '0') == '1'
+        # wgrad_defer (engines opt in; MLC_WGRAD_DEFER overrides): the side-stream weight
+        # gradients are never joined per layer - they form one free-running chain beside the
+        # input-gradient chain, their operands are kept alive for the side stream with
+        # record_stream, the gradient bucketer waits on the side stream as well, and the
+        # chain joins once, in flush_wgrad (bucketer.finish, before the optimizer)
+        self.wgrad_defer = False
         self._pending_wgrad = None
         self.dgrad_first = DGRAD_FIRST_ENV == '1'
 
@@ -105,10 +111,21 @@ class NativeContext:
         if self.device.type == 'cuda' and os.environ.get('MLC_WGRAD_STREAM', '1') in ('1', '2'):
             self.wgrad_stream = torch.cuda.Stream(self.device)
 
+    def default_wgrad_defer(self, on: bool):
+        """Engine default for the deferred weight-gradient join (MLC_WGRAD_DEFER overrides)."""
+        env = os.environ.get('MLC_WGRAD_DEFER')
+        self.wgrad_defer = (env == '1') if env is not None else on
+        self.arena.grad_streams = [self.wgrad_stream] if (self.wgrad_defer and self.wgrad_stream) else []
+
     def flush_wgrad(self):
         """Join the lagged weight gradient (if any) into the current stream and mark its
-        slot ready.  Must run before anything reads the gradient arena (the bucketer's
-        finish() calls it through ``arena.flush``)."""
+        slot ready; with wgrad_defer, join the whole side-stream chain.  Must run before
+        anything reads the gradient arena (the bucketer's finish() calls it through
+        ``arena.flush``)."""
+        if self.wgrad_defer and self.wgrad_stream is not None:
+            cur = torch.cuda.current_stream(self.device)
+            if cur != self.wgrad_stream:
+                cur.wait_stream(self.wgrad_stream)
         p = self._pending_wgrad
         if p is None:
             return

@@ -134,6 +134,12 @@ class GradBucketer:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.params.device))
             self.side.wait_event(ev)
+            # gradients written on streams that are not joined per layer (deferred weight
+            # gradients): everything they issued so far covers this bucket's slots
+            for s in getattr(self.params, 'grad_streams', ()):
+                e2 = torch.cuda.Event()
+                e2.record(s)
+                self.side.wait_event(e2)
             with torch.cuda.stream(self.side):
                 self._work(b, self.side)
         else:
