@@ -111,6 +111,7 @@ struct Plan {
 };
 
 std::mutex g_mu;
+std::mutex g_run_mu;
 std::map<int, DevRes> g_dev;
 std::map<Key, Plan> g_plans;
 
@@ -218,6 +219,9 @@ bool build_plan(DevRes* r, const Key& k, Plan& p, int epi) {
 int run_lib(DevRes* r, StreamRes* s, Plan& p, int algo, const Key& k, const void* A, const void* B, const void* Cin,
             void* D, const float* bias, float* bgrad, hipStream_t st) {
   const float alpha = 1.f, beta = Cin ? 1.f : 0.f;
+  // the bias pointer is an attribute of the shared descriptor: set it and enqueue the
+  // matmul as one step (ctypes callers release the GIL, so two host threads can get here)
+  std::lock_guard<std::mutex> g(g_run_mu);
   if (p.epi == 1) hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
   if (p.epi == 2) hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bgrad, sizeof(bgrad));
   const hipblasStatus_t e = hipblasLtMatmul(r->handle, p.desc, &alpha, B, p.a, A, p.b, &beta, Cin ? Cin : D, p.c, D,
