@@ -229,21 +229,26 @@ int run_lib(DevRes* r, StreamRes* s, Plan& p, int algo, const Key& k, const void
   return e == HIPBLAS_STATUS_SUCCESS ? 0 : -100 - (int)e;
 }
 
+// best of 3 x (1 warm + 5 timed) runs; `cutoff` (ms): a candidate whose first timed run is
+// slower than that is dropped after it (a hopeless library kernel on a tall-K weight
+// gradient can take milliseconds per call, and warm-up should not pay 18 of them)
 template <class F>
-float time_ms(F f, hipStream_t st) {
+float time_ms(F f, hipStream_t st, float cutoff = 1e30f) {
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
   float best = 1e30f;
   for (int rep = 0; rep < 3; ++rep) {
     f();
+    const int n = rep == 0 ? 1 : 5;
     hipEventRecord(a, st);
-    for (int i = 0; i < 5; ++i) f();
+    for (int i = 0; i < n; ++i) f();
     hipEventRecord(b, st);
     hipEventSynchronize(b);
     float ms = 0.f;
     hipEventElapsedTime(&ms, a, b);
-    best = std::min(best, ms / 5);
+    best = std::min(best, ms / n);
+    if (rep == 0 && best > cutoff) break;
   }
   hipEventDestroy(a);
   hipEventDestroy(b);
@@ -297,7 +302,7 @@ Plan* choose(const Key& k, hipStream_t st, size_t out_bytes, FN native, FL lib, 
   float tb = 1e30f;
   for (int i = 0; i < (int)p.algos.size(); ++i) {
     if (lib(r, s, p, i, out, bout) != 0) continue;
-    const float t = time_ms([&] { lib(r, s, p, i, out, bout); }, st);
+    const float t = time_ms([&] { lib(r, s, p, i, out, bout); }, st, 1.5f * p.t_native);
     if (t < tb) {
       tb = t;
       best = i;
