@@ -110,6 +110,7 @@ class NativeContext:
         self.arena.flush = self.flush_wgrad
         if self.device.type == 'cuda' and os.environ.get('MLC_WGRAD_STREAM', '1') in ('1', '2'):
             self.wgrad_stream = torch.cuda.Stream(self.device)
+        self.default_wgrad_defer(False)
 
     def default_wgrad_defer(self, on: bool):
         """Engine default for the deferred weight-gradient join (MLC_WGRAD_DEFER overrides)."""
@@ -345,6 +346,13 @@ class ConvBN:
                 self.wgrad(dy, x, in_affine)
         if side is not None and defer is not None:
             defer.append((dy, x, self.w))
+            return dx, dres
+        if side is not None and self.ctx.wgrad_defer:
+            # no per-layer join (NativeContext.wgrad_defer): dy / x stay alive for the side
+            # stream, the bucketer waits on it, flush_wgrad joins it before the optimizer
+            dy.record_stream(side)
+            x.record_stream(side)
+            arena.mark_ready(self.w)
             return dx, dres
         if side is not None and self.ctx.wgrad_lag:
             ev = torch.cuda.Event()
