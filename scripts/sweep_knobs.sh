@@ -1,5 +1,5 @@
 # Interleaved whole-step A/B of engine knobs on one GPU (bench.py, 30 steps):
-#   bash scripts/sweep_resnet_knobs.sh OUT_TAG "NAME ENV=VAL ..." "NAME2 ENV=VAL ..." ...
+#   bash scripts/sweep_knobs.sh OUT_TAG "NAME ENV=VAL ..." "NAME2 ENV=VAL ..." ...
 # Each round runs every config once; ROUNDS (default 2) rounds; BENCH_ARGS adds bench.py
 # arguments (e.g. "--model bert-base").  One line per run.
 set -o pipefail
