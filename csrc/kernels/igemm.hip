@@ -28,6 +28,8 @@
 #include "common.h"
 #include "convgeom.h"
 #include <stdlib.h>
+#include <map>
+#include <mutex>
 
 namespace igemm {
 
@@ -1387,26 +1389,57 @@ static int pick_dense_tile(int M, int N, int K, int& split) {
   }
   return 0;
 }
-constexpr int kSplitCounters = 1 << 16;
-// per-device tile counters for EpiSlabFused, allocated (zeroed) on first use outside stream
-// capture; nullptr -> the caller falls back to the separate reduction kernel
+constexpr int kSplitCounters = 1 << 16;          // tiles per eager stream region
+constexpr long kCapturedCounters = 1L << 21;      // per device, handed out once per captured launch
+// Tile counters for EpiSlabFused.  A counter is persistent state: every launch leaves its
+// tiles' counters zeroed, so two launches that count on the SAME counters at the same
+// time (a main-stream dgrad beside a side-stream weight gradient inside one graph, or an
+// eager launch on another stream beside a graph replay) make one split take a foreign
+// ticket.  The tile then finalizes early (partial sums) or never, and its counter is left
+// non-zero, so every later launch that uses it computes garbage: the "NaN within ~10 graph
+// replays once eager kernels ran on the NULL stream" of round 4 (docs/architecture.md).
+// Hence no two launches that can overlap share counters:
+//   * eager launches get one region per stream (launches on one stream are ordered);
+//   * a launch being captured gets a fresh region of its own from a per-device pool that is
+//     never recycled (the graph may replay it concurrently with anything else).
+// Everything is allocated (zeroed) outside capture; nullptr -> the caller falls back to
+// the separate reduction kernel, which needs no counters.
+struct CounterPool {
+  std::mutex mu;
+  unsigned* captured = nullptr;
+  long captured_used = 0;
+  std::map<hipStream_t, unsigned*> eager;
+};
+static unsigned* alloc_zeroed_counters(long n) {
+  unsigned* p = nullptr;
+  if (hipMalloc(&p, n * sizeof(unsigned)) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, n * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  return p;
+}
 static unsigned* split_counters(hipStream_t st, long tiles, int splits, int bm, int bn) {
-  static unsigned* buf[16] = {};
+  static CounterPool pools[16];
   if (tiles > kSplitCounters || (long)splits * bm * bn * 4 > (long)g_splitk_fused * 1024) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
-  if (!buf[dev]) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    unsigned* p = nullptr;
-    if (hipMalloc(&p, kSplitCounters * sizeof(unsigned)) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, kSplitCounters * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-      (void)hipFree(p);
-      return nullptr;
-    }
-    buf[dev] = p;
+  CounterPool& P = pools[dev];
+  std::lock_guard<std::mutex> lk(P.mu);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return nullptr;
+  if (cs != hipStreamCaptureStatusNone) {
+    if (!P.captured || P.captured_used + tiles > kCapturedCounters) return nullptr;
+    unsigned* r = P.captured + P.captured_used;
+    P.captured_used += (tiles + 63) & ~63L;   // keep regions on separate 256-B lines
+    return r;
   }
-  return buf[dev];
+  if (!P.captured) P.captured = alloc_zeroed_counters(kCapturedCounters);  // ready for a later capture
+  auto it = P.eager.find(st);
+  if (it != P.eager.end()) return it->second;
+  unsigned* r = alloc_zeroed_counters(kSplitCounters);
+  if (r) P.eager[st] = r;
+  return r;
 }
 static inline int tile_bm(int tile) { return tile == 1 || tile == 3 ? 256 : tile == 2 ? 64 : 128; }
 static inline int tile_bn(int tile) { return tile == 1 ? 64 : tile == 2 || tile == 4 ? 256 : 128; }

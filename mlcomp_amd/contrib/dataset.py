@@ -97,10 +97,10 @@ class ImageDataset(Dataset):
     def __len__(self):
         return len(self.data)
 
-    def _before_transform(self, row: dict, item: dict):
+    def _get_item_before_transform(self, row: dict, item: dict):
         pass
 
-    def _after_transform(self, row: dict, transformed: dict, res: dict):
+    def _get_item_after_transform(self, row: dict, transformed: dict, res: dict):
         if 'label' in row:
             t = ast.literal_eval(str(row['label']))
             res['targets'] = np.array(t, dtype=np.float32) if isinstance(t, list) else t
@@ -109,7 +109,7 @@ class ImageDataset(Dataset):
         row = self.data[index]
         image = self.read_image_file(row['image'], self.gray_scale)
         item = {'image': image}
-        self._before_transform(row, item)
+        self._get_item_before_transform(row, item)
         if self.transforms:
             item = self.transforms(**item)
         img = np.asarray(item['image'])
@@ -122,7 +122,7 @@ class ImageDataset(Dataset):
             res['image'] = image
         for c in self.meta_cols:
             res[c] = row[c]
-        self._after_transform(row, item, res)
+        self._get_item_after_transform(row, item, res)
         if self.postprocess_func:
             res = self.postprocess_func(res)
         return res
@@ -154,12 +154,12 @@ class ImageWithMaskDataset(ImageDataset):
         if 'mask' in row:
             row['mask'] = join(self.mask_folder, row['mask'])
 
-    def _before_transform(self, row: dict, item: dict):
+    def _get_item_before_transform(self, row: dict, item: dict):
         if 'mask' in row and self.mask_folder:
             item['mask'] = self.read_image_file(row['mask'], True)
-            self._crop_positive(item)
+            self._process_crop_positive(item)
 
-    def _after_transform(self, row: dict, transformed: dict, res: dict):
+    def _get_item_after_transform(self, row: dict, transformed: dict, res: dict):
         if 'mask' not in transformed:
             return
         mask = np.asarray(transformed['mask']).astype(np.int64)
@@ -179,7 +179,7 @@ class ImageWithMaskDataset(ImageDataset):
                 res[f'empty_{i}'] = int(c.sum() == 0)
             res['empty_all'] = int(mask.sum() == 0)
 
-    def _crop_positive(self, item: dict):
+    def _process_crop_positive(self, item: dict):
         if not self.crop_positive:
             return
         mask = item['mask']

@@ -413,6 +413,10 @@ class GenericNet:
 
     def __call__(self, x):
         gm = self.train_gm if self.training else self.eval_gm
+        # torch ops left in the graph as leaf modules (Dropout, Dropout2d, user modules) are
+        # the user model's own objects, shared by both graphs: their mode is set here, on
+        # every call, so the eval graph never runs a training-mode dropout
+        gm.train(self.training)
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.device.type == 'cuda'):
             return gm(x)
 

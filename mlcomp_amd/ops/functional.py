@@ -289,6 +289,21 @@ def side_stream(stream):
         _ROLE.side = prev
 
 
+@contextlib.contextmanager
+def capture_scope(store: dict):
+    """Workspaces requested while a graph is being captured live in ``store`` (owned by the
+    graph's owner) instead of the process-wide eager pool.  A captured graph bakes the
+    workspace pointers in; eager work on another stream (a second model, a validation pass)
+    must never write the slabs a replay may be using at the same time.  The kernel
+    library does the same for its split-K tile counters (``split_counters`` in igemm.hip)."""
+    prev = getattr(_ROLE, 'capture', None)
+    _ROLE.capture = store
+    try:
+        yield
+    finally:
+        _ROLE.capture = prev
+
+
 def workspace_key(device) -> str:
     device = torch.device(device)
     if device.type == 'cuda' and getattr(_ROLE, 'side', False):
@@ -296,16 +311,25 @@ def workspace_key(device) -> str:
     return str(device)
 
 
+def workspace_store(pool: dict) -> dict:
+    """The dict a workspace lives in: the capture scope's own while capturing, else ``pool``."""
+    cap = getattr(_ROLE, 'capture', None)
+    if cap is not None and torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        return cap.setdefault(id(pool), {})
+    return pool
+
+
 def slab_workspace(device, n: int) -> torch.Tensor:
     """fp32 split-K slab workspace (no zeroing needed), grown on demand - first during
-    eager warm-up, so graph capture reuses it.  One per stream role (workspace_key)."""
+    eager warm-up.  One per stream role (workspace_key) and per capture scope."""
     key = workspace_key(device)
-    buf = _SLAB.get(key)
+    store = workspace_store(_SLAB)
+    buf = store.get(key)
     if buf is None or buf.numel() < n:
         if buf is not None:
             _SLAB_OLD.append(buf)
         buf = torch.empty(max(n, 1 << 20), device=device, dtype=torch.float32)
-        _SLAB[key] = buf
+        store[key] = buf
     return buf
 
 

@@ -93,6 +93,8 @@ class ConvParams:
             self.Cip, self.Cop = ceil8(Ci), ceil8(Co)
             self.w = ctx.arena.weight(f'{name}.weight', (self.Cip, KH, KW, self.Cop))
             self.b = ctx.arena.vector(f'{name}.bias', (self.Cop,)) if (keep_bias and conv.bias is not None) else None
+            _freeze(self.w, conv.weight)
+            _freeze(self.b, conv.bias)
             self.uses = _Uses()
             return
         Co, Cg, KH, KW = conv.weight.shape
@@ -111,6 +113,8 @@ class ConvParams:
             self.Cip, self.Cop = self.Ci, Co
             self.w = ctx.arena.weight(f'{name}.weight', (Co, KH, KW, Cg))
         self.b = ctx.arena.vector(f'{name}.bias', (self.Cop,)) if (keep_bias and conv.bias is not None) else None
+        _freeze(self.w, conv.weight)
+        _freeze(self.b, conv.bias)
         self.uses = _Uses()
 
     def load_from_torch(self):
@@ -205,6 +209,15 @@ class ConvParams:
             self.ctx.arena.mark_ready(self.b)
 
 
+def _freeze(slot, param, force=False):
+    """A parameter the user froze (``requires_grad=False``: a fine-tuned backbone, the
+    reference model executor's frozen layers) keeps its value: its arena slot is marked
+    frozen, which the fused optimizers honour (no update, no weight decay), as torch.optim
+    skips a parameter whose grad is None."""
+    if slot is not None and (force or (param is not None and not param.requires_grad)):
+        slot.frozen = True
+
+
 class BNParams:
     """nn.BatchNorm2d / BatchNorm1d -> gamma / beta slots [Cp] + running statistics."""
 
@@ -218,6 +231,10 @@ class BNParams:
         self.track = bn.track_running_stats
         self.gamma = ctx.arena.vector(f'{name}.weight', (self.Cp,))
         self.beta = ctx.arena.vector(f'{name}.bias', (self.Cp,))
+        # affine=False: gamma = 1 / beta = 0 stay constants (the slots exist so the kernels
+        # have something to read, but the optimizer never moves or decays them)
+        _freeze(self.gamma, bn.weight if self.affine else None, force=not self.affine)
+        _freeze(self.beta, bn.bias if self.affine else None, force=not self.affine)
         self.run_mean = self.run_var = None
         self.uses = _Uses()
 
@@ -292,6 +309,8 @@ class LinearParams:
         self.Op, self.Ip = ceil8(self.O), ceil8(self.I)
         self.w = ctx.arena.weight(f'{name}.weight', (self.Op, self.Ip))
         self.b = ctx.arena.vector(f'{name}.bias', (self.Op,)) if lin.bias is not None else None
+        _freeze(self.w, lin.weight)
+        _freeze(self.b, lin.bias)
         self.uses = _Uses()
 
     def load_from_torch(self):

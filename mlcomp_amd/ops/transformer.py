@@ -121,10 +121,12 @@ def embed_bwd(ds, ids, tt, word_grad, pos_grad, tok_grad):
     H = ds.shape[-1]
     if _cuda(ds):
         ntypes = tok_grad.shape[0] if tok_grad is not None else 1
-        key = (str(ds.device), S * ntypes * H)
-        pt = _EMB_SCRATCH.get(key)
+        from .functional import workspace_key, workspace_store
+        key = (workspace_key(ds.device), S * ntypes * H)
+        store = workspace_store(_EMB_SCRATCH)
+        pt = store.get(key)
         if pt is None:    # [S][ntypes][H] partial sums, left zeroed by the kernel
-            pt = _EMB_SCRATCH[key] = torch.zeros(S * ntypes * H, device=ds.device, dtype=torch.float32)
+            pt = store[key] = torch.zeros(S * ntypes * H, device=ds.device, dtype=torch.float32)
         # contiguous copies bound to names: a temporary freed while the argument list is
         # still being built could hand its block to the next copy before the kernel runs
         dsc, idc = ds.contiguous(), ids.contiguous()
@@ -311,14 +313,15 @@ def gemm_workspace(device, n: int) -> torch.Tensor:
     """fp32 split-K slab workspace per device (``splits`` x M x N partial sums, fully
     overwritten by each split-K GEMM), grown on demand - first during eager warm-up, so
     graph capture reuses it."""
-    from .functional import workspace_key
+    from .functional import workspace_key, workspace_store
     key = workspace_key(device)
-    buf = _WS.get(key)
+    store = workspace_store(_WS)
+    buf = store.get(key)
     if buf is None or buf.numel() < n:
         if buf is not None:
             _WS_OLD.append(buf)
-        buf = torch.zeros(max(n, 1 << 20), device=device, dtype=torch.float32)
-        _WS[key] = buf
+        buf = torch.empty(max(n, 1 << 20), device=device, dtype=torch.float32)
+        store[key] = buf
     return buf
 
 
@@ -395,13 +398,17 @@ _SCRATCH = {}
 def colsum_scratch(device, C: int) -> torch.Tensor:
     """A zeroed NSTAT*C fp32 buffer per device, grown on demand; the kernel leaves it
     zeroed, so every call of a step (and a captured graph) can share it."""
-    key = str(device)
-    buf = _SCRATCH.get(key)
+    from .functional import workspace_key, workspace_store
+    # per stream role and capture scope, like the split-K slabs: the kernel relies on the
+    # buffer being zero on entry, so two colsums that overlap must never share one
+    key = workspace_key(device)
+    store = workspace_store(_SCRATCH)
+    buf = store.get(key)
     if buf is None or buf.numel() < NSTAT * C:
         if buf is not None:
             _WS_OLD.append(buf)
         buf = torch.zeros(NSTAT * max(C, 4096), device=device, dtype=torch.float32)
-        _SCRATCH[key] = buf
+        store[key] = buf
     return buf
 
 

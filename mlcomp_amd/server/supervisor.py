@@ -176,13 +176,23 @@ class SupervisorBuilder:
             done = [c.finished for c in kids if c.status == TaskStatus.Success.value and c.finished]
             if done and (now() - min(done)).total_seconds() < STRAGGLER_SECONDS:
                 return
-            for c in kids:
-                if c.status == TaskStatus.InProgress.value and c.pid and c.computer_assigned:
-                    q = queue_name(c.computer_assigned, c.docker_assigned or 'default', 'supervisor')
-                    ok = self.broker.call(q, 'kill', c.pid, timeout=10.0)
-                    if ok:
-                        c.status = TaskStatus.Success.value
+            # mark first, kill after: the killed rank's worker sees a non-zero exit code and
+            # must find the task already terminal (and flagged), or it would record a lost
+            # process - a Failed rank whose log line triggers _restart_on_fatal on a DAG
+            # whose training finished
+            victims = [c for c in kids if c.status == TaskStatus.InProgress.value and c.pid and c.computer_assigned]
+            for c in victims:
+                info = yaml_load(c.additional_info) or {}
+                info['killed_by_supervisor'] = True
+                c.additional_info = yaml_dump(info)
+                c.status = TaskStatus.Success.value
             self.provider.commit()
+            for c in victims:
+                q = queue_name(c.computer_assigned, c.docker_assigned or 'default', 'supervisor')
+                try:
+                    self.broker.call(q, 'kill', c.pid, timeout=10.0)
+                except Exception:
+                    pass   # the worker supervisor's liveness scan reaps it
 
     def _restart_on_fatal(self, task: Task):
         if task.type != TaskType.Train.value:

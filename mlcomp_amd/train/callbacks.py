@@ -80,7 +80,22 @@ class TimerCallback(Callback):
         fps = self.acc['samples'] / max(1e-9, self.acc['batch_time'])
         state.loader_metrics['_timer/_fps'] = fps
         if state.world_size > 1:
-            state.loader_metrics['_timer/_fps_node'] = fps * state.world_size
+            state.loader_metrics['_timer/_fps_node'] = self._node_sum(state, fps)
+
+    @staticmethod
+    def _node_sum(state, fps):
+        """Whole-job samples/s: the SUM of every rank's own rate (BASELINE.md's whole-node
+        metric), one all-reduce per loader; every rank runs this callback.  Falls back to
+        rank 0's rate x world size only when no process group is up."""
+        import torch
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() != state.world_size:
+            return fps * state.world_size
+        dev = getattr(getattr(state, 'runner', None), 'device', None)
+        on_gpu = dist.get_backend() == 'nccl' and dev is not None and dev.type == 'cuda'
+        t = torch.tensor([fps], dtype=torch.float64, device=dev if on_gpu else 'cpu')
+        dist.all_reduce(t)
+        return float(t.item())
 
 
 @register_callback

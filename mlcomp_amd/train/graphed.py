@@ -96,11 +96,15 @@ class GraphedStep:
         return bool(flag.item() > 0.5)
 
     def _capture(self):
+        from ..ops import functional as Fn
         torch.cuda.synchronize(self.device)
         graph = torch.cuda.CUDAGraph()
         err = None
+        # the graph's split-K slabs and zero-on-entry scratch belong to this step (and
+        # die with it): eager work elsewhere never writes what a replay reads
+        self._capture_ws = {}
         try:
-            with torch.cuda.graph(graph):
+            with torch.cuda.graph(graph), Fn.capture_scope(self._capture_ws):
                 self._body()
         except Exception as e:   # capture refused (a collective or op the runtime cannot
             err = e              # capture): decided collectively below

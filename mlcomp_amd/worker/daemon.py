@@ -163,6 +163,8 @@ class WorkerPool:
             if t is None or t.status != TaskStatus.InProgress.value:
                 return
             info = yaml_load(t.additional_info) or {}
+            if info.get('killed_by_supervisor'):
+                return     # a straggler rank the scheduler stopped on purpose
             for pid in info.get('child_processes', []):
                 kill_pid(pid)
             create_logger(session, 'WorkerPool', console=False).error(

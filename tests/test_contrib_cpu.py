@@ -112,6 +112,18 @@ def test_image_datasets(tmp_path):
     assert sorted(r['label'] for r in limited.data) == [0, 0, 0, 1, 1, 1]
     assert len(ImageDataset(img_folder=str(tmp_path / 'img'), fold_csv=str(tmp_path / 'fold.csv'), max_count=4)) == 4
 
+    class RefStyle(ImageDataset):
+        # a subclass written against the reference's hooks
+        # (/root/reference/mlcomp/contrib/dataset/classify.py:82-114)
+        def _get_item_before_transform(self, row, item):
+            item['image'] = item['image'] * 0 + 7
+
+        def _get_item_after_transform(self, row, transformed, res):
+            super()._get_item_after_transform(row, transformed, res)
+            res['extra'] = row['fold']
+    r = RefStyle(img_folder=str(tmp_path / 'img'), fold_csv=str(tmp_path / 'fold.csv'), fold=0)[0]
+    assert (r['features'] == 7).all() and 'extra' in r and r['targets'] in (0, 1)
+
 
 def test_video_dataset(tmp_path):
     import pandas as pd

@@ -240,6 +240,75 @@ def test_generic_step_optimizer_matches_torch_optim_semantics():
         assert step.last_loss() == pytest.approx(want, rel=0.02)
 
 
+def test_eval_graph_runs_dropout_in_eval_mode():
+    """A model with a live Dropout (p = 0.5): net.eval() outputs are deterministic and equal
+    torch's eval() outputs, and net.train() drops again (the leaf Dropout module is shared
+    by both lowered graphs and the user model)."""
+    class Drop(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc1 = nn.Linear(32, 64)
+            self.drop = nn.Dropout(0.5)
+            self.fc2 = nn.Linear(64, 8)
+
+        def forward(self, x):
+            return self.fc2(self.drop(F.relu(self.fc1(x))))
+
+    torch.manual_seed(0)
+    m = Drop()
+    ref = Drop()
+    ref.load_state_dict(m.state_dict())
+    net = GenericNet(m, 'cpu')
+    x = torch.randn(16, 32)
+    with torch.no_grad():
+        t1, t2 = net(x), net(x)
+        assert _rel(t1, t2) > 1e-2            # training graph: dropout active
+        net.eval()
+        e1, e2 = net(x), net(x)
+        assert torch.equal(e1, e2)
+        assert _rel(e1, ref.eval()(x)) < 2e-2
+        net.train()
+        assert _rel(net(x), net(x)) > 1e-2
+
+
+def test_frozen_and_non_affine_parameters_are_not_updated():
+    """requires_grad=False parameters and an affine=False BatchNorm's gamma / beta keep their
+    values through a fused SGD step with weight decay (torch.optim skips them), while the
+    trainable ones move."""
+    from mlcomp_amd.train.native_generic_step import NativeGenericStep
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.conv1 = nn.Conv2d(3, 16, 3, padding=1)
+            self.bn1 = nn.BatchNorm2d(16, affine=False)
+            self.conv2 = nn.Conv2d(16, 16, 3, padding=1)
+            self.bn2 = nn.BatchNorm2d(16)
+            self.fc = nn.Linear(16, 10)
+
+        def forward(self, x):
+            x = F.relu(self.bn1(self.conv1(x)))
+            x = F.relu(self.bn2(self.conv2(x)))
+            return self.fc(x.mean((2, 3)))
+
+    torch.manual_seed(0)
+    m = Net()
+    for p in list(m.conv1.parameters()) + list(m.bn2.parameters()):
+        p.requires_grad_(False)
+    x, y = torch.randn(4, 3, 8, 8), torch.randint(0, 10, (4,))
+    step = NativeGenericStep(m, x, y, device='cpu', use_graph=False, optimizer='SGD', lr=0.1, momentum=0.9,
+                             weight_decay=0.1)
+    by = step.net.arena.by_name
+    before = {k: s.master.clone() for k, s in by.items()}
+    step()
+    frozen = {k for k, s in by.items() if s.frozen}
+    # (conv1.bias has no slot: a bias in front of a batch-statistics BN only shifts its mean)
+    assert {'conv1.weight', 'bn1.weight', 'bn1.bias', 'bn2.weight', 'bn2.bias'} <= frozen, frozen
+    for k, s in by.items():
+        moved = not torch.equal(s.master, before[k])
+        assert moved != (k in frozen), (k, moved)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(('127.0.0.1', 0))

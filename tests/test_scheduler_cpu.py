@@ -316,3 +316,36 @@ def test_rccl_transport_summary():
         'node:123:456 [0] NCCL INFO RCCL version 2.22.3 via nothing',
     ])
     assert transport_summary(log) == {'P2P/IPC': 2, 'SHM/direct/direct': 1}
+
+
+def test_straggler_is_marked_before_the_kill_and_not_reported_lost(sched, monkeypatch):
+    """A Train parent with one rank finished and one still running (a DDP hang): the
+    straggler is Success (and flagged) BEFORE its kill is sent, so the worker that sees its
+    process die with a non-zero code does not fail it as a lost process (which would make
+    the fatal-restart matcher restart a finished DAG)."""
+    from mlcomp_amd.server import supervisor as S
+    from mlcomp_amd.worker.daemon import WorkerPool
+    from mlcomp_amd.db.models import now
+    s, sup, b = sched['s'], sched['sup'], sched['broker']
+    _computer(s, 'node1', gpu=2)
+    tid = _dag(s, {'t': {'type': 'catalyst', 'gpu': 2, 'distr': True}})['t'][0]
+    sup.build()
+    (r0, _), (r1, _) = _ranks(s, tid)
+    r0.status, r0.finished = TaskStatus.Success.value, now() - datetime.timedelta(minutes=10)
+    r1.status, r1.pid = TaskStatus.InProgress.value, 424242
+    s.commit()
+    monkeypatch.setattr(S, 'STRAGGLER_SECONDS', 0)
+    seen = {}
+
+    def call(queue, name, *args, timeout=None):
+        seen['status'] = _tasks(s, id=r1.id)[0].status        # the state the dying worker will read
+        return True
+    monkeypatch.setattr(b, 'call', call, raising=False)
+    sup.build()
+    assert seen['status'] == TaskStatus.Success.value
+    WorkerPool([0])._process_lost(0, r1.id, -9)
+    t = _tasks(s, id=r1.id)[0]
+    assert t.status == TaskStatus.Success.value
+    assert yaml_load(t.additional_info).get('killed_by_supervisor')
+    sup.build()
+    assert not (yaml_load(_tasks(s, id=tid)[0].additional_info) or {}).get('auto_restarts')

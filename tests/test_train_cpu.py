@@ -144,7 +144,7 @@ def _ddp_worker(rank, world, port, logdir, out):
     st = r.run_experiment()
     w = torch.cat([p.detach().flatten() for p in r.model.parameters()])
     torch.save({'w': w, 'n': len(r.loaders['train'].sampler), 'fps_node': st.epoch_metrics.get(
-        'train__timer/_fps_node')}, os.path.join(out, f'r{rank}.pt'))
+        'train__timer/_fps_node'), 'fps': st.epoch_metrics.get('train__timer/_fps')}, os.path.join(out, f'r{rank}.pt'))
     dist.destroy_process_group()
 
 
@@ -154,7 +154,9 @@ def test_ddp_gloo_two_ranks_stay_in_sync(tmp_path):
     b = torch.load(tmp_path / 'r1.pt', weights_only=True)
     assert a['n'] == b['n'] == 32          # 64 samples split over 2 ranks
     assert torch.allclose(a['w'], b['w'])  # gradients all-reduced -> identical weights
-    assert a['fps_node'] is not None
+    # whole-node throughput is the sum of the ranks' own rates, the same on every rank
+    assert a['fps_node'] == pytest.approx(a['fps'] + b['fps'], rel=1e-6)
+    assert b['fps_node'] == pytest.approx(a['fps_node'], rel=1e-9)
     assert (tmp_path / 'log' / 'checkpoints' / 'last_full.pth').exists()
 
 
