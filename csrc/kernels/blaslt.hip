@@ -16,8 +16,8 @@
 //     capturing runs native), so a captured step replays whatever warm-up chose;
 //   * deterministic mode (mlc_set_deterministic) always runs native.
 //
-// MLC_BLASLT=0 disables the library path, =1 forces it wherever it applies, unset/auto
-// times both.  Every hipBLASLt call gets a private workspace per (device, stream): the
+// MLC_BLASLT unset/0 disables the library path (the default since round 5: no vendor GEMM
+// on the training hot path), =1 forces it wherever it applies, =auto times both.  Every hipBLASLt call gets a private workspace per (device, stream): the
 // weight-gradient side stream and the main stream may run GEMMs concurrently.
 //
 // Row-major problem C[M][N] = op(A) op(B) maps onto hipBLASLt's column-major D = A' B'
@@ -63,7 +63,9 @@ int g_verbose = 0;
 int mode() {
   if (g_mode < 0) {
     const char* e = getenv("MLC_BLASLT");
-    g_mode = !e || !strcmp(e, "auto") ? 2 : atoi(e) ? 1 : 0;
+    // default OFF: the training steps run the native MFMA kernels only; the library
+    // remains as an opt-in A/B reference (MLC_BLASLT=auto times both, =1 forces it)
+    g_mode = !e ? 0 : !strcmp(e, "auto") ? 2 : atoi(e) ? 1 : 0;
     if (const char* m = getenv("MLC_BLASLT_MARGIN")) g_margin = (float)atof(m);
     if (const char* v = getenv("MLC_BLASLT_VERBOSE")) g_verbose = atoi(v);
   }
@@ -275,7 +277,9 @@ Plan* choose(const Key& k, hipStream_t st, size_t out_bytes, FN native, FL lib, 
   *sp = s;
   if (it != g_plans.end() && it->second.pick >= 0) return &it->second;
   Plan& p = g_plans[k];
-  bool built = build_plan(r, k, p, k.epi);
+  // kind 0 keys carry the residual-addend form in bit 1 (its own timing and plan); the
+  // library epilogue is the bias bit only
+  bool built = build_plan(r, k, p, k.kind == 0 ? (k.epi & 1) : k.epi);
   if (!built && k.kind == 1) {   // no BGRADB kernel for this problem: plain GEMM + column sums
     destroy_plan(p);
     built = build_plan(r, k, p, 0);
@@ -336,7 +340,7 @@ MLC_EXPORT int mlc_gemm_bf16_ex(const bf16* A, const bf16* B, bf16* C, int M, in
                                 const bf16* addend, const bf16* dact, float* ws, long ws_floats,
                                 hipStream_t st) {
   if (act == 0 && !preact && !dact && !(bias && addend) && mode()) {
-    const Key k{cur_dev(), 0, M, N, K, lda, ldb, ldc, ta, tb, bias ? 1 : 0};
+    const Key k{cur_dev(), 0, M, N, K, lda, ldb, ldc, ta, tb, (bias ? 1 : 0) | (addend ? 2 : 0)};
     DevRes* r = nullptr;
     StreamRes* s = nullptr;
     auto native = [&](void* out, float*) {

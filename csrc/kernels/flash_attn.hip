@@ -2,8 +2,9 @@
 //
 // transformer.hip's attn:: kernels hold a whole S x S score tile in registers and so only
 // take head dim 64 with S in {64, 128} (BERT-base fine-tuning).  These kernels stream the
-// keys (forward, dQ) or queries (dK/dV) through LDS in 64-row tiles, so S is any multiple
-// of 64 and the head dim D is 64 or 128; the per-step work is O(S) registers and LDS.
+// keys (forward, dQ) or queries (dK/dV) through LDS in 64-row tiles, so S is any length
+// (the last tile's rows past S are masked: -inf key bias / +inf log-sum-exp) and the head
+// dim D is 64 or 128; the per-step work is O(S) registers and LDS.
 // Reference behaviour: the attention inside the BERT encoder the reference fine-tunes
 // through Catalyst; numerics match ops/transformer.py attn_fwd/attn_bwd.
 //
@@ -112,10 +113,13 @@ template <int D>
 struct Tile {
   static constexpr int CH = D / 8, N = KT * CH / NT;
   uint4 v[N];
-  __device__ __forceinline__ void load(const bf16* src, int ld, int tid) {
+  __device__ __forceinline__ void load(const bf16* src, int ld, int tid, int valid = KT) {
+    // rows past `valid` (the tail tile of an S that is not a multiple of 64) re-read the
+    // last valid row: in bounds, finite, and masked out by the caller (-inf key bias /
+    // +inf log-sum-exp), so they contribute exactly zero
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      const int c = tid + NT * j, r = c / CH, ch = c % CH;
+      const int c = tid + NT * j, r = min(c / CH, valid - 1), ch = c % CH;
       v[j] = *reinterpret_cast<const uint4*>(src + (size_t)r * ld + ch * 8);
     }
   }
@@ -170,9 +174,10 @@ fwd_kernel(const bf16* __restrict__ qkv, const float* __restrict__ key_bias, bf1
   Tile<D> tk, tv;
   float kbv = 0.f;
   auto fetch = [&](int t) {
-    tk.load(Kg + (size_t)t * KT * ld, ld, tid);
-    tv.load(Vg + (size_t)t * KT * ld, ld, tid);
-    if (tid < KT) kbv = kb ? kb[t * KT + tid] * LOG2E : 0.f;
+    const int valid = min(KT, S - t * KT);
+    tk.load(Kg + (size_t)t * KT * ld, ld, tid, valid);
+    tv.load(Vg + (size_t)t * KT * ld, ld, tid, valid);
+    if (tid < KT) kbv = tid >= valid ? -INFINITY : kb ? kb[t * KT + tid] * LOG2E : 0.f;
   };
   auto put = [&](int t) {
     char* bp = smem + (t & 1) * BUF;
@@ -183,7 +188,7 @@ fwd_kernel(const bf16* __restrict__ qkv, const float* __restrict__ key_bias, bf1
   fetch(0);
   put(0);
   __syncthreads();
-  const int nt = S / KT;
+  const int nt = (S + KT - 1) / KT;   // a partial last tile is masked
   for (int t = 0; t < nt; ++t) {
     const char* Ki = smem + (t & 1) * BUF;
     const char* Vi = Ki + IMG;
@@ -300,9 +305,10 @@ dq_kernel(const bf16* __restrict__ qkv, const float* __restrict__ key_bias, cons
   Tile<D> tk, tv;
   float kbv = 0.f;
   auto fetch = [&](int t) {
-    tk.load(Kg + (size_t)t * KT * ld, ld, tid);
-    tv.load(Vg + (size_t)t * KT * ld, ld, tid);
-    if (tid < KT) kbv = kb ? kb[t * KT + tid] * LOG2E : 0.f;
+    const int valid = min(KT, S - t * KT);
+    tk.load(Kg + (size_t)t * KT * ld, ld, tid, valid);
+    tv.load(Vg + (size_t)t * KT * ld, ld, tid, valid);
+    if (tid < KT) kbv = tid >= valid ? -INFINITY : kb ? kb[t * KT + tid] * LOG2E : 0.f;
   };
   auto put = [&](int t) {
     char* bp = smem + (t & 1) * BUF;
@@ -313,7 +319,7 @@ dq_kernel(const bf16* __restrict__ qkv, const float* __restrict__ key_bias, cons
   fetch(0);
   put(0);
   __syncthreads();
-  const int nt = S / KT;
+  const int nt = (S + KT - 1) / KT;   // a partial last tile is masked
   for (int t = 0; t < nt; ++t) {
     const char* Ki = smem + (t & 1) * BUF;
     const char* Vi = Ki + IMG;
@@ -396,10 +402,12 @@ dkv_kernel(const bf16* __restrict__ qkv, const float* __restrict__ key_bias, con
   Tile<D> tq, to;
   float ld_v = 0.f;   // this thread's lse / dot element of the next tile (threads 0..127)
   auto fetch = [&](int t) {
-    tq.load(Qg + (size_t)t * KT * ld, ld, tid);
-    to.load(dOg + (size_t)t * KT * E, E, tid);
-    if (tid < KT) ld_v = Lg[t * KT + tid] * LOG2E;
-    else if (tid < 2 * KT) ld_v = Dg[t * KT + tid - KT];
+    const int valid = min(KT, S - t * KT);
+    tq.load(Qg + (size_t)t * KT * ld, ld, tid, valid);
+    to.load(dOg + (size_t)t * KT * E, E, tid, valid);
+    // queries past S: lse = +inf makes their probabilities exactly 0
+    if (tid < KT) ld_v = tid < valid ? Lg[t * KT + tid] * LOG2E : INFINITY;
+    else if (tid < 2 * KT) ld_v = tid - KT < valid ? Dg[t * KT + tid - KT] : 0.f;
   };
   auto put = [&](int t) {
     char* bp = smem + (t & 1) * BUF;
@@ -410,7 +418,7 @@ dkv_kernel(const bf16* __restrict__ qkv, const float* __restrict__ key_bias, con
   fetch(0);
   put(0);
   __syncthreads();
-  const int nt = S / KT;
+  const int nt = (S + KT - 1) / KT;   // a partial last tile is masked
   for (int t = 0; t < nt; ++t) {
     const char* bp = smem + (t & 1) * BUF;
     const char* Qi = bp;
@@ -738,13 +746,13 @@ fwd128_kernel(const bf16* __restrict__ qkv, const float* __restrict__ key_bias, 
 int g_bwd128 = -1;
 
 bool flash_shape_ok(int B, int S, int H, int D) {
-  return B > 0 && H > 0 && S >= KT && S % KT == 0 && (D == 64 || D == 128);
+  return B > 0 && H > 0 && S >= 1 && (D == 64 || D == 128);
 }
 
 }  // namespace
 
 // out [B*S][H*D] = softmax(scale * Q K^T + key_bias) V per head, lse [B*H*S] (natural log;
-// +inf for a fully masked row).  S % 64 == 0, D in {64, 128}.
+// +inf for a fully masked row).  Any S >= 1 (a partial last 64-key tile is masked), D in {64, 128}.
 MLC_EXPORT int mlc_flash_fwd(const bf16* qkv, const float* key_bias, bf16* out, float* lse, int B, int S, int H,
                              int D, float scale, float p, const uint32_t* seed, uint32_t salt, hipStream_t st) {
   if (!flash_shape_ok(B, S, H, D)) return -1;

@@ -221,13 +221,32 @@ def _attn_small(S: int, head_dim: int) -> bool:
 
 
 def _attn_flash(S: int, head_dim: int) -> bool:
-    """Shapes of the streaming kernels ``mlc_flash_fwd`` / ``mlc_flash_bwd`` (flash_attn.hip)."""
-    return head_dim in (64, 128) and S >= 64 and S % 64 == 0
+    """Shapes of the streaming kernels ``mlc_flash_fwd`` / ``mlc_flash_bwd`` (flash_attn.hip):
+    any S (a partial last 64-key tile is masked in the kernel), head dim 64 or 128."""
+    return head_dim in (64, 128) and S >= 1
+
+
+def _pad_dim(head_dim: int) -> int:
+    """The kernel head dim a head dim of ``head_dim`` runs at (zero-padded columns change
+    neither the scores nor the kept output columns)."""
+    return 64 if head_dim <= 64 else 128
 
 
 def attn_supported(S: int, head_dim: int) -> bool:
-    """Shapes the fused attention path takes (either kernel family)."""
-    return _attn_small(S, head_dim) or _attn_flash(S, head_dim)
+    """Shapes the fused attention path takes: every S >= 1 and head dim <= 128 (head dims
+    other than 64 / 128 run zero-padded to the next of the two)."""
+    return S >= 1 and 1 <= head_dim <= 128
+
+
+def _pad_heads(t, rows, groups, H, D, Dp):
+    """[rows, groups*H*D] -> [rows, groups*H*Dp] with zero columns after each head."""
+    out = torch.zeros(rows, groups, H, Dp, device=t.device, dtype=t.dtype)
+    out[..., :D] = t.view(rows, groups, H, D)
+    return out.view(rows, groups * H * Dp)
+
+
+def _unpad_heads(t, rows, groups, H, D, Dp):
+    return t.view(rows, groups, H, Dp)[..., :D].reshape(rows, groups * H * D)
 
 
 def _attn_ref_probs(qkv, key_bias, B, S, H, scale, D=64):
@@ -246,6 +265,11 @@ def attn_fwd(qkv, key_bias, B, S, H, scale, p=0.0, seed=None, salt=0, head_dim: 
     Attention-probability dropout uses the softmax kernel's mask indexing
     (((b*H + h)*S + q)*S + key), so every path drops the same elements."""
     D = head_dim
+    if _cuda(qkv) and D not in (64, 128):
+        assert attn_supported(S, D), (S, D)
+        Dp = _pad_dim(D)
+        ctx, lse = attn_fwd(_pad_heads(qkv, B * S, 3, H, D, Dp), key_bias, B, S, H, scale, p, seed, salt, Dp)
+        return _unpad_heads(ctx, B * S, 1, H, D, Dp), lse
     if _cuda(qkv):
         assert attn_supported(S, D) and qkv.is_contiguous() and tuple(qkv.shape) == (B * S, 3 * H * D)
         assert key_bias is None or (key_bias.is_contiguous() and tuple(key_bias.shape) == (B, S))
@@ -275,6 +299,12 @@ def attn_bwd(qkv, key_bias, dctx, lse, B, S, H, scale, p=0.0, seed=None, salt=0,
     """Gradient of :func:`attn_fwd` wrt ``qkv``: returns dqkv [B*S, 3*H*D] bf16.  ``ctx``
     (the forward output) is needed by the streaming kernels (rowsum(dO * O))."""
     D = head_dim
+    if _cuda(qkv) and D not in (64, 128):
+        assert attn_supported(S, D) and ctx is not None, (S, D)
+        Dp = _pad_dim(D)
+        dq = attn_bwd(_pad_heads(qkv, B * S, 3, H, D, Dp), key_bias, _pad_heads(dctx, B * S, 1, H, D, Dp), lse,
+                      B, S, H, scale, p, seed, salt, Dp, ctx=_pad_heads(ctx, B * S, 1, H, D, Dp))
+        return _unpad_heads(dq, B * S, 3, H, D, Dp)
     if _cuda(qkv):
         assert attn_supported(S, D) and qkv.is_contiguous() and tuple(qkv.shape) == (B * S, 3 * H * D)
         assert dctx.is_contiguous() and tuple(dctx.shape) == (B * S, H * D) and lse.numel() == B * H * S

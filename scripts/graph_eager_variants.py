@@ -18,13 +18,16 @@ VARIANTS = [
     'MLC_WORK_STREAM=0,SYNC=eager',
     'MLC_WORK_STREAM=0,EAGER_STREAM=1',
     'MLC_WORK_STREAM=1',
+    'MLC_WORK_STREAM=0,EAGER_TORCH=1',
+    'MLC_WORK_STREAM=0,GRAPH_STREAM=1',
 ]
 
 
 def child(spec):
     env = dict(kv.split('=') for kv in spec.split(',') if kv)
     import torch
-    sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'tests')]
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..')
+    sys.path[:0] = [root, os.path.join(root, 'tests')]
     from test_generic_gpu import _models, _no_stochastic
     from mlcomp_amd.train.native_generic_step import NativeGenericStep
     make, shape, ncls = _models()['efficientnet-b0']
@@ -34,6 +37,42 @@ def child(spec):
     x, y = torch.randn(*shape), torch.randint(0, ncls, (shape[0],))
     steps = [NativeGenericStep(m, x, y, device='cuda', use_graph=g, optimizer='SGD', lr=0.02, momentum=0.9)
              for m, g in zip(ms, (False, True))]
+    if env.get('EAGER_TORCH'):          # the eager twin on stock PyTorch ops (MIOpen / hipBLASLt)
+        tm = ms[0].cuda()
+        topt = torch.optim.SGD(tm.parameters(), lr=0.02, momentum=0.9)
+        xc, yc = x.cuda(), y.cuda()
+
+        class TorchStep:
+            _l = None
+
+            def __call__(self):
+                topt.zero_grad()
+                with torch.autocast('cuda', dtype=torch.bfloat16):
+                    out = tm(xc)
+                loss = torch.nn.functional.cross_entropy(out.float(), yc)
+                loss.backward()
+                topt.step()
+                self._l = loss.detach()
+
+            def last_loss(self):
+                return float(self._l.item())
+        steps[0] = TorchStep()
+    gs = torch.cuda.Stream() if env.get('GRAPH_STREAM') else None
+    if gs is not None:                  # replay the graphed twin on a created stream
+        inner = steps[1]
+
+        class OnStream:
+            graph = None
+
+            def __call__(self):
+                gs.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(gs):
+                    inner()
+                torch.cuda.current_stream().wait_stream(gs)
+
+            def last_loss(self):
+                return inner.last_loss()
+        steps[1] = OnStream()
     es = torch.cuda.Stream() if env.get('EAGER_STREAM') else None
     bad = {0: None, 1: None}
     losses = ([], [])

@@ -164,10 +164,14 @@ def test_fused_attention_fwd_bwd(B, S, H, p, masked, monkeypatch):
 
 @pytest.mark.parametrize('B,S,H,D,p,masked', [(2, 64, 2, 64, 0.0, False), (2, 192, 3, 64, 0.1, True),
                                                (1, 512, 2, 64, 0.1, True), (2, 128, 2, 128, 0.0, True),
-                                               (1, 320, 2, 128, 0.1, False), (3, 128, 4, 64, 0.1, True)])
+                                               (1, 320, 2, 128, 0.1, False), (3, 128, 4, 64, 0.1, True),
+                                               (2, 100, 2, 64, 0.1, True), (3, 45, 3, 128, 0.0, True),
+                                               (1, 1, 2, 64, 0.0, False), (2, 200, 2, 32, 0.1, True),
+                                               (2, 77, 2, 80, 0.0, True)])
 def test_flash_attention_fwd_bwd(B, S, H, D, p, masked, monkeypatch):
     """Streaming (flash) kernels vs the fp32 reference: S multiple of 64 incl. S % 128 != 0
-    (a block's last waves idle), head dims 64 / 128, key masks and attention dropout; the
+    (a block's last waves idle), S with a partial last key / query tile (100, 45, 1, 200, 77),
+    head dims 64 / 128 and zero-padded 32 / 80, key masks and attention dropout; the
     (3, 128, 4, 64) case forces the flash path on a shape the whole-tile kernel also takes."""
     import math
     monkeypatch.setattr(Tx, '_FLASH_ONLY', True)
@@ -256,7 +260,7 @@ def test_flash_attention_fully_masked_sequence(monkeypatch):
     assert ctx[:S].abs().max().item() > 0
 
 
-@pytest.mark.parametrize('S,hidden,heads', [(256, 128, 2), (192, 256, 2)])
+@pytest.mark.parametrize('S,hidden,heads', [(256, 128, 2), (192, 256, 2), (100, 128, 2), (70, 128, 4)])
 def test_native_bert_flash_matches_torch_autograd(S, hidden, heads):
     """Native BERT on the GPU with the flash attention path (S > 128, head dim 64 / 128)
     against fp32 autograd of the plain PyTorch model on the same weights."""
