@@ -49,7 +49,23 @@ def parse():
                         'pipeline (C++ gather threads + GPU augment kernel) instead of a resident batch')
     p.add_argument('--records', default=None, help='record file for --data records (default: a generated one)')
     p.add_argument('--loader-threads', type=int, default=12)
+    p.add_argument('--comm', default='auto', choices=['auto', 'rccl1'],
+                   help='rccl1: give a one-GPU run a world-1 RCCL communicator, so the production gradient '
+                        'bucketer issues its RCCL all-reduces on the side stream (overlap evidence)')
     return p.parse_args()
+
+
+def _world1_rccl(device):
+    """A one-rank RCCL communicator over a private TCP store (``--comm rccl1``)."""
+    import socket
+    import torch.distributed as dist
+    from mlcomp_amd.parallel.comm import RcclComm
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    store = dist.TCPStore('127.0.0.1', port, 1, True)
+    return RcclComm(0, 1, device, store=store, tag='bench')
 
 
 def main():
@@ -71,6 +87,7 @@ def main():
     if world > 1:
         dist.init_process_group('nccl', device_id=device)
 
+    comm = _world1_rccl(device) if (args.comm == 'rccl1' and world == 1 and args.impl == 'native') else None
     is_bert = args.model.startswith('bert')
     is_unet = args.model.split('-')[0] in ('unet', 'linknet', 'fpn', 'pspnet', 'deeplab')
     if args.batch is None:
@@ -93,13 +110,13 @@ def main():
         from mlcomp_amd.train.bert import build_bert_step
         step = build_bert_step(args.model, batch=args.batch, seq_len=args.seq_len, impl=args.impl,
                                device=device, world_size=world,
-                               use_graph=(args.graph if args.graph >= 0 else None))
+                               use_graph=(args.graph if args.graph >= 0 else None), comm=comm)
     else:
         from mlcomp_amd.train.imagenet import build_train_step
         step = build_train_step(args.model, batch=args.batch, impl=args.impl,
                                 image_size=args.image_size, device=device,
                                 world_size=world,
-                                use_graph=(args.graph if args.graph >= 0 else None))
+                                use_graph=(args.graph if args.graph >= 0 else None), comm=comm)
 
     feed = None
     if args.data == 'records':
@@ -202,6 +219,8 @@ def main():
                 'final_loss': loss,
             },
         }
+        if comm is not None:
+            out['config']['comm'] = 'world-1 RCCL communicator (bucketed all-reduces issued)'
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

@@ -57,6 +57,98 @@ def from_nhwc(y: torch.Tensor, C: int) -> torch.Tensor:
     return y.permute(0, 3, 1, 2)
 
 
+def frames_of(x: torch.Tensor) -> torch.Tensor:
+    """Logical [N, C, T, H, W] -> logical [N*T, C, H, W] (the T frames as images).  A view
+    when x is channels_last_3d ([N, T, H, W, C] in memory), which every 3D site emits."""
+    N, C, T, H, W = x.shape
+    return x.transpose(1, 2).reshape(N * T, C, H, W)
+
+
+def video_of(y: torch.Tensor, N: int) -> torch.Tensor:
+    """Inverse of :func:`frames_of`: logical [N*T, C, H, W] -> [N, C, T, H, W] (a view of a
+    channels_last frame tensor, i.e. channels_last_3d)."""
+    NT, C, H, W = y.shape
+    return y.reshape(N, NT // N, C, H, W).transpose(1, 2)
+
+
+class Conv3dAs2d:
+    """An nn.Conv3d (or nn.Conv1d) seen as the 2D conv over frames that computes it: the
+    kt temporal taps are unfolded into the channels (channel c*kt + dt holds frame
+    t*st + dt*dil - pad of channel c; per-group channels stay contiguous), so the filter is
+    the conv's own weight viewed as [Co, Cg*kt, kh, kw] - no copy, exports write through.
+    The 2D conv then runs over N*To frames on the implicit-GEMM / grouped / depthwise
+    kernels, and a BatchNorm3d over its output is a BatchNorm2d over those frames."""
+
+    def __init__(self, m: nn.Module):
+        self.src3d = m
+        if isinstance(m, nn.Conv1d):
+            (kt,), (st,), (pt,), (dt,) = m.kernel_size, m.stride, m.padding, m.dilation
+            kh = kw = 1
+            self.stride, self.padding, self.dilation = (1, 1), (0, 0), (1, 1)
+        else:
+            kt, kh, kw = m.kernel_size
+            st, pt, dt = m.stride[0], m.padding[0], m.dilation[0]
+            self.stride, self.padding, self.dilation = tuple(m.stride[1:]), tuple(m.padding[1:]), tuple(m.dilation[1:])
+        self.kt, self.st, self.pt, self.dt = kt, st, pt, dt
+        self.kernel_size = (kh, kw)
+        self.groups = m.groups
+        self.padding_mode = m.padding_mode
+        self.in_channels = m.in_channels * kt
+        self.out_channels = m.out_channels
+        self.bias = m.bias
+        self._shape = (m.weight.shape[0], m.weight.shape[1] * kt, kh, kw)
+
+    @property
+    def weight(self):
+        return self.src3d.weight.view(self._shape)
+
+    def unfold(self, x: torch.Tensor) -> torch.Tensor:
+        """Logical [N, C, T, H, W] (or [N, C, L]) -> the frames [N*To, C*kt, H, W] the 2D
+        conv reads (torch gather / pad ops: autograd folds the gradient back)."""
+        if x.dim() == 3:
+            x = x[:, :, :, None, None]
+        N, C, T, H, W = x.shape
+        kt, st, pt, dt = self.kt, self.st, self.pt, self.dt
+        if kt == 1 and st == 1 and pt == 0:
+            return frames_of(x)
+        To = (T + 2 * pt - dt * (kt - 1) - 1) // st + 1
+        if pt:
+            x = torch.nn.functional.pad(x, (0, 0, 0, 0, pt, pt))
+        idx = (torch.arange(To, device=x.device)[:, None] * st + torch.arange(kt, device=x.device)[None] * dt)
+        g = x.index_select(2, idx.reshape(-1)).reshape(N, C, To, kt, H, W)
+        return g.permute(0, 2, 1, 3, 4, 5).reshape(N * To, C * kt, H, W)
+
+    def fold_out(self, y: torch.Tensor, N: int, one_d: bool) -> torch.Tensor:
+        """The 2D conv's frame output back to the conv's logical output layout."""
+        out = video_of(y, N)
+        return out[:, :, :, 0, 0] if one_d else out
+
+    def frames_like_out(self, r: torch.Tensor) -> torch.Tensor:
+        """A tensor of the conv's output shape (a residual) as output frames."""
+        return frames_of(r[:, :, :, None, None] if r.dim() == 3 else r)
+
+
+class Frames(nn.Module):
+    """Runs a 2D site over the frames of a 5D (or, for Conv1d, 3D) tensor: temporal unfold
+    (convs), the site on N*T frames, the result back in the caller's layout."""
+
+    def __init__(self, site: nn.Module, conv: Optional[Conv3dAs2d] = None):
+        super().__init__()
+        self.site = site
+        self._conv = conv
+
+    def forward(self, x, res=None):
+        c = self._conv
+        if c is not None:
+            xf = c.unfold(x)
+            rf = c.frames_like_out(res) if res is not None else None
+            y = self.site(xf, rf) if rf is not None else self.site(xf)
+            return c.fold_out(y, x.shape[0], x.dim() == 3)
+        xf = frames_of(x)
+        y = self.site(xf)
+        return video_of(y, x.shape[0])
+
+
 class _Uses:
     """Counts the forward calls of a parameter set in a step; backward marks its slots ready
     only after the last of them (weight sharing across call sites)."""
@@ -495,12 +587,16 @@ class BNAct(Site):
             x = x[:, :, None, None]
         elif x.dim() == 3:
             x = x[:, :, :, None]
+        elif x.dim() == 5:            # BatchNorm3d: per channel over (N, T, H, W) = N*T frames
+            x = frames_of(x)
         return to_nhwc(x, self.bn.Cp)
 
     def _from(self, z, like):
         out = from_nhwc(z, self.bn.C)
         if like.dim() == 2:
             return out[:, :, 0, 0]
+        if like.dim() == 5:
+            return video_of(out, like.shape[0])
         return out[..., 0] if like.dim() == 3 else out
 
     def fwd(self, x, res=None):

@@ -48,13 +48,14 @@ class _TorchBertStep:
 
 
 def build_bert_step(model_name='bert-base', batch=32, seq_len=128, impl='native', device=None, world_size=1,
-                    use_graph: Optional[bool] = None, num_labels=2, lr=2e-5):
+                    use_graph: Optional[bool] = None, num_labels=2, lr=2e-5, comm=None):
     device = device or torch.device('cuda')
     if impl == 'torch':
         return _TorchBertStep(model_name, batch, seq_len, device, world_size, num_labels, lr)
     from .native_bert_step import NativeBertStep
     return NativeBertStep(model_name, batch=batch, seq_len=seq_len, device=device, world_size=world_size,
-                          use_graph=True if use_graph is None else use_graph, num_labels=num_labels, lr=lr)
+                          use_graph=True if use_graph is None else use_graph, num_labels=num_labels, lr=lr,
+                          comm=comm)
 
 
 __all__ = ['build_bert_step']

@@ -52,7 +52,7 @@ class _TorchStep:
 
 def build_train_step(model_name: str = 'resnet50', batch: int = 256, impl: str = 'native',
                      image_size: int = 224, device=None, world_size: int = 1,
-                     use_graph: Optional[bool] = None, num_classes: int = 1000):
+                     use_graph: Optional[bool] = None, num_classes: int = 1000, comm=None):
     device = device or torch.device('cuda')
     if impl == 'torch':
         return _TorchStep(model_name, batch, image_size, device, world_size, num_classes)
@@ -60,4 +60,4 @@ def build_train_step(model_name: str = 'resnet50', batch: int = 256, impl: str =
     return NativeClassifierStep(model_name, batch=batch, image_size=image_size,
                                 device=device, world_size=world_size,
                                 use_graph=(True if use_graph is None else use_graph),
-                                num_classes=num_classes)
+                                num_classes=num_classes, comm=comm)

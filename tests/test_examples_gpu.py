@@ -80,3 +80,38 @@ def test_unet_segmentation_train_then_valid_dag_on_gpu(cluster):
     assert all(v == TaskStatus.Success for v in res.values()), res
     t, eng = _engine_info(ids[0])
     assert t.executor == 'train' and eng['stage1']['engine'] == 'native', eng
+
+
+@pytest.mark.timeout(600)
+def test_resnet50_dag_train_task_throughput_matches_bench(cluster):
+    """The headline metric measured where the reference reports it: the ResNet-50 DAG train
+    task (examples/resnet50_ddp, batch 512 per GPU, native engine) through scheduler ->
+    broker -> worker -> runner, its ``_timer/_fps`` series of the warm epoch (reference:
+    migration/versions/002/report_layout/base_time.yml:9) within 5 % of bench.py's bare
+    step at the same config, run in the same test on the same GPU."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from mlcomp_amd.db.core import Session
+    from mlcomp_amd.db.enums import TaskStatus
+    from mlcomp_amd.db.models import ReportSeries
+    ids = _ids(_run_example(cluster['tmp'], 'resnet50_ddp/config.yml', params={
+        'executors/train/gpu': 1,
+        'executors/train/params/stages/data_params/steps': 120,
+        'executors/train/params/stages/state_params/num_epochs': 2}))
+    res = _wait_live(cluster, ids, timeout=480)
+    assert all(v == TaskStatus.Success for v in res.values()), res
+    s = Session.create_session(key='fps')
+    rows = s.query(ReportSeries).filter(ReportSeries.task.in_(ids), ReportSeries.name == '_timer/_fps',
+                                        ReportSeries.part == 'train').all()
+    assert rows, 'no _timer/_fps series'
+    dag_fps = max(rows, key=lambda r: r.epoch).value
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--steps', '30', '--warmup', '5'],
+                       capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    bench = json.loads(r.stdout.strip().splitlines()[-1])
+    print(f'DAG train task _timer/_fps {dag_fps:.1f} img/s (epoch {max(x.epoch for x in rows)}), '
+          f'bench.py {bench["value"]:.1f} img/s')
+    assert dag_fps >= 0.95 * bench['value'], (dag_fps, bench['value'])

@@ -449,3 +449,89 @@ def test_transposed_conv_sites_match_fp32_autograd():
 def test_linknet_lowers_completely():
     from mlcomp_amd.contrib.segmentation.models import Linknet
     assert lower_or_none(Linknet(encoder_name='resnet34', classes=1)) is None
+
+
+@pytest.mark.parametrize('kw', [
+    dict(residual_transformation_type='postactivated_bottleneck_transformation', num_groups=2, width_per_group=8),
+    dict(residual_transformation_type='basic_transformation'),
+    dict(residual_transformation_type='basic_r2plus1d_transformation', stem_name='r2plus1d_stem', stem_maxpool=True),
+    dict(residual_transformation_type='preactivated_bottleneck_transformation',
+         skip_transformation_type='preactivated_shortcut', stem_maxpool=True)])
+def test_video_resnext3d_lowers_and_matches_fp32_autograd(kw):
+    """The reference's 3D video models (ResNeXt3D / R(2+1)D stems, bottleneck / basic /
+    R(2+1)D blocks, pre- and post-activated shortcuts; `mlcomp/contrib/model/video/
+    resnext3d/resnext3d_stem.py:68-80`, `r2plus1_util.py:53-65`): every Conv3d / BatchNorm3d /
+    MaxPool3d becomes a native site (temporal taps unfolded into channels, the 2D kernels
+    over N*T frames); output and every conv weight gradient against fp32 autograd."""
+    from mlcomp_amd.contrib.video import ResNeXt3D
+    cfg = dict(num_blocks=(1, 1), stem_planes=16, stage_planes=16, stage_temporal_kernel_basis=([3], [3]),
+               temporal_conv_1x1=(False, True), stage_temporal_stride=(1, 2), stage_spatial_stride=(1, 2),
+               in_plane=32, num_classes=5, stem_spatial_kernel=3)
+    cfg.update(kw)
+    m, ref = _pair(lambda: ResNeXt3D(**cfg))
+    assert lower_or_none(m) is None
+    net = GenericNet(m, 'cpu')
+    left = [type(mod).__name__ for mod in net.train_gm.modules()
+            if isinstance(mod, (nn.Conv3d, nn.BatchNorm3d, nn.MaxPool3d, nn.Linear))]
+    assert not left, left
+    x = torch.randn(4, 3, 4, 16, 16)
+    y = torch.randint(0, 5, (4,))
+    out = net(x)
+    F.cross_entropy(out.float(), y).backward()
+    want = ref(x)
+    F.cross_entropy(want, y).backward()
+    assert _rel(out, want) < 2e-2
+    mods = dict(ref.named_modules())
+    n = 0
+    for p in net.param_sets():
+        if not hasattr(p, 'kind'):
+            continue
+        g3 = mods[p.name].weight.grad
+        g = g3.reshape(p.src.weight.shape)          # [Co, Cg*kt, kh, kw], as the lowering sees it
+        if p.kind == 'dense':
+            want_g = F.pad(g.permute(0, 2, 3, 1), (0, p.Cip - p.Ci, 0, 0, 0, 0, 0, p.Cop - p.Co))
+        elif p.kind == 'dw':
+            want_g = F.pad(g[:, 0].permute(1, 2, 0), (0, p.Cop - p.Co))
+        else:
+            want_g = g.permute(0, 2, 3, 1)
+        # bf16 activations through 6-10 BatchNorms over a few frames (and bf16 max-pool
+        # argmaxes): directions, not per-element magnitudes (a layout bug gives cos << 0.9)
+        assert _cos(p.w.grad, want_g) > 0.95, p.name
+        n += 1
+    assert n >= 6
+    # eval graph: running statistics, deterministic
+    net.eval()
+    ref.eval()
+    with torch.no_grad():
+        assert _rel(net(x), ref(x)) < 5e-2
+
+
+def test_conv1d_bn1d_lowers_and_matches_fp32_autograd():
+    """nn.Conv1d [-> BatchNorm1d -> ReLU] through the same temporal unfold (a Conv1d is a
+    Conv3d with a 1x1 spatial kernel)."""
+    class Net1d(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.c1 = nn.Conv1d(8, 16, 5, stride=2, padding=2, bias=False)
+            self.b1 = nn.BatchNorm1d(16)
+            self.c2 = nn.Conv1d(16, 16, 3, padding=2, dilation=2)
+            self.fc = nn.Linear(16, 4)
+
+        def forward(self, x):
+            x = F.relu(self.b1(self.c1(x)))
+            x = F.relu(self.c2(x))
+            return self.fc(x.mean(2))
+
+    m, ref = _pair(Net1d)
+    net = GenericNet(m, 'cpu')
+    x = torch.randn(4, 8, 40)
+    out = net(x)
+    out.float().sum().backward()
+    want = ref(x)
+    want.sum().backward()
+    assert _rel(out, want) < 2e-2
+    for name in ('c1', 'c2'):
+        p = [q for q in net.param_sets() if q.name == name][0]
+        g = getattr(ref, name).weight.grad.reshape(p.src.weight.shape)
+        want_g = F.pad(g.permute(0, 2, 3, 1), (0, p.Cip - p.Ci, 0, 0, 0, 0, 0, p.Cop - p.Co))
+        assert _cos(p.w.grad, want_g) > 0.98, name

@@ -152,6 +152,7 @@ def _models():
     from mlcomp_amd.models import build_model
     from mlcomp_amd.contrib.segmentation.models import Linknet, PSPNet, Unet
     from test_generic_cpu import RefCifarNet
+    from mlcomp_amd.contrib.video import ResNeXt3D
     return {
         'lenet': (lambda: build_model('LeNet', num_classes=10), (32, 1, 28, 28), 10),
         'cifarnet': (RefCifarNet, (32, 3, 32, 32), 10),
@@ -161,6 +162,21 @@ def _models():
         'unet-resnext50': (lambda: Unet(encoder_name='resnext50_32x4d', classes=1), (4, 3, 64, 64), None),
         'pspnet21': (lambda: PSPNet(encoder_name='resnet34', classes=21), (4, 3, 64, 64), 21),
         'linknet': (lambda: Linknet(encoder_name='resnet34', classes=1), (4, 3, 64, 64), None),
+        # the reference's 3D video models (Conv3d / BatchNorm3d / MaxPool3d on the 2D kernels
+        # over N*T frames, temporal taps unfolded into channels)
+        'resnext3d': (lambda: ResNeXt3D(residual_transformation_type='postactivated_bottleneck_transformation',
+                                        num_blocks=(1, 1, 1), stage_planes=32, stem_planes=32, num_groups=4,
+                                        width_per_group=8, in_plane=64, num_classes=5,
+                                        stage_temporal_kernel_basis=([3], [3], [1]),
+                                        temporal_conv_1x1=(False, True, False),
+                                        stage_temporal_stride=(1, 2, 1), stage_spatial_stride=(1, 2, 2)),
+                      (4, 3, 8, 32, 32), 5),
+        'r2plus1d': (lambda: ResNeXt3D(residual_transformation_type='basic_r2plus1d_transformation',
+                                       stem_name='r2plus1d_stem', stem_maxpool=True, num_blocks=(1, 1),
+                                       stage_planes=32, stem_planes=32, in_plane=64, num_classes=5,
+                                       stage_temporal_kernel_basis=([3], [3]), temporal_conv_1x1=(False, False),
+                                       stage_temporal_stride=(1, 2), stage_spatial_stride=(1, 2)),
+                     (4, 3, 8, 32, 32), 5),
     }
 
 
@@ -257,7 +273,8 @@ def test_generic_gpu_step_matches_cpu_native_within_bf16_noise(name):
           f'median grad rel {sorted(rg.values())[len(rg) // 2]:.4f} (noise {sorted(rn.values())[len(rn) // 2]:.4f})')
 
 
-@pytest.mark.parametrize('name,lr', [('cifarnet', 0.05), ('resnext50', 0.05), ('efficientnet-b0', 0.02)])
+@pytest.mark.parametrize('name,lr', [('cifarnet', 0.05), ('resnext50', 0.05), ('efficientnet-b0', 0.02),
+                                     ('resnext3d', 0.05)])
 def test_generic_step_graph_equals_eager_and_learns(name, lr):
     """The captured HIP graph replays the eager step (same losses on the same batches), and a
     fixed batch is fit: the loss falls by half within 30 steps."""
