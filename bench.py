@@ -118,6 +118,8 @@ def main():
                                 world_size=world,
                                 use_graph=(args.graph if args.graph >= 0 else None), comm=comm)
 
+    if comm is not None and getattr(step, 'bucketer', None) is not None:
+        step.bucketer.op = 'avg'     # world 1: scale 1.0, but RCCL launches its kernel per bucket
     feed = None
     if args.data == 'records':
         if is_bert or is_unet:

@@ -120,9 +120,14 @@ class GradBucketer:
             b.pending = len(b.slots)
             b.launched = False
 
+    # the bucket collective's reduction: 'sum' (the optimizer applies 1/world); the
+    # one-GPU overlap evidence (bench.py --comm rccl1) sets 'avg', because RCCL skips an
+    # in-place one-rank SUM entirely but runs its device kernel for AVG
+    op = 'sum'
+
     def _work(self, b: Bucket, stream=None):
         if self.comm is not None:
-            self.comm.all_reduce(b.view, 'sum', stream=stream)
+            self.comm.all_reduce(b.view, self.op, stream=stream)
         if self.opt is not None:
             self.opt.step_slice(b.arena, b.start, b.end)
 

@@ -35,12 +35,12 @@ def work_stream(device):
     (default) stream, fenced to it on both sides; a no-op off the GPU or when the caller is
     already on a non-default stream.
 
-    Measured on MI355X / ROCm 7 (scripts/debug/nan_test_loop.py): hundreds of eager native
-    kernels launched on the NULL stream between replays of a captured step graph make later
-    replays compute garbage (NaN within ~10 steps: a second model trained eagerly next to a
-    graphed one, an eager validation pass between graphed epochs); the same work on a
-    created stream does not.  The runner and every native step therefore keep their
-    kernels off the NULL stream."""
+    Why (profiles/round5/graph_null_stream.md): on ROCm 7 / PyTorch 2.10, eager work on the
+    legacy NULL stream in a process that replays a captured training-step graph corrupts
+    the replays - stock PyTorch reproduces it with no framework code
+    (scripts/graph_torch_twin.py), a device sync after each replay does not always help, and
+    the same eager work on a created stream is fine.  The runner, every native step and
+    predict therefore keep their kernels off the NULL stream."""
     device = torch.device(device)
     if device.type != 'cuda' or os.environ.get('MLC_WORK_STREAM', '1') == '0':
         yield

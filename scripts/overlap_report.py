@@ -16,7 +16,7 @@ import os
 import re
 import sys
 
-COLL = re.compile(r'(?i)(nccl|rccl)')
+COLL = re.compile(r'(?i)(nccl|rccl|oneRankReduce)')
 
 
 def union(iv):

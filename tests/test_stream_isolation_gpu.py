@@ -10,9 +10,8 @@ region of its own; the Python split-K slabs and zero-on-entry scratch buffers ar
 per stream role and per graph capture (``ops.functional.capture_scope``).
 
 * two fused split-K weight gradients on two streams at once equal the serial results;
-* an eagerly trained model next to a graph-replayed one, with all eager work on the NULL
-  stream (``MLC_WORK_STREAM=0``), replays the same losses as the eager model and stays
-  finite."""
+* an eagerly trained model next to a graph-replayed one, both driven from the NULL stream,
+  replay the same losses and stay finite."""
 import math
 
 import pytest
@@ -62,11 +61,16 @@ def test_concurrent_fused_splitk_wgrads_equal_serial(fused_splitk):
     assert ((again - want[0]).norm() / want[0].norm()).item() < 1e-5
 
 
-def test_graph_replay_next_to_null_stream_eager_model(monkeypatch):
-    """The round-4 reproducer (scripts formerly under scripts/debug/nan_test_loop.py, mode
-    ``eg``): EfficientNet-b0 trained eagerly on the NULL stream beside a graph-replayed
-    twin."""
-    monkeypatch.setenv('MLC_WORK_STREAM', '0')
+def test_graph_replay_next_to_eager_model_called_from_the_null_stream():
+    """The round-4 reproducer (EfficientNet-b0 trained eagerly beside a graph-replayed twin,
+    both called from the NULL stream).  Root cause, measured in round 5
+    (profiles/round5/graph_null_stream.md): replaying a captured training-step graph and then
+    running eager work on the legacy NULL stream corrupts later replays - with stock
+    PyTorch too (scripts/graph_torch_twin.py: a plain-PyTorch ResNeXt-50 twin goes NaN at
+    its 3rd replay, no mlcomp_amd code involved), while a device sync after each replay, or
+    the eager work on a created stream, avoids it.  The framework therefore never leaves its
+    work on the NULL stream (train/graphed.work_stream); this test drives it exactly like a
+    user would, from the NULL stream, and the twins must stay finite and agree."""
     import sys
     import os
     sys.path.insert(0, os.path.dirname(__file__))
