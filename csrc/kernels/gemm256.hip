@@ -99,8 +99,10 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int rb, int kk, int lane
 // dst, tid) issues the DMA of half h (rows r0 + h*R ..) of K-tile kt into `dst`; `dead`
 // (OOB or 0, wave-uniform) turns a copy past the last K-tile into a zero read.
 
-// K-contiguous matrix [rows][ld]
-template <int R, bool KTAIL>
+// K-contiguous matrix [rows][ld].  HR (<= R): rows of a half that are used - a 192-wide
+// block tile stages its 96-row B halves in 128-row images whose last 32 rows read zero
+// (OOB: no memory traffic) and are never multiplied.
+template <int R, bool KTAIL, int HR = R>
 struct MatKC {
   static constexpr bool KC = true;
   static constexpr int NC = R / 64;
@@ -113,13 +115,14 @@ struct MatKC {
       const int r = Img<R>::kc_row(w, c, l), ch = Img<R>::kc_chunk(w, c, l);
       st.kc[c] = (unsigned)ch * 8u;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) st.off[h][c] = r0 + h * R + r < rows ? (unsigned)(r * ld + ch * 8) * 2u : OOB;
+      for (int h = 0; h < 2; ++h)
+        st.off[h][c] = r < HR && r0 + h * HR + r < rows ? (unsigned)(r * ld + ch * 8) * 2u : OOB;
     }
   }
   __device__ void copy(const St& st, int r0, int h, int kt, unsigned dead, char* dst, int tid) const {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int k0 = kt * BK;
-    const Rsrc rs = rsrc(p + (size_t)(r0 + h * R) * ld + k0);
+    const Rsrc rs = rsrc(p + (size_t)(r0 + h * HR) * ld + k0);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       unsigned v = st.off[h][c] | dead;
@@ -129,8 +132,8 @@ struct MatKC {
   }
 };
 
-// MN-contiguous matrix [K][ld] (the operand's rows are its columns)
-template <int R, bool KTAIL>
+// MN-contiguous matrix [K][ld] (the operand's rows are its columns); HR as in MatKC
+template <int R, bool KTAIL, int HR = R>
 struct MatMC {
   static constexpr bool KC = false;
   static constexpr int NC = R / 64;
@@ -143,13 +146,14 @@ struct MatMC {
       const int kr = Img<R>::mc_krow(w, c, l), col = Img<R>::mc_col(w, c, l);
       st.kr[c] = kr;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) st.off[h][c] = r0 + h * R + col < cols ? (unsigned)(kr * ld + col) * 2u : OOB;
+      for (int h = 0; h < 2; ++h)
+        st.off[h][c] = col < HR && r0 + h * HR + col < cols ? (unsigned)(kr * ld + col) * 2u : OOB;
     }
   }
   __device__ void copy(const St& st, int r0, int h, int kt, unsigned dead, char* dst, int tid) const {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int k0 = kt * BK;
-    const Rsrc rs = rsrc(p + (size_t)k0 * ld + r0 + h * R);
+    const Rsrc rs = rsrc(p + (size_t)k0 * ld + r0 + h * HR);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       unsigned v = st.off[h][c] | dead;
@@ -272,6 +276,82 @@ struct EpiOut {
   }
 };
 
+// dense-layer epilogue with igemm.hip's DenseFinish semantics, four columns at a time:
+//   a = acc + bias;  act & 3: 0 none / 1 exact-erf GELU (u -> preact) / 2 GELU with the
+//   derivative gelu'(u) -> preact / 3 ReLU (pre-activation -> preact);  a *= act'(dact)
+//   (act & 4: dact holds the derivative; act 3: ReLU mask);  a += addend;  bf16 store
+__device__ __forceinline__ float erf_e(float x, float e) {   // erf(x) from e = exp(-x*x), A&S 7.1.26
+  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * fabsf(x));
+  const float p = ((((1.061405429f * t - 1.453152027f) * t + 1.421413741f) * t - 0.284496736f) * t + 0.254829592f) * t;
+  return copysignf(1.f - p * e, x);
+}
+struct EpiDense {
+  bf16* c; int ldc; const float* bias; int act; bf16* preact; const bf16* addend; const bf16* dact;
+  static constexpr bool STATS = false;
+  __device__ __forceinline__ static uint2 pk(const float (&a)[4]) {
+    return make_uint2(pack2_bf16(a[0], a[1]), pack2_bf16(a[2], a[3]));
+  }
+  __device__ __forceinline__ static void unpk(uint2 u, float (&z)[4]) {
+    z[0] = __uint_as_float(u.x << 16); z[1] = __uint_as_float(u.x & 0xffff0000u);
+    z[2] = __uint_as_float(u.y << 16); z[3] = __uint_as_float(u.y & 0xffff0000u);
+  }
+  __device__ __forceinline__ void quad(int m, int n, f32x4 v) const {
+    float a[4] = {v[0], v[1], v[2], v[3]};
+    const size_t o = (size_t)m * ldc + n;
+    if (bias) {
+      const f32x4 b = *reinterpret_cast<const f32x4*>(bias + n);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] += b[q];
+    }
+    const int mode = act & 3;
+    if (mode == 2) {
+      float d[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float u = a[q], ex = __expf(-0.5f * u * u);
+        const float cdf = 0.5f * (1.f + erf_e(u * 0.70710678118654752f, ex));
+        d[q] = cdf + u * 0.3989422804014327f * ex;
+        a[q] = u * cdf;
+      }
+      if (preact) *reinterpret_cast<uint2*>(preact + o) = pk(d);
+    } else {
+      if (preact) *reinterpret_cast<uint2*>(preact + o) = pk(a);
+      if (mode == 1) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          a[q] = 0.5f * a[q] * (1.f + erf_e(a[q] * 0.70710678118654752f, __expf(-0.5f * a[q] * a[q])));
+      } else if (mode == 3) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] = fmaxf(a[q], 0.f);
+      }
+    }
+    if (dact) {
+      float z[4];
+      unpk(*reinterpret_cast<const uint2*>(dact + o), z);
+      if (act & 4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] *= z[q];
+      } else if (mode == 3) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] = z[q] > 0.f ? a[q] : 0.f;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float ex = __expf(-0.5f * z[q] * z[q]);
+          a[q] *= 0.5f * (1.f + erf_e(z[q] * 0.70710678118654752f, ex)) + z[q] * 0.3989422804014327f * ex;
+        }
+      }
+    }
+    if (addend) {
+      float b[4];
+      unpk(*reinterpret_cast<const uint2*>(addend + o), b);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] += b[q];
+    }
+    *reinterpret_cast<uint2*>(c + o) = pk(a);
+  }
+};
+
 // conv forward: bf16 y store + per-channel BatchNorm partial sums of y and y^2 (of the
 // bf16-rounded values) into NSTAT copies [NSTAT][N]
 struct EpiConvStats {
@@ -289,16 +369,18 @@ struct EpiConvStats {
 template <int BN> struct Cfg {
   static constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
   static constexpr int RB = BN / 2;                      // B half rows (columns of C)
+  static constexpr int RBI = (RB + 63) / 64 * 64;        // rows of a B half's LDS image
   static constexpr int MT = 128 / WM / 16, NT = RB / WN / 16;   // 16x16 tiles per wave per half
-  static constexpr int CA = 2, CB = RB / 64;             // DMA copies per wave per half
-  static constexpr int STAGE = 2 * Img<128>::BYTES + 2 * Img<RB>::BYTES;
+  static constexpr int CA = 2, CB = RBI / 64;            // DMA copies per wave per half
+  static constexpr int STAGE = 2 * Img<128>::BYTES + 2 * Img<RBI>::BYTES;
+  static_assert(NT * WN * 16 == RB && MT * WM * 16 == 128, "tile / wave decomposition");
 };
 
 template <int BN, class LA, class LB, class EPI>
 __global__ void __launch_bounds__(NTHR, 2)
 gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K) {
   using C = Cfg<BN>;
-  constexpr int RA = 128, RB = C::RB, MT = C::MT, NT = C::NT;
+  constexpr int RA = 128, RB = C::RB, RBI = C::RBI, MT = C::MT, NT = C::NT;
   __shared__ __attribute__((aligned(1024))) char smem[2 * C::STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / C::WN, wc = wave % C::WN;
@@ -329,7 +411,7 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K) {
         for (int j = 0; j < NT; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   auto imgA = [&](int buf, int h) { return smem + buf * C::STAGE + h * Img<RA>::BYTES; };
-  auto imgB = [&](int buf, int h) { return smem + buf * C::STAGE + 2 * Img<RA>::BYTES + h * Img<RB>::BYTES; };
+  auto imgB = [&](int buf, int h) { return smem + buf * C::STAGE + 2 * Img<RA>::BYTES + h * Img<RBI>::BYTES; };
 
   // prologue: K-tile 0 into buffer 0, halves in the order the phases first read them
   la.copy(sa, m0, 0, 0, 0u, imgA(0, 0), tid);
@@ -361,7 +443,7 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K) {
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) bfr[j][kk] = frag<LB, RB>(img, wc * (NT * 16) + 16 * j, kk, lane);
+      for (int kk = 0; kk < 2; ++kk) bfr[j][kk] = frag<LB, RBI>(img, wc * (NT * 16) + 16 * j, kk, lane);
   };
 
   for (int t = 0; t < nt; ++t) {
@@ -462,6 +544,22 @@ static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int 
   return hipGetLastError();
 }
 
+// the block-tile width of a dense GEMM: the candidate whose tile count fills the 256 CUs
+// best (one 512-thread block per CU; a partial last round costs a whole round)
+static inline int pick_bn_dense(int M, int N) {
+  const long tm = (M + 255) / 256;
+  int best = 128;
+  double best_eff = -1.0;
+  for (int bn : {256, 192, 128}) {
+    if (bn > 128 && N <= 128) continue;
+    const long t = tm * ((N + bn - 1) / bn);
+    const long rounds = (t + 255) / 256;
+    const double eff = (double)M * N / ((double)rounds * 256 * 256 * bn);   // useful / issued tile work
+    if (eff > best_eff + 1e-9) { best_eff = eff; best = bn; }
+  }
+  return best;
+}
+
 // BN = 128 when the 256-wide tile would leave half its columns empty or too few blocks
 static inline int pick_bn(int M, int N) {
   if (N <= 128) return 128;
@@ -536,4 +634,27 @@ MLC_EXPORT int mlc_conv256_fwd(const bf16* x, const bf16* w, bf16* y, float* sum
   if (tail) G_CONV(128, true);
   G_CONV(128, false);
 #undef G_CONV
+}
+
+// Dense-layer GEMM on the 256-row engine: C[M][N] = A[M][K] . op(B) with the igemm.hip
+// mlc_gemm_bf16_ex_native epilogue (bias, act, preact, addend, dact).  tb = 1: B is [N][K]
+// (K-contiguous, the forward of x W^T); tb = 0: B is [K][N] (the input gradient dY W).
+// bn: 0 = auto (pick_bn_dense), 128, 192 or 256.  K % 8 == N % 8 == 0, A not transposed.
+MLC_EXPORT int mlc_g256_dense(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int lda, int ldb, int ldc,
+                              int tb, const float* bias, int act, bf16* preact, const bf16* addend, const bf16* dact,
+                              int bn, hipStream_t st) {
+  if (K % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || M <= 0 || N <= 0 || K <= 0) return -1;
+  if (bn == 0) bn = pick_bn_dense(M, N);
+  const bool tail = K % BK != 0;
+  const EpiDense epi{C, ldc, bias, act, preact, addend, dact};
+#define G_D(BNV, TAIL, HRV)                                                                              \
+  return tb ? (int)launch<BNV>(MatKC<128, TAIL>{A, lda, M, K}, MatKC<Cfg<BNV>::RBI, TAIL, HRV>{B, ldb, N, K}, \
+                               epi, M, N, K, st)                                                      \
+            : (int)launch<BNV>(MatKC<128, TAIL>{A, lda, M, K}, MatMC<Cfg<BNV>::RBI, TAIL, HRV>{B, ldb, K, N}, \
+                               epi, M, N, K, st)
+  if (bn == 256) { if (tail) G_D(256, true, 128); G_D(256, false, 128); }
+  if (bn == 192) { if (tail) G_D(192, true, 96); G_D(192, false, 96); }
+  if (tail) G_D(128, true, 64);
+  G_D(128, false, 64);
+#undef G_D
 }

@@ -43,6 +43,7 @@ _SIGS = {
     'mlc_gemm_f32out': [vp, vp, vp, vp] + [i32] * 11 + [vp],
     'mlc_gemm_bf16out': [vp, vp, vp] + [i32] * 8 + [vp],
     'mlc_gemm256_nt': [vp, vp, vp, vp] + [i32] * 6 + [vp, i32, vp, vp, i32, i32, vp],
+    'mlc_g256_dense': [vp, vp, vp] + [i32] * 7 + [vp, i32, vp, vp, vp, i32, vp],
     'mlc_gemm256_tn': [vp, vp, vp] + [i32] * 8 + [vp],
     'mlc_conv256_fwd': [vp] * 5 + [i32] * 13 + [vp],
     'mlc_augment': [vp, vp, vp, vp] + [i32] * 7 + [vp],
