@@ -40,6 +40,9 @@ def make(kind, device):
               FPN(encoder_name='resnet34', dropout=0.0) if kind == 'fpn' else
               PSPNet(encoder_name='resnet34', classes=1, dropout=0.0) if kind == 'pspnet' else
               DeepLab(backbone='resnet', num_classes=1))
+        for m in tm.modules():           # dropout masks come from different RNGs on CPU / GPU
+            if isinstance(m, (torch.nn.Dropout, torch.nn.Dropout2d)):
+                m.p = 0.0
         return NativeSegmentationStep(torch_model=tm, batch=B, image_size=R, device=device, use_graph=False, lr=0.0)
     if kind == 'bert':
         from mlcomp_amd.train.native_bert_step import NativeBertStep
