@@ -262,12 +262,12 @@ class _EmbedFn(torch.autograd.Function):
             return None, None, None, None
         d = ds.float().view(B, S, -1)
         if _lib.DETERMINISTIC:
-            # index_add_ races float atomics on repeated ids (and the sort-based scatter
-            # orders ties arbitrarily): a one-hot GEMM sums every row in a fixed order
+            # index_add_ races float atomics on repeated ids: a stable sort groups the rows
+            # of each id in token order and segment_reduce sums every group sequentially
+            # (no atomics, no one-hot GEMM), then the ids - now unique - are added once each
             dd = d.reshape(B * S, -1)
             for tbl, ix in ((net.word, ids), (net.tok_type, tt)):
-                oh = torch.nn.functional.one_hot(ix.reshape(-1), tbl.grad.shape[0]).to(dd.dtype)
-                tbl.grad.add_(oh.t() @ dd)
+                tbl.grad.index_add_(0, *_segment_sums(ix.reshape(-1), dd))
         else:
             net.word.grad.index_add_(0, ids.reshape(-1), d.reshape(B * S, -1))
             net.tok_type.grad.index_add_(0, tt.reshape(-1), d.reshape(B * S, -1))
@@ -275,6 +275,14 @@ class _EmbedFn(torch.autograd.Function):
         for sl in (net.word, net.pos, net.tok_type):
             net.ctx.arena.mark_ready(sl)
         return None, None, None, None
+
+
+def _segment_sums(ix: torch.Tensor, rows: torch.Tensor):
+    """(unique ids, per-id row sums) with a fixed summation order: a stable sort by id, then
+    one sequential sum per id (torch.segment_reduce)."""
+    order = torch.sort(ix, stable=True)[1]
+    uniq, counts = torch.unique_consecutive(ix[order], return_counts=True)
+    return uniq, torch.segment_reduce(rows[order], 'sum', lengths=counts, axis=0, unsafe=True)
 
 
 class _HeadFn(torch.autograd.Function):

@@ -541,8 +541,22 @@ class ConvBNAct(Site):
                 dres = dy
             if c.b is not None and c.kind != 'dense':
                 c.b.grad.add_(dy.float().sum(dim=(0, 1, 2)))
-        c.wgrad(dy, xn)
-        dx = c.dgrad(dy, xn.shape) if needs[0] else None
+        side = self.ctx.wgrad_stream if needs[0] else None
+        main = torch.cuda.current_stream(self.ctx.device) if side is not None else None
+        if side is not None and main != side:
+            # the weight gradient on the context's side stream, concurrently with the input
+            # gradient (as the hand engines do), joined before the site's backward returns:
+            # dy / xn are freed only after that join, in the main stream's order
+            fork = torch.cuda.Event()
+            fork.record(main)
+            dx = c.dgrad(dy, xn.shape)
+            side.wait_event(fork)
+            with Fn.side_stream(side):
+                c.wgrad(dy, xn)
+            main.wait_stream(side)
+        else:
+            c.wgrad(dy, xn)
+            dx = c.dgrad(dy, xn.shape) if needs[0] else None
         if c.uses.bwd_done():
             c.mark_ready()
         out = [from_nhwc(dx, c.Ci) if dx is not None else None]

@@ -128,3 +128,18 @@ def test_native_bert_predict_matches_torch_eval():
     assert logits.shape == (5, 3)
     assert _cos(logits, want) > 0.999 and (logits - want).abs().max() < 0.05
     assert net.loss_sum().item() == 0 and net.ctx.training and net.B == 4
+
+
+def test_deterministic_embedding_segment_sums_match_index_add():
+    """Deterministic mode's embedding backward: a stable sort + per-id sequential sums
+    (no atomics, no one-hot GEMM) equal index_add_ for repeated ids."""
+    import torch
+    from mlcomp_amd.models.native_bert import _segment_sums
+    g = torch.Generator().manual_seed(0)
+    ix = torch.randint(0, 97, (2048,), generator=g)
+    rows = torch.randn(2048, 24, generator=g)
+    u, sm = _segment_sums(ix, rows)
+    assert torch.equal(u, torch.unique(ix))
+    got = torch.zeros(97, 24).index_add_(0, u, sm)
+    want = torch.zeros(97, 24).index_add_(0, ix, rows)
+    assert torch.allclose(got, want, atol=1e-5)
