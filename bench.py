@@ -49,6 +49,9 @@ def parse():
                         'pipeline (C++ gather threads + GPU augment kernel) instead of a resident batch')
     p.add_argument('--records', default=None, help='record file for --data records (default: a generated one)')
     p.add_argument('--loader-threads', type=int, default=12)
+    p.add_argument('--precision', default='bf16', choices=['bf16', 'fp32'],
+                   help='fp32: --impl torch without autocast (the reference Catalyst default precision, which '
+                        'the runner trains on the torch engine); the native engines are bf16 with fp32 master weights')
     p.add_argument('--comm', default='auto', choices=['auto', 'rccl1'],
                    help='rccl1: give a one-GPU run a world-1 RCCL communicator, so the production gradient '
                         'bucketer issues its RCCL all-reduces on the side stream (overlap evidence)')
@@ -110,13 +113,15 @@ def main():
         from mlcomp_amd.train.bert import build_bert_step
         step = build_bert_step(args.model, batch=args.batch, seq_len=args.seq_len, impl=args.impl,
                                device=device, world_size=world,
-                               use_graph=(args.graph if args.graph >= 0 else None), comm=comm)
+                               use_graph=(args.graph if args.graph >= 0 else None), comm=comm,
+                               precision=args.precision)
     else:
         from mlcomp_amd.train.imagenet import build_train_step
         step = build_train_step(args.model, batch=args.batch, impl=args.impl,
                                 image_size=args.image_size, device=device,
                                 world_size=world,
-                                use_graph=(args.graph if args.graph >= 0 else None), comm=comm)
+                                use_graph=(args.graph if args.graph >= 0 else None), comm=comm,
+                                precision=args.precision)
 
     if comm is not None and getattr(step, 'bucketer', None) is not None:
         step.bucketer.op = 'avg'     # world 1: scale 1.0, but RCCL launches its kernel per bucket
@@ -175,7 +180,7 @@ def main():
             'metric': 'sequences/sec (whole node) BERT fine-tune DAG train task',
             'value': round(value, 2), 'unit': 'sequences/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': 'bf16',
+            'vs_baseline': None, 'dtype': args.precision,
             'data': f'synthetic (random token ids, seq_len {args.seq_len}, 2 labels, random-init weights)',
             'config': {'model': args.model, 'global_batch': args.batch * world, 'per_gpu_batch': args.batch,
                        'seq_len': args.seq_len, 'parallelism': f'dp{world}', 'impl': args.impl,
@@ -207,7 +212,7 @@ def main():
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
-            'dtype': 'bf16',
+            'dtype': args.precision,
             'data': 'synthetic (ImageNet-shape 224x224x3, 1000 classes, random-init weights)',
             'config': {
                 'model': args.model,

@@ -267,7 +267,7 @@ class _EmbedFn(torch.autograd.Function):
             # (no atomics, no one-hot GEMM), then the ids - now unique - are added once each
             dd = d.reshape(B * S, -1)
             for tbl, ix in ((net.word, ids), (net.tok_type, tt)):
-                tbl.grad.index_add_(0, *_segment_sums(ix.reshape(-1), dd))
+                tbl.grad.add_(_segment_sums(ix.reshape(-1), dd, tbl.grad.shape[0]))
         else:
             net.word.grad.index_add_(0, ids.reshape(-1), d.reshape(B * S, -1))
             net.tok_type.grad.index_add_(0, tt.reshape(-1), d.reshape(B * S, -1))
@@ -277,12 +277,13 @@ class _EmbedFn(torch.autograd.Function):
         return None, None, None, None
 
 
-def _segment_sums(ix: torch.Tensor, rows: torch.Tensor):
-    """(unique ids, per-id row sums) with a fixed summation order: a stable sort by id, then
-    one sequential sum per id (torch.segment_reduce)."""
+def _segment_sums(ix: torch.Tensor, rows: torch.Tensor, V: int) -> torch.Tensor:
+    """[V, H] per-id sums of ``rows`` in a fixed order, with static shapes (graph-capturable:
+    no host sync): a stable sort groups the rows of each id in token order, integer counts
+    give the segment lengths, and torch.segment_reduce sums every segment sequentially."""
     order = torch.sort(ix, stable=True)[1]
-    uniq, counts = torch.unique_consecutive(ix[order], return_counts=True)
-    return uniq, torch.segment_reduce(rows[order], 'sum', lengths=counts, axis=0, unsafe=True)
+    counts = torch.zeros(V, dtype=torch.long, device=ix.device).scatter_add_(0, ix, torch.ones_like(ix))
+    return torch.segment_reduce(rows[order], 'sum', lengths=counts, axis=0, unsafe=True)
 
 
 class _HeadFn(torch.autograd.Function):

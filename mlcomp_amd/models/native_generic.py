@@ -314,6 +314,65 @@ class _Lowering:
         new = self._site_node(node, GlobalAvgPool(self.net.ctx), [node.args[0]])
         self._replace([node], new)
 
+    def _link_residuals(self):
+        """Identity residuals: a value R used exactly twice - as the input of a 2D conv site
+        S1 and as the residual of a conv site S3 downstream of it - gets one gradient:
+        S3's backward hands its residual gradient to S1, whose dgrad adds it in the GEMM
+        epilogue (autograd would add the two branch gradients in a pass of its own).
+        S3's backward runs before S1's (S3 depends on S1's output)."""
+        mods = dict(self.gm.named_modules())
+        for n in self.gm.graph.nodes:
+            s3 = mods.get(n.target) if n.op == 'call_module' else None
+            if not isinstance(s3, ConvBNAct) or not s3.residual or len(n.args) < 2:
+                continue
+            r = n.args[1]
+            users = [u for u in r.users]
+            if len(users) != 2:
+                continue
+            other = users[0] if users[1] is n else users[1]
+            s1 = mods.get(other.target) if other.op == 'call_module' else None
+            if (not isinstance(s1, ConvBNAct) or s1 is s3 or other.args[0] is not r
+                    or (len(other.args) > 1 and other.args[1] is r) or s1.conv.Cip != s3.conv.Cop):
+                continue
+            if not self._reaches(other, n):
+                continue
+            object.__setattr__(s3, 'res_link', s1)
+
+    def _link_bn_backward(self):
+        """A conv+BN site A (ReLU or no activation, batch statistics) whose output is used
+        only as the input of a dense conv site B: B's dgrad epilogue produces A's output
+        gradient, so it also applies A's ReLU mask and accumulates A's BatchNorm-backward
+        sums (Fn.BnBwdSpec) and A's backward skips its reduction pass."""
+        mods = dict(self.gm.named_modules())
+        relu = A['relu']
+        for n in self.gm.graph.nodes:
+            sb = mods.get(n.target) if n.op == 'call_module' else None
+            if not isinstance(sb, ConvBNAct) or sb.conv.kind != 'dense' or not n.args:
+                continue
+            a = n.args[0]
+            sa = mods.get(a.target) if isinstance(a, fx.Node) and a.op == 'call_module' else None
+            if (not isinstance(sa, ConvBNAct) or sa is sb or sa.bn is None or sa.act not in (0, relu)
+                    or len(a.users) != 1 or sa.conv.Cop != sb.conv.Cip):
+                continue
+            if len(n.args) > 1 and n.args[1] is a:
+                continue
+            object.__setattr__(sb, 'bn_link', sa)
+            object.__setattr__(sa, 'bn_prereduced', True)
+
+    @staticmethod
+    def _reaches(a: fx.Node, b: fx.Node) -> bool:
+        """True when node ``b`` depends on node ``a`` (so ``a``'s backward runs after ``b``'s)."""
+        seen, todo = set(), [b]
+        while todo:
+            x = todo.pop()
+            if x is a:
+                return True
+            for p in x.all_input_nodes:
+                if p not in seen:
+                    seen.add(p)
+                    todo.append(p)
+        return False
+
     def run(self):
         g = self.gm.graph
         for node in list(g.nodes):
@@ -360,6 +419,8 @@ class _Lowering:
                     node.target = 'reshape'     # site outputs are channels_last views
                 elif node.target in ('matmul', 'mm', 'bmm'):
                     raise NativeUnsupported(f'{node.name}: Tensor.{node.target} has no native lowering')
+        self._link_residuals()
+        self._link_bn_backward()
         g.lint()
         self.gm.delete_all_unused_submodules()
         self.gm.recompile()

@@ -266,17 +266,22 @@ class ConvParams:
                                            self.dil, stats=stats)
         return Fn.gconv_fwd(x, wb, self.groups, self.stride, self.pad, self.dil, stats=stats)
 
-    def dgrad(self, dy, x_shape):
+    def dgrad(self, dy, x_shape, addend=None, bn=None):
+        """Input gradient (+ ``addend``: another branch's gradient of the same input, summed
+        in the dense GEMM's epilogue; ``bn``: the producing site's BatchNorm-backward
+        reduction and ReLU mask in the same epilogue, dense convs only)."""
         wb = self.w.bf16
         if self.kind == 'dense':
-            return Fn.conv2d_dgrad(dy, wb, x_shape, self.stride, self.pad, self.dil)
+            return Fn.conv2d_dgrad(dy, wb, x_shape, self.stride, self.pad, self.dil, addend=addend, bn=bn)
+        assert bn is None
         if self.kind == 'dw':
-            return Fn.dwconv_dgrad(dy, wb, x_shape, self.stride, self.pad, self.dil)
-        if self.kind == 'tr':     # a forward conv of dy over the same filter
+            dx = Fn.dwconv_dgrad(dy, wb, x_shape, self.stride, self.pad, self.dil)
+        elif self.kind == 'tr':     # a forward conv of dy over the same filter
             dx = Fn.conv2d_fwd(dy, wb, self.stride, self.pad, self.dil)
             assert tuple(dx.shape) == tuple(x_shape), (dx.shape, x_shape)
-            return dx
-        return Fn.gconv_dgrad(dy, wb, x_shape, self.groups, self.stride, self.pad, self.dil)
+        else:
+            dx = Fn.gconv_dgrad(dy, wb, x_shape, self.groups, self.stride, self.pad, self.dil)
+        return dx if addend is None else dx.add_(addend)
 
     def wgrad(self, dy, x):
         acc = self.ctx.grad_prezeroed
@@ -486,6 +491,20 @@ class ConvBNAct(Site):
         self.epi_act = 3 if (bn is None and conv.kind == 'dense' and act == 1 and not residual) else 0
         self.k_st = ctx.ws.request(f'{conv.name}@{id(self)}.st', 2 * Fn.NSTAT * conv.Cop) if bn is not None else None
         self.k_bw = ctx.ws.request(f'{conv.name}@{id(self)}.bw', 2 * Fn.NSTAT * conv.Cop) if bn is not None else None
+        # identity-residual link (set by the lowering): this site's residual input is also
+        # exactly one other site's conv input, and that site's backward runs later, so the
+        # residual gradient is handed over and summed in that site's dgrad epilogue instead
+        # of autograd adding the two branch gradients in a pass of its own
+        object.__setattr__(self, 'res_link', None)
+        object.__setattr__(self, '_pending', None)
+        # BN-backward link (set by the lowering): ``bn_link`` is the site whose output is this
+        # (dense) conv's only input; this site's dgrad epilogue applies that site's ReLU mask
+        # and accumulates its BatchNorm-backward sums, so its backward skips the reduction
+        # pass (``bn_prereduced``; the hand engines' BnBwdSpec, across fx sites)
+        object.__setattr__(self, 'bn_link', None)
+        object.__setattr__(self, 'bn_prereduced', False)
+        object.__setattr__(self, '_bn_stash', None)
+        object.__setattr__(self, '_bn_done', False)
 
     def forward(self, x, res=None):
         return _run(self, x, res) if res is not None else _run(self, x)
@@ -505,6 +524,9 @@ class ConvBNAct(Site):
             scale, shift, mean, inv = bn.finalize(stats[0] if stats else None, stats[1] if stats else None, rows)
             z = Fn.bnact_apply(y, rn, scale, shift, self.act, self.alpha)
             saved = [xn, y, z, rn if rn is not None else y, scale, shift, mean, inv]
+            if self.bn_prereduced and stats is not None and torch.is_grad_enabled():
+                object.__setattr__(self, '_bn_stash', (y, z, mean))   # read by the linked dgrad
+                object.__setattr__(self, '_bn_done', False)
             return from_nhwc(z, c.Co), saved, rn is not None
         y = c.fwd(xn, None, self.epi_act)        # dense: bias (+ ReLU) in the GEMM epilogue
         if c.b is not None and c.kind != 'dense':
@@ -522,9 +544,17 @@ class ConvBNAct(Site):
             xn, y, z, rn, scale, shift, mean, inv = saved
             ws = self.ctx.ws
             d = self._direct_bn_grads()
-            dy, dres = Fn.bnact_bwd(dz, z, y, rn if has_res else None, mean, scale, shift, inv, bn.gamma.master,
-                                    self.act, self.alpha, dgamma=_acc_view(bn.gamma, d), dbeta=_acc_view(bn.beta, d),
-                                    sums=ws[self.k_bw], want_dres=has_res)
+            if self.bn_prereduced and self._bn_done:
+                # the consumer's dgrad already masked dz and reduced the BN-backward sums
+                dy, dres = Fn.bn_bwd(dz, None, y, mean, inv, bn.gamma.master, want_dres=has_res,
+                                     dgamma=_acc_view(bn.gamma, d), dbeta=_acc_view(bn.beta, d), sums=ws[self.k_bw],
+                                     prereduced=True)
+            else:
+                dy, dres = Fn.bnact_bwd(dz, z, y, rn if has_res else None, mean, scale, shift, inv,
+                                        bn.gamma.master, self.act, self.alpha, dgamma=_acc_view(bn.gamma, d),
+                                        dbeta=_acc_view(bn.beta, d), sums=ws[self.k_bw], want_dres=has_res)
+            object.__setattr__(self, '_bn_stash', None)
+            object.__setattr__(self, '_bn_done', False)
             _acc_commit(bn.gamma, d)
             _acc_commit(bn.beta, d)
             if bn.uses.bwd_done():
@@ -541,6 +571,14 @@ class ConvBNAct(Site):
                 dres = dy
             if c.b is not None and c.kind != 'dense':
                 c.b.grad.add_(dy.float().sum(dim=(0, 1, 2)))
+        addend = self._pending                 # a later site's residual gradient of our input
+        object.__setattr__(self, '_pending', None)
+        spec = None
+        src = self.bn_link
+        if src is not None and needs[0] and src._bn_stash is not None:
+            ya, za, mean_a = src._bn_stash
+            spec = Fn.BnBwdSpec(za if src.act else None, [(ya, mean_a, self.ctx.ws[src.k_bw])])
+            object.__setattr__(src, '_bn_done', True)
         side = self.ctx.wgrad_stream if needs[0] else None
         main = torch.cuda.current_stream(self.ctx.device) if side is not None else None
         if side is not None and main != side:
@@ -549,19 +587,23 @@ class ConvBNAct(Site):
             # dy / xn are freed only after that join, in the main stream's order
             fork = torch.cuda.Event()
             fork.record(main)
-            dx = c.dgrad(dy, xn.shape)
+            dx = c.dgrad(dy, xn.shape, addend, spec)
             side.wait_event(fork)
             with Fn.side_stream(side):
                 c.wgrad(dy, xn)
             main.wait_stream(side)
         else:
             c.wgrad(dy, xn)
-            dx = c.dgrad(dy, xn.shape) if needs[0] else None
+            dx = c.dgrad(dy, xn.shape, addend, spec) if needs[0] else None
         if c.uses.bwd_done():
             c.mark_ready()
         out = [from_nhwc(dx, c.Ci) if dx is not None else None]
         if has_res:
-            out.append(from_nhwc(dres, c.Co) if needs[1] else None)
+            if needs[1] and self.res_link is not None:
+                object.__setattr__(self.res_link, '_pending', dres)    # summed by the linked dgrad
+                out.append(None)
+            else:
+                out.append(from_nhwc(dres, c.Co) if needs[1] else None)
         return out
 
 

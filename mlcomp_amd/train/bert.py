@@ -12,8 +12,9 @@ from mlcomp_amd.models import build_model
 
 
 class _TorchBertStep:
-    def __init__(self, model_name, batch, seq_len, device, world_size, num_labels=2, lr=2e-5):
+    def __init__(self, model_name, batch, seq_len, device, world_size, num_labels=2, lr=2e-5, precision='bf16'):
         torch.manual_seed(0)
+        self.amp = precision != 'fp32'
         self.model = build_model(model_name, num_labels=num_labels).to(device)
         self.net = self.model
         if world_size > 1:
@@ -35,7 +36,7 @@ class _TorchBertStep:
         self._loss = None
 
     def __call__(self):
-        with torch.autocast('cuda', dtype=torch.bfloat16):
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=self.amp):
             logits = self.net(self.ids, self.tt)
         loss = torch.nn.functional.cross_entropy(logits.float(), self.y)
         self.opt.zero_grad(set_to_none=True)
@@ -48,10 +49,10 @@ class _TorchBertStep:
 
 
 def build_bert_step(model_name='bert-base', batch=32, seq_len=128, impl='native', device=None, world_size=1,
-                    use_graph: Optional[bool] = None, num_labels=2, lr=2e-5, comm=None):
+                    use_graph: Optional[bool] = None, num_labels=2, lr=2e-5, comm=None, precision='bf16'):
     device = device or torch.device('cuda')
     if impl == 'torch':
-        return _TorchBertStep(model_name, batch, seq_len, device, world_size, num_labels, lr)
+        return _TorchBertStep(model_name, batch, seq_len, device, world_size, num_labels, lr, precision)
     from .native_bert_step import NativeBertStep
     return NativeBertStep(model_name, batch=batch, seq_len=seq_len, device=device, world_size=world_size,
                           use_graph=True if use_graph is None else use_graph, num_labels=num_labels, lr=lr,

@@ -21,7 +21,10 @@ from mlcomp_amd.models import build_model
 
 
 class _TorchStep:
-    def __init__(self, model_name, batch, image_size, device, world_size, num_classes=1000):
+    def __init__(self, model_name, batch, image_size, device, world_size, num_classes=1000, precision='bf16'):
+        # precision 'fp32': no autocast - what a reference config with the Catalyst default
+        # precision (fp32) runs when it lands on the torch engine
+        self.amp = precision != 'fp32'
         model = build_model(model_name, num_classes=num_classes)
         model = model.to(device=device, memory_format=torch.channels_last)
         self.model = model
@@ -38,7 +41,7 @@ class _TorchStep:
         self._loss = None
 
     def __call__(self):
-        with torch.autocast('cuda', dtype=torch.bfloat16):
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=self.amp):
             out = self.model(self.x)
             loss = F.cross_entropy(out.float(), self.y)
         self.opt.zero_grad(set_to_none=True)
@@ -52,10 +55,11 @@ class _TorchStep:
 
 def build_train_step(model_name: str = 'resnet50', batch: int = 256, impl: str = 'native',
                      image_size: int = 224, device=None, world_size: int = 1,
-                     use_graph: Optional[bool] = None, num_classes: int = 1000, comm=None):
+                     use_graph: Optional[bool] = None, num_classes: int = 1000, comm=None,
+                     precision: str = 'bf16'):
     device = device or torch.device('cuda')
     if impl == 'torch':
-        return _TorchStep(model_name, batch, image_size, device, world_size, num_classes)
+        return _TorchStep(model_name, batch, image_size, device, world_size, num_classes, precision)
     from mlcomp_amd.train.native_step import NativeClassifierStep
     return NativeClassifierStep(model_name, batch=batch, image_size=image_size,
                                 device=device, world_size=world_size,

@@ -535,3 +535,42 @@ def test_conv1d_bn1d_lowers_and_matches_fp32_autograd():
         g = getattr(ref, name).weight.grad.reshape(p.src.weight.shape)
         want_g = F.pad(g.permute(0, 2, 3, 1), (0, p.Cip - p.Ci, 0, 0, 0, 0, 0, p.Cop - p.Co))
         assert _cos(p.w.grad, want_g) > 0.98, name
+
+
+def test_identity_residual_and_bn_backward_links_are_exact():
+    """ResNet basic blocks: the identity residual's gradient is handed from the block's last
+    conv site to its first conv site's dgrad epilogue (one gradient per value, no autograd
+    sum), and a conv site whose input is another conv site's BN-ReLU output computes that
+    BN's backward reduction and ReLU mask in its dgrad epilogue (no reduction pass).  Input
+    and weight gradients equal the unlinked ones and match fp32 autograd."""
+    m, ref = _pair(lambda: build_model('resnet18', num_classes=10))
+    net = GenericNet(m, 'cpu')
+    links = [s for s in net.train_gm.modules() if getattr(s, 'res_link', None) is not None]
+    assert len(links) == 5, len(links)            # 8 blocks, 3 of them with a downsample shortcut
+    bn_links = [s for s in net.train_gm.modules() if getattr(s, 'bn_link', None) is not None]
+    assert len(bn_links) == 8, len(bn_links)      # each block's second conv reads its first conv's BN-ReLU
+    torch.manual_seed(3)
+    x = torch.randn(4, 3, 32, 32)
+    y = torch.randint(0, 10, (4,))
+
+    def run(linked):
+        for s in links:
+            object.__setattr__(s, '_saved_link', getattr(s, '_saved_link', s.res_link))
+            object.__setattr__(s, 'res_link', s._saved_link if linked else None)
+        for s in bn_links:
+            object.__setattr__(s, '_saved_bn', getattr(s, '_saved_bn', s.bn_link))
+            object.__setattr__(s, 'bn_link', s._saved_bn if linked else None)
+            object.__setattr__(s._saved_bn, 'bn_prereduced', linked)
+        net.ctx.ws.zero()                 # what the step does first (BN reduction scratch)
+        net.arena.zero_grad()
+        xi = x.clone().requires_grad_()
+        F.cross_entropy(net(xi).float(), y).backward()
+        return xi.grad.clone(), [(p.w if hasattr(p, 'w') else p.gamma).grad.clone() for p in net.param_sets()]
+    gx_l, gw_l = run(True)
+    gx_u, gw_u = run(False)
+    assert _rel(gx_l, gx_u) < 1e-2
+    for a, b in zip(gw_l, gw_u):
+        assert _rel(a, b) < 1e-2
+    xr = x.clone().requires_grad_()
+    F.cross_entropy(ref(xr), y).backward()
+    assert _cos(gx_l, xr.grad) > 0.98
