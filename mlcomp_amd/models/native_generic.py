@@ -340,9 +340,10 @@ class _Lowering:
 
     def _link_bn_backward(self):
         """A conv+BN site A (ReLU or no activation, batch statistics) whose output is used
-        only as the input of a dense conv site B: B's dgrad epilogue produces A's output
-        gradient, so it also applies A's ReLU mask and accumulates A's BatchNorm-backward
-        sums (Fn.BnBwdSpec) and A's backward skips its reduction pass."""
+        only as the input of a dense conv site B (and, at a residual block boundary, as the
+        identity residual that B's dgrad already sums): B's dgrad epilogue produces A's whole
+        output gradient, so it also applies A's ReLU mask and accumulates A's BatchNorm-
+        backward sums (Fn.BnBwdSpec) and A's backward skips its reduction pass."""
         mods = dict(self.gm.named_modules())
         relu = A['relu']
         for n in self.gm.graph.nodes:
@@ -352,7 +353,13 @@ class _Lowering:
             a = n.args[0]
             sa = mods.get(a.target) if isinstance(a, fx.Node) and a.op == 'call_module' else None
             if (not isinstance(sa, ConvBNAct) or sa is sb or sa.bn is None or sa.act not in (0, relu)
-                    or len(a.users) != 1 or sa.conv.Cop != sb.conv.Cip):
+                    or sa.conv.Cop != sb.conv.Cip):
+                continue
+            others = [u for u in a.users if u is not n]
+            # the only other user may be a site whose residual gradient B's dgrad already sums
+            # (an identity-residual link): B's dgrad output is then A's whole output gradient
+            if others and not (len(others) == 1 and others[0].op == 'call_module'
+                               and getattr(mods.get(others[0].target), 'res_link', None) is sb):
                 continue
             if len(n.args) > 1 and n.args[1] is a:
                 continue

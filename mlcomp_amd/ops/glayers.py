@@ -524,7 +524,7 @@ class ConvBNAct(Site):
             scale, shift, mean, inv = bn.finalize(stats[0] if stats else None, stats[1] if stats else None, rows)
             z = Fn.bnact_apply(y, rn, scale, shift, self.act, self.alpha)
             saved = [xn, y, z, rn if rn is not None else y, scale, shift, mean, inv]
-            if self.bn_prereduced and stats is not None and torch.is_grad_enabled():
+            if self.bn_prereduced and stats is not None and self.ctx.training:
                 object.__setattr__(self, '_bn_stash', (y, z, mean))   # read by the linked dgrad
                 object.__setattr__(self, '_bn_done', False)
             return from_nhwc(z, c.Co), saved, rn is not None
@@ -546,6 +546,7 @@ class ConvBNAct(Site):
             d = self._direct_bn_grads()
             if self.bn_prereduced and self._bn_done:
                 # the consumer's dgrad already masked dz and reduced the BN-backward sums
+                object.__setattr__(self, 'n_prereduced', getattr(self, 'n_prereduced', 0) + 1)
                 dy, dres = Fn.bn_bwd(dz, None, y, mean, inv, bn.gamma.master, want_dres=has_res,
                                      dgamma=_acc_view(bn.gamma, d), dbeta=_acc_view(bn.beta, d), sums=ws[self.k_bw],
                                      prereduced=True)

@@ -548,7 +548,10 @@ def test_identity_residual_and_bn_backward_links_are_exact():
     links = [s for s in net.train_gm.modules() if getattr(s, 'res_link', None) is not None]
     assert len(links) == 5, len(links)            # 8 blocks, 3 of them with a downsample shortcut
     bn_links = [s for s in net.train_gm.modules() if getattr(s, 'bn_link', None) is not None]
-    assert len(bn_links) == 8, len(bn_links)      # each block's second conv reads its first conv's BN-ReLU
+    # each block's second conv reads its first conv's BN-ReLU (8); the first conv of 4 of the
+    # 5 identity blocks also reads the previous block's output, whose residual it already sums
+    # (layer1.0's input is the max-pool's output)
+    assert len(bn_links) == 12, len(bn_links)
     torch.manual_seed(3)
     x = torch.randn(4, 3, 32, 32)
     y = torch.randint(0, 10, (4,))
@@ -567,7 +570,9 @@ def test_identity_residual_and_bn_backward_links_are_exact():
         F.cross_entropy(net(xi).float(), y).backward()
         return xi.grad.clone(), [(p.w if hasattr(p, 'w') else p.gamma).grad.clone() for p in net.param_sets()]
     gx_l, gw_l = run(True)
+    assert sum(getattr(s._saved_bn, 'n_prereduced', 0) for s in bn_links) == 12   # the fused path ran
     gx_u, gw_u = run(False)
+    assert sum(getattr(s._saved_bn, 'n_prereduced', 0) for s in bn_links) == 12
     assert _rel(gx_l, gx_u) < 1e-2
     for a, b in zip(gw_l, gw_u):
         assert _rel(a, b) < 1e-2
