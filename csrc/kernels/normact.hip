@@ -121,10 +121,15 @@ stats_kernel(const bf16* __restrict__ x, float* __restrict__ sum, float* __restr
   }
 }
 
+// The elementwise passes are instantiated for the identity and ReLU codes (ACT = 0 / 1: the
+// activation folds to straight-line code, so the loop keeps its loads in flight) and once for
+// any code read at run time (ACT = -1: the switch of act_f / act_df per element).
+template <int ACT>
 __global__ void __launch_bounds__(NT)
 apply_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf16* __restrict__ z,
              const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ rscale,
-             const float* __restrict__ rshift, long rows, int C, int act, float alpha) {
+             const float* __restrict__ rshift, long rows, int C, int act_, float alpha) {
+  const int act = ACT >= 0 ? ACT : act_;
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
   const long stride = (long)gridDim.x * NT;
@@ -150,8 +155,10 @@ apply_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf16* __r
 }
 
 // dU of one chunk: dz * act'(a), a recomputed from y (and res) with the forward's affine
+template <int ACT>
 __device__ __forceinline__ void dU8(float (&d)[8], const uint4& zv, const uint4& yv, const uint4& rv, bool has_res,
-                                    const Ch& c, int act, float alpha) {
+                                    const Ch& c, int act_, float alpha) {
+  const int act = ACT >= 0 ? ACT : act_;
   if (act == 0) return;
   float yy[8], zz[8], a[8];
   unpack8(yv, yy);
@@ -168,6 +175,7 @@ __device__ __forceinline__ void dU8(float (&d)[8], const uint4& zv, const uint4&
   for (int j = 0; j < 8; ++j) d[j] *= act_df(a[j], zz[j], act, alpha);
 }
 
+template <int ACT>
 __global__ void __launch_bounds__(NT)
 bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const bf16* __restrict__ y,
                   const bf16* __restrict__ res, const float* __restrict__ mean, const float* __restrict__ scale,
@@ -199,7 +207,7 @@ bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const
       float d[8], yy[8];
       unpack8(dv[k], d);
       unpack8(yv[k], yy);
-      dU8(d, zv[k], yv[k], rv[k], res != nullptr, c, act, alpha);
+      dU8<ACT>(d, zv[k], yv[k], rv[k], res != nullptr, c, act, alpha);
 #pragma unroll
       for (int j = 0; j < 8; ++j) { s1[j] += d[j]; s2[j] += d[j] * (yy[j] - mu[j]); }
     }
@@ -237,6 +245,7 @@ bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const
 }
 
 // dy = k1*dU + k2 + k3*(y - mean) (coef from mlc_bn_bwd_finalize), dres = dU
+template <int ACT>
 __global__ void __launch_bounds__(NT)
 bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const bf16* __restrict__ y,
                  const bf16* __restrict__ res, const float* __restrict__ mean, const float* __restrict__ coef,
@@ -265,7 +274,7 @@ bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const 
     float d[8], yy[8], o[8];
     unpack8(dv, d);
     unpack8(yv, yy);
-    dU8(d, zv, yv, rv, res != nullptr, c, act, alpha);
+    dU8<ACT>(d, zv, yv, rv, res != nullptr, c, act, alpha);
     if (dres) *reinterpret_cast<uint4*>(dres + i * 8) = pack8(d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = k1[j] * d[j] + k2[j] + k3[j] * (yy[j] - mu[j]);
@@ -343,6 +352,14 @@ inline int grid_for(long rows, int C, int cap = 1024) {
   return (int)(((blocks + m - 1) / m) * m);
 }
 
+// launch an ACT-templated pass with the specialisation of the run-time code `act`
+#define NA_LAUNCH(K, grid, st, act, ...)                                                              \
+  do {                                                                                              \
+    if ((act) == 0) hipLaunchKernelGGL(K<0>, dim3(grid), dim3(NT), 0, st, __VA_ARGS__);             \
+    else if ((act) == 1) hipLaunchKernelGGL(K<1>, dim3(grid), dim3(NT), 0, st, __VA_ARGS__);        \
+    else hipLaunchKernelGGL(K<-1>, dim3(grid), dim3(NT), 0, st, __VA_ARGS__);                       \
+  } while (0)
+
 // block cap of the reducing passes: every block ends in C*2 float atomics onto one of 32
 // partial copies, so the per-address atomic chains grow with the block count (A/B knob
 // MLC_NORMACT_CAP; the streaming loop is unrolled by two to keep enough loads in flight)
@@ -376,8 +393,8 @@ MLC_EXPORT int mlc_bnact_apply(const bf16* y, const bf16* res, bf16* z, const fl
                                const float* rscale, const float* rshift, long rows, int C, int act, float alpha,
                                hipStream_t st) {
   if (C % 8 || (rscale && !rshift)) return -1;
-  hipLaunchKernelGGL(apply_kernel, dim3(grid_for(rows, C, 768)), dim3(NT), 0, st, y, res, z, scale, shift, rscale,
-                     rshift, rows, C, act, alpha);
+  NA_LAUNCH(apply_kernel, grid_for(rows, C, 768), st, act, y, res, z, scale, shift, rscale, rshift, rows, C, act,
+            alpha);
   return hipGetLastError();
 }
 
@@ -386,32 +403,35 @@ MLC_EXPORT int mlc_bnact_bwd_reduce(const bf16* dz, const bf16* z, const bf16* y
                                     const float* scale, const float* shift, const float* rscale, const float* rshift,
                                     float* sums, long rows, int C, int act, float alpha, hipStream_t st) {
   if (C % 8) return -1;
-  hipLaunchKernelGGL(bwd_reduce_kernel, dim3(grid_for(rows, C, reduce_cap())), dim3(NT), 0, st, dz, z, y, res, mean,
-                     scale, shift,
-                     rscale, rshift, sums, rows, C, act, alpha, 0);
+  NA_LAUNCH(bwd_reduce_kernel, grid_for(rows, C, reduce_cap()), st, act, dz, z, y, res, mean, scale, shift, rscale,
+            rshift, sums, rows, C, act, alpha, 0);
   return hipGetLastError();
 }
 
 // The whole BN(+act) backward in one call, with the reduction written as one row of partial
 // sums per block (plain stores; `part` holds part_floats >= blocks*2*C floats, C <= 2048)
 // instead of float atomics onto 32 copies: reduce -> finalize over the rows -> apply.
+// rscale / rshift (optional): the residual is another BatchNorm's input, applied in the
+// forward as res*rscale + rshift (a folded shortcut BN); the activation derivative is taken
+// at that pre-activation.
 MLC_EXPORT int mlc_bnact_bwd(const bf16* dz, const bf16* z, const bf16* y, const bf16* res, const float* mean,
-                             const float* scale, const float* shift, const float* invstd, const float* gamma,
+                             const float* scale, const float* shift, const float* rscale, const float* rshift,
+                             const float* invstd, const float* gamma,
                              float* part, long part_floats, float* coef, float* dgamma, float* dbeta, bf16* dy,
                              bf16* dres, long rows, int C, int act, float alpha, hipStream_t st) {
   const int G = C >> 3;
-  if (C % 8 || G > NT || part_floats < 2L * C) return -1;
+  if (C % 8 || G > NT || part_floats < 2L * C || (rscale && !rshift)) return -1;
   long cap = part_floats / (2L * C);
   if (cap > reduce_cap()) cap = reduce_cap();
   int blocks = grid_for(rows, C, (int)cap);
   while (blocks > cap && blocks > 1) blocks = grid_for(rows, C, blocks / 2);   // rounding to C/8 multiples
   if ((long)blocks * 2 * C > part_floats) return -1;
-  hipLaunchKernelGGL(bwd_reduce_kernel, dim3(blocks), dim3(NT), 0, st, dz, z, y, res, mean, scale, shift,
-                     (const float*)nullptr, (const float*)nullptr, part, rows, C, act, alpha, 1);
+  NA_LAUNCH(bwd_reduce_kernel, blocks, st, act, dz, z, y, res, mean, scale, shift, rscale, rshift, part, rows, C, act,
+            alpha, 1);
   hipLaunchKernelGGL(bwd_finalize_rows_kernel, dim3((C + NT / 64 - 1) / (NT / 64)), dim3(NT), 0, st, part, blocks,
                      invstd, gamma, coef, dgamma, dbeta, rows, C);
-  hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_for(rows, C, 768)), dim3(NT), 0, st, dz, z, y, res, mean, coef,
-                     scale, shift, (const float*)nullptr, (const float*)nullptr, dy, dres, rows, C, act, alpha);
+  NA_LAUNCH(bwd_apply_kernel, grid_for(rows, C, 768), st, act, dz, z, y, res, mean, coef, scale, shift, rscale, rshift,
+            dy, dres, rows, C, act, alpha);
   return hipGetLastError();
 }
 
@@ -420,8 +440,8 @@ MLC_EXPORT int mlc_bnact_bwd_apply(const bf16* dz, const bf16* z, const bf16* y,
                                    const float* rshift, bf16* dy, bf16* dres, long rows, int C, int act, float alpha,
                                    hipStream_t st) {
   if (C % 8) return -1;
-  hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_for(rows, C, 768)), dim3(NT), 0, st, dz, z, y, res, mean, coef,
-                     scale, shift, rscale, rshift, dy, dres, rows, C, act, alpha);
+  NA_LAUNCH(bwd_apply_kernel, grid_for(rows, C, 768), st, act, dz, z, y, res, mean, coef, scale, shift, rscale, rshift,
+            dy, dres, rows, C, act, alpha);
   return hipGetLastError();
 }
 

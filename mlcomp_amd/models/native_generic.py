@@ -35,6 +35,7 @@ seven architectures; this module covers the rest:
 from __future__ import annotations
 
 import operator
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -307,6 +308,19 @@ class _Lowering:
             _pair(d, 'dilation')
         if d != 1 or ret or k * k > 255:
             raise NativeUnsupported(f'max_pool2d(k={k}, dilation={d}, return_indices={ret})')
+        src = node.args[0]
+        site = self.modules.get(src.target) if isinstance(src, fx.Node) and src.op == 'call_module' else None
+        if site is None and isinstance(src, fx.Node) and src.op == 'call_module':
+            site = getattr(self.gm, src.target, None)
+        if ((k, s, p, bool(ceil)) == (3, 2, 1, False) and isinstance(site, ConvBNAct) and site.bn is not None
+                and site.act == A['relu'] and not site.residual and len(src.users) == 1
+                and site.conv.Co == site.conv.Cop and Fn.stem_pool_ok(site.conv.Cop)):
+            # conv -> BN -> ReLU -> 3x3/2 max-pool (a ResNet stem): one fused pass (stem.hip)
+            object.__setattr__(site, 'pool3', True)
+            node.replace_all_uses_with(src)
+            self.gm.graph.erase_node(node)
+            self.erased.add(node)
+            return
         new = self._site_node(node, MaxPool(self.net.ctx, k, s, p, bool(ceil)), [node.args[0]])
         self._replace([node], new)
 
@@ -338,6 +352,52 @@ class _Lowering:
                 continue
             object.__setattr__(s3, 'res_link', s1)
 
+    def _fold_shortcut_bns(self):
+        """A conv+BN site D without activation or residual whose output is only the residual
+        input of a conv+BN site S (a bottleneck's downsample shortcut): S applies D's BN as
+        its residual's affine in its own apply pass, so D skips its apply pass (the hand
+        ResNet engine's fold; in backward the residual gradient S returns is that BN's
+        output gradient, D's BN backward unchanged)."""
+        mods = dict(self.gm.named_modules())
+        for n in self.gm.graph.nodes:
+            s = mods.get(n.target) if n.op == 'call_module' else None
+            if not isinstance(s, ConvBNAct) or s.bn is None or not s.residual or len(n.args) < 2:
+                continue
+            r = n.args[1]
+            d = mods.get(r.target) if isinstance(r, fx.Node) and r.op == 'call_module' else None
+            if (not isinstance(d, ConvBNAct) or d is s or d.bn is None or d.act != 0 or d.residual
+                    or len(r.users) != 1 or n.args[0] is r or d.conv.Cop != s.conv.Cop or d.conv.Co != d.conv.Cop):
+                continue
+            object.__setattr__(s, 'res_bn', d)
+            object.__setattr__(d, 'bn_folded', True)
+
+    def _link_dgrads(self):
+        """A value that is the conv input of exactly two dense conv sites P (earlier in the
+        graph) and Q (later) - a residual block's first conv and its downsample shortcut -
+        where Q's backward runs before P's: Q depends on P (the shortcut site that also sums
+        the block), or Q's only user is a site P reaches (once that user's backward ran, Q is
+        ready no later than P and, created later, runs first: autograd's ready queue takes
+        the higher sequence number).  Q hands its input gradient to P's dgrad epilogue (no
+        autograd add), so P's epilogue holds the value's whole gradient (which lets the
+        value's producer link its BN backward to P)."""
+        mods = dict(self.gm.named_modules())
+        order = {n: i for i, n in enumerate(self.gm.graph.nodes)}
+        for x in self.gm.graph.nodes:
+            users = sorted(x.users, key=order.get)
+            if len(users) != 2:
+                continue
+            sites = [mods.get(u.target) if u.op == 'call_module' else None for u in users]
+            if not all(isinstance(s, ConvBNAct) and s.conv.kind == 'dense' and u.args[0] is x
+                       and not (len(u.args) > 1 and u.args[1] is x) for s, u in zip(sites, users)):
+                continue
+            (p, q), (sp, sq) = users, sites
+            qu = list(q.users)
+            q_first = self._reaches(p, q) or (len(qu) == 1 and self._reaches(p, qu[0]))
+            if sp is sq or sp.conv.Cip != sq.conv.Cip or sq.grad_link is not None or sp.grad_expected or not q_first:
+                continue
+            object.__setattr__(sq, 'grad_link', sp)
+            object.__setattr__(sp, 'grad_expected', True)
+
     def _link_bn_backward(self):
         """A conv+BN site A (ReLU or no activation, batch statistics) whose output is used
         only as the input of a dense conv site B (and, at a residual block boundary, as the
@@ -353,18 +413,22 @@ class _Lowering:
             a = n.args[0]
             sa = mods.get(a.target) if isinstance(a, fx.Node) and a.op == 'call_module' else None
             if (not isinstance(sa, ConvBNAct) or sa is sb or sa.bn is None or sa.act not in (0, relu)
-                    or sa.conv.Cop != sb.conv.Cip):
+                    or sa.conv.Cop != sb.conv.Cip or sa.pool3):
                 continue
             others = [u for u in a.users if u is not n]
-            # the only other user may be a site whose residual gradient B's dgrad already sums
-            # (an identity-residual link): B's dgrad output is then A's whole output gradient
-            if others and not (len(others) == 1 and others[0].op == 'call_module'
-                               and getattr(mods.get(others[0].target), 'res_link', None) is sb):
+            # the only other user may be a site whose residual gradient (an identity-residual
+            # link) or input gradient (a sibling-conv hand-off) B's dgrad already sums: B's
+            # dgrad output is then A's whole output gradient
+            o = mods.get(others[0].target) if len(others) == 1 and others[0].op == 'call_module' else None
+            if others and not (o is not None and (getattr(o, 'res_link', None) is sb
+                                                  or getattr(o, 'grad_link', None) is sb)):
                 continue
             if len(n.args) > 1 and n.args[1] is a:
                 continue
             object.__setattr__(sb, 'bn_link', sa)
             object.__setattr__(sa, 'bn_prereduced', True)
+            if sa.res_bn is not None:       # its folded shortcut BN is reduced there as well
+                object.__setattr__(sa.res_bn, 'bn_prereduced', True)
 
     @staticmethod
     def _reaches(a: fx.Node, b: fx.Node) -> bool:
@@ -426,7 +490,9 @@ class _Lowering:
                     node.target = 'reshape'     # site outputs are channels_last views
                 elif node.target in ('matmul', 'mm', 'bmm'):
                     raise NativeUnsupported(f'{node.name}: Tensor.{node.target} has no native lowering')
+        self._fold_shortcut_bns()
         self._link_residuals()
+        self._link_dgrads()
         self._link_bn_backward()
         g.lint()
         self.gm.delete_all_unused_submodules()
@@ -442,7 +508,10 @@ class GenericNet:
         self.torch_model = model
         self.device = torch.device(device)
         ctx = self.ctx = NativeContext()
-        ctx.wt = None                      # generic sites read filters directly
+        # MLC_GENERIC_WT=1 (default): dense convs keep a transposed, flipped filter copy for
+        # their input gradients (Fn.WtTable, refreshed once per training forward), as the
+        # hand engines do; 0: the dgrads read the filters directly
+        ctx.wt = Fn.WtTable() if os.environ.get('MLC_GENERIC_WT', '1') == '1' else None
         ctx.grad_prezeroed = True          # the step zeroes the grad arena once
         self._params: Dict[str, object] = {}
         was = model.training
@@ -543,6 +612,8 @@ class GenericNet:
         # the user model's own objects, shared by both graphs: their mode is set here, on
         # every call, so the eval graph never runs a training-mode dropout
         gm.train(self.training)
+        if self.training and self.ctx.wt is not None:
+            self.ctx.wt.refresh()          # the weights are fixed until this step's optimizer
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.device.type == 'cuda'):
             return gm(x)
 

@@ -590,6 +590,12 @@ def stem_w_from_s2d(w2, Ci=3):
     return w8[:, :Ci, :7, :7].contiguous()
 
 
+def stem_pool_ok(C: int) -> bool:
+    """Channel counts the fused stem kernels take: C/8 a power of two <= 64."""
+    G = C // 8
+    return C % 8 == 0 and 1 <= G <= 64 and G & (G - 1) == 0
+
+
 def stem_pool_fwd(y, scale, shift):
     """ResNet stem tail: pooled = maxpool3x3/2(relu(y*scale + shift)) without
     materialising the activation (csrc/kernels/stem.hip).  Returns (pooled, idx); idx is
@@ -1121,11 +1127,14 @@ def bnact_apply(y, res, scale, shift, act=0, alpha=0.0, res_affine=None):
 
 
 def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0, dgamma=None, dbeta=None,
-              sums=None, coef=None, want_dres=False):
-    """Backward of z = act(BN(y) [+ res]) with the forward's (scale, shift): returns (dy, dres
-    or None) and writes dgamma / dbeta.  ``sums`` (NSTAT*2*C fp32) must be zero on entry."""
+              sums=None, coef=None, want_dres=False, res_affine=None):
+    """Backward of z = act(BN(y) [+ res (*rscale + rshift)]) with the forward's (scale, shift):
+    returns (dy, dres or None) and writes dgamma / dbeta; dres is the gradient of the residual
+    term (before ``res_affine``, i.e. of a folded shortcut BN's output).  ``sums`` (NSTAT*2*C
+    fp32) must be zero on entry."""
     C = y.shape[-1]
     rows = y.numel() // C
+    rs, rh = res_affine if res_affine is not None else (None, None)
     if _cuda(dz):
         if coef is None:
             coef = torch.empty(3 * C, device=dz.device, dtype=torch.float32)
@@ -1136,26 +1145,28 @@ def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0
             dy = torch.empty_like(y)
             dres = torch.empty_like(y) if want_dres else None
             _lib.call('mlc_bnact_bwd', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
-                      _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(invstd), _lib.ptr(gamma), _lib.ptr(part), part.numel(),
-                      _lib.ptr(coef), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(dy), _lib.ptr(dres), rows, C,
+                      _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(rs), _lib.ptr(rh), _lib.ptr(invstd), _lib.ptr(gamma),
+                      _lib.ptr(part), part.numel(), _lib.ptr(coef), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(dy), _lib.ptr(dres), rows, C,
                       int(act), float(alpha), _lib.stream())
             return dy, dres
         if sums is None:
             sums = torch.zeros(NSTAT * 2 * C, device=dz.device, dtype=torch.float32)
         _lib.call('mlc_bnact_bwd_reduce', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
-                  _lib.ptr(scale), _lib.ptr(shift), None, None, _lib.ptr(sums), rows, C, int(act), float(alpha),
+                  _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(rs), _lib.ptr(rh), _lib.ptr(sums), rows, C, int(act),
+                  float(alpha),
                   _lib.stream())
         _lib.call('mlc_bn_bwd_finalize', _lib.ptr(sums), _lib.ptr(invstd), _lib.ptr(gamma), _lib.ptr(coef),
                   _lib.ptr(dgamma), _lib.ptr(dbeta), rows, C, _lib.stream())
         dy = torch.empty_like(y)
         dres = torch.empty_like(y) if want_dres else None
         _lib.call('mlc_bnact_bwd_apply', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
-                  _lib.ptr(coef), _lib.ptr(scale), _lib.ptr(shift), None, None, _lib.ptr(dy), _lib.ptr(dres), rows, C,
-                  int(act), float(alpha), _lib.stream())
+                  _lib.ptr(coef), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(rs), _lib.ptr(rh), _lib.ptr(dy),
+                  _lib.ptr(dres), rows, C, int(act), float(alpha), _lib.stream())
         return dy, dres
     a = y.float().reshape(rows, C) * scale + shift
     if res is not None:
-        a = a + res.float().reshape(rows, C)
+        r = res.float().reshape(rows, C)
+        a = a + (r * rs + rh if rs is not None else r)
     d = dz.float().reshape(rows, C)
     if act:
         if act in (4, 5):

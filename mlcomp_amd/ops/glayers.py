@@ -192,10 +192,15 @@ class ConvParams:
         Co, Cg, KH, KW = conv.weight.shape
         self.Ci, self.Co, self.Cg = Cg * conv.groups, Co, Cg
         self.k = (KH, KW)
+        self.wt_idx = None
         if self.groups == 1:
             self.kind = 'dense'
             self.Cip, self.Cop = ceil8(self.Ci), ceil8(Co)
             self.w = ctx.arena.weight(f'{name}.weight', (self.Cop, KH, KW, self.Cip))
+            if ctx.wt is not None and isinstance(self.pad, int):
+                # the transposed, flipped filter copy (one batched refresh per training step,
+                # GenericNet.__call__): the dgrad GEMM reads both operands K-contiguous
+                self.wt_idx = ctx.wt.add(self.w)
         elif self.groups == self.Ci and Co == self.Ci:
             self.kind = 'dw'
             self.Cip = self.Cop = ceil8(Co)
@@ -272,7 +277,8 @@ class ConvParams:
         reduction and ReLU mask in the same epilogue, dense convs only)."""
         wb = self.w.bf16
         if self.kind == 'dense':
-            return Fn.conv2d_dgrad(dy, wb, x_shape, self.stride, self.pad, self.dil, addend=addend, bn=bn)
+            wt = self.ctx.wt[self.wt_idx] if self.wt_idx is not None else None
+            return Fn.conv2d_dgrad(dy, wb, x_shape, self.stride, self.pad, self.dil, addend=addend, bn=bn, wt=wt)
         assert bn is None
         if self.kind == 'dw':
             dx = Fn.dwconv_dgrad(dy, wb, x_shape, self.stride, self.pad, self.dil)
@@ -505,6 +511,26 @@ class ConvBNAct(Site):
         object.__setattr__(self, 'bn_prereduced', False)
         object.__setattr__(self, '_bn_stash', None)
         object.__setattr__(self, '_bn_done', False)
+        # input-gradient hand-off (set by the lowering): this site's input is also the input of
+        # ``grad_link``, a dense conv site whose backward runs after this one's (a block's
+        # first conv beside its downsample shortcut), so this site's input gradient is summed
+        # in that site's dgrad epilogue instead of by autograd; ``grad_expected`` marks the
+        # receiving site, which fails loudly if the hand-off did not arrive
+        object.__setattr__(self, 'grad_link', None)
+        object.__setattr__(self, 'grad_expected', False)
+        # folded shortcut BatchNorm (set by the lowering): ``res_bn`` is the conv+BN site (no
+        # activation) whose output is only this site's residual; it returns its pre-BN conv
+        # output (``bn_folded``) and this site applies its BN as the residual's affine in its
+        # own apply pass (the hand engine's downsample fold), so that BN costs no pass of its
+        # own; the residual gradient this site returns is the gradient of that BN's output
+        object.__setattr__(self, 'res_bn', None)
+        object.__setattr__(self, 'bn_folded', False)
+        object.__setattr__(self, '_fold', None)
+        # fused 3x3/2 max-pool (set by the lowering): conv -> BN -> ReLU -> max-pool with the
+        # activation used only by the pool (a ResNet stem) runs BN-apply + ReLU + pool in one
+        # pass and its backward as pool-scatter + BN-backward passes (stem.hip); the full-
+        # resolution activation is never written
+        object.__setattr__(self, 'pool3', False)
 
     def forward(self, x, res=None):
         return _run(self, x, res) if res is not None else _run(self, x)
@@ -522,8 +548,21 @@ class ConvBNAct(Site):
             y = c.fwd(xn, stats)
             rows = y.numel() // y.shape[-1]
             scale, shift, mean, inv = bn.finalize(stats[0] if stats else None, stats[1] if stats else None, rows)
-            z = Fn.bnact_apply(y, rn, scale, shift, self.act, self.alpha)
+            rsh = None
+            if self.pool3:
+                out, idx = Fn.stem_pool_fwd(y, scale, shift)
+                return from_nhwc(out, c.Co), [xn, y, idx, y, scale, shift, mean, inv], False
+            if self.bn_folded:
+                z = y                                  # the consumer applies (scale, shift)
+                object.__setattr__(self, '_fold', (scale, shift))
+            else:
+                if self.res_bn is not None and rn is not None:
+                    rsh = self.res_bn._fold
+                    object.__setattr__(self.res_bn, '_fold', None)
+                z = Fn.bnact_apply(y, rn, scale, shift, self.act, self.alpha, res_affine=rsh)
             saved = [xn, y, z, rn if rn is not None else y, scale, shift, mean, inv]
+            if rsh is not None:
+                saved += list(rsh)
             if self.bn_prereduced and stats is not None and self.ctx.training:
                 object.__setattr__(self, '_bn_stash', (y, z, mean))   # read by the linked dgrad
                 object.__setattr__(self, '_bn_done', False)
@@ -541,10 +580,16 @@ class ConvBNAct(Site):
         dz = to_nhwc(dout, c.Cop)
         dres = None
         if bn is not None:
-            xn, y, z, rn, scale, shift, mean, inv = saved
+            xn, y, z, rn, scale, shift, mean, inv = saved[:8]
+            rsh = tuple(saved[8:10]) if len(saved) > 8 else None
             ws = self.ctx.ws
             d = self._direct_bn_grads()
-            if self.bn_prereduced and self._bn_done:
+            if self.pool3:
+                # dz: the pooled output's gradient; z holds the window argmax
+                dy = Fn.stem_pool_bwd(dz.contiguous(), z, y, mean, inv, bn.gamma.master, _acc_view(bn.gamma, d),
+                                      _acc_view(bn.beta, d), ws[self.k_bw],
+                                      torch.empty(3 * c.Cop, device=dz.device, dtype=torch.float32))
+            elif self.bn_prereduced and self._bn_done:
                 # the consumer's dgrad already masked dz and reduced the BN-backward sums
                 object.__setattr__(self, 'n_prereduced', getattr(self, 'n_prereduced', 0) + 1)
                 dy, dres = Fn.bn_bwd(dz, None, y, mean, inv, bn.gamma.master, want_dres=has_res,
@@ -553,7 +598,8 @@ class ConvBNAct(Site):
             else:
                 dy, dres = Fn.bnact_bwd(dz, z, y, rn if has_res else None, mean, scale, shift, inv,
                                         bn.gamma.master, self.act, self.alpha, dgamma=_acc_view(bn.gamma, d),
-                                        dbeta=_acc_view(bn.beta, d), sums=ws[self.k_bw], want_dres=has_res)
+                                        dbeta=_acc_view(bn.beta, d), sums=ws[self.k_bw], want_dres=has_res,
+                                        res_affine=rsh)
             object.__setattr__(self, '_bn_stash', None)
             object.__setattr__(self, '_bn_done', False)
             _acc_commit(bn.gamma, d)
@@ -572,13 +618,23 @@ class ConvBNAct(Site):
                 dres = dy
             if c.b is not None and c.kind != 'dense':
                 c.b.grad.add_(dy.float().sum(dim=(0, 1, 2)))
-        addend = self._pending                 # a later site's residual gradient of our input
+        addend = self._pending                 # another site's gradient of our input
         object.__setattr__(self, '_pending', None)
+        if self.grad_expected and needs[0] and addend is None:
+            raise RuntimeError(f'{c.name}: the input-gradient hand-off of its sibling conv site did not arrive '
+                               '(backward order differs from the one the lowering assumed)')
         spec = None
         src = self.bn_link
         if src is not None and needs[0] and src._bn_stash is not None:
             ya, za, mean_a = src._bn_stash
-            spec = Fn.BnBwdSpec(za if src.act else None, [(ya, mean_a, self.ctx.ws[src.k_bw])])
+            ys = [(ya, mean_a, self.ctx.ws[src.k_bw])]
+            fold = src.res_bn
+            if fold is not None and fold._bn_stash is not None:
+                # the producer's folded shortcut BN shares its output gradient: both sums here
+                yf, _, mean_f = fold._bn_stash
+                ys.append((yf, mean_f, self.ctx.ws[fold.k_bw]))
+                object.__setattr__(fold, '_bn_done', True)
+            spec = Fn.BnBwdSpec(za if src.act else None, ys)
             object.__setattr__(src, '_bn_done', True)
         side = self.ctx.wgrad_stream if needs[0] else None
         main = torch.cuda.current_stream(self.ctx.device) if side is not None else None
@@ -598,6 +654,9 @@ class ConvBNAct(Site):
             dx = c.dgrad(dy, xn.shape, addend, spec) if needs[0] else None
         if c.uses.bwd_done():
             c.mark_ready()
+        if dx is not None and self.grad_link is not None:
+            object.__setattr__(self.grad_link, '_pending', dx)       # summed by the sibling's dgrad
+            dx = None
         out = [from_nhwc(dx, c.Ci) if dx is not None else None]
         if has_res:
             if needs[1] and self.res_link is not None:

@@ -540,18 +540,27 @@ def test_conv1d_bn1d_lowers_and_matches_fp32_autograd():
 def test_identity_residual_and_bn_backward_links_are_exact():
     """ResNet basic blocks: the identity residual's gradient is handed from the block's last
     conv site to its first conv site's dgrad epilogue (one gradient per value, no autograd
-    sum), and a conv site whose input is another conv site's BN-ReLU output computes that
-    BN's backward reduction and ReLU mask in its dgrad epilogue (no reduction pass).  Input
-    and weight gradients equal the unlinked ones and match fp32 autograd."""
+    sum); a downsample block's shortcut conv hands its input gradient to the block's first
+    conv the same way and applies the folded BN of the block's last conv as its residual's
+    affine; a conv site whose input is another conv site's BN(-ReLU) output computes that
+    BN's (and its folded partner's) backward reduction and ReLU mask in its dgrad epilogue
+    (no reduction pass).  Input and weight gradients equal the unlinked ones and match fp32
+    autograd."""
     m, ref = _pair(lambda: build_model('resnet18', num_classes=10))
     net = GenericNet(m, 'cpu')
-    links = [s for s in net.train_gm.modules() if getattr(s, 'res_link', None) is not None]
+    sites = list(net.train_gm.modules())
+    links = [s for s in sites if getattr(s, 'res_link', None) is not None]
     assert len(links) == 5, len(links)            # 8 blocks, 3 of them with a downsample shortcut
-    bn_links = [s for s in net.train_gm.modules() if getattr(s, 'bn_link', None) is not None]
-    # each block's second conv reads its first conv's BN-ReLU (8); the first conv of 4 of the
-    # 5 identity blocks also reads the previous block's output, whose residual it already sums
-    # (layer1.0's input is the max-pool's output)
-    assert len(bn_links) == 12, len(bn_links)
+    glinks = [s for s in sites if getattr(s, 'grad_link', None) is not None]
+    folds = [s for s in sites if getattr(s, 'res_bn', None) is not None]
+    assert len(glinks) == 3 and len(folds) == 3, (len(glinks), len(folds))
+    # the stem's conv -> BN -> ReLU -> max-pool runs as one fused site
+    assert sum(bool(getattr(s, 'pool3', False)) for s in sites) == 1
+    bn_links = [s for s in sites if getattr(s, 'bn_link', None) is not None]
+    # each block's second conv reads its first conv's BN-ReLU (8); the first conv of every
+    # block after layer1.0 (whose input is the max-pool's output) also reads the previous
+    # block's output, whose other gradient (identity residual or shortcut conv) it sums (7)
+    assert len(bn_links) == 15, len(bn_links)
     torch.manual_seed(3)
     x = torch.randn(4, 3, 32, 32)
     y = torch.randint(0, 10, (4,))
@@ -560,6 +569,15 @@ def test_identity_residual_and_bn_backward_links_are_exact():
         for s in links:
             object.__setattr__(s, '_saved_link', getattr(s, '_saved_link', s.res_link))
             object.__setattr__(s, 'res_link', s._saved_link if linked else None)
+        for s in glinks:
+            object.__setattr__(s, '_saved_glink', getattr(s, '_saved_glink', s.grad_link))
+            object.__setattr__(s, 'grad_link', s._saved_glink if linked else None)
+            object.__setattr__(s._saved_glink, 'grad_expected', linked)
+        for s in folds:
+            object.__setattr__(s, '_saved_fold', getattr(s, '_saved_fold', s.res_bn))
+            object.__setattr__(s, 'res_bn', s._saved_fold if linked else None)
+            object.__setattr__(s._saved_fold, 'bn_folded', linked)
+            object.__setattr__(s._saved_fold, 'bn_prereduced', linked)
         for s in bn_links:
             object.__setattr__(s, '_saved_bn', getattr(s, '_saved_bn', s.bn_link))
             object.__setattr__(s, 'bn_link', s._saved_bn if linked else None)
@@ -570,9 +588,12 @@ def test_identity_residual_and_bn_backward_links_are_exact():
         F.cross_entropy(net(xi).float(), y).backward()
         return xi.grad.clone(), [(p.w if hasattr(p, 'w') else p.gamma).grad.clone() for p in net.param_sets()]
     gx_l, gw_l = run(True)
-    assert sum(getattr(s._saved_bn, 'n_prereduced', 0) for s in bn_links) == 12   # the fused path ran
+    # the fused path ran for every link and every folded shortcut BN
+    assert sum(getattr(s._saved_bn, 'n_prereduced', 0) for s in bn_links) == 15
+    assert sum(getattr(s._saved_fold, 'n_prereduced', 0) for s in folds) == 3
     gx_u, gw_u = run(False)
-    assert sum(getattr(s._saved_bn, 'n_prereduced', 0) for s in bn_links) == 12
+    assert sum(getattr(s._saved_bn, 'n_prereduced', 0) for s in bn_links) == 15
+    assert sum(getattr(s._saved_fold, 'n_prereduced', 0) for s in folds) == 3
     assert _rel(gx_l, gx_u) < 1e-2
     for a, b in zip(gw_l, gw_u):
         assert _rel(a, b) < 1e-2
