@@ -126,6 +126,15 @@ class _Dense:
         else:
             join = self.bwd_params_async(dy, x)
             dx = self.dgrad(dy, **dgrad_kw)
+        side = self.ctx.wgrad_stream
+        if side is not None and self.ctx.wgrad_lag and not self.ctx.wgrad_defer:
+            # lagged join (MLC_WGRAD_LAG=1): this weight gradient is joined after the NEXT
+            # dense layer's input gradient, so the main stream never waits on a wgrad that
+            # just started; holding dy / x until then keeps their memory from being reused
+            ev = torch.cuda.Event()
+            ev.record(side)
+            self.ctx.lag_wgrad(ev, (dy, x), (self.w, self.b))
+            return dx
         join()
         self.mark()
         return dx
@@ -347,7 +356,14 @@ class NativeBert:
         self.k_loss = ctx.ws.request('loss', 1)
         self.k_correct = ctx.ws.request('correct', 1)
         ctx.finalize(device)
-        ctx.default_wgrad_defer(False)
+        # weight gradients: captured after each dense layer's input gradient and forked from
+        # the point before it (dgrad_first), never joined per layer (one free-running side
+        # chain, joined before the optimizer).  Interleaved A/B on one MI355X (bench.py,
+        # 2 rounds): per-layer join 5,139 / 5,155 seq/s, lagged join by 1 / 3 layers 5,348 /
+        # 5,556, this 5,612 / 5,610 (profiles/round5/bert_wgrad_join_ab.txt); round 4's
+        # deferral without dgrad_first lost 3-6 %.  MLC_WGRAD_DEFER / MLC_DGRAD_FIRST override.
+        ctx.default_wgrad_defer(True)
+        ctx.default_dgrad_first(True)
         self.device = ctx.device
         self.seed = torch.zeros(1, device=self.device, dtype=torch.int32)
         self.ln_fin = Tx.LnFinalizer()

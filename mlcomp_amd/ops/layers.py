@@ -82,17 +82,18 @@ class NativeContext:
         # forward pass (refresh_wt)
         self.wt = Fn.WtTable() if os.environ.get('MLC_DGRAD_WT', '1') == '1' else None
         self.wt_stale = False
-        # MLC_WGRAD_LAG=1: a layer's side-stream weight gradient is joined at the end of the
-        # NEXT layer's backward (event per layer) instead of its own, so the main stream does
-        # not stall on a just-finished wgrad; flush_wgrad joins the last one
-        self.wgrad_lag = os.environ.get('MLC_WGRAD_LAG', '0') == '1'
+        # MLC_WGRAD_LAG=N (engines may set a default): a layer's side-stream weight gradient
+        # is joined N layers later (event per layer) instead of at the end of its own
+        # backward, so the main stream does not stall on a wgrad that just started;
+        # flush_wgrad joins the remaining ones
+        self.wgrad_lag = int(os.environ.get('MLC_WGRAD_LAG', '0') or 0)
         # wgrad_defer (engines opt in; MLC_WGRAD_DEFER overrides): the side-stream weight
         # gradients are never joined per layer - they form one free-running chain beside the
         # input-gradient chain, their operands are kept alive for the side stream with
         # record_stream, the gradient bucketer waits on the side stream as well, and the
         # chain joins once, in flush_wgrad (bucketer.finish, before the optimizer)
         self.wgrad_defer = False
-        self._pending_wgrad = None
+        self._pending_wgrad = []       # (event, operands kept alive, slots to mark), oldest first
         self.dgrad_first = DGRAD_FIRST_ENV == '1'
 
     def default_dgrad_first(self, on: bool):
@@ -127,15 +128,31 @@ class NativeContext:
             cur = torch.cuda.current_stream(self.device)
             if cur != self.wgrad_stream:
                 cur.wait_stream(self.wgrad_stream)
-        p = self._pending_wgrad
-        if p is None:
-            return
-        self._pending_wgrad = None
-        ev, _dy, _x, w = p
-        cur = torch.cuda.current_stream(self.device)
-        if cur != self.wgrad_stream:
-            cur.wait_event(ev)
-        self.arena.mark_ready(w)
+        self.join_wgrads(0)
+
+    def default_wgrad_lag(self, n: int):
+        """Engine default for the lagged join depth (MLC_WGRAD_LAG overrides it)."""
+        if os.environ.get('MLC_WGRAD_LAG') is None:
+            self.wgrad_lag = n
+
+    def lag_wgrad(self, ev, keep, slots):
+        """Queue a side-stream weight gradient (``ev`` recorded after it; ``keep``: its operands,
+        held until the join so their memory is not reused early) and join the ones beyond
+        the lag depth."""
+        self._pending_wgrad.append((ev, keep, slots))
+        self.join_wgrads(self.wgrad_lag)
+
+    def join_wgrads(self, keep_last: int):
+        """Join queued weight gradients into the current stream, oldest first, until at most
+        ``keep_last`` remain, and mark their slots ready."""
+        q = self._pending_wgrad
+        while len(q) > keep_last:
+            ev, _keep, slots = q.pop(0)
+            cur = torch.cuda.current_stream(self.device)
+            if cur != self.wgrad_stream:
+                cur.wait_event(ev)
+            for s in (slots if isinstance(slots, (list, tuple)) else (slots,)):
+                self.arena.mark_ready(s)
 
     def refresh_wt(self):
         """Re-derive the transposed filters from the current weights (one launch, on the
@@ -357,8 +374,7 @@ class ConvBN:
         if side is not None and self.ctx.wgrad_lag:
             ev = torch.cuda.Event()
             ev.record(side)
-            self.ctx.flush_wgrad()                 # join the previous layer's wgrad
-            self.ctx._pending_wgrad = (ev, dy, x, self.w)   # keeps dy, x alive until joined
+            self.ctx.lag_wgrad(ev, (dy, x), self.w)   # keeps dy, x alive until joined
             return dx, dres
         if side is not None:
             main.wait_stream(side)                 # join: the weight gradient is complete

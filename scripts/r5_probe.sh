@@ -1,14 +1,19 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/q3; mkdir -p $O
-chk() { rc=$1; if [ $rc -ne 0 ]; then echo "step failed rc=$rc: stopping"; exit $rc; fi; }
-timeout -k 10 500 python -u -m pytest tests/test_generic_gpu.py tests/test_kernels_gpu.py -x -q --timeout 300 --timeout-method thread > $O/gen_tests.log 2>&1; chk $?; tail -2 $O/gen_tests.log
-for r in 1 2; do for wt in 1 0; do
-  MLC_GENERIC_WT=$wt timeout -k 10 300 python -u scripts/bench_generic.py --model resnet50 --batch 512 --size 224 --impl native 2>>$O/err.log | sed "s/^/wt$wt /" >> $O/gen.log; chk $?
-done; done
-for m in "resnext50_32x4d --batch 128" "efficientnet-b0 --batch 256"; do
-  timeout -k 10 300 python -u scripts/bench_generic.py --model $m --size 224 --impl native >> $O/gen.log 2>>$O/err.log; chk $?
+O=gpurun_out/q6; mkdir -p $O
+chk() { rc=$1; if [ $rc -ge 124 ]; then echo "step failed hard rc=$rc: stopping"; exit $rc; fi; }
+timeout -k 10 900 python -u -m pytest tests/test_transformer_gpu.py tests/test_deterministic_gpu.py tests/test_dp_gpu.py tests/test_engines_det_gpu.py tests/test_engines_gpu_vs_cpu.py tests/test_native_eval_gpu.py tests/test_graphed_gpu.py -x -q --timeout 600 --timeout-method thread > $O/tests.log 2>&1; rc=$?; tail -3 $O/tests.log; [ $rc -ne 0 ] && exit $rc
+run() { tag=$1; shift; env "$@" timeout -k 10 300 python -u bench.py --model bert-base --steps 40 --warmup 10 2>>$O/err.log | tail -1 | sed "s/^/$tag /" >> $O/bench.txt; chk $?; }
+runr() { tag=$1; shift; env "$@" timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 2>>$O/err.log | tail -1 | sed "s/^/$tag /" >> $O/bench.txt; chk $?; }
+for r in 1 2; do
+  run bert_default MLC_X=0
+  runr rn_base MLC_X=0
+  runr rn_deferdf MLC_WGRAD_DEFER=1 MLC_DGRAD_FIRST=1
+  runr rn_df MLC_DGRAD_FIRST=1
 done
-cut -c1-160 $O/gen.log
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o gen -- python3 scripts/bench_generic.py --model resnet50 --batch 512 --size 224 --impl native --steps 6 --warmup 3 > $O/gen_prof.log 2>&1; chk $?
-python scripts/steady_kernels.py $O/prof --marker sgd_kernel --steps 3 > $O/gen_kernels.txt 2>&1; head -30 $O/gen_kernels.txt
+python - <<'PY'
+import json
+for l in open('gpurun_out/q6/bench.txt'):
+    tag, js = l.split(' ', 1)
+    d = json.loads(js); print(tag, d['value'], d['ms_per_step'])
+PY
