@@ -1300,8 +1300,10 @@ static int g_split_target_mat = 128;
 // dense-layer weight gradients (mlc_linear_wgrad_bias, mlc_gemm_f32out), A/B knob 9.
 // Round 2 kept 256 (128 lost 3 %); once the bf16 dgrads stopped splitting (knob 12 = 0)
 // 128 became the better point: BERT-base 5041/5096 vs 5021/4991 seq/s at 256, 64 lost
-// 2 % (profiles/round3/session2/wgrad_split_ab.txt)
-static int g_split_target_dense = 128;
+// 2 % (profiles/round3/session2/wgrad_split_ab.txt).  Since round 5 the weight gradients
+// run as one unjoined side chain (native_bert.py) and 256 is the better point again:
+// 5720/5731 vs 5643/5658 seq/s, 192 and 320 lose (profiles/round5/bert_wgrad_join_ab.txt)
+static int g_split_target_dense = 256;
 // bf16-output dense GEMMs on the 128x128 path (BERT's input gradients with MN-contiguous
 // weights) split K until tiles * splits reaches this (A/B knob 12, MLC_DENSE_SPLIT_TARGET;
 // 0 never splits).  Default 0 since round 3: unsplit 192-tile dgrads with the epilogue in
