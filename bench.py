@@ -85,10 +85,17 @@ def main():
     if not torch.cuda.is_available():
         print('bench.py needs a GPU', file=sys.stderr)
         sys.exit(2)
-    torch.cuda.set_device(local_rank)
-    device = torch.device('cuda', local_rank)
+    # one GPU per rank; MLC_DIST_BACKEND=gloo (with --graph 0) rehearses the multi-rank path
+    # with several ranks sharing the GPUs there are (local rank modulo the device count)
+    backend = os.environ.get('MLC_DIST_BACKEND', 'nccl')
+    dev_index = local_rank % torch.cuda.device_count() if backend != 'nccl' else local_rank
+    torch.cuda.set_device(dev_index)
+    device = torch.device('cuda', dev_index)
     if world > 1:
-        dist.init_process_group('nccl', device_id=device)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     comm = _world1_rccl(device) if (args.comm == 'rccl1' and world == 1 and args.impl == 'native') else None
     is_bert = args.model.startswith('bert')

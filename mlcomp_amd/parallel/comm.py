@@ -196,6 +196,9 @@ def make_comm(device: Optional[torch.device] = None):
         return None
     rank = dist.get_rank()
     _COMMS_MADE += 1
-    if device is not None and torch.device(device).type == 'cuda':
+    # GPU tensors under an nccl (= RCCL) process group: the framework's own RCCL
+    # communicator; any other backend (gloo: CPU runs, or several ranks sharing one GPU in a
+    # rehearsal of the multi-rank path) goes through torch.distributed itself
+    if device is not None and torch.device(device).type == 'cuda' and dist.get_backend() == 'nccl':
         return RcclComm(rank, world, device, tag=f'mlc{_COMMS_MADE}')
     return TorchComm(rank, world)
