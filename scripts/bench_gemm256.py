@@ -126,7 +126,10 @@ def timeit(fns, rounds=5, iters=20):
 
 
 def bench():
-    for (M, N, K) in [(4096, 4096, 4096), (4096, 2304, 768), (4096, 3072, 768), (4096, 768, 3072),
+    import os
+    conv_only = os.environ.get('CONV_ONLY') == '1'     # only the ResNet conv shapes
+    nb = int(os.environ.get('CONV_BATCH', 256))        # their batch
+    for (M, N, K) in [] if conv_only else [(4096, 4096, 4096), (4096, 2304, 768), (4096, 3072, 768), (4096, 768, 3072),
                       (50176, 1024, 256), (12544, 2048, 512)]:
         a = torch.rand(M, K, device='cuda').sub(0.5).to(torch.bfloat16)
         b = torch.rand(N, K, device='cuda').sub(0.5).to(torch.bfloat16)
@@ -135,7 +138,7 @@ def bench():
                     'igemm': lambda: old_nt(a, b, out), 'torch': lambda: torch.matmul(a, b.t(), out=out)})
         fl = 2.0 * M * N * K
         print(json.dumps({'nt': [M, N, K], **{k: round(fl / v / 1e9, 1) for k, v in t.items()}}), flush=True)
-    for (M, N, K) in [(512, 4608, 12544), (256, 2304, 50176), (768, 3072, 4096), (3072, 768, 4096)]:
+    for (M, N, K) in [] if conv_only else [(512, 4608, 12544), (256, 2304, 50176), (768, 3072, 4096), (3072, 768, 4096)]:
         a = torch.rand(K, M, device='cuda').sub(0.5).to(torch.bfloat16)
         b = torch.rand(K, N, device='cuda').sub(0.5).to(torch.bfloat16)
         out = torch.empty(M, N, device='cuda')
@@ -143,11 +146,11 @@ def bench():
                     'igemm_atomic': lambda: (out.zero_(), old_tn(a, b, out))})
         fl = 2.0 * M * N * K
         print(json.dumps({'tn': [M, N, K], **{k: round(fl / v / 1e9, 1) for k, v in t.items()}}), flush=True)
-    # ResNet-50 (batch 256) 3x3 convs + stem (s2d 4x4 over 16 channels)
-    for (Nb, H, C, Co, k, s, p) in [(256, 56, 64, 64, 3, 1, 1), (256, 56, 128, 128, 3, 2, 1),
-                                    (256, 28, 128, 128, 3, 1, 1), (256, 28, 256, 256, 3, 2, 1),
-                                    (256, 14, 256, 256, 3, 1, 1), (256, 14, 512, 512, 3, 2, 1),
-                                    (256, 7, 512, 512, 3, 1, 1), (256, 112, 16, 64, 4, 1, 0)]:
+    # ResNet-50 (batch CONV_BATCH) 3x3 convs + stem (s2d 4x4 over 16 channels)
+    for (Nb, H, C, Co, k, s, p) in [(nb, 56, 64, 64, 3, 1, 1), (nb, 56, 128, 128, 3, 2, 1),
+                                    (nb, 28, 128, 128, 3, 1, 1), (nb, 28, 256, 256, 3, 2, 1),
+                                    (nb, 14, 256, 256, 3, 1, 1), (nb, 14, 512, 512, 3, 2, 1),
+                                    (nb, 7, 512, 512, 3, 1, 1), (nb, 112, 16, 64, 4, 1, 0)]:
         x = torch.rand(Nb, H + (1 if k == 4 else 0), H + (1 if k == 4 else 0), C, device='cuda').sub(0.5).to(torch.bfloat16)
         w = torch.rand(Co, k, k, C, device='cuda').sub(0.5).to(torch.bfloat16)
         Ho = (x.shape[1] + 2 * p - k) // s + 1
@@ -164,5 +167,7 @@ def bench():
 
 
 if __name__ == '__main__':
-    check()
+    import os
+    if os.environ.get('CONV_ONLY') != '1':
+        check()
     bench()

@@ -1,4 +1,4 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/q10; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_dp_bench_gpu.py -x -v --timeout 280 --timeout-method thread > $O/tests.log 2>&1; rc=$?; tail -30 $O/tests.log; exit $rc
+O=gpurun_out/q11; mkdir -p $O
+CONV_ONLY=1 CONV_BATCH=512 timeout -k 10 300 python -u scripts/bench_gemm256.py > $O/conv512.log 2>&1; rc=$?; cat $O/conv512.log | grep conv; exit $rc
