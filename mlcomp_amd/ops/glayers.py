@@ -642,12 +642,18 @@ class ConvBNAct(Site):
             # the weight gradient on the context's side stream, concurrently with the input
             # gradient (as the hand engines do), joined before the site's backward returns:
             # dy / xn are freed only after that join, in the main stream's order
+            # captured weight gradient first (unless ctx.dgrad_first), as the hand conv
+            # engines do: the first-dispatched GEMM takes the CUs, and a squeezed-in wgrad
+            # would make the join below the critical path
             fork = torch.cuda.Event()
             fork.record(main)
-            dx = c.dgrad(dy, xn.shape, addend, spec)
+            if self.ctx.dgrad_first:
+                dx = c.dgrad(dy, xn.shape, addend, spec)
             side.wait_event(fork)
             with Fn.side_stream(side):
                 c.wgrad(dy, xn)
+            if not self.ctx.dgrad_first:
+                dx = c.dgrad(dy, xn.shape, addend, spec)
             main.wait_stream(side)
         else:
             c.wgrad(dy, xn)
