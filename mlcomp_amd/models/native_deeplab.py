@@ -79,8 +79,14 @@ class NativeDeepLab(NativeUnet):
         yield self.body1
         yield self.body2
 
+    def _default_schedule(self):
+        """The ResNet-101 backbone's long per-layer GEMMs keep the per-conv join (as
+        ResNet-50 does): the unjoined chain measured 1,868 / 1,874 vs 1,989 / 1,985 img/s
+        (profiles/round5/seg_wgrad_join_ab.txt)."""
+
     def _finish_init(self, device):
         self.ctx.finalize(device)
+        self._default_schedule()
         for u in self._units():
             u.load_from_torch()
         self.head.conv.load_from_torch()

@@ -337,6 +337,7 @@ class NativeFPN(NativeUnet):
 
     def _finish_init(self, device):
         self.ctx.finalize(device)
+        self._default_schedule()
         for u in self._units():
             u.load_from_torch()
         for u in self._dec_units():

@@ -86,6 +86,7 @@ class NativePSPNet(NativeUnet):
 
     def _finish_init(self, device):
         self.ctx.finalize(device)
+        self._default_schedule()
         for u in self._all_units():
             u.load_from_torch()
         self.ctx.arena.decay.refresh_mirror()

@@ -145,6 +145,15 @@ class NativeUnet:
         self.fuse_pair = os.environ.get('MLC_UNET_PAIR', '1') == '1'
         self._finish_init(device)
 
+    def _default_schedule(self):
+        """Segmentation engines (32 images @256²: short per-layer GEMMs): the weight
+        gradients form one unjoined side chain (joined before the optimizer) instead of a
+        join per conv, each of which costs ~10 us of cross-queue latency.  Interleaved A/B on
+        one MI355X, 2 rounds: U-Net 4,184 / 4,168 -> 4,565 / 4,563 img/s, LinkNet 4,533 / 4,632
+        -> 5,003 / 4,979, FPN 4,052 / 4,072 -> 4,278 / 4,303 (profiles/round5/seg_wgrad_join_ab.txt).
+        MLC_WGRAD_DEFER=0 restores the per-conv join."""
+        self.ctx.default_wgrad_defer(True)
+
     def _lower_encoder(self, model) -> NativeContext:
         """Context + the ResNet encoder's native stem / pool / blocks (shared with the
         LinkNet engine).  The stage outputs that feed decoder skips unlink the next block."""
@@ -165,6 +174,7 @@ class NativeUnet:
 
     def _finish_init(self, device):
         self.ctx.finalize(device)
+        self._default_schedule()
         for u in self._units():
             u.load_from_torch()
         self.head.load_from_torch()
