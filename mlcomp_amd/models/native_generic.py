@@ -540,6 +540,14 @@ class GenericNet:
             if isinstance(p, BNParams):
                 p.single_site = uses.get(id(p), 0) == 1
         ctx.finalize(self.device)
+        # weight gradients as one unjoined side chain, each forked before its site's input
+        # gradient (BERT's and the segmentation engines' schedule).  Interleaved A/B on one
+        # MI355X (profiles/round5/generic/bench_ab_defer.jsonl): ResNeXt-50 @128 7,451 ->
+        # 7,721 img/s, EfficientNet-b0 @256 10,291 -> 10,925, U-Net-ResNeXt-50 @16 561 -> 580;
+        # ResNet-50 @512 12,831 -> 12,750 (its long GEMMs prefer the per-site join:
+        # MLC_WGRAD_DEFER=0 MLC_DGRAD_FIRST=0)
+        ctx.default_wgrad_defer(True)
+        ctx.default_dgrad_first(True)
         for p in self._params.values():
             p.load_from_torch()
         self._bind_residual()

@@ -654,7 +654,13 @@ class ConvBNAct(Site):
                 c.wgrad(dy, xn)
             if not self.ctx.dgrad_first:
                 dx = c.dgrad(dy, xn.shape, addend, spec)
-            main.wait_stream(side)
+            if self.ctx.wgrad_defer:
+                # no per-site join (NativeContext.wgrad_defer): dy / xn stay alive for the side
+                # stream, the bucketer waits on it, flush_wgrad joins it before the optimizer
+                dy.record_stream(side)
+                xn.record_stream(side)
+            else:
+                main.wait_stream(side)
         else:
             c.wgrad(dy, xn)
             dx = c.dgrad(dy, xn.shape, addend, spec) if needs[0] else None
