@@ -1296,6 +1296,10 @@ static int g_prefetch = 2;
 static int g_split_target = 384;
 // single-LDS-stage variant for single-K-tile splits (A/B knob 5)
 static int g_single_stage = 1;
+// ... and for splits of up to this many K-tiles (A/B knob 13, MLC_SINGLE_STAGE_KT): one LDS
+// stage fits 4 blocks per CU instead of 2, which hides the load / store latency of short-K
+// GEMMs (ResNet's channel-expanding 1x1 convs) across blocks instead of within one
+static int g_single_stage_kt = 1;
 static int g_split_target_mat = 128;
 // dense-layer weight gradients (mlc_linear_wgrad_bias, mlc_gemm_f32out), A/B knob 9.
 // Round 2 kept 256 (128 lost 3 %); once the bf16 dgrads stopped splitting (knob 12 = 0)
@@ -1326,7 +1330,7 @@ static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int 
   const int per = ktiles > 0 ? (ktiles + splits - 1) / splits : 0;
   splits = per > 0 ? (ktiles + per - 1) / per : 1;
   dim3 grid(tiles, 1, splits);
-  if (per <= 1 && g_single_stage) {
+  if (per <= (g_single_stage_kt > 1 ? g_single_stage_kt : 1) && g_single_stage) {
     hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, EPI, 0>), grid, dim3(NTHR), 0, st, la, lb, epi, M, N, K, per);
     return hipGetLastError();
   }
@@ -1505,7 +1509,7 @@ MLC_EXPORT int mlc_gemm_get_set(int key, int value) {
           : key == 6 ? &igemm::g_splitk_fused : key == 7 ? &igemm::g_dense_narrow
           : key == 8 ? &igemm::g_gemm_dma : key == 9 ? &igemm::g_split_target_dense
           : key == 10 ? &igemm::g_dense_tile : key == 11 ? &igemm::g_dense_split
-          : key == 12 ? &igemm::g_dense_bf16_split_target : nullptr;
+          : key == 12 ? &igemm::g_dense_bf16_split_target : key == 13 ? &igemm::g_single_stage_kt : nullptr;
   if (!k) return -1;
   if (key == 10 || key == 11) {   // resolve the env defaults before the first override
     int sp = 1;

@@ -156,7 +156,7 @@ def load():
         # A/B knobs of the GEMM engine (tile policy / min blocks for the wide-wave tiles)
         for key, env in ((1, 'MLC_SPLIT_TARGET'), (2, 'MLC_SPLIT_TARGET_MAT'), (3, 'MLC_GEMM_BIG'),
                          (4, 'MLC_GEMM_BIG_MIN'), (5, 'MLC_GEMM_SINGLE_STAGE'), (6, 'MLC_SPLITK_FUSED'),
-                         (9, 'MLC_SPLIT_TARGET_DENSE'), (12, 'MLC_DENSE_SPLIT_TARGET')):
+                         (9, 'MLC_SPLIT_TARGET_DENSE'), (12, 'MLC_DENSE_SPLIT_TARGET'), (13, 'MLC_SINGLE_STAGE_KT')):
             if os.environ.get(env):
                 lib.mlc_gemm_get_set(key, int(os.environ[env]))
         for key, env in ((0, 'MLC_BN_UNROLL'), (1, 'MLC_BN_BLOCKS')):   # BN elementwise passes
