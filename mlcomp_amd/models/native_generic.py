@@ -44,8 +44,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from mlcomp_amd.ops import functional as Fn
-from mlcomp_amd.ops.glayers import (BNAct, BNParams, Conv3dAs2d, ConvBNAct, ConvParams, Frames, GlobalAvgPool,
-                                    LinearAct, LinearParams, MaxPool)
+from mlcomp_amd.ops.glayers import (BilinearUp, BNAct, BNParams, Conv3dAs2d, ConvBNAct, ConvParams, Frames,
+                                    GlobalAvgPool, LinearAct, LinearParams, MaxPool, UpCat)
 from mlcomp_amd.ops.layers import NativeContext
 from mlcomp_amd.train.native_spec import NativeUnsupported
 
@@ -324,6 +324,40 @@ class _Lowering:
         new = self._site_node(node, MaxPool(self.net.ctx, k, s, p, bool(ceil)), [node.args[0]])
         self._replace([node], new)
 
+    def interpolate(self, node):
+        """F.interpolate: nearest x2 [-> torch.cat([up, skip], 1)] -> ``UpCat`` (one NHWC pass,
+        the U-Net decoder input); bilinear with align_corners=True -> ``BilinearUp``.  Other
+        modes stay torch ops."""
+        names = ('input', 'size', 'scale_factor', 'mode', 'align_corners', 'recompute_scale_factor', 'antialias')
+        a = dict(zip(names, node.args))
+        a.update(node.kwargs)
+        x, size, scale = a.get('input'), a.get('size'), a.get('scale_factor')
+        mode, align = a.get('mode', 'nearest'), a.get('align_corners')
+        if a.get('recompute_scale_factor') or a.get('antialias') or not isinstance(x, fx.Node):
+            return
+        if isinstance(scale, (tuple, list)):
+            scale = tuple(float(s) for s in scale) if len(set(scale)) == 1 or mode == 'bilinear' else None
+        elif isinstance(scale, (int, float)):
+            scale = (float(scale), float(scale))
+        if mode == 'nearest' and size is None and scale == (2.0, 2.0):
+            chain, skip = [node], None
+            u = _only_user(node)
+            if u is not None and u.op == 'call_function' and u.target is torch.cat:
+                seq = u.args[0]
+                dim = u.kwargs.get('dim', u.args[1] if len(u.args) > 1 else 0)
+                if (dim == 1 and isinstance(seq, (list, tuple)) and len(seq) == 2 and seq[0] is node
+                        and isinstance(seq[1], fx.Node) and seq[1] is not node):
+                    skip = seq[1]
+                    chain.append(u)
+            new = self._site_node(chain[-1], UpCat(self.net.ctx), [x] + ([skip] if skip is not None else []))
+            self._replace(chain, new)
+        elif mode == 'bilinear' and align is True and (size is not None or scale is not None):
+            if size is not None:
+                new = self._site_node(node, BilinearUp(self.net.ctx), [x, size])
+            else:
+                new = self._site_node(node, BilinearUp(self.net.ctx, scale), [x])
+            self._replace([node], new)
+
     def avgpool(self, node):
         new = self._site_node(node, GlobalAvgPool(self.net.ctx), [node.args[0]])
         self._replace([node], new)
@@ -477,6 +511,8 @@ class _Lowering:
                                  kw.get('padding', args[3] if args[3] is not None else 0),
                                  kw.get('dilation', args[4] if args[4] is not None else 1),
                                  kw.get('ceil_mode', args[5] or False), kw.get('return_indices', args[6] or False))
+                elif t is F.interpolate:
+                    self.interpolate(node)
                 elif t is F.adaptive_avg_pool2d and _pair(node.args[1] if len(node.args) > 1
                                                           else node.kwargs['output_size'], 'output_size') == 1:
                     self.avgpool(node)

@@ -31,6 +31,7 @@ import torch
 import torch.nn as nn
 
 from . import functional as Fn
+from . import seg as Seg
 from .layers import NativeContext
 
 
@@ -822,6 +823,72 @@ class LinearAct(Site):
                 dx = dx[:, :p.I]
             dx = dx.reshape(*dout.shape[:-1], p.I)
         return [dx]
+
+
+class UpCat(Site):
+    """``F.interpolate(x, scale_factor=2, mode='nearest')`` [-> ``torch.cat([up, skip], 1)``]
+    as one NHWC pass (``seg.hip`` upcat: the U-Net decoder's input) and its backward (2x2
+    sum-pool of the upsampled channels, slice of the skip's).  Channel counts that are not
+    multiples of 8 take the same math in torch ops."""
+
+    def forward(self, x, skip=None):
+        return _run(self, x, skip) if skip is not None else _run(self, x)
+
+    def fwd(self, x, skip=None):
+        if x.dim() != 4:
+            raise ValueError(f'UpCat: a {x.dim()}-D input (the native upsample takes NCHW images)')
+        C1, C2 = x.shape[1], (skip.shape[1] if skip is not None else 0)
+        xn = to_nhwc(x)
+        sn = to_nhwc(skip) if skip is not None else None
+        if xn.is_cuda and (C1 % 8 or C2 % 8):
+            up = xn.repeat_interleave(2, 1).repeat_interleave(2, 2)
+            out = torch.cat([up, sn], 3) if sn is not None else up.contiguous()
+        else:
+            out = Seg.upcat_fwd(xn, sn)
+        return from_nhwc(out, C1 + C2), [], (C1, C2)
+
+    def bwd(self, dout, saved, keep, needs):
+        C1, C2 = keep
+        dn = to_nhwc(dout)
+        if dn.is_cuda and (C1 % 8 or C2 % 8):
+            N, H, W, _ = dn.shape
+            d = dn.float()
+            dlo = d[..., :C1].reshape(N, H // 2, 2, W // 2, 2, C1).sum((2, 4)).to(torch.bfloat16)
+            dskip = d[..., C1:].to(torch.bfloat16).contiguous() if C2 else None
+        else:
+            dlo, dskip = Seg.upcat_bwd(dn, C1)
+        out = [from_nhwc(dlo, C1) if needs[0] else None]
+        if C2:
+            out.append(from_nhwc(dskip, C2) if needs[1] else None)
+        return out
+
+
+class BilinearUp(Site):
+    """``F.interpolate(x, size | scale_factor, mode='bilinear', align_corners=True)`` on the
+    NHWC kernels (``seg.hip``; channels padded to 8)."""
+
+    def __init__(self, ctx, scale=None):
+        super().__init__(ctx)
+        self.scale = scale
+
+    def forward(self, x, size=None):
+        return _run(self, x, size) if size is not None else _run(self, x)
+
+    def fwd(self, x, size=None):
+        N, C, H, W = x.shape
+        if size is not None:
+            Ho, Wo = (int(size), int(size)) if isinstance(size, int) else (int(size[0]), int(size[1]))
+        else:
+            sh, sw = self.scale
+            Ho, Wo = int(H * sh), int(W * sw)
+        xn = to_nhwc(x, ceil8(C))
+        y = Seg.bilinear_up_fwd(xn, Ho, Wo)
+        return from_nhwc(y, C), [], (C, H, W)
+
+    def bwd(self, dout, saved, keep, needs):
+        C, H, W = keep
+        dx = Seg.bilinear_up_bwd(to_nhwc(dout, ceil8(C)), H, W)
+        return [from_nhwc(dx, C)] + ([None] if len(needs) > 1 else [])
 
 
 class MaxPool(Site):

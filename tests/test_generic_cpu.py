@@ -446,6 +446,52 @@ def test_transposed_conv_sites_match_fp32_autograd():
     assert torch.allclose(m.up2.weight, ref.up2.weight)
 
 
+class _UpcatNet(nn.Module):
+    """A two-level decoder: nearest x2 + concat with a skip (one with 5 / 3 channels, the
+    other with multiples of 8), a standalone nearest x2, bilinear (align_corners) by scale
+    and by a traced size."""
+
+    def __init__(self):
+        super().__init__()
+        self.enc = nn.Conv2d(3, 16, 3, 2, 1)
+        self.mid = nn.Conv2d(16, 5, 3, 2, 1)
+        self.dec1 = nn.Conv2d(5 + 16, 8, 3, 1, 1)
+        self.dec2 = nn.Conv2d(8 + 3, 8, 3, 1, 1)
+        self.head = nn.Conv2d(8, 8, 1)
+
+    def forward(self, x):
+        e = torch.relu(self.enc(x))                                       # 16 @ H/2
+        m = torch.relu(self.mid(e))                                       # 5 @ H/4
+        d = F.interpolate(m, scale_factor=2, mode='nearest')
+        d = torch.relu(self.dec1(torch.cat([d, e], 1)))                   # 8 @ H/2
+        d = torch.cat([F.interpolate(d, scale_factor=2, mode='nearest'), x], 1)
+        d = torch.relu(self.dec2(d))                                      # 8 @ H
+        h = self.head(F.interpolate(d, scale_factor=2, mode='nearest'))   # 8 @ 2H
+        h = F.interpolate(h, scale_factor=0.5, mode='bilinear', align_corners=True)
+        return F.interpolate(h, size=x.shape[-2:], mode='bilinear', align_corners=True)
+
+
+def test_upsample_concat_sites_match_fp32_autograd():
+    """nearest x2 [+ concat] lowers to UpCat and bilinear (align_corners) to BilinearUp;
+    forward and every gradient match the fp32 torch graph."""
+    m, ref = _pair(_UpcatNet)
+    net = GenericNet(m, 'cpu')
+    kinds = [type(s).__name__ for s in net.train_gm.modules()]
+    assert kinds.count('UpCat') == 3 and kinds.count('BilinearUp') == 2, kinds
+    assert not [n for n in net.train_gm.graph.nodes if n.op == 'call_function' and n.target is torch.cat]
+    x = torch.randn(2, 3, 16, 16)
+    xi, xr = x.clone().requires_grad_(), x.clone().requires_grad_()
+    out, want = net(xi), ref(xr)
+    assert out.shape == want.shape == (2, 8, 16, 16)
+    g = torch.randn_like(want)
+    (out.float() * g).sum().backward()
+    (want * g).sum().backward()
+    assert _rel(out, want) < 2e-2
+    assert _cos(xi.grad, xr.grad) > 0.98
+    for p in net.param_sets():
+        assert _cos(p.w.grad, _torch_grad(p, ref)) > 0.98, p.name
+
+
 def test_linknet_lowers_completely():
     from mlcomp_amd.contrib.segmentation.models import Linknet
     assert lower_or_none(Linknet(encoder_name='resnet34', classes=1)) is None
