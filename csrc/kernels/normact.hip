@@ -121,9 +121,10 @@ stats_kernel(const bf16* __restrict__ x, float* __restrict__ sum, float* __restr
   }
 }
 
-// The elementwise passes are instantiated for the identity and ReLU codes (ACT = 0 / 1: the
-// activation folds to straight-line code, so the loop keeps its loads in flight) and once for
-// any code read at run time (ACT = -1: the switch of act_f / act_df per element).
+// The elementwise passes are instantiated per activation code (ACT = 0..10: the activation
+// folds to straight-line code, so the loop keeps its loads in flight; a run-time code made
+// the switch of act_f / act_df a per-element branch, which cost EfficientNet's SiLU passes
+// 2-3x their memory time) and once for a code read at run time (ACT = -1).
 template <int ACT>
 __global__ void __launch_bounds__(NT)
 apply_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf16* __restrict__ z,
@@ -311,8 +312,10 @@ bwd_finalize_rows_kernel(const float* __restrict__ part, int nrow, const float* 
 }
 
 // y = act(x) and dx = dy * act'(x) for a torch-free activation between native ops
+template <int ACT>
 __global__ void __launch_bounds__(NT)
-act_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long n8, int act, float alpha) {
+act_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long n8, int act_, float alpha) {
+  const int act = ACT >= 0 ? ACT : act_;
   for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
     float f[8];
     unpack8(ldg16(x + i * 8), f);
@@ -322,9 +325,11 @@ act_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long n8, int ac
   }
 }
 
+template <int ACT>
 __global__ void __launch_bounds__(NT)
 act_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, const bf16* __restrict__ y,
-               bf16* __restrict__ dx, long n8, int act, float alpha) {
+               bf16* __restrict__ dx, long n8, int act_, float alpha) {
+  const int act = ACT >= 0 ? ACT : act_;
   for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
     float d[8], a[8], z[8];
     unpack8(ldg16(dy + i * 8), d);
@@ -333,6 +338,102 @@ act_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, const bf
 #pragma unroll
     for (int j = 0; j < 8; ++j) d[j] *= act_df(a[j], z[j], act, alpha);
     *reinterpret_cast<uint4*>(dx + i * 8) = pack8(d);
+  }
+}
+
+// channel gate (squeeze-excitation): out[n, p, c] = act(y[n, p, c] * g[n, c] [+ res[n, p, c]])
+// over NHWC y [N, HW, C] and g [N, C] (bf16); act: 0 none, 1 ReLU (SE-ResNeXt's block tail)
+__global__ void __launch_bounds__(NT)
+chscale_fwd_kernel(const bf16* __restrict__ y, const bf16* __restrict__ g, const bf16* __restrict__ res,
+                   bf16* __restrict__ out, long total, long plane, int G, int relu) {
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const long n = i / plane;
+    const int cg = (int)(i % G);
+    float f[8], s[8], r[8];
+    unpack8(ldg16(y + i * 8), f);
+    unpack8(ldg16(g + (n * G + cg) * 8), s);
+    if (res) unpack8(ldg16(res + i * 8), r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      f[e] *= s[e];
+      if (res) f[e] += r[e];
+      if (relu) f[e] = fmaxf(f[e], 0.f);
+    }
+    *reinterpret_cast<uint4*>(out + i * 8) = pack8(f);
+  }
+}
+
+// its backward in one pass: dy = dout * g, dg[n, c] += sum_p dout * y (fp32, zeroed by the
+// caller).  Block (x, n, t) covers CS_ROWS pixel rows of image n and a tile of CT <= 64
+// channel groups (16-byte chunks); thread t keeps ONE channel group (t % CT) and walks rows
+// t / CT, + R, ... (R = 256 / CT rows per sweep), so its sums stay in registers; the R row
+// partials are combined through LDS in a fixed order and leave the block as one float atomic
+// per channel.
+constexpr int CS_ROWS = 128;
+__global__ void __launch_bounds__(NT)
+chscale_bwd_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ y, const bf16* __restrict__ g,
+                   const bf16* __restrict__ z, bf16* __restrict__ dy, bf16* __restrict__ dres, float* __restrict__ dg,
+                   int HW, int G) {
+  __shared__ float part[NT * 8];
+  const int n = blockIdx.y;
+  const int CT = G < 64 ? G : 64, R = NT / CT;
+  const int ct0 = blockIdx.z * CT;
+  const int t = threadIdx.x, cgl = t % CT, rs = t / CT;
+  const int cg = ct0 + cgl;
+  const bool act = rs < R && cg < G;
+  const int r0 = blockIdx.x * CS_ROWS, r1 = min(HW, r0 + CS_ROWS);
+  float a[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = 0.f;
+  if (act) {
+    float s[8];
+    unpack8(ldg16(g + ((long)n * G + cg) * 8), s);
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+    constexpr int U = 2;
+    for (int rb = r0 + rs; rb < r1; rb += R * U) {
+      uint4 dv[U], yv[U], zv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = min(rb + u * R, r1 - 1);      // clamped: always a valid row
+        const long i = ((long)n * HW + r) * G + cg;
+        dv[u] = ldg16(dout + i * 8);
+        yv[u] = ldg16(y + i * 8);
+        zv[u] = z ? ldg16(z + i * 8) : zero;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = rb + u * R;
+        if (r >= r1) break;
+        const long i = ((long)n * HW + r) * G + cg;
+        float d[8], f[8];
+        unpack8(dv[u], d);
+        unpack8(yv[u], f);
+        if (z) {
+          float m[8];
+          unpack8(zv[u], m);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
+        }
+        if (dres) *reinterpret_cast<uint4*>(dres + i * 8) = pack8(d);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          a[e] += d[e] * f[e];
+          d[e] *= s[e];
+        }
+        *reinterpret_cast<uint4*>(dy + i * 8) = pack8(d);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[t * 8 + e] = a[e];
+  __syncthreads();
+  // channel c of the tile: the R row partials of its group, in row order
+  for (int c = t; c < CT * 8; c += NT) {
+    const int gl = c >> 3, e = c & 7;
+    if (ct0 + gl >= G) continue;
+    float acc = 0.f;
+    for (int q = 0; q < R; ++q) acc += part[(q * CT + gl) * 8 + e];
+    atomicAdd(dg + ((long)n * G + ct0 + gl) * 8 + e, acc);
   }
 }
 
@@ -353,11 +454,19 @@ inline int grid_for(long rows, int C, int cap = 1024) {
 }
 
 // launch an ACT-templated pass with the specialisation of the run-time code `act`
+#define NA_CASE(K, A, grid, st, ...) \
+  case A: hipLaunchKernelGGL(K<A>, dim3(grid), dim3(NT), 0, st, __VA_ARGS__); break;
 #define NA_LAUNCH(K, grid, st, act, ...)                                                              \
   do {                                                                                              \
-    if ((act) == 0) hipLaunchKernelGGL(K<0>, dim3(grid), dim3(NT), 0, st, __VA_ARGS__);             \
-    else if ((act) == 1) hipLaunchKernelGGL(K<1>, dim3(grid), dim3(NT), 0, st, __VA_ARGS__);        \
-    else hipLaunchKernelGGL(K<-1>, dim3(grid), dim3(NT), 0, st, __VA_ARGS__);                       \
+    switch (act) {                                                                                  \
+      NA_CASE(K, 0, grid, st, __VA_ARGS__) NA_CASE(K, 1, grid, st, __VA_ARGS__)                     \
+      NA_CASE(K, 2, grid, st, __VA_ARGS__) NA_CASE(K, 3, grid, st, __VA_ARGS__)                     \
+      NA_CASE(K, 4, grid, st, __VA_ARGS__) NA_CASE(K, 5, grid, st, __VA_ARGS__)                     \
+      NA_CASE(K, 6, grid, st, __VA_ARGS__) NA_CASE(K, 7, grid, st, __VA_ARGS__)                     \
+      NA_CASE(K, 8, grid, st, __VA_ARGS__) NA_CASE(K, 9, grid, st, __VA_ARGS__)                     \
+      NA_CASE(K, 10, grid, st, __VA_ARGS__)                                                         \
+      default: hipLaunchKernelGGL(K<-1>, dim3(grid), dim3(NT), 0, st, __VA_ARGS__);                 \
+    }                                                                                               \
   } while (0)
 
 // block cap of the reducing passes: every block ends in C*2 float atomics onto one of 32
@@ -447,13 +556,32 @@ MLC_EXPORT int mlc_bnact_bwd_apply(const bf16* dz, const bf16* z, const bf16* y,
 
 MLC_EXPORT int mlc_act_fwd(const bf16* x, bf16* y, long n, int act, float alpha, hipStream_t st) {
   if (n % 8) return -1;
-  hipLaunchKernelGGL(act_fwd_kernel, dim3(blocks_for(n / 8)), dim3(NT), 0, st, x, y, n / 8, act, alpha);
+  NA_LAUNCH(act_fwd_kernel, blocks_for(n / 8), st, act, x, y, n / 8, act, alpha);
+  return hipGetLastError();
+}
+
+MLC_EXPORT int mlc_chscale_fwd(const bf16* y, const bf16* g, const bf16* res, bf16* out, int N, long HW, int C,
+                               int relu, hipStream_t st) {
+  if (C % 8) return -1;
+  const long total = (long)N * HW * (C / 8);
+  hipLaunchKernelGGL(chscale_fwd_kernel, dim3(blocks_for(total)), dim3(NT), 0, st, y, g, res, out, total,
+                     HW * (C / 8), C / 8, relu);
+  return hipGetLastError();
+}
+
+// dg: N*C fp32, zeroed by the caller; z / dres optional (ReLU mask, residual gradient)
+MLC_EXPORT int mlc_chscale_bwd(const bf16* dout, const bf16* y, const bf16* g, const bf16* z, bf16* dy, bf16* dres,
+                               float* dg, int N, int HW, int C, hipStream_t st) {
+  if (C % 8 || N > 65535) return -1;
+  const int G = C / 8, CT = G < 64 ? G : 64;
+  hipLaunchKernelGGL(chscale_bwd_kernel, dim3((HW + CS_ROWS - 1) / CS_ROWS, N, (G + CT - 1) / CT), dim3(NT), 0, st,
+                     dout, y, g, z, dy, dres, dg, HW, G);
   return hipGetLastError();
 }
 
 MLC_EXPORT int mlc_act_bwd(const bf16* dy, const bf16* x, const bf16* y, bf16* dx, long n, int act, float alpha,
                            hipStream_t st) {
   if (n % 8) return -1;
-  hipLaunchKernelGGL(act_bwd_kernel, dim3(blocks_for(n / 8)), dim3(NT), 0, st, dy, x, y, dx, n / 8, act, alpha);
+  NA_LAUNCH(act_bwd_kernel, blocks_for(n / 8), st, act, dy, x, y, dx, n / 8, act, alpha);
   return hipGetLastError();
 }

@@ -44,8 +44,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from mlcomp_amd.ops import functional as Fn
-from mlcomp_amd.ops.glayers import (BilinearUp, BNAct, BNParams, Conv3dAs2d, ConvBNAct, ConvParams, Frames,
-                                    GlobalAvgPool, LinearAct, LinearParams, MaxPool, UpCat)
+from mlcomp_amd.ops.glayers import (BilinearUp, BNAct, BNParams, ChannelGate, Conv3dAs2d, ConvBNAct, ConvParams,
+                                    Frames, GlobalAvgPool, LinearAct, LinearParams, MaxPool, UpCat)
 from mlcomp_amd.ops.layers import NativeContext
 from mlcomp_amd.train.native_spec import NativeUnsupported
 
@@ -358,6 +358,48 @@ class _Lowering:
                 new = self._site_node(node, BilinearUp(self.net.ctx, scale), [x])
             self._replace([node], new)
 
+    def _gate_source(self, g: fx.Node, depth: int = 8):
+        """The value whose global average a gate ``g`` is computed from (walking back through
+        single-input sites and activations to a GlobalAvgPool site), or None."""
+        for _ in range(depth):
+            if not isinstance(g, fx.Node):
+                return None
+            if g.op == 'call_module':
+                m = getattr(self.gm, g.target, None)
+                if isinstance(m, GlobalAvgPool):
+                    return g.args[0]
+                if not (isinstance(m, (ConvBNAct, LinearAct, BNAct)) or _act_of(g, self.modules) is not None):
+                    return None
+                if len(g.args) != 1:
+                    return None
+            elif not (g.op in ('call_function', 'call_method') and _act_of(g, self.modules) is not None):
+                return None
+            g = g.args[0]
+        return None
+
+    def gate(self, node):
+        """``y * g`` where g is computed from y's global average (squeeze-excitation) ->
+        ChannelGate."""
+        if len(node.args) != 2 or node.kwargs:
+            return
+        a, b = node.args
+        if not (isinstance(a, fx.Node) and isinstance(b, fx.Node)) or a is b:
+            return
+        if self._gate_source(b) is a:
+            y, g = a, b
+        elif self._gate_source(a) is b:
+            y, g = b, a
+        else:
+            return
+        # SE-ResNeXt's block tail: (y * g) + residual -> ReLU in the same pass
+        chain = [node]
+        res, act, alpha = self._tail(node, chain)
+        if act not in (0, A['relu']):       # another activation: gate only, the rest stays torch
+            chain, res, act = [node], None, 0
+        site = ChannelGate(self.net.ctx, relu=act == A['relu'], residual=res is not None)
+        new = self._site_node(chain[-1], site, [y, g] + ([res] if res is not None else []))
+        self._replace(chain, new)
+
     def avgpool(self, node):
         new = self._site_node(node, GlobalAvgPool(self.net.ctx), [node.args[0]])
         self._replace([node], new)
@@ -513,6 +555,8 @@ class _Lowering:
                                  kw.get('ceil_mode', args[5] or False), kw.get('return_indices', args[6] or False))
                 elif t is F.interpolate:
                     self.interpolate(node)
+                elif t in (operator.mul, torch.mul):
+                    self.gate(node)
                 elif t is F.adaptive_avg_pool2d and _pair(node.args[1] if len(node.args) > 1
                                                           else node.kwargs['output_size'], 'output_size') == 1:
                     self.avgpool(node)
@@ -524,6 +568,8 @@ class _Lowering:
             elif node.op == 'call_method':
                 if node.target == 'view':
                     node.target = 'reshape'     # site outputs are channels_last views
+                elif node.target == 'mul':
+                    self.gate(node)
                 elif node.target in ('matmul', 'mm', 'bmm'):
                     raise NativeUnsupported(f'{node.name}: Tensor.{node.target} has no native lowering')
         self._fold_shortcut_bns()

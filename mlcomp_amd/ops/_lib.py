@@ -115,6 +115,8 @@ _SIGS = {
     'mlc_bnact_bwd_apply': [vp] * 12 + [i64, i32, i32, f32, vp],
     'mlc_act_fwd': [vp, vp, i64, i32, f32, vp],
     'mlc_act_bwd': [vp] * 4 + [i64, i32, f32, vp],
+    'mlc_chscale_fwd': [vp] * 4 + [i32, i64, i32, i32, vp],
+    'mlc_chscale_bwd': [vp] * 7 + [i32] * 3 + [vp],
     'mlc_conv_fwd_ex': [vp] * 4 + [i32] * 13 + [vp],
     'mlc_conv_wgrad_bias': [vp] * 4 + [i32] * 13 + [vp, i64, vp],
     'mlc_comm_unique_id_bytes': [],

@@ -1193,6 +1193,44 @@ def act_fwd(x, act, alpha=0.0):
     return act_ref(x.float(), act, alpha).to(torch.bfloat16)
 
 
+def chscale_fwd(y, g, res=None, relu=False):
+    """Channel gate (squeeze-excitation): act(y * g [+ res]) with y [N, H, W, C] NHWC bf16, g
+    [N, C] per image and channel, an optional residual of y's shape and an optional ReLU."""
+    N, H, W, C = y.shape
+    if _cuda(y) and C % 8 == 0:
+        out = torch.empty_like(y)
+        _lib.call('mlc_chscale_fwd', _lib.ptr(y), _lib.ptr(g.contiguous()), _lib.ptr(res), _lib.ptr(out), N, H * W, C,
+                  int(relu), _lib.stream())
+        return out
+    a = y.float() * g.float().view(N, 1, 1, C)
+    if res is not None:
+        a = a + res.float()
+    if relu:
+        a = a.clamp_min(0)
+    return a.to(torch.bfloat16)
+
+
+def chscale_bwd(dout, y, g, z=None, want_dres=False):
+    """(dy, dg, dres) of :func:`chscale_fwd`: the ReLU mask from its output ``z`` (if it had a
+    ReLU), dres = the masked gradient (if it had a residual), dy = that * g, dg [N, C] (fp32)
+    = its sum over pixels times y - one pass (float atomics per channel; deterministic mode
+    sums in torch)."""
+    N, H, W, C = y.shape
+    if _cuda(y) and C % 8 == 0 and not _lib.DETERMINISTIC:
+        dy = torch.empty_like(y)
+        dres = torch.empty_like(y) if want_dres else None
+        dg = torch.zeros(N, C, device=y.device, dtype=torch.float32)
+        _lib.call('mlc_chscale_bwd', _lib.ptr(dout.contiguous()), _lib.ptr(y), _lib.ptr(g.contiguous()), _lib.ptr(z),
+                  _lib.ptr(dy), _lib.ptr(dres), _lib.ptr(dg), N, H * W, C, _lib.stream())
+        return dy, dg, dres
+    d = dout.float()
+    if z is not None:
+        d = d * (z.float() > 0)
+    dres = d.to(torch.bfloat16) if want_dres else None
+    dy = (d * g.float().view(N, 1, 1, C)).to(torch.bfloat16)
+    return dy, (d * y.float()).sum((1, 2)), dres
+
+
 def act_bwd(dy, x, y, act, alpha=0.0):
     if _cuda(dy) and dy.numel() % 8 == 0:
         dx = torch.empty_like(dy)

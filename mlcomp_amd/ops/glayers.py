@@ -863,6 +863,47 @@ class UpCat(Site):
         return out
 
 
+class ChannelGate(Site):
+    """``act(y * g [+ res])`` with g = [N, C, 1, 1] a gate computed from y's global average
+    (squeeze-excitation: EfficientNet's MBConv; SE-ResNeXt's block tail with its residual add
+    and ReLU): one NHWC pass forward, one backward (ReLU mask, the residual's gradient,
+    dy = d * g and dg = sum over pixels of d * y together)."""
+
+    def __init__(self, ctx, relu: bool = False, residual: bool = False):
+        super().__init__(ctx)
+        self.relu, self.residual = relu, residual
+
+    def forward(self, y, g, res=None):
+        return _run(self, y, g, res) if res is not None else _run(self, y, g)
+
+    def fwd(self, y, g, res=None):
+        N, C = y.shape[:2]
+        if y.dim() != 4 or tuple(g.shape) != (N, C, 1, 1):
+            raise ValueError(f'ChannelGate: {tuple(y.shape)} * {tuple(g.shape)} is not an image times a '
+                             'per-channel gate')
+        Cp = ceil8(C)
+        yn = to_nhwc(y, Cp)
+        rn = to_nhwc(res, Cp) if res is not None else None
+        gn = g.reshape(N, C).to(torch.bfloat16)
+        if Cp != C:
+            gn = torch.nn.functional.pad(gn, (0, Cp - C))
+        gn = gn.contiguous()
+        z = Fn.chscale_fwd(yn, gn, rn, self.relu)
+        return from_nhwc(z, C), [yn, gn, z if self.relu else gn], (C, g.dtype, rn is not None)
+
+    def bwd(self, dout, saved, keep, needs):
+        yn, gn, z = saved
+        C, gdt, has_res = keep
+        dy, dg, dres = Fn.chscale_bwd(to_nhwc(dout, yn.shape[-1]), yn, gn, z if self.relu else None,
+                                      want_dres=has_res and needs[2])
+        N = yn.shape[0]
+        out = [from_nhwc(dy, C) if needs[0] else None,
+               dg[:, :C].to(gdt).reshape(N, C, 1, 1) if needs[1] else None]
+        if has_res:
+            out.append(from_nhwc(dres, C) if needs[2] else None)
+        return out
+
+
 class BilinearUp(Site):
     """``F.interpolate(x, size | scale_factor, mode='bilinear', align_corners=True)`` on the
     NHWC kernels (``seg.hip``; channels padded to 8)."""

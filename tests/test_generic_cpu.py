@@ -492,6 +492,46 @@ def test_upsample_concat_sites_match_fp32_autograd():
         assert _cos(p.w.grad, _torch_grad(p, ref)) > 0.98, p.name
 
 
+class _SENet(nn.Module):
+    """Squeeze-excitation twice: EfficientNet's form (the gate multiplies its source) with 20
+    channels (not a multiple of 8) and SE-ResNeXt's form (gate first) with 32."""
+
+    def __init__(self):
+        super().__init__()
+        self.c1 = nn.Conv2d(3, 20, 3, 1, 1)
+        self.se1 = nn.Sequential(nn.AdaptiveAvgPool2d(1), nn.Conv2d(20, 5, 1), nn.SiLU(), nn.Conv2d(5, 20, 1),
+                                 nn.Sigmoid())
+        self.c2 = nn.Conv2d(20, 32, 3, 2, 1)
+        self.fc1, self.fc2 = nn.Conv2d(32, 8, 1), nn.Conv2d(8, 32, 1)
+        self.head = nn.Linear(32, 6)
+
+    def forward(self, x):
+        y = F.silu(self.c1(x))
+        y = y * self.se1(y)
+        z = torch.relu(self.c2(y))
+        g = torch.sigmoid(self.fc2(torch.relu(self.fc1(F.adaptive_avg_pool2d(z, 1)))))
+        z = g * z
+        return self.head(F.adaptive_avg_pool2d(z, 1).flatten(1))
+
+
+def test_squeeze_excitation_gates_match_fp32_autograd():
+    m, ref = _pair(_SENet)
+    net = GenericNet(m, 'cpu')
+    kinds = [type(s).__name__ for s in net.train_gm.modules()]
+    assert kinds.count('ChannelGate') == 2, kinds
+    x = torch.randn(4, 3, 12, 12)
+    xi, xr = x.clone().requires_grad_(), x.clone().requires_grad_()
+    out, want = net(xi), ref(xr)
+    g = torch.randn_like(want)
+    (out.float() * g).sum().backward()
+    (want * g).sum().backward()
+    assert _rel(out, want) < 2e-2
+    assert _cos(xi.grad, xr.grad) > 0.98
+    for p in net.param_sets():
+        gg = p.w.grad if hasattr(p, 'w') else p.gamma.grad
+        assert _cos(gg, _torch_grad(p, ref)) > 0.98, p.name
+
+
 def test_linknet_lowers_completely():
     from mlcomp_amd.contrib.segmentation.models import Linknet
     assert lower_or_none(Linknet(encoder_name='resnet34', classes=1)) is None
