@@ -482,6 +482,17 @@ inline int reduce_cap() {
   return v;
 }
 
+// block cap of the streaming (apply) passes (A/B knob MLC_NORMACT_APPLY_CAP)
+inline int apply_cap() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MLC_NORMACT_APPLY_CAP");
+    v = e ? atoi(e) : 768;
+    if (v < 32) v = 32;
+  }
+  return v;
+}
+
 inline int blocks_for(long work) {
   long b = (work + NT - 1) / NT;
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
@@ -502,7 +513,7 @@ MLC_EXPORT int mlc_bnact_apply(const bf16* y, const bf16* res, bf16* z, const fl
                                const float* rscale, const float* rshift, long rows, int C, int act, float alpha,
                                hipStream_t st) {
   if (C % 8 || (rscale && !rshift)) return -1;
-  NA_LAUNCH(apply_kernel, grid_for(rows, C, 768), st, act, y, res, z, scale, shift, rscale, rshift, rows, C, act,
+  NA_LAUNCH(apply_kernel, grid_for(rows, C, apply_cap()), st, act, y, res, z, scale, shift, rscale, rshift, rows, C, act,
             alpha);
   return hipGetLastError();
 }
@@ -539,7 +550,7 @@ MLC_EXPORT int mlc_bnact_bwd(const bf16* dz, const bf16* z, const bf16* y, const
             alpha, 1);
   hipLaunchKernelGGL(bwd_finalize_rows_kernel, dim3((C + NT / 64 - 1) / (NT / 64)), dim3(NT), 0, st, part, blocks,
                      invstd, gamma, coef, dgamma, dbeta, rows, C);
-  NA_LAUNCH(bwd_apply_kernel, grid_for(rows, C, 768), st, act, dz, z, y, res, mean, coef, scale, shift, rscale, rshift,
+  NA_LAUNCH(bwd_apply_kernel, grid_for(rows, C, apply_cap()), st, act, dz, z, y, res, mean, coef, scale, shift, rscale, rshift,
             dy, dres, rows, C, act, alpha);
   return hipGetLastError();
 }
@@ -549,7 +560,7 @@ MLC_EXPORT int mlc_bnact_bwd_apply(const bf16* dz, const bf16* z, const bf16* y,
                                    const float* rshift, bf16* dy, bf16* dres, long rows, int C, int act, float alpha,
                                    hipStream_t st) {
   if (C % 8) return -1;
-  NA_LAUNCH(bwd_apply_kernel, grid_for(rows, C, 768), st, act, dz, z, y, res, mean, coef, scale, shift, rscale, rshift,
+  NA_LAUNCH(bwd_apply_kernel, grid_for(rows, C, apply_cap()), st, act, dz, z, y, res, mean, coef, scale, shift, rscale, rshift,
             dy, dres, rows, C, act, alpha);
   return hipGetLastError();
 }

@@ -1141,7 +1141,7 @@ def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0
         zz = z if act in (4, 5) else None        # sigmoid / tanh read their derivative off z
         if C <= 2048:          # (fixed summation order: deterministic as well)
             # one call: reduce to per-block partial rows (no float atomics), finalize, apply
-            part = slab_workspace(dz.device, 512 * 2 * C)
+            part = slab_workspace(dz.device, 2048 * 2 * C)    # the kernel caps the blocks (MLC_NORMACT_CAP)
             dy = torch.empty_like(y)
             dres = torch.empty_like(y) if want_dres else None
             _lib.call('mlc_bnact_bwd', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
