@@ -62,6 +62,13 @@ __device__ __forceinline__ float act_df(float a, float z, int act, float alpha) 
 struct Ch {
   float sc[8], sh[8], rs[8], rh[8];
 };
+// per-sample factor of the BN output (stochastic depth: the drop-path mask / keep of a block,
+// folded into its last BN's passes), s[n] for rows n*hw .. (n+1)*hw - 1; identity only (act 0)
+struct RowScale {
+  const float* s;
+  long hw;
+};
+
 __device__ __forceinline__ void load_ch(Ch& c, const float* scale, const float* shift, const float* rscale,
                                         const float* rshift, int c0) {
 #pragma unroll
@@ -129,7 +136,7 @@ template <int ACT>
 __global__ void __launch_bounds__(NT)
 apply_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf16* __restrict__ z,
              const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ rscale,
-             const float* __restrict__ rshift, long rows, int C, int act_, float alpha) {
+             const float* __restrict__ rshift, long rows, int C, int act_, float alpha, RowScale rsc) {
   const int act = ACT >= 0 ? ACT : act_;
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
@@ -143,6 +150,11 @@ apply_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf16* __r
     unpack8(ldg16(y + i * 8), f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = f[j] * c.sc[j] + c.sh[j];
+    if (rsc.s) {
+      const float m = rsc.s[(i / G) / rsc.hw];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= m;
+    }
     if (res) {
       float r[8];
       unpack8(ldg16(res + i * 8), r);
@@ -181,7 +193,7 @@ __global__ void __launch_bounds__(NT)
 bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const bf16* __restrict__ y,
                   const bf16* __restrict__ res, const float* __restrict__ mean, const float* __restrict__ scale,
                   const float* __restrict__ shift, const float* __restrict__ rscale, const float* __restrict__ rshift,
-                  float* __restrict__ sums, long rows, int C, int act, float alpha, int direct) {
+                  float* __restrict__ sums, long rows, int C, int act, float alpha, int direct, RowScale rsc) {
   __shared__ float rb[NT][17];
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
@@ -209,6 +221,11 @@ bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const
       unpack8(dv[k], d);
       unpack8(yv[k], yy);
       dU8<ACT>(d, zv[k], yv[k], rv[k], res != nullptr, c, act, alpha);
+      if (rsc.s) {
+        const float m = rsc.s[((k ? i1 : i0) / G) / rsc.hw];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] *= m;
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) { s1[j] += d[j]; s2[j] += d[j] * (yy[j] - mu[j]); }
     }
@@ -252,7 +269,7 @@ bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const 
                  const bf16* __restrict__ res, const float* __restrict__ mean, const float* __restrict__ coef,
                  const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ rscale,
                  const float* __restrict__ rshift, bf16* __restrict__ dy, bf16* __restrict__ dres, long rows, int C,
-                 int act, float alpha) {
+                 int act, float alpha, RowScale rsc) {
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
   const long stride = (long)gridDim.x * NT;
@@ -277,6 +294,11 @@ bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const 
     unpack8(yv, yy);
     dU8<ACT>(d, zv, yv, rv, res != nullptr, c, act, alpha);
     if (dres) *reinterpret_cast<uint4*>(dres + i * 8) = pack8(d);
+    if (rsc.s) {
+      const float m = rsc.s[(i / G) / rsc.hw];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] *= m;
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = k1[j] * d[j] + k2[j] + k3[j] * (yy[j] - mu[j]);
     *reinterpret_cast<uint4*>(dy + i * 8) = pack8(o);
@@ -511,20 +533,23 @@ MLC_EXPORT int mlc_bn_stats(const bf16* x, float* sum, float* sumsq, long rows, 
 
 MLC_EXPORT int mlc_bnact_apply(const bf16* y, const bf16* res, bf16* z, const float* scale, const float* shift,
                                const float* rscale, const float* rshift, long rows, int C, int act, float alpha,
-                               hipStream_t st) {
-  if (C % 8 || (rscale && !rshift)) return -1;
+                               const float* row_scale, long hw, hipStream_t st) {
+  if (C % 8 || (rscale && !rshift) || (row_scale && (act != 0 || hw < 1))) return -1;
+  const RowScale rsc{row_scale, hw};
   NA_LAUNCH(apply_kernel, grid_for(rows, C, apply_cap()), st, act, y, res, z, scale, shift, rscale, rshift, rows, C, act,
-            alpha);
+            alpha, rsc);
   return hipGetLastError();
 }
 
 // sums: 32*2*C fp32, zeroed by the caller
 MLC_EXPORT int mlc_bnact_bwd_reduce(const bf16* dz, const bf16* z, const bf16* y, const bf16* res, const float* mean,
                                     const float* scale, const float* shift, const float* rscale, const float* rshift,
-                                    float* sums, long rows, int C, int act, float alpha, hipStream_t st) {
-  if (C % 8) return -1;
+                                    float* sums, long rows, int C, int act, float alpha, const float* row_scale, long hw,
+                                    hipStream_t st) {
+  if (C % 8 || (row_scale && (act != 0 || hw < 1))) return -1;
+  const RowScale rsc{row_scale, hw};
   NA_LAUNCH(bwd_reduce_kernel, grid_for(rows, C, reduce_cap()), st, act, dz, z, y, res, mean, scale, shift, rscale,
-            rshift, sums, rows, C, act, alpha, 0);
+            rshift, sums, rows, C, act, alpha, 0, rsc);
   return hipGetLastError();
 }
 
@@ -538,7 +563,10 @@ MLC_EXPORT int mlc_bnact_bwd(const bf16* dz, const bf16* z, const bf16* y, const
                              const float* scale, const float* shift, const float* rscale, const float* rshift,
                              const float* invstd, const float* gamma,
                              float* part, long part_floats, float* coef, float* dgamma, float* dbeta, bf16* dy,
-                             bf16* dres, long rows, int C, int act, float alpha, hipStream_t st) {
+                             bf16* dres, long rows, int C, int act, float alpha, const float* row_scale, long hw,
+                             hipStream_t st) {
+  if (row_scale && (act != 0 || hw < 1)) return -1;
+  const RowScale rsc{row_scale, hw};
   const int G = C >> 3;
   if (C % 8 || G > NT || part_floats < 2L * C || (rscale && !rshift)) return -1;
   long cap = part_floats / (2L * C);
@@ -547,21 +575,22 @@ MLC_EXPORT int mlc_bnact_bwd(const bf16* dz, const bf16* z, const bf16* y, const
   while (blocks > cap && blocks > 1) blocks = grid_for(rows, C, blocks / 2);   // rounding to C/8 multiples
   if ((long)blocks * 2 * C > part_floats) return -1;
   NA_LAUNCH(bwd_reduce_kernel, blocks, st, act, dz, z, y, res, mean, scale, shift, rscale, rshift, part, rows, C, act,
-            alpha, 1);
+            alpha, 1, rsc);
   hipLaunchKernelGGL(bwd_finalize_rows_kernel, dim3((C + NT / 64 - 1) / (NT / 64)), dim3(NT), 0, st, part, blocks,
                      invstd, gamma, coef, dgamma, dbeta, rows, C);
   NA_LAUNCH(bwd_apply_kernel, grid_for(rows, C, apply_cap()), st, act, dz, z, y, res, mean, coef, scale, shift, rscale, rshift,
-            dy, dres, rows, C, act, alpha);
+            dy, dres, rows, C, act, alpha, rsc);
   return hipGetLastError();
 }
 
 MLC_EXPORT int mlc_bnact_bwd_apply(const bf16* dz, const bf16* z, const bf16* y, const bf16* res, const float* mean,
                                    const float* coef, const float* scale, const float* shift, const float* rscale,
                                    const float* rshift, bf16* dy, bf16* dres, long rows, int C, int act, float alpha,
-                                   hipStream_t st) {
-  if (C % 8) return -1;
+                                   const float* row_scale, long hw, hipStream_t st) {
+  if (C % 8 || (row_scale && (act != 0 || hw < 1))) return -1;
+  const RowScale rsc{row_scale, hw};
   NA_LAUNCH(bwd_apply_kernel, grid_for(rows, C, apply_cap()), st, act, dz, z, y, res, mean, coef, scale, shift, rscale, rshift,
-            dy, dres, rows, C, act, alpha);
+            dy, dres, rows, C, act, alpha, rsc);
   return hipGetLastError();
 }
 

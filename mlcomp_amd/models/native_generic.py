@@ -428,6 +428,51 @@ class _Lowering:
                 continue
             object.__setattr__(s3, 'res_link', s1)
 
+    def _fuse_drop_path(self):
+        """Stochastic depth before a residual add - ``add(truediv(mul(s, mask), keep), x)`` with
+        s a conv+BN site (no activation, no residual) and mask = rand_like(s[:, :1, :1, :1]) < keep
+        (EfficientNet's MBConv in training): the site takes x as its residual and the mask as a
+        third input and applies mask / keep to its BN output in the same pass.  The mask's
+        shape source is re-pointed at the site's input (same batch), so it no longer depends
+        on the site."""
+        mods = dict(self.gm.named_modules())
+        adds = {operator.add, torch.add}
+        for n in list(self.gm.graph.nodes):
+            if n.op != 'call_function' or n.target not in adds or len(n.args) != 2 or n.kwargs:
+                continue
+            for t, x in (n.args, n.args[::-1]):
+                if not (isinstance(t, fx.Node) and isinstance(x, fx.Node) and t.op == 'call_function'
+                        and t.target is operator.truediv and len(t.args) == 2 and isinstance(t.args[1], float)
+                        and len(t.users) == 1):
+                    continue
+                m, keep = t.args
+                if not (isinstance(m, fx.Node) and m.op == 'call_function' and m.target in (operator.mul, torch.mul)
+                        and len(m.args) == 2 and len(m.users) == 1):
+                    continue
+                s_node, mask = m.args
+                site = mods.get(s_node.target) if isinstance(s_node, fx.Node) and s_node.op == 'call_module' else None
+                if not (isinstance(site, ConvBNAct) and site.bn is not None and site.act == 0 and not site.residual
+                        and len(s_node.args) == 1 and isinstance(mask, fx.Node) and mask.op == 'call_function'
+                        and mask.target is operator.lt):
+                    continue
+                rl = mask.args[0]
+                gi = rl.args[0] if isinstance(rl, fx.Node) and rl.op == 'call_function' and rl.args else None
+                while (isinstance(gi, fx.Node) and gi.op == 'call_method' and gi.target in ('float', 'to', 'double')
+                       and len(gi.users) == 1):           # dtype casts of the shape source
+                    gi = gi.args[0]
+                if not (isinstance(gi, fx.Node) and gi.op == 'call_function' and gi.target is operator.getitem
+                        and gi.args[0] is s_node and set(s_node.users) == {m, gi} and len(gi.users) == 1):
+                    continue
+                gi.args = (s_node.args[0],) + tuple(gi.args[1:])
+                s_node.args = (s_node.args[0], x, mask)
+                mask.append(s_node)              # after the mask (and x, which precedes the block)
+                n.replace_all_uses_with(s_node)
+                for dead in (n, t, m):
+                    self.gm.graph.erase_node(dead)
+                object.__setattr__(site, 'residual', True)
+                object.__setattr__(site, 'drop_keep', float(keep))
+                break
+
     def _fold_shortcut_bns(self):
         """A conv+BN site D without activation or residual whose output is only the residual
         input of a conv+BN site S (a bottleneck's downsample shortcut): S applies D's BN as
@@ -489,7 +534,7 @@ class _Lowering:
             a = n.args[0]
             sa = mods.get(a.target) if isinstance(a, fx.Node) and a.op == 'call_module' else None
             if (not isinstance(sa, ConvBNAct) or sa is sb or sa.bn is None or sa.act not in (0, relu)
-                    or sa.conv.Cop != sb.conv.Cip or sa.pool3):
+                    or sa.conv.Cop != sb.conv.Cip or sa.pool3 or sa.drop_keep is not None):
                 continue
             others = [u for u in a.users if u is not n]
             # the only other user may be a site whose residual gradient (an identity-residual
@@ -572,6 +617,7 @@ class _Lowering:
                     self.gate(node)
                 elif node.target in ('matmul', 'mm', 'bmm'):
                     raise NativeUnsupported(f'{node.name}: Tensor.{node.target} has no native lowering')
+        self._fuse_drop_path()
         self._fold_shortcut_bns()
         self._link_residuals()
         self._link_dgrads()

@@ -109,10 +109,10 @@ _SIGS = {
     'mlc_dwconv_dgrad': [vp] * 3 + [i32] * 11 + [vp],
     'mlc_dwconv_wgrad': [vp] * 4 + [i32] * 12 + [vp],
     'mlc_bn_stats': [vp, vp, vp, i64, i32, vp],
-    'mlc_bnact_apply': [vp] * 7 + [i64, i32, i32, f32, vp],
-    'mlc_bnact_bwd_reduce': [vp] * 10 + [i64, i32, i32, f32, vp],
-    'mlc_bnact_bwd': [vp] * 12 + [i64] + [vp] * 5 + [i64, i32, i32, f32, vp],
-    'mlc_bnact_bwd_apply': [vp] * 12 + [i64, i32, i32, f32, vp],
+    'mlc_bnact_apply': [vp] * 7 + [i64, i32, i32, f32, vp, i64, vp],
+    'mlc_bnact_bwd_reduce': [vp] * 10 + [i64, i32, i32, f32, vp, i64, vp],
+    'mlc_bnact_bwd': [vp] * 12 + [i64] + [vp] * 5 + [i64, i32, i32, f32, vp, i64, vp],
+    'mlc_bnact_bwd_apply': [vp] * 12 + [i64, i32, i32, f32, vp, i64, vp],
     'mlc_act_fwd': [vp, vp, i64, i32, f32, vp],
     'mlc_act_bwd': [vp] * 4 + [i64, i32, f32, vp],
     'mlc_chscale_fwd': [vp] * 4 + [i32, i64, i32, i32, vp],

@@ -1107,17 +1107,22 @@ def bn_finalize(s1, s2, rows, gamma, beta, save_mean, save_invstd, scale, shift,
         run_var.mul_(1 - momentum).add_(momentum * var * rows / max(rows - 1, 1))
 
 
-def bnact_apply(y, res, scale, shift, act=0, alpha=0.0, res_affine=None):
-    """z = act(y*scale + shift [+ res (*rscale + rshift)]) (NHWC bf16)."""
+def bnact_apply(y, res, scale, shift, act=0, alpha=0.0, res_affine=None, row_scale=None):
+    """z = act(y*scale + shift [* row_scale[n]] [+ res (*rscale + rshift)]) (NHWC bf16 [N, H, W, C]);
+    ``row_scale`` [N] fp32: a per-sample factor of the BN output (a block's drop-path mask /
+    keep), identity activation only."""
     C = y.shape[-1]
     rows = y.numel() // C
+    hw = rows // y.shape[0]
     if _cuda(y):
         z = torch.empty_like(y)
         rs, rh = res_affine if res_affine is not None else (None, None)
         _lib.call('mlc_bnact_apply', _lib.ptr(y), _lib.ptr(res), _lib.ptr(z), _lib.ptr(scale), _lib.ptr(shift),
-                  _lib.ptr(rs), _lib.ptr(rh), rows, C, int(act), float(alpha), _lib.stream())
+                  _lib.ptr(rs), _lib.ptr(rh), rows, C, int(act), float(alpha), _lib.ptr(row_scale), hw, _lib.stream())
         return z
     a = y.float() * scale + shift
+    if row_scale is not None:
+        a = a * row_scale.view(-1, *([1] * (y.dim() - 1)))
     if res is not None:
         r = res.float()
         if res_affine is not None:
@@ -1127,13 +1132,14 @@ def bnact_apply(y, res, scale, shift, act=0, alpha=0.0, res_affine=None):
 
 
 def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0, dgamma=None, dbeta=None,
-              sums=None, coef=None, want_dres=False, res_affine=None):
-    """Backward of z = act(BN(y) [+ res (*rscale + rshift)]) with the forward's (scale, shift):
-    returns (dy, dres or None) and writes dgamma / dbeta; dres is the gradient of the residual
-    term (before ``res_affine``, i.e. of a folded shortcut BN's output).  ``sums`` (NSTAT*2*C
-    fp32) must be zero on entry."""
+              sums=None, coef=None, want_dres=False, res_affine=None, row_scale=None):
+    """Backward of z = act(BN(y) [* row_scale[n]] [+ res (*rscale + rshift)]) with the forward's
+    (scale, shift): returns (dy, dres or None) and writes dgamma / dbeta; dres is the gradient
+    of the residual term (before ``res_affine``, i.e. of a folded shortcut BN's output).
+    ``sums`` (NSTAT*2*C fp32) must be zero on entry."""
     C = y.shape[-1]
     rows = y.numel() // C
+    hw = rows // y.shape[0]
     rs, rh = res_affine if res_affine is not None else (None, None)
     if _cuda(dz):
         if coef is None:
@@ -1146,24 +1152,26 @@ def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0
             dres = torch.empty_like(y) if want_dres else None
             _lib.call('mlc_bnact_bwd', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
                       _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(rs), _lib.ptr(rh), _lib.ptr(invstd), _lib.ptr(gamma),
-                      _lib.ptr(part), part.numel(), _lib.ptr(coef), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(dy), _lib.ptr(dres), rows, C,
-                      int(act), float(alpha), _lib.stream())
+                      _lib.ptr(part), part.numel(), _lib.ptr(coef), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(dy),
+                      _lib.ptr(dres), rows, C, int(act), float(alpha), _lib.ptr(row_scale), hw, _lib.stream())
             return dy, dres
         if sums is None:
             sums = torch.zeros(NSTAT * 2 * C, device=dz.device, dtype=torch.float32)
         _lib.call('mlc_bnact_bwd_reduce', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
                   _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(rs), _lib.ptr(rh), _lib.ptr(sums), rows, C, int(act),
-                  float(alpha),
-                  _lib.stream())
+                  float(alpha), _lib.ptr(row_scale), hw, _lib.stream())
         _lib.call('mlc_bn_bwd_finalize', _lib.ptr(sums), _lib.ptr(invstd), _lib.ptr(gamma), _lib.ptr(coef),
                   _lib.ptr(dgamma), _lib.ptr(dbeta), rows, C, _lib.stream())
         dy = torch.empty_like(y)
         dres = torch.empty_like(y) if want_dres else None
         _lib.call('mlc_bnact_bwd_apply', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
                   _lib.ptr(coef), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(rs), _lib.ptr(rh), _lib.ptr(dy),
-                  _lib.ptr(dres), rows, C, int(act), float(alpha), _lib.stream())
+                  _lib.ptr(dres), rows, C, int(act), float(alpha), _lib.ptr(row_scale), hw, _lib.stream())
         return dy, dres
+    rsc = row_scale.repeat_interleave(hw)[:, None] if row_scale is not None else None
     a = y.float().reshape(rows, C) * scale + shift
+    if rsc is not None:
+        a = a * rsc
     if res is not None:
         r = res.float().reshape(rows, C)
         a = a + (r * rs + rh if rs is not None else r)
@@ -1174,6 +1182,9 @@ def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0
             d = d * (zf * (1 - zf) if act == 4 else 1 - zf * zf)
         else:
             d = d * act_grad_ref(a, act, alpha)
+    dres = d.reshape(y.shape).to(torch.bfloat16) if want_dres else None
+    if rsc is not None:
+        d = d * rsc
     yc = y.float().reshape(rows, C) - mean
     S1, S2 = d.sum(0), (d * yc).sum(0)
     if dgamma is not None:
@@ -1181,7 +1192,6 @@ def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0
         dbeta.copy_(S1)
     k1 = gamma * invstd
     dyf = k1 * d - k1 * S1 / rows - k1 * invstd * invstd * S2 / rows * yc
-    dres = d.reshape(y.shape).to(torch.bfloat16) if want_dres else None
     return dyf.reshape(y.shape).to(torch.bfloat16), dres
 
 

@@ -532,11 +532,17 @@ class ConvBNAct(Site):
         # pass and its backward as pool-scatter + BN-backward passes (stem.hip); the full-
         # resolution activation is never written
         object.__setattr__(self, 'pool3', False)
+        # stochastic depth folded in (set by the lowering): the BN output is multiplied by a
+        # per-sample drop-path factor mask / drop_keep before the residual add (EfficientNet's
+        # MBConv in training), in the same apply pass; the third input is the [N,1,1,1] mask
+        object.__setattr__(self, 'drop_keep', None)
 
-    def forward(self, x, res=None):
+    def forward(self, x, res=None, mask=None):
+        if mask is not None:
+            return _run(self, x, res, mask)
         return _run(self, x, res) if res is not None else _run(self, x)
 
-    def fwd(self, x, res=None):
+    def fwd(self, x, res=None, mask=None):
         c, bn = self.conv, self.bn
         xn = to_nhwc(x, c.Cip)
         rn = to_nhwc(res, c.Cop) if res is not None else None
@@ -560,10 +566,15 @@ class ConvBNAct(Site):
                 if self.res_bn is not None and rn is not None:
                     rsh = self.res_bn._fold
                     object.__setattr__(self.res_bn, '_fold', None)
-                z = Fn.bnact_apply(y, rn, scale, shift, self.act, self.alpha, res_affine=rsh)
+                rsc = None
+                if mask is not None:
+                    rsc = mask.reshape(-1).float() / self.drop_keep
+                z = Fn.bnact_apply(y, rn, scale, shift, self.act, self.alpha, res_affine=rsh, row_scale=rsc)
             saved = [xn, y, z, rn if rn is not None else y, scale, shift, mean, inv]
             if rsh is not None:
                 saved += list(rsh)
+            if mask is not None:
+                saved.append(rsc)
             if self.bn_prereduced and stats is not None and self.ctx.training:
                 object.__setattr__(self, '_bn_stash', (y, z, mean))   # read by the linked dgrad
                 object.__setattr__(self, '_bn_done', False)
@@ -582,7 +593,9 @@ class ConvBNAct(Site):
         dres = None
         if bn is not None:
             xn, y, z, rn, scale, shift, mean, inv = saved[:8]
-            rsh = tuple(saved[8:10]) if len(saved) > 8 else None
+            rsc = saved[-1] if (self.drop_keep is not None and len(needs) > 2) else None
+            nfold = len(saved) - 8 - (1 if rsc is not None else 0)
+            rsh = tuple(saved[8:10]) if nfold == 2 else None
             ws = self.ctx.ws
             d = self._direct_bn_grads()
             if self.pool3:
@@ -600,7 +613,7 @@ class ConvBNAct(Site):
                 dy, dres = Fn.bnact_bwd(dz, z, y, rn if has_res else None, mean, scale, shift, inv,
                                         bn.gamma.master, self.act, self.alpha, dgamma=_acc_view(bn.gamma, d),
                                         dbeta=_acc_view(bn.beta, d), sums=ws[self.k_bw], want_dres=has_res,
-                                        res_affine=rsh)
+                                        res_affine=rsh, row_scale=rsc)
             object.__setattr__(self, '_bn_stash', None)
             object.__setattr__(self, '_bn_done', False)
             _acc_commit(bn.gamma, d)
@@ -677,6 +690,8 @@ class ConvBNAct(Site):
                 out.append(None)
             else:
                 out.append(from_nhwc(dres, c.Co) if needs[1] else None)
+        if len(needs) > 2:
+            out.append(None)                      # the drop-path mask
         return out
 
 

@@ -31,3 +31,29 @@ def test_chscale_matches_fp32(N, H, C, res, relu):
     assert (dg - ref_dg).abs().max() <= 1e-3 * ref_dg.abs().max() + 1e-3
     if res:
         assert (dres.float() - d).abs().max() <= 1e-2 * d.abs().max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('C', [16, 40, 320])
+def test_bn_row_scale_matches_cpu_reference(C):
+    """BatchNorm apply / backward with a per-sample factor (the folded drop-path mask / keep)
+    and a residual: GPU kernels vs the fp32 CPU reference of the same functions."""
+    torch.manual_seed(1)
+    N, H = 6, 9
+    y = torch.randn(N, H, H, C).to(torch.bfloat16)
+    res = torch.randn(N, H, H, C).to(torch.bfloat16)
+    dz = torch.randn(N, H, H, C).to(torch.bfloat16)
+    scale, shift = torch.rand(C) + 0.5, torch.randn(C) * 0.1
+    mean, inv, gamma = torch.randn(C) * 0.1, torch.rand(C) + 0.5, torch.rand(C) + 0.5
+    rsc = (torch.rand(N) < 0.7).float() / 0.7
+    outs = {}
+    for dev in ('cpu', 'cuda'):
+        t = [v.to(dev) for v in (y, res, dz, scale, shift, mean, inv, gamma, rsc)]
+        yy, rr, dd, sc, sh, mu, iv, ga, rs = t
+        z = Fn.bnact_apply(yy, rr, sc, sh, 0, 0.0, row_scale=rs)
+        dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        dy, dres = Fn.bnact_bwd(dd, z, yy, rr, mu, sc, sh, iv, ga, 0, 0.0, dgamma=dg, dbeta=db,
+                                sums=torch.zeros(Fn.NSTAT * 2 * C, device=dev), want_dres=True, row_scale=rs)
+        outs[dev] = [v.float().cpu() for v in (z, dy, dres, dg, db)]
+    for a, b in zip(outs['cpu'], outs['cuda']):
+        assert (a - b).abs().max() <= 2e-2 * a.abs().max() + 1e-4

@@ -10,6 +10,8 @@ import os
 import socket
 
 import pytest
+import operator
+
 import torch
 import torch.multiprocessing as mp
 import torch.nn as nn
@@ -527,6 +529,49 @@ def test_squeeze_excitation_gates_match_fp32_autograd():
     (want * g).sum().backward()
     assert _rel(out, want) < 2e-2
     assert _cos(xi.grad, xr.grad) > 0.98
+    for p in net.param_sets():
+        gg = p.w.grad if hasattr(p, 'w') else p.gamma.grad
+        assert _cos(gg, _torch_grad(p, ref)) > 0.98, p.name
+
+
+class _DropPathNet(nn.Module):
+    """Residual blocks ending in conv -> BN -> stochastic depth -> + x (EfficientNet's MBConv)."""
+
+    def __init__(self):
+        super().__init__()
+        self.stem = nn.Conv2d(3, 16, 3, 1, 1)
+        self.blocks = nn.ModuleList([nn.Sequential(nn.Conv2d(16, 32, 1), nn.BatchNorm2d(32), nn.SiLU(),
+                                                   nn.Conv2d(32, 16, 1, bias=False), nn.BatchNorm2d(16))
+                                     for _ in range(2)])
+        self.head = nn.Linear(16, 5)
+
+    def forward(self, x):
+        x = self.stem(x)
+        for i, b in enumerate(self.blocks):
+            y = b(x)
+            keep = 0.75 - 0.25 * i
+            mask = torch.rand_like(y[:, :1, :1, :1].float()) < keep   # fp32 draws in both graphs
+            x = y * mask / keep + x
+        return self.head(F.adaptive_avg_pool2d(x, 1).flatten(1))
+
+
+def test_drop_path_residual_folds_into_the_bn_site():
+    """stochastic depth + residual add lower into the block's last conv+BN site (mask / keep
+    applied in its BN pass); the same RNG draws give the torch graph's output and gradients."""
+    m, ref = _pair(_DropPathNet)
+    net = GenericNet(m, 'cpu')
+    sites = list(net.train_gm.modules())
+    assert sum(getattr(s, 'drop_keep', None) is not None for s in sites) == 2
+    assert not [n for n in net.train_gm.graph.nodes if n.op == 'call_function' and n.target is operator.truediv]
+    x = torch.randn(8, 3, 8, 8)
+    torch.manual_seed(11)
+    out = net(x)
+    torch.manual_seed(11)
+    want = ref(x)
+    g = torch.randn_like(want)
+    (out.float() * g).sum().backward()
+    (want * g).sum().backward()
+    assert _rel(out, want) < 2e-2
     for p in net.param_sets():
         gg = p.w.grad if hasattr(p, 'w') else p.gamma.grad
         assert _cos(gg, _torch_grad(p, ref)) > 0.98, p.name
