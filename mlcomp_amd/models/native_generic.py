@@ -45,7 +45,7 @@ import torch.nn.functional as F
 
 from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops.glayers import (BilinearUp, BNAct, BNParams, ChannelGate, Conv3dAs2d, ConvBNAct, ConvParams,
-                                    Frames, GlobalAvgPool, LinearAct, LinearParams, MaxPool, UpCat)
+                                    Frames, GlobalAvgPool, LinearAct, LinearParams, MaxPool, TemporalAs2d, UpCat)
 from mlcomp_amd.ops.layers import NativeContext
 from mlcomp_amd.train.native_spec import NativeUnsupported
 
@@ -244,7 +244,8 @@ class _Lowering:
         ``Frames``."""
         m = self.modules[node.target]
         _check_conv3d(node.target, m)
-        proxy = Conv3dAs2d(m)
+        # purely temporal stride-1 convs run over the [N, T, H*W, C] view (no unfold copy)
+        proxy = TemporalAs2d(m) if TemporalAs2d.applies(m) else Conv3dAs2d(m)
         chain = [node]
         bn_node = _only_user(node)
         bn = None

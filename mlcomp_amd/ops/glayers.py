@@ -129,6 +129,46 @@ class Conv3dAs2d:
         return frames_of(r[:, :, :, None, None] if r.dim() == 3 else r)
 
 
+class TemporalAs2d:
+    """A purely temporal nn.Conv3d - kernel (kt, 1, 1), stride 1, padding (pt, 0, 0), no
+    dilation, groups 1 (R(2+1)D's temporal convs) - as the 2D conv with kernel (kt, 1) and
+    padding (pt, 0) over the [N, T, H*W, C] image: a channels_last_3d activation already IS
+    that image, so unlike the frame unfold (:class:`Conv3dAs2d`, kt copies of the input)
+    there is no copy in either direction."""
+
+    def __init__(self, m: nn.Module):
+        kt = m.kernel_size[0]
+        self.src3d = m
+        self.kernel_size = (kt, 1)
+        self.stride, self.padding, self.dilation = (1, 1), (m.padding[0], 0), (1, 1)
+        self.groups = 1
+        self.padding_mode = m.padding_mode
+        self.in_channels, self.out_channels = m.in_channels, m.out_channels
+        self.bias = m.bias
+        self._shape = (m.weight.shape[0], m.weight.shape[1], kt, 1)
+        self._hw = None
+
+    @staticmethod
+    def applies(m: nn.Module) -> bool:
+        return (isinstance(m, nn.Conv3d) and tuple(m.kernel_size[1:]) == (1, 1) and tuple(m.stride) == (1, 1, 1)
+                and tuple(m.padding[1:]) == (0, 0) and tuple(m.dilation) == (1, 1, 1) and m.groups == 1
+                and not isinstance(m.padding, str))
+
+    @property
+    def weight(self):
+        return self.src3d.weight.view(self._shape)
+
+    def unfold(self, x: torch.Tensor) -> torch.Tensor:
+        self._hw = x.shape[3:]
+        return x.flatten(3)                  # [N, C, T, H*W], channels_last strides: a view
+
+    def fold_out(self, y: torch.Tensor, N: int, one_d: bool) -> torch.Tensor:
+        return y.unflatten(3, tuple(self._hw))
+
+    def frames_like_out(self, r: torch.Tensor) -> torch.Tensor:
+        return r.flatten(3)
+
+
 class Frames(nn.Module):
     """Runs a 2D site over the frames of a 5D (or, for Conv1d, 3D) tensor: temporal unfold
     (convs), the site on N*T frames, the result back in the caller's layout."""
