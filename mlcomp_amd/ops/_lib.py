@@ -90,6 +90,7 @@ _SIGS = {
     'mlc_stem_pool_bwd_reduce': [vp] * 5 + [i32] * 4 + [vp],
     'mlc_stem_pool_bwd_apply': [vp] * 6 + [i32] * 4 + [vp],
     'mlc_stem_s2d': [vp, vp] + [i32] * 5 + [vp],
+    'mlc_stem_conv_fwd': [vp] * 5 + [i32] * 3 + [vp],
     'mlc_avgpool_fwd': [vp, vp, i32, i32, i32, vp],
     'mlc_avgpool_bwd': [vp, vp, i32, i32, i32, vp],
     'mlc_softmax_ce': [vp] * 5 + [i32, i32, i32, f32, f32, vp],

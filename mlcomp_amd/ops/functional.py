@@ -567,6 +567,25 @@ def stem_s2d(x, pad=3):
     return F.pad(xp, (0, 4)).to(torch.bfloat16).contiguous()
 
 
+_STEM_CONV = os.environ.get('MLC_STEM_CONV', '1') == '1'
+
+
+def stem_conv_fwd(xs, w, stats=None):
+    """The space-to-depth stem conv (4x4/1 over the [N, Hb, Wb, 16] image, w [64, 4, 4, 16])
+    through the persistent register-resident-filter kernel (csrc/kernels/stemconv.hip);
+    :func:`conv2d_fwd` on the CPU, in deterministic mode, with MLC_STEM_CONV=0 or for other
+    shapes.  ``stats`` as in :func:`conv2d_fwd`."""
+    if _cuda(xs) and _STEM_CONV and not _lib.DETERMINISTIC and tuple(w.shape) == (64, 4, 4, 16) \
+            and xs.shape[-1] == 16 and xs.is_contiguous() and w.is_contiguous():
+        N, Hb, Wb, _ = xs.shape
+        y = torch.empty(N, Hb - 3, Wb - 3, 64, device=xs.device, dtype=torch.bfloat16)
+        s1, s2 = stats if stats is not None else (None, None)
+        _lib.call('mlc_stem_conv_fwd', _lib.ptr(xs), _lib.ptr(w), _lib.ptr(y), _lib.ptr(s1), _lib.ptr(s2),
+                  N, Hb, Wb, _lib.stream())
+        return y
+    return conv2d_fwd(xs, w, 1, 0, 1, stats=stats)
+
+
 def stem_s2d_to_nhwc(xs, pad=3):
     """Inverse of :func:`stem_s2d`: [N, Hb, Wb, 16] -> the [N, H, W, 3] image (float)."""
     N, Hb, Wb, _ = xs.shape

@@ -291,6 +291,8 @@ class ConvBN:
 
     # the three GEMMs of the unit (overridden by ConvTBN)
     def _conv(self, x, stats, in_affine=None):
+        if self.s2d and in_affine is None:
+            return Fn.stem_conv_fwd(x, self.w.bf16, stats=stats)
         return Fn.conv2d_fwd(x, self.w.bf16, self.stride, self.pad, self.dil, stats=stats, in_affine=in_affine)
 
     def _dgrad(self, dy, x_shape, addend=None, out=None, bn=None):
