@@ -225,14 +225,19 @@ class _Lowering:
             bm = self.modules[bn_node.target]
             if bm.num_features == m.out_channels and bm.momentum is not None:
                 bn = bm
+        # an image stem (7x7/2 pad 3 over <= 3 channels) reading the graph input: the
+        # space-to-depth form (MLC_GENERIC_S2D=0 keeps the direct 7x7 conv)
+        src = node.args[0]
+        s2d = (os.environ.get('MLC_GENERIC_S2D', '1') == '1' and isinstance(src, fx.Node)
+               and src.op == 'placeholder' and ConvParams.s2d_ok(m))
         if bn is not None:
             chain.append(bn_node)
             res, act, alpha = self._tail(bn_node, chain)
-            cp = self.net.conv_params(node.target, m, keep_bias=False)
+            cp = self.net.conv_params(node.target, m, keep_bias=False, s2d=s2d)
             bp = self.net.bn_params(bn_node.target, bn, conv_bias=m.bias)
         else:
             res, act, alpha = self._tail(node, chain, allow_res=False)
-            cp = self.net.conv_params(node.target, m, keep_bias=True)
+            cp = self.net.conv_params(node.target, m, keep_bias=True, s2d=s2d)
             bp = None
         site = ConvBNAct(self.net.ctx, cp, bp, act, alpha, residual=res is not None)
         new = self._site_node(chain[-1], site, [node.args[0]] + ([res] if res is not None else []))
@@ -688,10 +693,10 @@ class GenericNet:
         gm = fx.symbolic_trace(model)
         return _Lowering(self, gm).run()
 
-    def conv_params(self, name, m, keep_bias):
-        key = f'conv:{name}:{keep_bias}'
+    def conv_params(self, name, m, keep_bias, s2d=False):
+        key = f'conv:{name}:{keep_bias}:{s2d}'
         if key not in self._params:
-            self._params[key] = ConvParams(self.ctx, name, m, keep_bias)
+            self._params[key] = ConvParams(self.ctx, name, m, keep_bias, s2d=s2d)
         return self._params[key]
 
     def bn_params(self, name, m, conv_bias=None):

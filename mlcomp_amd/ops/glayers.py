@@ -211,10 +211,37 @@ class ConvParams:
     depthwise [KH, KW, Cp] (tap-major); nn.ConvTranspose2d -> 'tr' [Cip, KH, KW, Cop] (the
     filter of the conv whose input gradient the transposed conv is); optional bias [Cop]."""
 
-    def __init__(self, ctx: NativeContext, name: str, conv: nn.Module, keep_bias: bool):
+    @staticmethod
+    def s2d_ok(conv: nn.Module) -> bool:
+        """A 7x7/2 pad-3 conv over <= 3 channels (an image stem): it can run as a 4x4/1 conv
+        over the 2x2 space-to-depth image (kind 's2d', as the hand ResNet engine's stem)."""
+        return (type(conv) is nn.Conv2d and conv.groups == 1 and conv.in_channels <= 3
+                and tuple(conv.kernel_size) == (7, 7) and tuple(conv.stride) == (2, 2)
+                and tuple(conv.padding) == (3, 3) and tuple(conv.dilation) == (1, 1))
+
+    def __init__(self, ctx: NativeContext, name: str, conv: nn.Module, keep_bias: bool, s2d: bool = False):
         self.ctx, self.name, self.src = ctx, name, conv
         self.groups = conv.groups
         self.stride, self.pad, self.dil = conv.stride[0], conv.padding[0], conv.dilation[0]
+        if s2d:
+            # the image stem as a 4x4/1 conv over the space-to-depth image (K = 256, and the
+            # persistent stem kernel for 64 channels, csrc/kernels/stemconv.hip); its input is
+            # the graph input.  Filter [Cop, 4, 4, 16]: the 7x7
+            # filter zero-extended to 8x8 and regrouped (Fn.stem_w_to_s2d); the extension taps
+            # and the 4 pad channels are masked out of every weight gradient
+            assert ConvParams.s2d_ok(conv)
+            Co = conv.out_channels
+            self.kind = 's2d'
+            self.Ci, self.Co, self.Cg = conv.in_channels, Co, conv.in_channels
+            self.k = (7, 7)
+            self.wt_idx = None
+            self.Cip, self.Cop = ceil8(self.Ci), ceil8(Co)
+            self.w = ctx.arena.weight(f'{name}.weight', (self.Cop, 4, 4, 16))
+            self.b = ctx.arena.vector(f'{name}.bias', (self.Cop,)) if (keep_bias and conv.bias is not None) else None
+            _freeze(self.w, conv.weight)
+            _freeze(self.b, conv.bias)
+            self.uses = _Uses()
+            return
         if not isinstance(conv, nn.ConvTranspose2d) and conv.groups == 1 and conv.padding[0] != conv.padding[1]:
             self.pad = (conv.padding[0], conv.padding[1])   # per-axis (dense convs: Inception's 1x7 / 7x1)
         if isinstance(conv, nn.ConvTranspose2d):
@@ -258,7 +285,11 @@ class ConvParams:
     def load_from_torch(self):
         w = self.src.weight.detach().float()
         dev = self.ctx.device
-        if self.kind == 'dense':
+        if self.kind == 's2d':
+            w = torch.nn.functional.pad(Fn.stem_w_to_s2d(w.cpu()), (0, 0, 0, 0, 0, 0, 0, self.Cop - self.Co))
+            ones = torch.ones(self.Cop, self.Ci, 7, 7)
+            self._gmask = (Fn.stem_w_to_s2d(ones) != 0).float().to(dev)
+        elif self.kind == 'dense':
             w = w.permute(0, 2, 3, 1)
             w = torch.nn.functional.pad(w, (0, self.Cip - self.Ci, 0, 0, 0, 0, 0, self.Cop - self.Co))
         elif self.kind == 'tr':
@@ -275,7 +306,9 @@ class ConvParams:
 
     def export_to_torch(self):
         m = self.w.master.detach()
-        if self.kind == 'dense':
+        if self.kind == 's2d':
+            w = Fn.stem_w_from_s2d(m[:self.Co].float().cpu(), self.Ci)
+        elif self.kind == 'dense':
             w = m[:self.Co, :, :, :self.Ci].permute(0, 3, 1, 2)
         elif self.kind == 'tr':
             w = m[:self.Ci, :, :, :self.Co].permute(0, 3, 1, 2)
@@ -299,6 +332,11 @@ class ConvParams:
         """x: NHWC bf16 with Cip channels -> y [N, Ho, Wo, Cop] (bias and a ReLU act fused for
         dense convs without BN: ``act`` 3)."""
         wb = self.w.bf16
+        if self.kind == 's2d':       # x: the s2d image (s2d_input)
+            if self.b is not None or act:
+                assert stats is None
+                return Fn.conv2d_fwd_ex(x, wb, self.b.master if self.b is not None else None, act, 1, 0, 1)
+            return Fn.stem_conv_fwd(x, wb, stats=stats)
         if self.kind == 'dense':
             if self.b is not None or act:
                 assert stats is None
@@ -317,6 +355,14 @@ class ConvParams:
         in the dense GEMM's epilogue; ``bn``: the producing site's BatchNorm-backward
         reduction and ReLU mask in the same epilogue, dense convs only)."""
         wb = self.w.bf16
+        if self.kind == 's2d':
+            # rare (an input that requires grad): the s2d image's gradient, mapped back
+            assert bn is None
+            dxs = Fn.conv2d_dgrad(dy, wb, x_shape, 1, 0, 1)
+            H, W = self._in_hw
+            dx = Fn.stem_s2d_to_nhwc(dxs, 3)[:, :H, :W]
+            dx = torch.nn.functional.pad(dx, (0, self.Cip - dx.shape[-1])).to(torch.bfloat16).contiguous()
+            return dx if addend is None else dx.add_(addend)
         if self.kind == 'dense':
             wt = self.ctx.wt[self.wt_idx] if self.wt_idx is not None else None
             return Fn.conv2d_dgrad(dy, wb, x_shape, self.stride, self.pad, self.dil, addend=addend, bn=bn, wt=wt)
@@ -330,8 +376,24 @@ class ConvParams:
             dx = Fn.gconv_dgrad(dy, wb, x_shape, self.groups, self.stride, self.pad, self.dil)
         return dx if addend is None else dx.add_(addend)
 
+    def s2d_input(self, xn):
+        """[N, H, W, Cip] image -> the [N, (H+6)/2, (W+6)/2, 16] space-to-depth image of its
+        pad-3 version (an odd H / W gets one zero row / column first: same output)."""
+        H, W = xn.shape[1], xn.shape[2]
+        self._in_hw = (H, W)                  # for an input gradient (dgrad)
+        if H % 2 or W % 2:
+            xn = torch.nn.functional.pad(xn, (0, 0, 0, W % 2, 0, H % 2))
+        return Fn.stem_s2d(xn, 3)
+
     def wgrad(self, dy, x):
         acc = self.ctx.grad_prezeroed
+        if self.kind == 's2d':
+            if self.b is not None:
+                Fn.conv2d_wgrad_bias(dy, x, self.w.shape, self.b.grad, 1, 0, 1, out=self.w.grad, accumulate=acc)
+            else:
+                Fn.conv2d_wgrad(dy, x, self.w.shape, 1, 0, 1, out=self.w.grad, accumulate=acc)
+            self.w.grad.mul_(self._gmask)
+            return
         if self.kind == 'dense':
             if self.b is not None:
                 Fn.conv2d_wgrad_bias(dy, x, self.w.shape, self.b.grad, self.stride, self.pad, self.dil,
@@ -585,6 +647,8 @@ class ConvBNAct(Site):
     def fwd(self, x, res=None, mask=None):
         c, bn = self.conv, self.bn
         xn = to_nhwc(x, c.Cip)
+        if c.kind == 's2d':
+            xn = c.s2d_input(xn)              # saved for the weight gradient as well
         rn = to_nhwc(res, c.Cop) if res is not None else None
         if bn is not None:
             stats = None

@@ -59,6 +59,8 @@ def _torch_grad(p, ref):
         return _torch_grad_tr(p, ref)
     if hasattr(p, 'kind'):
         g = m.weight.grad
+        if p.kind == 's2d':
+            return F.pad(Fn.stem_w_to_s2d(g), (0, 0, 0, 0, 0, 0, 0, p.Cop - p.Co))
         if p.kind == 'dense':
             return F.pad(g.permute(0, 2, 3, 1), (0, p.Cip - p.Ci, 0, 0, 0, 0, 0, p.Cop - p.Co))
         if p.kind == 'dw':
