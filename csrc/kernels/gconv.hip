@@ -21,6 +21,7 @@
 // threads, as the BatchNorm passes) and walk pixels; the weight gradient reduces per
 // thread, then per block (LDS), then over 32 partial copies.
 #include "common.h"
+#include <stdlib.h>
 
 namespace gconv {
 
@@ -166,6 +167,174 @@ gconv_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wb, bf16* __r
       *reinterpret_cast<uint4*>(out + m * g.Co + oc0 + 8 * (lane & 1)) =
           *reinterpret_cast<const uint4*>(st + (lane >> 1) * 16 + 8 * (lane & 1));
   }
+}
+
+// ------------------------------------------------------------------ grouped fwd / dgrad, row-band tiles
+// gconv_kernel gives each block ONE 16-channel output block, so every A-operand load is a
+// 16-byte half of a 32-byte per-pixel chunk, scattered C*2 bytes apart: ~1 TB/s
+// (profiles/round5/generic/gconv_resnext_b128.jsonl).  Here a block owns R full output rows
+// of one image and a 64-channel slab (4 output blocks, one per wave, whole groups: in == out
+// channels per group, Cg | 64 or Cg == 64): the slab's input rows (with the conv padding) are
+// staged once into LDS as 128-byte pixel rows with coalesced 16-byte loads, every A fragment
+// is a ds_read_b128 from there (16-byte chunk c of pixel i at c ^ ((i >> 1) & 7), pixel
+// parity picking the 128-byte half of the bank row: conflict-free at stride 1), and the
+// output slab goes back through the same LDS as 128-byte pixel rows.  FLIP: the stride-1
+// input gradient as a forward conv of dy with the transposed filter (tr = 1 expansion), taps
+// mirrored and pad (KH-1)*D - P.
+constexpr int TB_CS = 64;           // channel slab
+constexpr int TB_MAXPX = 256;       // output pixels per block (16 MFMA rows)
+constexpr int TB_LDS = 48 * 1024;
+
+struct TGeom {
+  int Hi, Wi, C;                    // operand image [N][Hi][Wi][C]
+  int Ho, Wo;                       // output image [N][Ho][Wo][C]
+  int KH, KW, S, P, D, T, Kp;
+  int Cog, Cg;                      // output / K-side channels per group
+  int R, rows_in, Wp, bands;        // output rows per block, staged input rows / cols, blocks per image
+};
+
+__device__ __forceinline__ int tb_off(int pix, int c) { return pix * 128 + ((c ^ ((pix >> 1) & 7)) << 4); }
+
+template <int KB, bool FLIP>
+__global__ void __launch_bounds__(NT)
+gconv_band_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wb, bf16* __restrict__ out,
+                  float* __restrict__ sum, float* __restrict__ sumsq, TGeom g) {
+  __shared__ __attribute__((aligned(16))) char lds[TB_LDS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = blockIdx.x / g.bands, oh0 = (blockIdx.x - n * g.bands) * g.R;
+  const int cs0 = blockIdx.y * TB_CS;
+  const int rows = min(g.R, g.Ho - oh0), npx = rows * g.Wo;
+  const int hi0 = oh0 * g.S - g.P;
+  // ---- stage the slab's input rows hi0 .. hi0+rows_in-1, columns -P .. -P+Wp-1 (zeros outside)
+  const int nchunk = g.rows_in * g.Wp * 8;
+  for (int i0 = 0; i0 < nchunk; i0 += NT * 4) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * NT + tid;
+      const int pix = i >> 3, c = i & 7;
+      const int ir = pix / g.Wp, ic = pix - ir * g.Wp;
+      const int hi = hi0 + ir, wi = ic - g.P;
+      v[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (i < nchunk && (unsigned)hi < (unsigned)g.Hi && (unsigned)wi < (unsigned)g.Wi)
+        v[u] = ldg16(in + (((long)n * g.Hi + hi) * g.Wi + wi) * g.C + cs0 + 8 * c);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * NT + tid;
+      if (i < nchunk) *reinterpret_cast<uint4*>(lds + tb_off(i >> 3, i & 7)) = v[u];
+    }
+  }
+  // ---- B fragments of this wave's 16-channel output block (all K-steps, registers)
+  constexpr int MAXKS = (9 * KB + 31) / 32;   // up to 3x3 taps
+  const int ob = wave, oc0 = cs0 + 16 * ob;
+  const int nks = g.Kp / 32;
+  const int cb = blk_cbase(oc0, g.Cog, g.Cg) - cs0;   // first K-side channel in the slab
+  const int hl = lane >> 4, j = lane & 15;
+  bf16x8 bfr[MAXKS];
+  const bf16* wrow = wb + (long)(oc0 + j) * g.Kp + 8 * hl;
+#pragma unroll
+  for (int ks = 0; ks < MAXKS; ++ks) bfr[ks] = ks < nks ? ldfrag(wrow + 32 * ks) : bf16x8{};
+  // per K-step: this lane's tap offset (in staged pixels) and LDS chunk; -1 = padding k
+  int toff[MAXKS], tch[MAXKS];
+#pragma unroll
+  for (int ks = 0; ks < MAXKS; ++ks) {
+    const int k = 32 * ks + 8 * hl, t = k / KB, kb = k - t * KB;
+    if (ks < nks && t < g.T) {
+      int r = t / g.KW, c = t - r * g.KW;
+      if (FLIP) { r = g.KH - 1 - r; c = g.KW - 1 - c; }
+      toff[ks] = r * g.D * g.Wp + c * g.D;
+      tch[ks] = (cb + kb) >> 3;
+    } else {
+      toff[ks] = -1;
+      tch[ks] = 0;
+    }
+  }
+  __syncthreads();
+  // ---- MFMA rows of 16 output pixels (flattened over the band's rows)
+  const int nrow = (npx + 15) / 16;
+  f32x4 acc[TB_MAXPX / 16];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int m = 0; m < TB_MAXPX / 16; ++m) {
+    acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (m < nrow) {   // block-uniform
+      const int q = min(16 * m + j, npx - 1);
+      const int oh = q / g.Wo, ow = q - oh * g.Wo;
+      const int base = oh * g.S * g.Wp + ow * g.S;
+#pragma unroll
+      for (int ks = 0; ks < MAXKS; ++ks) {
+        if (ks < nks) {
+          bf16x8 a = {};
+          if (toff[ks] >= 0) a = *reinterpret_cast<const bf16x8*>(lds + tb_off(base + toff[ks], tch[ks]));
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[ks], acc[m], 0, 0, 0);
+        }
+      }
+      if (sum) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = 16 * m + 4 * hl + i < npx ? acc[m][i] : 0.f;
+          s1 += v;
+          s2 += v * v;
+        }
+      }
+    }
+  }
+  if (sum) {
+    s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
+    if (lane < 16) {
+      const int slot = (int)((blockIdx.x * 4 + wave) % NCOPY);
+      atomicAdd(sum + (long)slot * g.C + oc0 + j, s1);
+      atomicAdd(sumsq + (long)slot * g.C + oc0 + j, s2);
+    }
+  }
+  // ---- output slab through LDS: [px][64 ch] rows, then 16-byte stores, 128 B per pixel
+  __syncthreads();   // every wave is done reading the staged input
+#pragma unroll
+  for (int m = 0; m < TB_MAXPX / 16; ++m) {
+    if (m < nrow) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = 16 * m + 4 * hl + i;
+        const int ch = 16 * ob + j;
+        *reinterpret_cast<bf16*>(lds + tb_off(q, ch >> 3) + (ch & 7) * 2) = (bf16)acc[m][i];
+      }
+    }
+  }
+  __syncthreads();
+  bf16* ob_base = out + ((long)n * g.Ho + oh0) * g.Wo * g.C + cs0;
+  for (int i = tid; i < npx * 8; i += NT) {
+    const int q = i >> 3, c = i & 7;
+    *reinterpret_cast<uint4*>(ob_base + (long)q * g.C + 8 * c) = *reinterpret_cast<const uint4*>(lds + tb_off(q, c));
+  }
+}
+
+// band geometry when the row-band kernel applies (else false): in == out channels per group,
+// 64-channel slabs of whole groups, taps <= 3x3, the staged input rows within TB_LDS
+inline bool band_geom(TGeom& t, int Hi, int Wi, int C, int Co, int Ho, int Wo, int KH, int KW, int S, int P, int D,
+                      int Cg, int Cog, int KB, int Kp) {
+  static const int on = getenv("MLC_GCONV_BAND") ? atoi(getenv("MLC_GCONV_BAND")) : 1;
+  if (!on) return false;   // MLC_GCONV_BAND=0: the per-16-channel kernel only
+  if (C != Co || Cg != Cog || C % TB_CS || !(KB == 16 || KB == 32 || KB == 64) || KH * KW > 9) return false;
+  if (!(Cg <= 16 ? 16 % Cg == 0 : TB_CS % Cg == 0)) return false;
+  const int Wp = (Wo - 1) * S + (KW - 1) * D + 1;
+  int R = min(Ho, TB_MAXPX / Wo);
+  while (R >= 1 && ((R - 1) * S + (KH - 1) * D + 1) * Wp * 128 > TB_LDS) --R;
+  if (R < 1 || R * Wo * 128 > TB_LDS) return false;
+  t.Hi = Hi; t.Wi = Wi; t.C = C; t.Ho = Ho; t.Wo = Wo; t.KH = KH; t.KW = KW; t.S = S; t.P = P; t.D = D;
+  t.T = KH * KW; t.Kp = Kp; t.Cog = Cog; t.Cg = Cg;
+  t.R = R; t.rows_in = (R - 1) * S + (KH - 1) * D + 1; t.Wp = Wp; t.bands = (Ho + R - 1) / R;
+  return true;
+}
+
+template <bool FLIP>
+inline void launch_band(const TGeom& t, int N, int KB, const bf16* in, const bf16* wb, bf16* out, float* sum,
+                        float* sumsq, hipStream_t st) {
+  const dim3 grid((unsigned)(N * t.bands), t.C / TB_CS);
+  if (KB == 16) hipLaunchKernelGGL((gconv_band_kernel<16, FLIP>), grid, dim3(NT), 0, st, in, wb, out, sum, sumsq, t);
+  else if (KB == 32) hipLaunchKernelGGL((gconv_band_kernel<32, FLIP>), grid, dim3(NT), 0, st, in, wb, out, sum, sumsq, t);
+  else hipLaunchKernelGGL((gconv_band_kernel<64, FLIP>), grid, dim3(NT), 0, st, in, wb, out, sum, sumsq, t);
 }
 
 // ------------------------------------------------------------------ grouped wgrad
@@ -762,6 +931,11 @@ MLC_EXPORT int mlc_gconv_fwd(const bf16* x, const bf16* w, bf16* wb, bf16* y, fl
   const GGeom g = mkg(N, H, W, C, Ho, Wo, Co, KH, KW, S, P, D, C / groups, Co / groups);
   hipLaunchKernelGGL(expand_kernel, dim3(blocks_for((long)(Co + 15) / 16 * 16 * g.Kp)), dim3(NT), 0, st, w, wb, Co,
                      C, g.T, g.Cg, g.Cog, g.KB, g.Kp, 0);
+  TGeom t;
+  if (band_geom(t, H, W, C, Co, Ho, Wo, KH, KW, S, P, D, g.Cg, g.Cog, g.KB, g.Kp)) {
+    launch_band<false>(t, N, g.KB, x, wb, y, sum, sumsq, st);
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)((g.M + 127) / 128), (Co + 15) / 16);
   hipLaunchKernelGGL(gconv_kernel<false>, grid, dim3(NT), 0, st, x, wb, y, sum, sumsq, g);
   return hipGetLastError();
@@ -775,6 +949,13 @@ MLC_EXPORT int mlc_gconv_dgrad(const bf16* dy, const bf16* w, bf16* wb, bf16* dx
   const GGeom g = mkg(N, Ho, Wo, Co, H, W, C, KH, KW, S, P, D, Co / groups, C / groups);
   hipLaunchKernelGGL(expand_kernel, dim3(blocks_for((long)(C + 15) / 16 * 16 * g.Kp)), dim3(NT), 0, st, w, wb, C,
                      Co, g.T, g.Cg, g.Cog, g.KB, g.Kp, 1);
+  TGeom t;
+  // stride 1: a forward conv of dy over the transposed filter, taps mirrored
+  if (S == 1 && D * (KH - 1) >= P && D * (KW - 1) - P == D * (KH - 1) - P &&
+      band_geom(t, Ho, Wo, Co, C, H, W, KH, KW, 1, D * (KH - 1) - P, D, g.Cg, g.Cog, g.KB, g.Kp)) {
+    launch_band<true>(t, N, g.KB, dy, wb, dx, nullptr, nullptr, st);
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)((g.M + 127) / 128), (C + 15) / 16);
   hipLaunchKernelGGL(gconv_kernel<true>, grid, dim3(NT), 0, st, dy, wb, dx, nullptr, nullptr, g);
   return hipGetLastError();

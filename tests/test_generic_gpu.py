@@ -33,7 +33,11 @@ def _bf(*shape, scale=1.0):
     # dpn92 (3 channels per group), dpn107 (200 channels, x50), senet154 (2 in / 4 out per group),
     # a depthwise conv with channel multiplier 2, and 24-wide groups
     (2, 9, 10, 96, 3, 3, 1, 1, 1, 96), (2, 8, 8, 200, 4, 3, 2, 1, 1, 200), (2, 7, 9, 128, 2, 3, 1, 1, 1, 256),
-    (2, 8, 8, 32, 1, 3, 1, 1, 1, 64), (2, 6, 7, 96, 24, 3, 1, 1, 1, 96)])
+    (2, 8, 8, 32, 1, 3, 1, 1, 1, 64), (2, 6, 7, 96, 24, 3, 1, 1, 1, 96),
+    # ResNeXt-50 32x4d / 101 32x8d shapes on the row-band kernel (several bands per image,
+    # stride 2, dilation 2, 64-wide groups)
+    (2, 56, 56, 128, 4, 3, 1, 1, 1, 128), (2, 56, 56, 256, 8, 3, 2, 1, 1, 256), (2, 28, 28, 512, 16, 3, 1, 1, 1, 512),
+    (3, 7, 7, 1024, 32, 3, 1, 1, 1, 1024), (2, 20, 22, 256, 64, 3, 1, 2, 2, 256)])
 def test_grouped_conv_kernels_vs_fp32(N, H, W, C, Cg, k, s, p, d, Co):
     torch.manual_seed(0)
     groups = C // Cg
