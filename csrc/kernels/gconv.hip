@@ -191,11 +191,17 @@ struct TGeom {
   int KH, KW, S, P, D, T, Kp;
   int Cog, Cg;                      // output / K-side channels per group
   int R, rows_in, Wp, bands;        // output rows per block, staged input rows / cols, blocks per image
+  int wc0;                          // operand column of staged column 0 (-P, or the strided origin)
 };
+
+__host__ __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 
 __device__ __forceinline__ int tb_off(int pix, int c) { return pix * 128 + ((c ^ ((pix >> 1) & 7)) << 4); }
 
-template <int KB, bool FLIP>
+// MODE 0: forward; 1: stride-1 input gradient (FLIP); 2: strided input gradient - output
+// pixel (oh, ow) takes tap (r, c) from dy pixel ((oh + P - rD) / S, (ow + P - cD) / S) when
+// both divide (the transposed conv; the operand rows staged are those the band reaches)
+template <int KB, int MODE>
 __global__ void __launch_bounds__(NT)
 gconv_band_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wb, bf16* __restrict__ out,
                   float* __restrict__ sum, float* __restrict__ sumsq, TGeom g) {
@@ -204,7 +210,7 @@ gconv_band_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wb, bf16
   const int n = blockIdx.x / g.bands, oh0 = (blockIdx.x - n * g.bands) * g.R;
   const int cs0 = blockIdx.y * TB_CS;
   const int rows = min(g.R, g.Ho - oh0), npx = rows * g.Wo;
-  const int hi0 = oh0 * g.S - g.P;
+  const int hi0 = MODE == 2 ? floordiv(oh0 + g.P - (g.KH - 1) * g.D, g.S) : oh0 * g.S - g.P;
   // ---- stage the slab's input rows hi0 .. hi0+rows_in-1, columns -P .. -P+Wp-1 (zeros outside)
   const int nchunk = g.rows_in * g.Wp * 8;
   for (int i0 = 0; i0 < nchunk; i0 += NT * 4) {
@@ -214,7 +220,7 @@ gconv_band_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wb, bf16
       const int i = i0 + u * NT + tid;
       const int pix = i >> 3, c = i & 7;
       const int ir = pix / g.Wp, ic = pix - ir * g.Wp;
-      const int hi = hi0 + ir, wi = ic - g.P;
+      const int hi = hi0 + ir, wi = ic + g.wc0;
       v[u] = make_uint4(0u, 0u, 0u, 0u);
       if (i < nchunk && (unsigned)hi < (unsigned)g.Hi && (unsigned)wi < (unsigned)g.Wi)
         v[u] = ldg16(in + (((long)n * g.Hi + hi) * g.Wi + wi) * g.C + cs0 + 8 * c);
@@ -236,14 +242,21 @@ gconv_band_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wb, bf16
 #pragma unroll
   for (int ks = 0; ks < MAXKS; ++ks) bfr[ks] = ks < nks ? ldfrag(wrow + 32 * ks) : bf16x8{};
   // per K-step: this lane's tap offset (in staged pixels) and LDS chunk; -1 = padding k
-  int toff[MAXKS], tch[MAXKS];
+  // (MODE 2: toff = r*D, tcol = c*D of the unmirrored tap)
+  int toff[MAXKS], tch[MAXKS], tcol[MAXKS];
 #pragma unroll
   for (int ks = 0; ks < MAXKS; ++ks) {
     const int k = 32 * ks + 8 * hl, t = k / KB, kb = k - t * KB;
+    tcol[ks] = 0;
     if (ks < nks && t < g.T) {
       int r = t / g.KW, c = t - r * g.KW;
-      if (FLIP) { r = g.KH - 1 - r; c = g.KW - 1 - c; }
-      toff[ks] = r * g.D * g.Wp + c * g.D;
+      if (MODE == 1) { r = g.KH - 1 - r; c = g.KW - 1 - c; }
+      if (MODE == 2) {
+        toff[ks] = r * g.D;
+        tcol[ks] = c * g.D;
+      } else {
+        toff[ks] = r * g.D * g.Wp + c * g.D;
+      }
       tch[ks] = (cb + kb) >> 3;
     } else {
       toff[ks] = -1;
@@ -262,11 +275,19 @@ gconv_band_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wb, bf16
       const int q = min(16 * m + j, npx - 1);
       const int oh = q / g.Wo, ow = q - oh * g.Wo;
       const int base = oh * g.S * g.Wp + ow * g.S;
+      const int ro = oh0 + oh + g.P - hi0 * g.S, co = ow + g.P - g.wc0 * g.S;   // MODE 2 (oh: row in band)
 #pragma unroll
       for (int ks = 0; ks < MAXKS; ++ks) {
         if (ks < nks) {
           bf16x8 a = {};
-          if (toff[ks] >= 0) a = *reinterpret_cast<const bf16x8*>(lds + tb_off(base + toff[ks], tch[ks]));
+          if (MODE == 2) {
+            const int nh = ro - toff[ks], nw = co - tcol[ks];
+            const int qh = g.S == 2 ? nh >> 1 : nh / g.S, qw = g.S == 2 ? nw >> 1 : nw / g.S;
+            if (toff[ks] >= 0 && qh * g.S == nh && qw * g.S == nw)
+              a = *reinterpret_cast<const bf16x8*>(lds + tb_off(qh * g.Wp + qw, tch[ks]));
+          } else if (toff[ks] >= 0) {
+            a = *reinterpret_cast<const bf16x8*>(lds + tb_off(base + toff[ks], tch[ks]));
+          }
           acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[ks], acc[m], 0, 0, 0);
         }
       }
@@ -325,16 +346,32 @@ inline bool band_geom(TGeom& t, int Hi, int Wi, int C, int Co, int Ho, int Wo, i
   t.Hi = Hi; t.Wi = Wi; t.C = C; t.Ho = Ho; t.Wo = Wo; t.KH = KH; t.KW = KW; t.S = S; t.P = P; t.D = D;
   t.T = KH * KW; t.Kp = Kp; t.Cog = Cog; t.Cg = Cg;
   t.R = R; t.rows_in = (R - 1) * S + (KH - 1) * D + 1; t.Wp = Wp; t.bands = (Ho + R - 1) / R;
+  t.wc0 = -P;
   return true;
 }
 
-template <bool FLIP>
+// the strided input gradient (MODE 2): operand dy [Hi=Hdy][Wi=Wdy], output dx [Ho][Wo]; the
+// staged dy rows of a band of R dx rows are at most (R-1+(KH-1)D)/S + 2, columns wc0 ..
+inline bool band_geom_tr(TGeom& t, int Hi, int Wi, int C, int Co, int Ho, int Wo, int KH, int KW, int S, int P,
+                         int D, int Cg, int Cog, int KB, int Kp) {
+  if (!band_geom(t, Hi, Wi, C, Co, Ho, Wo, KH, KW, 1, 0, 1, Cg, Cog, KB, Kp)) return false;  // shape gates
+  const int wc0 = floordiv(P - (KW - 1) * D, S);
+  const int Wp = floordiv(Wo - 1 + P, S) - wc0 + 1;
+  auto rows_in = [&](int R) { return (R - 1 + (KH - 1) * D) / S + 2; };
+  int R = min(Ho, TB_MAXPX / Wo);
+  while (R >= 1 && rows_in(R) * Wp * 128 > TB_LDS) --R;
+  if (R < 1) return false;
+  t.S = S; t.P = P; t.D = D; t.R = R; t.rows_in = rows_in(R); t.Wp = Wp; t.bands = (Ho + R - 1) / R; t.wc0 = wc0;
+  return true;
+}
+
+template <int MODE>
 inline void launch_band(const TGeom& t, int N, int KB, const bf16* in, const bf16* wb, bf16* out, float* sum,
                         float* sumsq, hipStream_t st) {
   const dim3 grid((unsigned)(N * t.bands), t.C / TB_CS);
-  if (KB == 16) hipLaunchKernelGGL((gconv_band_kernel<16, FLIP>), grid, dim3(NT), 0, st, in, wb, out, sum, sumsq, t);
-  else if (KB == 32) hipLaunchKernelGGL((gconv_band_kernel<32, FLIP>), grid, dim3(NT), 0, st, in, wb, out, sum, sumsq, t);
-  else hipLaunchKernelGGL((gconv_band_kernel<64, FLIP>), grid, dim3(NT), 0, st, in, wb, out, sum, sumsq, t);
+  if (KB == 16) hipLaunchKernelGGL((gconv_band_kernel<16, MODE>), grid, dim3(NT), 0, st, in, wb, out, sum, sumsq, t);
+  else if (KB == 32) hipLaunchKernelGGL((gconv_band_kernel<32, MODE>), grid, dim3(NT), 0, st, in, wb, out, sum, sumsq, t);
+  else hipLaunchKernelGGL((gconv_band_kernel<64, MODE>), grid, dim3(NT), 0, st, in, wb, out, sum, sumsq, t);
 }
 
 // ------------------------------------------------------------------ grouped wgrad
@@ -933,7 +970,7 @@ MLC_EXPORT int mlc_gconv_fwd(const bf16* x, const bf16* w, bf16* wb, bf16* y, fl
                      C, g.T, g.Cg, g.Cog, g.KB, g.Kp, 0);
   TGeom t;
   if (band_geom(t, H, W, C, Co, Ho, Wo, KH, KW, S, P, D, g.Cg, g.Cog, g.KB, g.Kp)) {
-    launch_band<false>(t, N, g.KB, x, wb, y, sum, sumsq, st);
+    launch_band<0>(t, N, g.KB, x, wb, y, sum, sumsq, st);
     return hipGetLastError();
   }
   const dim3 grid((unsigned)((g.M + 127) / 128), (Co + 15) / 16);
@@ -953,7 +990,11 @@ MLC_EXPORT int mlc_gconv_dgrad(const bf16* dy, const bf16* w, bf16* wb, bf16* dx
   // stride 1: a forward conv of dy over the transposed filter, taps mirrored
   if (S == 1 && D * (KH - 1) >= P && D * (KW - 1) - P == D * (KH - 1) - P &&
       band_geom(t, Ho, Wo, Co, C, H, W, KH, KW, 1, D * (KH - 1) - P, D, g.Cg, g.Cog, g.KB, g.Kp)) {
-    launch_band<true>(t, N, g.KB, dy, wb, dx, nullptr, nullptr, st);
+    launch_band<1>(t, N, g.KB, dy, wb, dx, nullptr, nullptr, st);
+    return hipGetLastError();
+  }
+  if (S > 1 && band_geom_tr(t, Ho, Wo, Co, C, H, W, KH, KW, S, P, D, g.Cg, g.Cog, g.KB, g.Kp)) {
+    launch_band<2>(t, N, g.KB, dy, wb, dx, nullptr, nullptr, st);
     return hipGetLastError();
   }
   const dim3 grid((unsigned)((g.M + 127) / 128), (C + 15) / 16);

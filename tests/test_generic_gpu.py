@@ -37,7 +37,9 @@ def _bf(*shape, scale=1.0):
     # ResNeXt-50 32x4d / 101 32x8d shapes on the row-band kernel (several bands per image,
     # stride 2, dilation 2, 64-wide groups)
     (2, 56, 56, 128, 4, 3, 1, 1, 1, 128), (2, 56, 56, 256, 8, 3, 2, 1, 1, 256), (2, 28, 28, 512, 16, 3, 1, 1, 1, 512),
-    (3, 7, 7, 1024, 32, 3, 1, 1, 1, 1024), (2, 20, 22, 256, 64, 3, 1, 2, 2, 256)])
+    (3, 7, 7, 1024, 32, 3, 1, 1, 1, 1024), (2, 20, 22, 256, 64, 3, 1, 2, 2, 256),
+    # strided input gradients on the band kernel: odd sizes, dilation, pad 0
+    (2, 17, 15, 128, 4, 3, 2, 1, 1, 128), (2, 21, 19, 64, 16, 3, 2, 2, 2, 64), (2, 12, 13, 128, 32, 3, 2, 0, 1, 128)])
 def test_grouped_conv_kernels_vs_fp32(N, H, W, C, Cg, k, s, p, d, Co):
     torch.manual_seed(0)
     groups = C // Cg
