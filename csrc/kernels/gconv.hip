@@ -198,6 +198,28 @@ __host__ __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ?
 
 __device__ __forceinline__ int tb_off(int pix, int c) { return pix * 128 + ((c ^ ((pix >> 1) & 7)) << 4); }
 
+// LDS-DMA staging (buffer_load ... lds, no VGPR round trip, every load of the stage in flight
+// at once): `npix` staged pixels of 128-byte slab rows into `img` in the tb_off layout.  A
+// wave instruction fills 8 consecutive pixel rows (1 KB, lane-linear), so the swizzle moves to
+// the source side: lane l fetches logical chunk (l & 7) ^ ((P >> 1) & 7) of pixel P.  voff(P, c)
+// is that chunk's byte offset from the resource base, or TB_OOB for zeros (padding).
+typedef __amdgpu_buffer_rsrc_t TRsrc;
+constexpr unsigned TB_OOB = 0x80000000u;
+__device__ __forceinline__ TRsrc tb_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7ffffff0, 0x00020000);
+}
+template <class F>
+__device__ __forceinline__ void tb_dma(char* img, int npix, TRsrc rs, F voff) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  char* dst0 = img + __builtin_amdgcn_readfirstlane(wave) * 1024;
+  for (int r = 0; r * 32 < npix; ++r) {
+    const int P = r * 32 + wave * 8 + (lane >> 3), c = (lane & 7) ^ ((P >> 1) & 7);
+    const unsigned vo = P < npix ? voff(P, c) : TB_OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst0 + r * 4096), 16, vo,
+                                             0, 0, 0);
+  }
+}
+
 // MODE 0: forward; 1: stride-1 input gradient (FLIP); 2: strided input gradient - output
 // pixel (oh, ow) takes tap (r, c) from dy pixel ((oh + P - rD) / S, (ow + P - cD) / S) when
 // both divide (the transposed conv; the operand rows staged are those the band reaches)
@@ -211,25 +233,15 @@ gconv_band_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wb, bf16
   const int cs0 = blockIdx.y * TB_CS;
   const int rows = min(g.R, g.Ho - oh0), npx = rows * g.Wo;
   const int hi0 = MODE == 2 ? floordiv(oh0 + g.P - (g.KH - 1) * g.D, g.S) : oh0 * g.S - g.P;
-  // ---- stage the slab's input rows hi0 .. hi0+rows_in-1, columns -P .. -P+Wp-1 (zeros outside)
-  const int nchunk = g.rows_in * g.Wp * 8;
-  for (int i0 = 0; i0 < nchunk; i0 += NT * 4) {
-    uint4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = i0 + u * NT + tid;
-      const int pix = i >> 3, c = i & 7;
+  // ---- stage the slab's input rows hi0 .. hi0+rows_in-1, columns wc0 .. wc0+Wp-1 (zeros outside)
+  {
+    const TRsrc rs = tb_rsrc(in + (long)n * g.Hi * g.Wi * g.C + cs0);
+    tb_dma(lds, g.rows_in * g.Wp, rs, [&](int pix, int c) -> unsigned {
       const int ir = pix / g.Wp, ic = pix - ir * g.Wp;
       const int hi = hi0 + ir, wi = ic + g.wc0;
-      v[u] = make_uint4(0u, 0u, 0u, 0u);
-      if (i < nchunk && (unsigned)hi < (unsigned)g.Hi && (unsigned)wi < (unsigned)g.Wi)
-        v[u] = ldg16(in + (((long)n * g.Hi + hi) * g.Wi + wi) * g.C + cs0 + 8 * c);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = i0 + u * NT + tid;
-      if (i < nchunk) *reinterpret_cast<uint4*>(lds + tb_off(i >> 3, i & 7)) = v[u];
-    }
+      return (unsigned)hi < (unsigned)g.Hi && (unsigned)wi < (unsigned)g.Wi
+                 ? (unsigned)((hi * g.Wi + wi) * g.C + 8 * c) * 2u : TB_OOB;
+    });
   }
   // ---- B fragments of this wave's 16-channel output block (all K-steps, registers)
   constexpr int MAXKS = (9 * KB + 31) / 32;   // up to 3x3 taps
@@ -263,6 +275,7 @@ gconv_band_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wb, bf16
       tch[ks] = 0;
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's DMA (and B loads) landed
   __syncthreads();
   // ---- MFMA rows of 16 output pixels (flattened over the band's rows)
   const int nrow = (npx + 15) / 16;
@@ -372,6 +385,101 @@ inline void launch_band(const TGeom& t, int N, int KB, const bf16* in, const bf1
   if (KB == 16) hipLaunchKernelGGL((gconv_band_kernel<16, MODE>), grid, dim3(NT), 0, st, in, wb, out, sum, sumsq, t);
   else if (KB == 32) hipLaunchKernelGGL((gconv_band_kernel<32, MODE>), grid, dim3(NT), 0, st, in, wb, out, sum, sumsq, t);
   else hipLaunchKernelGGL((gconv_band_kernel<64, MODE>), grid, dim3(NT), 0, st, in, wb, out, sum, sumsq, t);
+}
+
+// ------------------------------------------------------------------ grouped wgrad, row bands
+// dw[oc][t][ci] (+)= sum_p dy[p][oc] x[p@t][ci] with the forward's row-band staging: a block
+// walks a run of (image, band) pairs of one 64-channel slab, stages the band's x rows and its
+// dy pixels [px][64] in LDS with coalesced 16-byte loads, and each wave (one 16-channel output
+// block) runs K = 32 pixels per MFMA with both operands read transposed (ds_read_b64_tr_b16,
+// as gconv_wgrad_kernel's tr_frag, from the swizzled 128-byte pixel rows); the T x KB/16
+// accumulator tiles stay in registers over the whole run, then one atomic per in-group weight.
+typedef short s16x4b __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8 band_tr_frag(const char* lds, int pa, int pb, int ch) {
+  // lane rows pa (8g+q) and pb (8g+4+q), channels ch..ch+3 (ch % 4 == 0)
+  const int within = (ch & 7) * 2;
+  const s16x4b lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4b))(lds + tb_off(pa, ch >> 3) + within));
+  const s16x4b hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4b))(lds + tb_off(pb, ch >> 3) + within));
+  typedef short s16x8b __attribute__((ext_vector_type(8)));
+  const s16x8b r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+template <int KB>
+__global__ void __launch_bounds__(NT)
+gconv_band_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* __restrict__ dw, TGeom g,
+                        int nb_total, int per_block) {
+  __shared__ __attribute__((aligned(16))) char ldx[TB_LDS];
+  __shared__ __attribute__((aligned(16))) char ldy[TB_MAXPX * 128];
+  constexpr int NSUB = KB / 16, MAXT = 9;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cs0 = blockIdx.y * TB_CS, ob = wave, oc0 = cs0 + 16 * ob;
+  const int cb = blk_cbase(oc0, g.Cog, g.Cg) - cs0;
+  const int gq = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  // tap offsets (staged pixels) for this kernel's taps
+  int toff[MAXT];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    const int r = t / g.KW, c = t - r * g.KW;
+    toff[t] = t < g.T ? r * g.D * g.Wp + c * g.D : 0;
+  }
+  f32x4 acc[MAXT][NSUB];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t)
+#pragma unroll
+    for (int sb = 0; sb < NSUB; ++sb) acc[t][sb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int b0 = blockIdx.x * per_block, b1 = min(nb_total, b0 + per_block);
+  for (int bb = b0; bb < b1; ++bb) {
+    const int n = bb / g.bands, oh0 = (bb - n * g.bands) * g.R;
+    const int rows = min(g.R, g.Ho - oh0), npx = rows * g.Wo, npx32 = (npx + 31) & ~31;
+    const int hi0 = oh0 * g.S - g.P;
+    __syncthreads();   // the previous band's LDS reads are done
+    tb_dma(ldx, g.rows_in * g.Wp, tb_rsrc(x + (long)n * g.Hi * g.Wi * g.C + cs0), [&](int pix, int c) -> unsigned {
+      const int ir = pix / g.Wp, ic = pix - ir * g.Wp;
+      const int hi = hi0 + ir, wi = ic + g.wc0;
+      return (unsigned)hi < (unsigned)g.Hi && (unsigned)wi < (unsigned)g.Wi
+                 ? (unsigned)((hi * g.Wi + wi) * g.C + 8 * c) * 2u : TB_OOB;
+    });
+    tb_dma(ldy, npx32, tb_rsrc(dy + ((long)n * g.Ho + oh0) * g.Wo * g.C + cs0), [&](int q, int c) -> unsigned {
+      return q < npx ? (unsigned)(q * g.C + 8 * c) * 2u : TB_OOB;
+    });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int px0 = 0; px0 < npx32; px0 += 32) {
+      const int ra = px0 + 8 * gq + qq, rb = ra + 4;
+      const bf16x8 fa = band_tr_frag(ldy, ra, rb, 16 * ob + 4 * pp);
+      // the x pixels of rows ra / rb at tap (0, 0) (dy is zero past npx: clamp)
+      const int qa = min(ra, npx - 1), qb = min(rb, npx - 1);
+      const int oha = qa / g.Wo, ohb = qb / g.Wo;
+      const int basea = oha * g.S * g.Wp + (qa - oha * g.Wo) * g.S;
+      const int baseb = ohb * g.S * g.Wp + (qb - ohb * g.Wo) * g.S;
+#pragma unroll
+      for (int t = 0; t < MAXT; ++t) {
+        if (t < g.T) {
+#pragma unroll
+          for (int sb = 0; sb < NSUB; ++sb) {
+            const bf16x8 fb = band_tr_frag(ldx, basea + toff[t], baseb + toff[t], cb + 16 * sb + 4 * pp);
+            acc[t][sb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[t][sb], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+  // D[m = oc][n = ci]: lane column n = lane & 15, rows 4*(lane>>4) + i; off-group products dropped
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    if (t < g.T) {
+#pragma unroll
+      for (int sb = 0; sb < NSUB; ++sb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int oc = oc0 + 4 * gq + i, ci = cs0 + cb + 16 * sb + i16;
+          const int grp = oc / g.Cog;
+          if (ci / g.Cg == grp && ci < g.C) atomicAdd(dw + ((long)oc * g.T + t) * g.Cg + (ci - grp * g.Cg), acc[t][sb][i]);
+        }
+    }
+  }
 }
 
 // ------------------------------------------------------------------ grouped wgrad
@@ -1008,6 +1116,19 @@ MLC_EXPORT int mlc_gconv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, 
   if (!grouped_ok(C, Co, groups)) return -1;
   const GGeom g = mkg(N, H, W, C, Ho, Wo, Co, KH, KW, S, P, D, C / groups, Co / groups);
   if (!accumulate) mlc_zero_f32(dw, (long)Co * g.T * g.Cg, st);
+  TGeom t;
+  static const int band_wg = getenv("MLC_GCONV_BAND_WGRAD") ? atoi(getenv("MLC_GCONV_BAND_WGRAD")) : 1;
+  if (band_wg && band_geom(t, H, W, C, Co, Ho, Wo, KH, KW, S, P, D, g.Cg, g.Cog, g.KB, g.Kp)) {
+    // runs of bands per block: ~640 blocks over the chip (2 per CU fit the 80 KB of LDS)
+    const int slabs = C / TB_CS, nb_total = N * t.bands;
+    int per = (int)(((long)nb_total * slabs + 639) / 640);
+    if (per < 1) per = 1;
+    const dim3 grid((unsigned)((nb_total + per - 1) / per), slabs);
+    if (g.KB == 16) hipLaunchKernelGGL(gconv_band_wgrad_kernel<16>, grid, dim3(NT), 0, st, dy, x, dw, t, nb_total, per);
+    else if (g.KB == 32) hipLaunchKernelGGL(gconv_band_wgrad_kernel<32>, grid, dim3(NT), 0, st, dy, x, dw, t, nb_total, per);
+    else hipLaunchKernelGGL(gconv_band_wgrad_kernel<64>, grid, dim3(NT), 0, st, dy, x, dw, t, nb_total, per);
+    return hipGetLastError();
+  }
   const int ncb = g.T * (g.KB / 16);
   const int zb = (ncb + WG_NCB - 1) / WG_NCB;
   const int base = ((Co + 15) / 16) * zb;
