@@ -851,55 +851,44 @@ dw_fwd_strip_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, bf16
 
 // weight gradient of filter row r = blockIdx.y: acc[q] = sum over pixels dy[p] * x[p@(r,q)],
 // reduced per block (LDS) and added into copy (block % NCOPY) of ws[NCOPY][KH*KW][C]
-template <int KW, int S, int SW, bool PIPE>
+template <int KW, int S>
 __global__ void __launch_bounds__(NT)
 dw_wgrad_strip_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* __restrict__ ws, int N,
                       int H, int W, int C, int Ho, int Wo, int KH, int P) {
-  constexpr int XS = (SW - 1) * S + KW;
-  __shared__ float rb[NT][8 + 1];     // one tap at a time in the block reduction
+  constexpr int XS = (DW_SW - 1) * S + KW;
+  __shared__ float rb[NT][KW * 8 + 1];
   const int G = C >> 3;
   const int r = blockIdx.y;
-  const int Wq = (Wo + SW - 1) / SW;
+  const int Wq = (Wo + DW_SW - 1) / DW_SW;
   const long total = (long)N * Ho * Wq * G;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
-  const long stride = (long)gridDim.x * NT;
   const int cg = (int)(gtid % G);
   float acc[KW][8];
 #pragma unroll
   for (int q = 0; q < KW; ++q)
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[q][e] = 0.f;
-  // software-pipelined: the next item's strips are loaded while this one's FMAs run (a row
-  // outside the image or an item past the end loads zeros)
-  auto load = [&](long i, uint4 (&gv)[SW], uint4 (&xv)[XS]) {
-    const bool in = i < total;
-    const long ii = in ? i : gtid;
-    long t = ii / G;
+  for (long i = gtid; i < total; i += (long)gridDim.x * NT) {
+    long t = i / G;
     const int wq = (int)(t % Wq); t /= Wq;
     const int ho = (int)(t % Ho);
     const int n = (int)(t / Ho);
     const int hi = ho * S - P + r;
-    const bool rowok = in && (unsigned)hi < (unsigned)H;
-    const int wo0 = wq * SW;
+    if ((unsigned)hi >= (unsigned)H) continue;
+    const int wo0 = wq * DW_SW;
     const int wi0 = wo0 * S - P;
     const bf16* dyr = dy + ((long)n * Ho + ho) * Wo * C + cg * 8;
-    const bf16* xr = x + ((long)n * H + (rowok ? hi : 0)) * W * C + cg * 8;
+    const bf16* xr = x + ((long)n * H + hi) * W * C + cg * 8;
+    uint4 gv[DW_SW], xv[XS];
 #pragma unroll
-    for (int o = 0; o < SW; ++o) gv[o] = ld_or_zero(dyr, (long)(wo0 + o) * C, rowok && wo0 + o < Wo);
+    for (int o = 0; o < DW_SW; ++o) gv[o] = ld_or_zero(dyr, (long)(wo0 + o) * C, wo0 + o < Wo);
 #pragma unroll
     for (int j = 0; j < XS; ++j) {
       const int wi = wi0 + j;
-      xv[j] = ld_or_zero(xr, (long)wi * C, rowok && (unsigned)wi < (unsigned)W);
+      xv[j] = ld_or_zero(xr, (long)wi * C, (unsigned)wi < (unsigned)W);
     }
-  };
-  uint4 gv[SW], xv[XS];
-  if (PIPE) load(gtid, gv, xv);
-  for (long i = gtid; i < total; i += stride) {
-    uint4 gn[SW], xn[XS];
-    if (PIPE) load(i + stride, gn, xn);
-    else load(i, gv, xv);
 #pragma unroll
-    for (int o = 0; o < SW; ++o) {
+    for (int o = 0; o < DW_SW; ++o) {
       float gf[8];
       unpack8(gv[o], gf);
 #pragma unroll
@@ -910,30 +899,23 @@ dw_wgrad_strip_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, f
         for (int e = 0; e < 8; ++e) acc[q][e] += gf[e] * xf[e];
       }
     }
-    if (PIPE) {
-#pragma unroll
-      for (int o = 0; o < SW; ++o) gv[o] = gn[o];
-#pragma unroll
-      for (int j = 0; j < XS; ++j) xv[j] = xn[j];
-    }
   }
   const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < KW; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) rb[tid][q * 8 + e] = acc[q][e];
+  __syncthreads();
   const int lanes = NT < G ? NT : G;
   const int base_cg = (int)(((long)blockIdx.x * NT) % G);
   float* dst = ws + (long)(blockIdx.x % NCOPY) * KH * KW * C;
-#pragma unroll
-  for (int q = 0; q < KW; ++q) {
-    if (q) __syncthreads();
-#pragma unroll
-    for (int e = 0; e < 8; ++e) rb[tid][e] = acc[q][e];
-    __syncthreads();
-    for (int qq = tid; qq < lanes * 8; qq += NT) {
-      const int l = qq % lanes, e = qq / lanes;
-      float a = 0.f;
-      for (int u = l; u < NT; u += G) a += rb[u][e];
-      const int c = ((base_cg + l) % G) * 8 + e;
-      atomicAdd(dst + (long)(r * KW + q) * C + c, a);
-    }
+  for (int qq = tid; qq < lanes * KW * 8; qq += NT) {
+    const int l = qq % lanes, ke = qq / lanes;
+    const int q = ke >> 3, e = ke & 7;
+    float a = 0.f;
+    for (int u = l; u < NT; u += G) a += rb[u][q * 8 + e];
+    const int c = ((base_cg + l) % G) * 8 + e;
+    atomicAdd(dst + (long)(r * KW + q) * C + c, a);
   }
 }
 
@@ -1210,15 +1192,12 @@ MLC_EXPORT int mlc_dwconv_wgrad(const bf16* dy, const bf16* x, float* dw, float*
   const int G = C / 8, T = KH * KW;
   mlc_zero_f32(ws, (long)NCOPY * T * C, st);
   if (D == 1 && (S == 1 || S == 2) && (KW == 3 || KW == 5 || KW == 7) && dw_strips()) {
-    // 3x3: the next strip's loads in flight during this one's FMAs (PIPE; EfficientNet-b0's
-    // 3x3 wgrads 0.90 -> 0.84 ms); 5x5 / 7x7 keep the plain loop: their double-buffered strips
-    // cost occupancy, and narrower strips re-read more (5x5 2.2 -> 3.0 ms, not kept)
     const long work = (long)N * Ho * ((Wo + DW_SW - 1) / DW_SW) * G;
     const dim3 grid(grid_groups(work, G, 512), KH);
-#define DWW(K, SS, PIPE) hipLaunchKernelGGL((dw_wgrad_strip_kernel<K, SS, DW_SW, PIPE>), grid, dim3(NT), 0, st, dy, x, \
-                                            ws, N, H, W, C, Ho, Wo, KH, P)
-    if (S == 1) { if (KW == 3) DWW(3, 1, true); else if (KW == 5) DWW(5, 1, false); else DWW(7, 1, false); }
-    else { if (KW == 3) DWW(3, 2, false); else if (KW == 5) DWW(5, 2, false); else DWW(7, 2, false); }
+#define DWW(K, SS) hipLaunchKernelGGL((dw_wgrad_strip_kernel<K, SS>), grid, dim3(NT), 0, st, dy, x, ws, N, H, W, C, \
+                                      Ho, Wo, KH, P)
+    if (S == 1) { if (KW == 3) DWW(3, 1); else if (KW == 5) DWW(5, 1); else DWW(7, 1); }
+    else { if (KW == 3) DWW(3, 2); else if (KW == 5) DWW(5, 2); else DWW(7, 2); }
 #undef DWW
     hipLaunchKernelGGL(copies_reduce_kernel, dim3(blocks_for((long)T * C)), dim3(NT), 0, st, ws, dw, (long)T * C,
                        accumulate);
