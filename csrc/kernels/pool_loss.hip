@@ -227,6 +227,81 @@ cast_f32_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, long n8)
   }
 }
 
+// ------------------------------------------------------------------ windowed average pool
+// y[n,ho,wo,c] = sum over the KxK/S window (pad P) / div, div = K*K (count_include_pad) or the
+// number of in-image taps; one thread per (output pixel, 8-channel group), fp32 sums.  The
+// backward gathers, per input pixel, the (at most ceil(K/S)^2) windows that cover it.  Inception's
+// 3x3/1 branch pools (the stock NHWC avg_pool2d backward ran ~260 us per call at batch 80).
+__device__ __forceinline__ int ap_div(int ho, int wo, int H, int W, int K, int S, int P, int cip) {
+  if (cip) return K * K;
+  const int h0 = ho * S - P, w0 = wo * S - P;
+  const int nh = min(h0 + K, H) - max(h0, 0), nw = min(w0 + K, W) - max(w0, 0);
+  return nh * nw;
+}
+
+__global__ void __launch_bounds__(NT)
+avgpool2d_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N, int H, int W, int C, int Ho,
+                     int Wo, int K, int S, int P, int cip) {
+  const int G = C / 8;
+  const long total = (long)N * Ho * Wo * G;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int g = (int)(i % G);
+    long t = i / G;
+    const int wo = (int)(t % Wo);
+    t /= Wo;
+    const int ho = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int kh = 0; kh < K; ++kh) {
+      const int h = ho * S - P + kh;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int kw = 0; kw < K; ++kw) {
+        const int w = wo * S - P + kw;
+        if ((unsigned)w >= (unsigned)W) continue;
+        float f[8];
+        unpack8(ldg16(x + (((long)n * H + h) * W + w) * C + g * 8), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += f[e];
+      }
+    }
+    const float inv = 1.f / (float)ap_div(ho, wo, H, W, K, S, P, cip);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    *reinterpret_cast<uint4*>(y + i * 8) = pack8(acc);
+  }
+}
+
+__global__ void __launch_bounds__(NT)
+avgpool2d_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx, int N, int H, int W, int C, int Ho,
+                     int Wo, int K, int S, int P, int cip) {
+  const int G = C / 8;
+  const long total = (long)N * H * W * G;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int g = (int)(i % G);
+    long t = i / G;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    // windows ho with ho*S - P <= h <= ho*S - P + K - 1
+    const int ho_lo = max(0, (h + P - K + S) / S), ho_hi = min(Ho - 1, (h + P) / S);
+    const int wo_lo = max(0, (w + P - K + S) / S), wo_hi = min(Wo - 1, (w + P) / S);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+      if (h + P - ho * S >= K || h + P - ho * S < 0) continue;
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        if (w + P - wo * S >= K || w + P - wo * S < 0) continue;
+        float f[8];
+        unpack8(ldg16(dy + (((long)n * Ho + ho) * Wo + wo) * C + g * 8), f);
+        const float inv = 1.f / (float)ap_div(ho, wo, H, W, K, S, P, cip);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += f[e] * inv;
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + i * 8) = pack8(acc);
+  }
+}
+
 static int blocks_for(long work) {
   long b = (work + NT - 1) / NT;
   if (b > 4096) b = 4096;
@@ -285,5 +360,21 @@ MLC_EXPORT int mlc_nchw_to_nhwc(const float* x, bf16* y, int N, int C, int HW, i
 MLC_EXPORT int mlc_cast_f32_bf16(const float* x, bf16* y, long n, hipStream_t st) {
   if (n % 8) return -1;
   hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(blocks_for(n / 8)), dim3(NT), 0, st, x, y, n / 8);
+  return hipGetLastError();
+}
+
+MLC_EXPORT int mlc_avgpool2d_fwd(const bf16* x, bf16* y, int N, int H, int W, int C, int Ho, int Wo, int K, int S,
+                                 int P, int cip, hipStream_t st) {
+  if (C % 8) return -1;
+  hipLaunchKernelGGL(avgpool2d_fwd_kernel, dim3(blocks_for((long)N * Ho * Wo * (C / 8))), dim3(NT), 0, st, x, y, N, H,
+                     W, C, Ho, Wo, K, S, P, cip);
+  return hipGetLastError();
+}
+
+MLC_EXPORT int mlc_avgpool2d_bwd(const bf16* dy, bf16* dx, int N, int H, int W, int C, int Ho, int Wo, int K, int S,
+                                 int P, int cip, hipStream_t st) {
+  if (C % 8) return -1;
+  hipLaunchKernelGGL(avgpool2d_bwd_kernel, dim3(blocks_for((long)N * H * W * (C / 8))), dim3(NT), 0, st, dy, dx, N, H,
+                     W, C, Ho, Wo, K, S, P, cip);
   return hipGetLastError();
 }

@@ -44,7 +44,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from mlcomp_amd.ops import functional as Fn
-from mlcomp_amd.ops.glayers import (BilinearUp, BNAct, BNParams, ChannelGate, Conv3dAs2d, ConvBNAct, ConvParams,
+from mlcomp_amd.ops.glayers import (AvgPool, BilinearUp, BNAct, BNParams, ChannelGate, Conv3dAs2d, ConvBNAct, ConvParams,
                                     Frames, GlobalAvgPool, LinearAct, LinearParams, MaxPool, TemporalAs2d, UpCat)
 from mlcomp_amd.ops.layers import NativeContext
 from mlcomp_amd.train.native_spec import NativeUnsupported
@@ -308,6 +308,18 @@ class _Lowering:
         site = LinearAct(self.net.ctx, self.net.linear_params(node.target, m), act)
         new = self._site_node(chain[-1], site, [node.args[0]])
         self._replace(chain, new)
+
+    def avgpool2d(self, node, k, s, p, ceil=False, cip=True, div=None):
+        """A square, floor-mode average pool without a divisor override -> ``AvgPool``
+        (others stay torch ops)."""
+        try:
+            k, s, p = _pair(k, 'kernel_size'), _pair(s if s is not None else k, 'stride'), _pair(p, 'padding')
+        except NativeUnsupported:
+            return
+        if ceil or div is not None or not isinstance(node.args[0], fx.Node):
+            return
+        new = self._site_node(node, AvgPool(self.net.ctx, k, s, p, bool(cip)), [node.args[0]])
+        self._replace([node], new)
 
     def maxpool(self, node, k, s, p, d=1, ceil=False, ret=False):
         k, s, p, d = _pair(k, 'kernel_size'), _pair(s if s is not None else k, 'stride'), _pair(p, 'padding'), \
@@ -592,6 +604,9 @@ class _Lowering:
                     self.maxpool(node, m.kernel_size, m.stride, m.padding, m.dilation, m.ceil_mode, m.return_indices)
                 elif isinstance(m, nn.AdaptiveAvgPool2d) and _pair(m.output_size, 'output_size') == 1:
                     self.avgpool(node)
+                elif isinstance(m, nn.AvgPool2d):
+                    self.avgpool2d(node, m.kernel_size, m.stride, m.padding, m.ceil_mode, m.count_include_pad,
+                                   m.divisor_override)
                 elif isinstance(m, (nn.ConvTranspose1d, nn.ConvTranspose3d, nn.LSTM, nn.GRU, nn.RNN,
                                     nn.MultiheadAttention, nn.Bilinear, nn.InstanceNorm2d)):
                     raise NativeUnsupported(f'{node.target}: {type(m).__name__} has no native lowering')
@@ -604,6 +619,16 @@ class _Lowering:
                                  kw.get('padding', args[3] if args[3] is not None else 0),
                                  kw.get('dilation', args[4] if args[4] is not None else 1),
                                  kw.get('ceil_mode', args[5] or False), kw.get('return_indices', args[6] or False))
+                elif t in (F.avg_pool2d, torch._C._nn.avg_pool2d):
+                    args = list(node.args) + [None] * 6
+                    kw = node.kwargs
+                    k = kw.get('kernel_size', args[1])
+                    st = kw.get('stride', args[2])
+                    self.avgpool2d(node, k, st if st not in (None, []) else k,
+                                   kw.get('padding', args[3] if args[3] is not None else 0),
+                                   kw.get('ceil_mode', args[4] or False),
+                                   kw.get('count_include_pad', args[5] if args[5] is not None else True),
+                                   kw.get('divisor_override', args[6]))
                 elif t is F.interpolate:
                     self.interpolate(node)
                 elif t in (operator.mul, torch.mul):

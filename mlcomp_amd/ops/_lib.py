@@ -93,6 +93,8 @@ _SIGS = {
     'mlc_stem_conv_fwd': [vp] * 5 + [i32] * 3 + [vp],
     'mlc_avgpool_fwd': [vp, vp, i32, i32, i32, vp],
     'mlc_avgpool_bwd': [vp, vp, i32, i32, i32, vp],
+    'mlc_avgpool2d_fwd': [vp, vp] + [i32] * 10 + [vp],
+    'mlc_avgpool2d_bwd': [vp, vp] + [i32] * 10 + [vp],
     'mlc_softmax_ce': [vp] * 5 + [i32, i32, i32, f32, f32, vp],
     'mlc_colsum': [vp, vp, i32, i32, vp],
     'mlc_nchw_to_nhwc': [vp, vp, i32, i32, i32, i32, vp],

@@ -658,6 +658,33 @@ def stem_pool_bwd(dp, idx, y, mean, invstd, gamma, dgamma, dbeta, sums, coef):
     return dy
 
 
+def avgpool2d_fwd(x, k, s, p, count_include_pad=True):
+    """KxK/s average pool (pad p, floor mode) of NHWC bf16 ``x`` (pool_loss.hip)."""
+    N, H, W, C = x.shape
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    if _cuda(x):
+        y = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.bfloat16)
+        _lib.call('mlc_avgpool2d_fwd', _lib.ptr(x), _lib.ptr(y), N, H, W, C, Ho, Wo, k, s, p, int(count_include_pad),
+                  _lib.stream())
+        return y
+    yf = F.avg_pool2d(_nchw(x), k, s, p, count_include_pad=count_include_pad)
+    return yf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+
+
+def avgpool2d_bwd(dy, x_shape, k, s, p, count_include_pad=True):
+    N, H, W, C = x_shape
+    _, Ho, Wo, _ = dy.shape
+    if _cuda(dy):
+        dx = torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
+        _lib.call('mlc_avgpool2d_bwd', _lib.ptr(dy.contiguous()), _lib.ptr(dx), N, H, W, C, Ho, Wo, k, s, p,
+                  int(count_include_pad), _lib.stream())
+        return dx
+    with torch.enable_grad():             # called from autograd backward (grad mode off)
+        xf = torch.zeros(N, C, H, W, requires_grad=True)
+        F.avg_pool2d(xf, k, s, p, count_include_pad=count_include_pad).backward(_nchw(dy))
+    return xf.grad.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+
+
 def avgpool_fwd(x):
     N, H, W, C = x.shape
     if _cuda(x):

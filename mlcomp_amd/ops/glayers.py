@@ -1072,6 +1072,29 @@ class MaxPool(Site):
         return [from_nhwc(dx, C)]
 
 
+class AvgPool(Site):
+    """avg_pool2d(x, k, s, p) (square, floor mode, no divisor override) as one NHWC pass each way
+    (pool_loss.hip): Inception's 3x3/1 branch pools, DenseNet's 2x2/2 transitions."""
+
+    def __init__(self, ctx, k, s, p, count_include_pad=True):
+        super().__init__(ctx)
+        self.k, self.s, self.p, self.cip = k, s, p, bool(count_include_pad)
+
+    def forward(self, x):
+        return _run(self, x)
+
+    def fwd(self, x):
+        C = x.shape[1]
+        xn = to_nhwc(x, ceil8(C))
+        y = Fn.avgpool2d_fwd(xn, self.k, self.s, self.p, self.cip)
+        return from_nhwc(y, C), [], tuple(xn.shape)
+
+    def bwd(self, dout, saved, xshape, needs):
+        C = dout.shape[1]
+        dx = Fn.avgpool2d_bwd(to_nhwc(dout, xshape[-1]), xshape, self.k, self.s, self.p, self.cip)
+        return [from_nhwc(dx, C)]
+
+
 class GlobalAvgPool(Site):
     """adaptive_avg_pool2d(x, 1): [N, C, H, W] -> [N, C, 1, 1]."""
 

@@ -57,3 +57,20 @@ def test_bn_row_scale_matches_cpu_reference(C):
         outs[dev] = [v.float().cpu() for v in (z, dy, dres, dg, db)]
     for a, b in zip(outs['cpu'], outs['cuda']):
         assert (a - b).abs().max() <= 2e-2 * a.abs().max() + 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N,H,W,C,k,s,p,cip', [(2, 17, 17, 192, 3, 1, 1, True), (3, 14, 15, 40, 2, 2, 0, True),
+                                               (2, 13, 11, 64, 3, 2, 1, False), (1, 9, 9, 2048, 3, 1, 1, True)])
+def test_avgpool2d_kernels_match_cpu_reference(N, H, W, C, k, s, p, cip):
+    """Windowed average pool (pool_loss.hip) forward / backward vs the fp32 CPU path."""
+    torch.manual_seed(2)
+    x = torch.randn(N, H, W, C).to(torch.bfloat16)
+    y_ref = Fn.avgpool2d_fwd(x, k, s, p, cip)
+    dy = torch.randn_like(y_ref.float()).to(torch.bfloat16)
+    dx_ref = Fn.avgpool2d_bwd(dy, x.shape, k, s, p, cip)
+    y = Fn.avgpool2d_fwd(x.cuda(), k, s, p, cip)
+    dx = Fn.avgpool2d_bwd(dy.cuda(), x.shape, k, s, p, cip)
+    torch.cuda.synchronize()
+    assert (y.float().cpu() - y_ref.float()).abs().max() <= 1e-2 * y_ref.float().abs().max()
+    assert (dx.float().cpu() - dx_ref.float()).abs().max() <= 1e-2 * dx_ref.float().abs().max()

@@ -733,3 +733,41 @@ def test_identity_residual_and_bn_backward_links_are_exact():
     xr = x.clone().requires_grad_()
     F.cross_entropy(ref(xr), y).backward()
     assert _cos(gx_l, xr.grad) > 0.98
+
+
+class _AvgPoolNet(nn.Module):
+    """Inception's 3x3/1 pad-1 branch pool (functional), a DenseNet 2x2/2 transition (module),
+    and a 3x3/2 pad-1 pool without the padding in the divisor, on 20 channels."""
+
+    def __init__(self):
+        super().__init__()
+        self.c1 = nn.Conv2d(3, 20, 3, 1, 1)
+        self.b1 = nn.BatchNorm2d(20)
+        self.trans = nn.AvgPool2d(2, 2)
+        self.c2 = nn.Conv2d(20, 16, 1)
+        self.head = nn.Linear(16, 6)
+
+    def forward(self, x):
+        y = torch.relu(self.b1(self.c1(x)))
+        y = F.avg_pool2d(y, kernel_size=3, stride=1, padding=1) + y
+        y = self.trans(y)
+        y = F.avg_pool2d(self.c2(y), 3, 2, 1, count_include_pad=False)
+        return self.head(F.adaptive_avg_pool2d(y, 1).flatten(1))
+
+
+def test_average_pools_lower_and_match_fp32_autograd():
+    m, ref = _pair(_AvgPoolNet)
+    net = GenericNet(m, 'cpu')
+    kinds = [type(s).__name__ for s in net.train_gm.modules()]
+    assert kinds.count('AvgPool') == 3, kinds
+    x = torch.randn(4, 3, 13, 15)
+    xi, xr = x.clone().requires_grad_(), x.clone().requires_grad_()
+    out, want = net(xi), ref(xr)
+    g = torch.randn_like(want)
+    (out.float() * g).sum().backward()
+    (want * g).sum().backward()
+    assert _rel(out, want) < 2e-2
+    assert _cos(xi.grad, xr.grad) > 0.98
+    for p in net.param_sets():
+        gg = p.w.grad if hasattr(p, 'w') else p.gamma.grad
+        assert _cos(gg, _torch_grad(p, ref)) > 0.98, p.name
