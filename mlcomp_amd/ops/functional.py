@@ -231,7 +231,7 @@ def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=1, pad=0, di
         _lib.call('mlc_conv_dgrad', _lib.ptr(dy), _lib.ptr(w), _lib.ptr(dx), _lib.ptr(addend), N, H, W, C,
                   Co, KH, KW, stride, pack_pad(pad), dil, Ho, Wo, *[_lib.ptr(t) for t in b], _lib.stream())
         return dx
-    if wt is not None and dgrad_as_fwd_conv(KH, KW, stride, pad, dil):   # forward conv over wt
+    if wt is not None and isinstance(pad, int) and dgrad_as_fwd_conv(KH, KW, stride, pad, dil):   # fwd conv over wt
         dxf = F.conv2d(dy.permute(0, 3, 1, 2).float(), wt.permute(0, 3, 1, 2).float(), None, 1,
                        dil * (KH - 1) - pad, dil)
     else:

@@ -265,9 +265,10 @@ class ConvParams:
             self.kind = 'dense'
             self.Cip, self.Cop = ceil8(self.Ci), ceil8(Co)
             self.w = ctx.arena.weight(f'{name}.weight', (self.Cop, KH, KW, self.Cip))
-            if ctx.wt is not None and isinstance(self.pad, int):
+            if ctx.wt is not None:
                 # the transposed, flipped filter copy (one batched refresh per training step,
-                # GenericNet.__call__): the dgrad GEMM reads both operands K-contiguous
+                # GenericNet.__call__): the dgrad GEMM reads both operands K-contiguous (per-axis
+                # pads too: Inception's 1x7 / 7x1 convs)
                 self.wt_idx = ctx.wt.add(self.w)
         elif self.groups == self.Ci and Co == self.Ci:
             self.kind = 'dw'

@@ -74,3 +74,19 @@ def test_avgpool2d_kernels_match_cpu_reference(N, H, W, C, k, s, p, cip):
     torch.cuda.synchronize()
     assert (y.float().cpu() - y_ref.float()).abs().max() <= 1e-2 * y_ref.float().abs().max()
     assert (dx.float().cpu() - dx_ref.float()).abs().max() <= 1e-2 * dx_ref.float().abs().max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('k,pad', [((1, 7), (0, 3)), ((7, 1), (3, 0)), ((1, 3), (0, 1)), ((3, 1), (1, 0))])
+def test_dgrad_with_transposed_filter_per_axis_pad(k, pad):
+    """Input gradient of Inception's 1xn / nx1 convs through the transposed-filter GEMM
+    (mlc_conv_dgrad_t, per-axis padding) vs the fp32 CPU reference."""
+    torch.manual_seed(3)
+    N, H, W, C, Co = 2, 17, 17, 64, 96
+    w = (torch.randn(Co, k[0], k[1], C) * 0.1).to(torch.bfloat16)
+    dy = torch.randn(N, H, W, Co).to(torch.bfloat16)
+    want = Fn.conv2d_dgrad(dy, w, (N, H, W, C), 1, pad, 1)
+    wt = Fn.wt_flip_transpose(w.cuda())
+    got = Fn.conv2d_dgrad(dy.cuda(), w.cuda(), (N, H, W, C), 1, pad, 1, wt=wt)
+    torch.cuda.synchronize()
+    assert (got.float().cpu() - want.float()).abs().max() <= 1e-2 * want.float().abs().max()
