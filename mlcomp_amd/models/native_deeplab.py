@@ -82,7 +82,9 @@ class NativeDeepLab(NativeUnet):
     def _default_schedule(self):
         """The ResNet-101 backbone's long per-layer GEMMs keep the per-conv join (as
         ResNet-50 does): the unjoined chain measured 1,868 / 1,874 vs 1,989 / 1,985 img/s
-        (profiles/round5/seg_wgrad_join_ab.txt)."""
+        (profiles/round5/seg_wgrad_join_ab.txt); their split-K weight gradients add with
+        atomics (1,971 / 1,976 -> 2,005 / 1,998, profiles/round5/wgrad_slab_ab.txt)."""
+        self.ctx.default_wgrad_slab(False)
 
     def _finish_init(self, device):
         self.ctx.finalize(device)

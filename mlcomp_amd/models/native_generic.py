@@ -667,6 +667,9 @@ class GenericNet:
         self.torch_model = model
         self.device = torch.device(device)
         ctx = self.ctx = NativeContext()
+        # split-K conv weight gradients with atomics (ResNet-50 @512 12.89-12.96k -> 13.06-13.11k
+        # img/s, profiles/round5/wgrad_slab_ab.txt)
+        ctx.default_wgrad_slab(False)
         # MLC_GENERIC_WT=1 (default): dense convs keep a transposed, flipped filter copy for
         # their input gradients (Fn.WtTable, refreshed once per training forward), as the
         # hand engines do; 0: the dgrads read the filters directly

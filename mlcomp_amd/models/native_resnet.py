@@ -69,6 +69,9 @@ class NativeResNet:
                  s2d_stem: bool = True):
         self.torch_model = model
         ctx = self.ctx = NativeContext()
+        # split-K weight gradients with atomics, not slabs + a reduce pass: 13,264-13,318 ->
+        # 13,348-13,393 img/s at 512 (interleaved, profiles/round5/wgrad_slab_ab.txt)
+        ctx.default_wgrad_slab(False)
         self.stem, self.pool, self.blocks, _ = lower_resnet_body(ctx, model, s2d_stem=s2d_stem)
         # the classifier never reads the un-pooled stem activation: fuse BN+ReLU+maxpool
         self.stem_pool = StemPool(self.stem) if fuse_stem_pool else None

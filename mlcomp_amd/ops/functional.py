@@ -334,16 +334,19 @@ def slab_workspace(device, n: int) -> torch.Tensor:
 
 
 def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride=1, pad=0, dil=1,
-                 out: Optional[torch.Tensor] = None, accumulate=False, in_affine=None) -> torch.Tensor:
+                 out: Optional[torch.Tensor] = None, accumulate=False, in_affine=None,
+                 slab: Optional[bool] = None) -> torch.Tensor:
     """fp32 weight gradient in [Co, KH, KW, Ci] order (written into ``out`` if given).
-    Split-K partial sums go through a slab workspace and one reduction pass.
+    Split-K partial sums go through a slab workspace and one reduction pass (``slab``; None =
+    MLC_WGRAD_SLAB, default on), or are added with fp32 atomics (``slab=False``).
     ``in_affine``: as in :func:`conv2d_fwd` (x is pre-BN, the input is relu(x*sc + sh))."""
     Co, KH, KW, Ci = w_shape
     N, H, W, C = x.shape
     _, Ho, Wo, _ = dy.shape
     if _cuda(dy):
         dw = out if out is not None else torch.empty(Co, KH, KW, Ci, device=dy.device, dtype=torch.float32)
-        ws = slab_workspace(dy.device, min(32 * Co * KH * KW * Ci, 64 << 20)) if _USE_SLAB else None
+        use = _USE_SLAB if slab is None else slab
+        ws = slab_workspace(dy.device, min(32 * Co * KH * KW * Ci, 64 << 20)) if use else None
         sc, sh = in_affine if in_affine is not None else (None, None)
         _lib.call('mlc_conv_wgrad', _lib.ptr(dy), _lib.ptr(x), _lib.ptr(dw), N, H, W, C, Co, KH, KW,
                   stride, pack_pad(pad), dil, Ho, Wo, 0, int(accumulate), _lib.ptr(ws),
@@ -1103,14 +1106,15 @@ def conv2d_fwd_ex(x, w, bias=None, act=0, stride=1, pad=0, dil=1):
     return yf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
 
 
-def conv2d_wgrad_bias(dy, x, w_shape, dbias, stride=1, pad=0, dil=1, out=None, accumulate=False):
+def conv2d_wgrad_bias(dy, x, w_shape, dbias, stride=1, pad=0, dil=1, out=None, accumulate=False, slab=None):
     """fp32 weight gradient [Co, KH, KW, Ci] and dbias[Co] += colsum(dy), one GEMM."""
     Co, KH, KW, Ci = w_shape
     N, H, W, C = x.shape
     _, Ho, Wo, _ = dy.shape
     if _cuda(dy):
         dw = out if out is not None else torch.empty(Co, KH, KW, Ci, device=dy.device, dtype=torch.float32)
-        ws = slab_workspace(dy.device, min(32 * Co * KH * KW * Ci, 64 << 20)) if _USE_SLAB else None
+        use = _USE_SLAB if slab is None else slab
+        ws = slab_workspace(dy.device, min(32 * Co * KH * KW * Ci, 64 << 20)) if use else None
         _lib.call('mlc_conv_wgrad_bias', _lib.ptr(dy), _lib.ptr(x), _lib.ptr(dw), _lib.ptr(dbias), N, H, W, C, Co,
                   KH, KW, stride, pack_pad(pad), dil, Ho, Wo, int(accumulate), _lib.ptr(ws), ws.numel() if ws is not None else 0,
                   _lib.stream())

@@ -390,22 +390,24 @@ class ConvParams:
         acc = self.ctx.grad_prezeroed
         if self.kind == 's2d':
             if self.b is not None:
-                Fn.conv2d_wgrad_bias(dy, x, self.w.shape, self.b.grad, 1, 0, 1, out=self.w.grad, accumulate=acc)
+                Fn.conv2d_wgrad_bias(dy, x, self.w.shape, self.b.grad, 1, 0, 1, out=self.w.grad, accumulate=acc,
+                                     slab=self.ctx.wgrad_slab)
             else:
-                Fn.conv2d_wgrad(dy, x, self.w.shape, 1, 0, 1, out=self.w.grad, accumulate=acc)
+                Fn.conv2d_wgrad(dy, x, self.w.shape, 1, 0, 1, out=self.w.grad, accumulate=acc, slab=self.ctx.wgrad_slab)
             self.w.grad.mul_(self._gmask)
             return
         if self.kind == 'dense':
             if self.b is not None:
                 Fn.conv2d_wgrad_bias(dy, x, self.w.shape, self.b.grad, self.stride, self.pad, self.dil,
-                                     out=self.w.grad, accumulate=acc)
+                                     out=self.w.grad, accumulate=acc, slab=self.ctx.wgrad_slab)
             else:
                 Fn.conv2d_wgrad(dy, x, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad,
-                                accumulate=acc)
+                                accumulate=acc, slab=self.ctx.wgrad_slab)
         elif self.kind == 'dw':
             Fn.dwconv_wgrad(dy, x, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad, accumulate=acc)
         elif self.kind == 'tr':   # the conv wgrad with the roles of x and dy swapped
-            Fn.conv2d_wgrad(x, dy, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad, accumulate=acc)
+            Fn.conv2d_wgrad(x, dy, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad, accumulate=acc,
+                            slab=self.ctx.wgrad_slab)
         else:
             Fn.gconv_wgrad(dy, x, self.w.shape, self.groups, self.stride, self.pad, self.dil, out=self.w.grad,
                            accumulate=acc)

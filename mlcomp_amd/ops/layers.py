@@ -95,6 +95,16 @@ class NativeContext:
         self.wgrad_defer = False
         self._pending_wgrad = []       # (event, operands kept alive, slots to mark), oldest first
         self.dgrad_first = DGRAD_FIRST_ENV == '1'
+        # split-K conv weight gradients through fp32 slabs + a reduce pass (True) or straight
+        # fp32 atomics (False); engines pick their measured default, MLC_WGRAD_SLAB overrides
+        self.wgrad_slab = os.environ.get('MLC_WGRAD_SLAB', '1') != '0'
+
+    def default_wgrad_slab(self, on: bool):
+        """Engine default for the conv weight-gradient split-K reduction (MLC_WGRAD_SLAB
+        overrides).  Interleaved A/B, profiles/round5/wgrad_slab_ab.txt: atomics win on ResNet-50
+        (hand +0.6 %, generic +1.2 %) and DeepLab (+1.3 %), slabs on U-Net (+1.5 %)."""
+        if os.environ.get('MLC_WGRAD_SLAB') is None:
+            self.wgrad_slab = on
 
     def default_dgrad_first(self, on: bool):
         """Engine default for the capture order (MLC_DGRAD_FIRST overrides it)."""
@@ -322,7 +332,7 @@ class ConvBN:
         slot ready once nothing later in backward reads the weight (its dgrad): a marked
         bucket may be updated by the optimizer right away (GradBucketer)."""
         Fn.conv2d_wgrad(dy, x, self.w.shape, self.stride, self.pad, self.dil, out=self.w.grad,
-                        accumulate=self.ctx.grad_prezeroed, in_affine=in_affine)
+                        accumulate=self.ctx.grad_prezeroed, in_affine=in_affine, slab=self.ctx.wgrad_slab)
         if self.s2d:
             self.w.grad.mul_(self._gmask)
 
