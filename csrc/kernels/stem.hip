@@ -31,8 +31,8 @@ __device__ __forceinline__ uint4 ld16(const bf16* p) { return *reinterpret_cast<
 __global__ void __launch_bounds__(NT)
 stem_pool_fwd_kernel(const bf16* __restrict__ y, const float* __restrict__ scale,
                      const float* __restrict__ shift, bf16* __restrict__ out,
-                     uint8_t* __restrict__ idx, int H, int W, int C, int Ho, int Wo, int rows_total,
-                     int ROWS, int gshift) {
+                     uint8_t* __restrict__ idx, bf16* __restrict__ ymax, int H, int W, int C, int Ho, int Wo,
+                     int rows_total, int ROWS, int gshift) {
   const int G = C >> 3;
   const int cg = threadIdx.x & (G - 1);
   const int c0 = cg * 8;
@@ -51,10 +51,10 @@ stem_pool_fwd_kernel(const bf16* __restrict__ y, const float* __restrict__ scale
     {
       const int h0 = 2 * ho - 1;
       const int w0 = 2 * wo - 1;
-      float best[8];
+      float best[8], bv[8];
       int arg[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; }
+      for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; bv[j] = 0.f; }
       // branch-free: the 9 taps load from clamped (always valid) addresses, all in flight
       // at once; taps outside the image are masked out of the max
       uint4 v[3][3];
@@ -76,7 +76,7 @@ stem_pool_fwd_kernel(const bf16* __restrict__ y, const float* __restrict__ scale
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float a = ok ? f[j] * sc[j] + sh[j] : -INFINITY;
-            if (a > best[j]) { best[j] = a; arg[j] = kh * 3 + kw; }
+            if (a > best[j]) { best[j] = a; arg[j] = kh * 3 + kw; bv[j] = f[j]; }
           }
         }
       }
@@ -90,6 +90,9 @@ stem_pool_fwd_kernel(const bf16* __restrict__ y, const float* __restrict__ scale
       const size_t o = ((size_t)row * Wo + wo) * C + c0;
       *reinterpret_cast<uint4*>(out + o) = pack8(best);
       *reinterpret_cast<uint2*>(idx + o) = make_uint2(lo, hi);
+      // the pre-BN value at the argmax: the backward's reduction runs over the pooled tensor
+      // (exact: y is bf16, so is this copy)
+      if (ymax) *reinterpret_cast<uint4*>(ymax + o) = pack8(bv);
     }
   }
 }
@@ -268,6 +271,60 @@ stem_s2d_kernel(const bf16* __restrict__ x, bf16* __restrict__ out, int N, int H
 
 constexpr int ROWS_PER_BLOCK = 4;
 
+// The backward's reduction from the pooled side: sum dU = sum over pooled outputs of dp
+// (ReLU-active windows), sum dU*(y-mean) = sum of dp*(ymax-mean) (an input pixel chosen by
+// several windows gets each window's gradient: the same sums as over the scattered dU).  Reads
+// dp, idx and ymax (4x smaller than y) instead of y plus a 2x2 window gather per input pixel.
+__global__ void __launch_bounds__(NT)
+stem_pool_reduce_pooled_kernel(const bf16* __restrict__ dp, const uint8_t* __restrict__ idx,
+                               const bf16* __restrict__ ymax, const float* __restrict__ mean,
+                               float* __restrict__ sums, int C, long total_groups, int ncopy) {
+  const int G = C >> 3;
+  const int cg = threadIdx.x & (G - 1);    // constant per thread: G | 256, stride NT*gridDim
+  const int c0 = cg * 8;
+  float mu[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; s1[j] = 0.f; s2[j] = 0.f; }
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total_groups; i += (long)gridDim.x * NT) {
+    const size_t o = (size_t)i * 8;
+    float g[8], v[8];
+    unpack8(ld16(dp + o), g);
+    unpack8(ld16(ymax + o), v);
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 a = *reinterpret_cast<const u32x2*>(idx + o);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t word = j < 4 ? a.x : a.y;
+      const bool on = ((word >> (8 * (j & 3))) & 0xffu) != NOGRAD;
+      const float d = on ? g[j] : 0.f;
+      s1[j] += d;
+      s2[j] += d * (v[j] - mu[j]);
+    }
+  }
+  __shared__ float red[NT / 64][64][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    for (int o = G; o < 64; o <<= 1) {
+      s1[j] += __shfl_xor(s1[j], o, 64);
+      s2[j] += __shfl_xor(s2[j], o, 64);
+    }
+  }
+  if (lane < G) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { red[wave][lane][j] = s1[j]; red[wave][lane][8 + j] = s2[j]; }
+  }
+  __syncthreads();
+  if (threadIdx.x < G * 16) {
+    const int g = threadIdx.x >> 4, v = threadIdx.x & 15;
+    float acc = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < NT / 64; ++wv) acc += red[wv][g][v];
+    float* dst = sums + (size_t)(blockIdx.x % ncopy) * 2 * C;
+    atomicAdd(dst + (v < 8 ? 0 : C) + g * 8 + (v & 7), acc);
+  }
+}
+
 bool shape_ok(int C) {   // G = C/8 a power of two <= 64 (one wave covers every group)
   const int G = C >> 3;
   return C % 8 == 0 && G >= 1 && G <= 64 && (G & (G - 1)) == 0;
@@ -276,13 +333,13 @@ bool shape_ok(int C) {   // G = C/8 a power of two <= 64 (one wave covers every 
 }  // namespace
 
 MLC_EXPORT int mlc_stem_pool_fwd(const bf16* y, const float* scale, const float* shift, bf16* out,
-                                 uint8_t* idx, int N, int H, int W, int C, hipStream_t st) {
+                                 uint8_t* idx, bf16* ymax, int N, int H, int W, int C, hipStream_t st) {
   if (!shape_ok(C)) return -1;
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;   // 3x3, stride 2, pad 1
   const int rows = N * Ho;
   const int blocks = (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
-  hipLaunchKernelGGL(stem_pool_fwd_kernel, dim3(blocks), dim3(NT), 0, st, y, scale, shift, out, idx, H,
-                     W, C, Ho, Wo, rows, ROWS_PER_BLOCK, __builtin_ctz(C >> 3));
+  hipLaunchKernelGGL(stem_pool_fwd_kernel, dim3(blocks), dim3(NT), 0, st, y, scale, shift, out, idx, ymax,
+                     H, W, C, Ho, Wo, rows, ROWS_PER_BLOCK, __builtin_ctz(C >> 3));
   return hipGetLastError();
 }
 
@@ -298,6 +355,21 @@ MLC_EXPORT int mlc_stem_pool_bwd_reduce(const bf16* dp, const uint8_t* idx, cons
   hipLaunchKernelGGL(stem_pool_bwd_kernel<false>, dim3(blocks), dim3(NT), 0, st, dp, idx, y, mean,
                      nullptr, sums, nullptr, H, W, C, Ho, Wo, rows, ROWS_PER_BLOCK, __builtin_ctz(C >> 3),
                      g_mlc_ncopy);
+  return hipGetLastError();
+}
+
+// the same sums from the pooled side (ymax from mlc_stem_pool_fwd)
+MLC_EXPORT int mlc_stem_pool_bwd_reduce_pooled(const bf16* dp, const uint8_t* idx, const bf16* ymax,
+                                               const float* mean, float* sums, int N, int H, int W, int C,
+                                               hipStream_t st) {
+  if (!shape_ok(C)) return -1;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const long groups = (long)N * Ho * Wo * (C / 8);
+  long blocks = (groups + NT - 1) / NT;
+  if (blocks > 1024) blocks = 1024;
+  if (g_mlc_det && blocks > g_mlc_ncopy) return -2;
+  hipLaunchKernelGGL(stem_pool_reduce_pooled_kernel, dim3((unsigned)blocks), dim3(NT), 0, st, dp, idx, ymax, mean,
+                     sums, C, groups, g_mlc_ncopy);
   return hipGetLastError();
 }
 

@@ -86,7 +86,8 @@ _SIGS = {
     'mlc_bn_bwd_apply': [vp] * 7 + [i64, i32, vp],
     'mlc_maxpool_fwd': [vp, vp, vp] + [i32] * 9 + [vp],
     'mlc_maxpool_bwd': [vp, vp, vp] + [i32] * 9 + [vp],
-    'mlc_stem_pool_fwd': [vp] * 5 + [i32] * 4 + [vp],
+    'mlc_stem_pool_fwd': [vp] * 6 + [i32] * 4 + [vp],
+    'mlc_stem_pool_bwd_reduce_pooled': [vp] * 5 + [i32] * 4 + [vp],
     'mlc_stem_pool_bwd_reduce': [vp] * 5 + [i32] * 4 + [vp],
     'mlc_stem_pool_bwd_apply': [vp] * 6 + [i32] * 4 + [vp],
     'mlc_stem_s2d': [vp, vp] + [i32] * 5 + [vp],

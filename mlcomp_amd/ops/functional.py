@@ -618,6 +618,9 @@ def stem_pool_ok(C: int) -> bool:
     return C % 8 == 0 and 1 <= G <= 64 and G & (G - 1) == 0
 
 
+_POOLED_REDUCE = os.environ.get('MLC_STEM_POOLED_REDUCE', '1') == '1'
+
+
 def stem_pool_fwd(y, scale, shift):
     """ResNet stem tail: pooled = maxpool3x3/2(relu(y*scale + shift)) without
     materialising the activation (csrc/kernels/stem.hip).  Returns (pooled, idx); idx is
@@ -627,9 +630,14 @@ def stem_pool_fwd(y, scale, shift):
     Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
     if _cuda(y):
         out = torch.empty(N, Ho, Wo, C, device=y.device, dtype=torch.bfloat16)
-        idx = torch.empty(N, Ho, Wo, C, device=y.device, dtype=torch.uint8)
+        # one buffer: the argmax bytes, then (MLC_STEM_POOLED_REDUCE=1, default) the pre-BN
+        # value at the argmax, from which the backward's reduction runs over the pooled tensor
+        n = N * Ho * Wo * C
+        off = (n + 15) // 16 * 16          # 16-byte aligned ymax
+        idx = torch.empty(off + 2 * n if _POOLED_REDUCE else n, device=y.device, dtype=torch.uint8)
+        ymax = idx[off:].view(torch.bfloat16) if _POOLED_REDUCE else None
         _lib.call('mlc_stem_pool_fwd', _lib.ptr(y), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(out),
-                  _lib.ptr(idx), N, H, W, C, _lib.stream())
+                  _lib.ptr(idx), _lib.ptr(ymax), N, H, W, C, _lib.stream())
         return out, idx
     a = (y.float() * scale + shift).permute(0, 3, 1, 2)
     m, ind = F.max_pool2d(a, 3, 2, 1, return_indices=True)
@@ -645,8 +653,15 @@ def stem_pool_bwd(dp, idx, y, mean, invstd, gamma, dgamma, dbeta, sums, coef):
     N, H, W, C = y.shape
     rows = N * H * W
     if _cuda(dp):
-        _lib.call('mlc_stem_pool_bwd_reduce', _lib.ptr(dp), _lib.ptr(idx), _lib.ptr(y), _lib.ptr(mean),
-                  _lib.ptr(sums), N, H, W, C, _lib.stream())
+        n = dp.numel()
+        off = (n + 15) // 16 * 16
+        if idx.numel() == off + 2 * n:   # pooled-side reduction (stem_pool_fwd kept ymax)
+            _lib.call('mlc_stem_pool_bwd_reduce_pooled', _lib.ptr(dp), _lib.ptr(idx),
+                      _lib.ptr(idx[off:].view(torch.bfloat16)), _lib.ptr(mean), _lib.ptr(sums), N, H, W, C,
+                      _lib.stream())
+        else:
+            _lib.call('mlc_stem_pool_bwd_reduce', _lib.ptr(dp), _lib.ptr(idx), _lib.ptr(y), _lib.ptr(mean),
+                      _lib.ptr(sums), N, H, W, C, _lib.stream())
         _lib.call('mlc_bn_bwd_finalize', _lib.ptr(sums), _lib.ptr(invstd), _lib.ptr(gamma), _lib.ptr(coef),
                   _lib.ptr(dgamma), _lib.ptr(dbeta), rows, C, _lib.stream())
         dy = torch.empty_like(y)
