@@ -1,11 +1,18 @@
-set -o pipefail
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/q38; mkdir -p $O
-chk() { rc=$1; if [ $rc -ne 0 ]; then echo "step failed rc=$rc: stopping"; exit $rc; fi; }
-for impl in native torch; do
-  timeout -k 10 300 python -u scripts/bench_generic.py --model densenet121 --batch 64 --size 224 --impl $impl --steps 10 --warmup 3 2>>$O/err.log >> $O/gen.log; chk $?
-  timeout -k 10 300 python -u scripts/bench_generic.py --model inceptionv3 --batch 80 --size 299 --impl $impl --steps 10 --warmup 3 2>>$O/err.log >> $O/gen.log; chk $?
+# Interleaved in-step A/B of environment configurations on one GPU box (how the round-5
+# profiles/round5/*_ab*.txt tables were taken).  Run through gpurun, e.g.
+#   gpurun -- 'CONFIGS="base;MLC_WGRAD_SLAB=0" ROUNDS=2 BENCH="bench.py --steps 30 --warmup 10" bash scripts/r5_probe.sh'
+# Each config runs once per round, in order, so box drift hits every config alike; one line
+# per run goes to gpurun_out/ab.log.
+set -e
+mkdir -p gpurun_out
+CONFIGS=${CONFIGS:-base}
+ROUNDS=${ROUNDS:-2}
+BENCH=${BENCH:-bench.py --steps 30 --warmup 10}
+IFS=';' read -ra CFG <<< "$CONFIGS"
+for i in $(seq "$ROUNDS"); do
+  for cfg in "${CFG[@]}"; do
+    e=""; [ "$cfg" != base ] && e="$cfg"
+    env $e timeout -k 10 300 python -u $BENCH > gpurun_out/ab_run.txt 2>/dev/null
+    echo "$cfg $(tail -1 gpurun_out/ab_run.txt)" >> gpurun_out/ab.log
+  done
 done
-cut -c1-160 $O/gen.log
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o d -- python3 scripts/bench_generic.py --model densenet121 --batch 64 --size 224 --impl native --steps 6 --warmup 3 > $O/p1.log 2>&1; chk $?
-python scripts/steady_kernels.py $O/prof --marker sgd_kernel --steps 3 > $O/d_kernels.txt 2>&1; head -22 $O/d_kernels.txt
