@@ -78,3 +78,19 @@ def test_native_export_roundtrip():
     step.net.export_to_torch()
     for k, v in tm.state_dict().items():
         assert torch.allclose(v.float(), sd[k].float()), k
+
+
+def test_engine_wgrad_reduction_defaults(monkeypatch):
+    """Per-engine split-K weight-gradient reduction (profiles/round5/wgrad_slab_ab.txt): atomics
+    for the ResNet engine and the generic engine, slabs elsewhere; MLC_WGRAD_SLAB overrides."""
+    from mlcomp_amd.models.native_generic import GenericNet
+    from mlcomp_amd.models.native_resnet import NativeResNet
+    from mlcomp_amd.ops.layers import NativeContext
+    monkeypatch.delenv('MLC_WGRAD_SLAB', raising=False)
+    assert NativeContext().wgrad_slab is True
+    assert NativeResNet(build_model('resnet18', num_classes=4), 'cpu').ctx.wgrad_slab is False
+    assert GenericNet(build_model('LeNet', num_classes=4), 'cpu').ctx.wgrad_slab is False
+    monkeypatch.setenv('MLC_WGRAD_SLAB', '1')
+    assert NativeResNet(build_model('resnet18', num_classes=4), 'cpu').ctx.wgrad_slab is True
+    monkeypatch.setenv('MLC_WGRAD_SLAB', '0')
+    assert NativeContext().wgrad_slab is False
