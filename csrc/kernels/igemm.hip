@@ -1293,7 +1293,10 @@ static int g_prefetch = 2;
 // operands (3x3 / 7x7 convs) want more occupancy.  Re-tuned on the whole step once the
 // weight gradients ran beside the LDS-DMA forward / dgrad GEMMs: gathered 768 -> 384 and
 // plain (1x1 conv) 256 -> 128 gave ResNet-50 +1.5 %, U-Net +3.6 % (profiles/round2_ab/split_retune).
-static int g_split_target = 384;
+// Round 5 (atomic wgrads on ResNet-50, unjoined chains on the segmentation engines): gathered
+// 384 -> 256 gives U-Net / LinkNet / FPN +2.1-2.5 %, DeepLab +1.7 %, U-Net-ResNeXt-50 +1.1 %,
+// ResNet-50 neutral (profiles/round5/split_target_256_ab.txt).
+static int g_split_target = 256;
 // single-LDS-stage variant for single-K-tile splits (A/B knob 5)
 static int g_single_stage = 1;
 // ... and for splits of up to this many K-tiles (A/B knob 13, MLC_SINGLE_STAGE_KT): one LDS
