@@ -25,6 +25,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // Host-side state, defined in batchnorm.hip; launchers pass ncopy to their kernels.
 extern int g_mlc_ncopy;
 extern int g_mlc_det;
+// ordered per-channel statistics pass (normact.hip), shared by the conv launchers
+extern "C" int mlc_bn_stats(const bf16* x, float* sum, float* sumsq, long rows, int C, hipStream_t st);
 
 static __device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
 static __device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }

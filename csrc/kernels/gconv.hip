@@ -993,20 +993,26 @@ copies_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long
 
 // threads of a grid-stride pass over (row, 8-channel group) keep one group when the thread
 // count is a multiple of G = C/8 (as batchnorm.hip's grid_for)
+// block counts of the channel-group passes are multiples of this (a thread keeps one group)
+inline long group_mult(int G) {
+  if (G > NT) return G % NT == 0 ? G / NT : G;
+  int a = G, b = NT;
+  while (b) { const int r = a % b; a = b; b = r; }
+  return G / a;
+}
 inline int grid_groups(long work, int G, int cap) {
   long blocks = (work + NT * 4 - 1) / (NT * 4);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  long m;
-  if (G > NT) {
-    m = G % NT == 0 ? G / NT : G;
-  } else {
-    int a = G, b = NT;
-    while (b) { const int r = a % b; a = b; b = r; }
-    m = G / a;
-  }
+  const long m = group_mult(G);
   blocks = ((blocks + m - 1) / m) * m;
   return (int)blocks;
+}
+// deterministic mode: the largest block cap whose rounded grid stays within NCOPY blocks
+// (one ws copy per block), 0 when no such grid exists
+inline int det_group_cap(int G) {
+  const long m = group_mult(G);
+  return m <= NCOPY ? (int)((NCOPY / m) * m) : 0;
 }
 
 inline int blocks_for(long work) {
@@ -1073,6 +1079,12 @@ MLC_EXPORT int mlc_gconv_fwd(const bf16* x, const bf16* w, bf16* wb, bf16* y, fl
                              int W, int C, int Co, int KH, int KW, int S, int P, int D, int Ho, int Wo, int groups,
                              hipStream_t st) {
   if (!grouped_ok(C, Co, groups) || ((sum == nullptr) != (sumsq == nullptr))) return -1;
+  if (g_mlc_det && sum) {
+    // deterministic mode: the epilogue's statistics are float atomics from many blocks per
+    // copy; take them in the ordered statistics pass over y instead
+    const int rc = mlc_gconv_fwd(x, w, wb, y, nullptr, nullptr, N, H, W, C, Co, KH, KW, S, P, D, Ho, Wo, groups, st);
+    return rc ? rc : mlc_bn_stats(y, sum, sumsq, (long)N * Ho * Wo, Co, st);
+  }
   const GGeom g = mkg(N, H, W, C, Ho, Wo, Co, KH, KW, S, P, D, C / groups, Co / groups);
   hipLaunchKernelGGL(expand_kernel, dim3(blocks_for((long)(Co + 15) / 16 * 16 * g.Kp)), dim3(NT), 0, st, w, wb, Co,
                      C, g.T, g.Cg, g.Cog, g.KB, g.Kp, 0);
@@ -1118,7 +1130,9 @@ MLC_EXPORT int mlc_gconv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, 
   if (!accumulate) mlc_zero_f32(dw, (long)Co * g.T * g.Cg, st);
   TGeom t;
   static const int band_wg = getenv("MLC_GCONV_BAND_WGRAD") ? atoi(getenv("MLC_GCONV_BAND_WGRAD")) : 1;
-  if (band_wg && band_geom(t, H, W, C, Co, Ho, Wo, KH, KW, S, P, D, g.Cg, g.Cog, g.KB, g.Kp)) {
+  // deterministic mode: no band kernel (several blocks add into one weight element) and a
+  // single pixel chunk below, so every element gets exactly one add
+  if (band_wg && !g_mlc_det && band_geom(t, H, W, C, Co, Ho, Wo, KH, KW, S, P, D, g.Cg, g.Cog, g.KB, g.Kp)) {
     // runs of bands per block: ~640 blocks over the chip (2 per CU fit the 80 KB of LDS)
     const int slabs = C / TB_CS, nb_total = N * t.bands;
     int per = (int)(((long)nb_total * slabs + 639) / 640);
@@ -1136,6 +1150,7 @@ MLC_EXPORT int mlc_gconv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, 
   long chunks = (2048 + base - 1) / base;
   const long maxc = (g.M + 127) / 128;
   if (chunks > maxc) chunks = maxc;
+  if (g_mlc_det) chunks = 1;
   if (chunks < 1) chunks = 1;
   long chunk = (g.M + chunks - 1) / chunks;
   chunk = (chunk + 127) / 128 * 128;
@@ -1149,6 +1164,10 @@ MLC_EXPORT int mlc_gconv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, 
 MLC_EXPORT int mlc_dwconv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, float* sumsq, int N, int H, int W,
                               int C, int KH, int KW, int S, int P, int D, int Ho, int Wo, hipStream_t st) {
   if (C % 8 || ((sum == nullptr) != (sumsq == nullptr))) return -1;
+  if (g_mlc_det && sum) {   // ordered statistics pass instead of the epilogue's atomics
+    const int rc = mlc_dwconv_fwd(x, w, y, nullptr, nullptr, N, H, W, C, KH, KW, S, P, D, Ho, Wo, st);
+    return rc ? rc : mlc_bn_stats(y, sum, sumsq, (long)N * Ho * Wo, C, st);
+  }
   const int G = C / 8;
   if (D == 1 && (S == 1 || S == 2) && (KW == 3 || KW == 5 || KW == 7) && dw_strips()) {
     const long work = (long)N * Ho * ((Wo + DW_SW - 1) / DW_SW) * G;
@@ -1191,9 +1210,13 @@ MLC_EXPORT int mlc_dwconv_wgrad(const bf16* dy, const bf16* x, float* dw, float*
   if (C % 8) return -1;
   const int G = C / 8, T = KH * KW;
   mlc_zero_f32(ws, (long)NCOPY * T * C, st);
+  // deterministic mode: at most NCOPY blocks, so every copy of ws has one adder per element
+  // (copies_reduce_kernel sums the copies in a fixed order)
+  const int cap_strip = g_mlc_det ? det_group_cap(G) : 512, cap_tap = g_mlc_det ? det_group_cap(G) : 1024;
+  if (cap_strip == 0) return -2;
   if (D == 1 && (S == 1 || S == 2) && (KW == 3 || KW == 5 || KW == 7) && dw_strips()) {
     const long work = (long)N * Ho * ((Wo + DW_SW - 1) / DW_SW) * G;
-    const dim3 grid(grid_groups(work, G, 512), KH);
+    const dim3 grid(grid_groups(work, G, cap_strip), KH);
 #define DWW(K, SS) hipLaunchKernelGGL((dw_wgrad_strip_kernel<K, SS>), grid, dim3(NT), 0, st, dy, x, ws, N, H, W, C, \
                                       Ho, Wo, KH, P)
     if (S == 1) { if (KW == 3) DWW(3, 1); else if (KW == 5) DWW(5, 1); else DWW(7, 1); }
@@ -1204,7 +1227,7 @@ MLC_EXPORT int mlc_dwconv_wgrad(const bf16* dy, const bf16* x, float* dw, float*
     return hipGetLastError();
   }
   const long work = (long)N * Ho * Wo * G;
-  const int blocks = grid_groups(work, G, 1024);
+  const int blocks = grid_groups(work, G, cap_tap);
   for (int t0 = 0; t0 < T; t0 += DW_TC)
     hipLaunchKernelGGL(dw_wgrad_kernel, dim3(blocks), dim3(NT), 0, st, dy, x, ws, N, H, W, C, Ho, Wo, KH, KW, S, P, D,
                        t0);

@@ -30,6 +30,9 @@
 #include <stdlib.h>
 #include <map>
 #include <mutex>
+#include <vector>
+#include <algorithm>
+#include <cstdio>
 
 namespace igemm {
 
@@ -1409,46 +1412,133 @@ constexpr long kCapturedCounters = 1L << 21;      // per device, handed out once
 // replays once eager kernels ran on the NULL stream" of round 4 (docs/architecture.md).
 // Hence no two launches that can overlap share counters:
 //   * eager launches get one region per stream (launches on one stream are ordered);
-//   * a launch being captured gets a fresh region of its own from a per-device pool that is
-//     never recycled (the graph may replay it concurrently with anything else).
+//   * a launch being captured gets a region of its own from a per-device pool, tagged with
+//     the capture's owner id (mlc_counters_owner, set by the Python capture scope).  When
+//     the owning graph is dropped its regions go back to the pool (mlc_counters_release):
+//     every launch leaves its counters zeroed, and a later capture starts after a device
+//     synchronize, so a recycled region is never counted on by two live graphs.
 // Everything is allocated (zeroed) outside capture; nullptr -> the caller falls back to
-// the separate reduction kernel, which needs no counters.
+// the separate reduction kernel, which needs no counters (logged once per device).
+struct CounterRegion {
+  long off, len;
+  int owner;
+};
 struct CounterPool {
   std::mutex mu;
   unsigned* captured = nullptr;
   long captured_used = 0;
+  std::vector<CounterRegion> live;          // owned regions of captured launches
+  std::vector<std::pair<long, long>> free;  // released (off, len), first fit
+  bool warned = false;
   std::map<hipStream_t, unsigned*> eager;
 };
-static unsigned* alloc_zeroed_counters(long n) {
+static CounterPool g_counter_pools[16];
+static int g_counter_owner = 0;             // owner id of captures in progress (0: none)
+
+static unsigned* alloc_zeroed_counters(long n, hipStream_t st) {
   unsigned* p = nullptr;
   if (hipMalloc(&p, n * sizeof(unsigned)) != hipSuccess) return nullptr;
-  if (hipMemset(p, 0, n * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+  // zeroed on the stream that first uses the region (stream order covers that use); no
+  // device-wide synchronize, which would invalidate a capture running on another stream
+  if (hipMemsetAsync(p, 0, n * sizeof(unsigned), st) != hipSuccess) {
     (void)hipFree(p);
     return nullptr;
   }
   return p;
 }
+static long take_captured(CounterPool& P, long n) {
+  for (size_t i = 0; i < P.free.size(); ++i) {
+    if (P.free[i].second >= n) {
+      const long off = P.free[i].first;
+      P.free[i].first += n;
+      P.free[i].second -= n;
+      if (P.free[i].second == 0) P.free.erase(P.free.begin() + i);
+      return off;
+    }
+  }
+  if (P.captured_used + n > kCapturedCounters) return -1;
+  const long off = P.captured_used;
+  P.captured_used += n;
+  return off;
+}
 static unsigned* split_counters(hipStream_t st, long tiles, int splits, int bm, int bn) {
-  static CounterPool pools[16];
   if (tiles > kSplitCounters || (long)splits * bm * bn * 4 > (long)g_splitk_fused * 1024) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
-  CounterPool& P = pools[dev];
+  CounterPool& P = g_counter_pools[dev];
   std::lock_guard<std::mutex> lk(P.mu);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess) return nullptr;
   if (cs != hipStreamCaptureStatusNone) {
-    if (!P.captured || P.captured_used + tiles > kCapturedCounters) return nullptr;
-    unsigned* r = P.captured + P.captured_used;
-    P.captured_used += (tiles + 63) & ~63L;   // keep regions on separate 256-B lines
-    return r;
+    const long n = (tiles + 63) & ~63L;      // keep regions on separate 256-B lines
+    const long off = P.captured ? take_captured(P, n) : -1;
+    if (off < 0) {
+      if (!P.warned) {
+        fprintf(stderr, "[mlcomp] split-K counter pool of device %d exhausted (%ld of %ld in use): captured "
+                        "split-K GEMMs fall back to the separate reduction pass\n", dev, P.captured_used,
+                kCapturedCounters);
+        P.warned = true;
+      }
+      return nullptr;
+    }
+    P.live.push_back({off, n, g_counter_owner});
+    return P.captured + off;
   }
-  if (!P.captured) P.captured = alloc_zeroed_counters(kCapturedCounters);  // ready for a later capture
+  if (!P.captured) P.captured = alloc_zeroed_counters(kCapturedCounters, st);  // ready for a later capture
   auto it = P.eager.find(st);
   if (it != P.eager.end()) return it->second;
-  unsigned* r = alloc_zeroed_counters(kSplitCounters);
+  unsigned* r = alloc_zeroed_counters(kSplitCounters, st);
   if (r) P.eager[st] = r;
   return r;
+}
+
+// Owner id for the captured counter regions handed out from now on (0: unowned, kept for
+// the life of the process).  Called by the capture scope around a graph capture.
+MLC_EXPORT void mlc_counters_owner(int owner) { g_counter_owner = owner; }
+
+// Return every captured region of ``owner`` (a dropped graph) to the device's pool; the
+// number of counters freed.
+MLC_EXPORT long mlc_counters_release(int owner) {
+  if (owner == 0) return 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
+  CounterPool& P = g_counter_pools[dev];
+  std::lock_guard<std::mutex> lk(P.mu);
+  long freed = 0;
+  for (size_t i = 0; i < P.live.size();) {
+    if (P.live[i].owner == owner) {
+      P.free.push_back({P.live[i].off, P.live[i].len});
+      freed += P.live[i].len;
+      P.live[i] = P.live.back();
+      P.live.pop_back();
+    } else {
+      ++i;
+    }
+  }
+  // coalesce neighbours, then give a free tail back to the bump pointer
+  std::sort(P.free.begin(), P.free.end());
+  std::vector<std::pair<long, long>> merged;
+  for (auto& f : P.free) {
+    if (!merged.empty() && merged.back().first + merged.back().second == f.first) merged.back().second += f.second;
+    else merged.push_back(f);
+  }
+  if (!merged.empty() && merged.back().first + merged.back().second == P.captured_used) {
+    P.captured_used = merged.back().first;
+    merged.pop_back();
+  }
+  P.free.swap(merged);
+  return freed;
+}
+
+// Counters of the device's captured pool in use (bump pointer minus released holes).
+MLC_EXPORT long mlc_counters_in_use() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
+  CounterPool& P = g_counter_pools[dev];
+  std::lock_guard<std::mutex> lk(P.mu);
+  long holes = 0;
+  for (auto& f : P.free) holes += f.second;
+  return P.captured_used - holes;
 }
 static inline int tile_bm(int tile) { return tile == 1 || tile == 3 ? 256 : tile == 2 ? 64 : 128; }
 static inline int tile_bn(int tile) { return tile == 1 ? 64 : tile == 2 || tile == 4 ? 256 : 128; }

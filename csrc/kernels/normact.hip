@@ -81,7 +81,8 @@ __device__ __forceinline__ void load_ch(Ch& c, const float* scale, const float* 
 }
 
 __global__ void __launch_bounds__(NT)
-stats_kernel(const bf16* __restrict__ x, float* __restrict__ sum, float* __restrict__ sumsq, long rows, int C) {
+stats_kernel(const bf16* __restrict__ x, float* __restrict__ sum, float* __restrict__ sumsq, long rows, int C,
+             int ncopy) {
   __shared__ float rb[NT][17];
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
@@ -119,7 +120,7 @@ stats_kernel(const bf16* __restrict__ x, float* __restrict__ sum, float* __restr
 #pragma unroll
       for (int e = 0; e < 8; ++e) { a[e] += rb[u][e]; b[e] += rb[u][8 + e]; }
     const int cg = (base_cg + t) % G;
-    const long slot = blockIdx.x % NCOPY;
+    const long slot = blockIdx.x % ncopy;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       atomicAdd(sum + slot * C + cg * 8 + e, a[e]);
@@ -193,7 +194,8 @@ __global__ void __launch_bounds__(NT)
 bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const bf16* __restrict__ y,
                   const bf16* __restrict__ res, const float* __restrict__ mean, const float* __restrict__ scale,
                   const float* __restrict__ shift, const float* __restrict__ rscale, const float* __restrict__ rshift,
-                  float* __restrict__ sums, long rows, int C, int act, float alpha, int direct, RowScale rsc) {
+                  float* __restrict__ sums, long rows, int C, int act, float alpha, int direct, RowScale rsc,
+                  int ncopy) {
   __shared__ float rb[NT][17];
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
@@ -252,7 +254,7 @@ bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const
         dst[C + cg * 8 + e] = b[e];
       }
     } else {
-      float* dst = sums + (long)(blockIdx.x % NCOPY) * 2 * C;
+      float* dst = sums + (long)(blockIdx.x % ncopy) * 2 * C;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         atomicAdd(dst + cg * 8 + e, a[e]);
@@ -525,9 +527,17 @@ inline int blocks_for(long work) {
 using namespace normact;
 
 // sum/sumsq: 32*C fp32 each, zeroed by the caller; C % 8 == 0
+// Atomic partial-sum copies of the reductions below: NCOPY, or in deterministic mode one copy per
+// block (g_mlc_ncopy of them; every copy then has exactly one adder per element, and the
+// finalize kernels sum the copies in a fixed order).
+inline int det_blocks_ok(int blocks) { return !g_mlc_det || blocks <= g_mlc_ncopy; }
+inline int atomic_copies() { return g_mlc_det ? g_mlc_ncopy : NCOPY; }
+
 MLC_EXPORT int mlc_bn_stats(const bf16* x, float* sum, float* sumsq, long rows, int C, hipStream_t st) {
   if (C % 8) return -1;
-  hipLaunchKernelGGL(stats_kernel, dim3(grid_for(rows, C, reduce_cap())), dim3(NT), 0, st, x, sum, sumsq, rows, C);
+  const int blocks = grid_for(rows, C, reduce_cap());
+  if (!det_blocks_ok(blocks)) return -2;
+  hipLaunchKernelGGL(stats_kernel, dim3(blocks), dim3(NT), 0, st, x, sum, sumsq, rows, C, atomic_copies());
   return hipGetLastError();
 }
 
@@ -548,8 +558,10 @@ MLC_EXPORT int mlc_bnact_bwd_reduce(const bf16* dz, const bf16* z, const bf16* y
                                     hipStream_t st) {
   if (C % 8 || (row_scale && (act != 0 || hw < 1))) return -1;
   const RowScale rsc{row_scale, hw};
-  NA_LAUNCH(bwd_reduce_kernel, grid_for(rows, C, reduce_cap()), st, act, dz, z, y, res, mean, scale, shift, rscale,
-            rshift, sums, rows, C, act, alpha, 0, rsc);
+  const int blocks = grid_for(rows, C, reduce_cap());
+  if (!det_blocks_ok(blocks)) return -2;
+  NA_LAUNCH(bwd_reduce_kernel, blocks, st, act, dz, z, y, res, mean, scale, shift, rscale,
+            rshift, sums, rows, C, act, alpha, 0, rsc, atomic_copies());
   return hipGetLastError();
 }
 
@@ -575,7 +587,7 @@ MLC_EXPORT int mlc_bnact_bwd(const bf16* dz, const bf16* z, const bf16* y, const
   while (blocks > cap && blocks > 1) blocks = grid_for(rows, C, blocks / 2);   // rounding to C/8 multiples
   if ((long)blocks * 2 * C > part_floats) return -1;
   NA_LAUNCH(bwd_reduce_kernel, blocks, st, act, dz, z, y, res, mean, scale, shift, rscale, rshift, part, rows, C, act,
-            alpha, 1, rsc);
+            alpha, 1, rsc, 1);
   hipLaunchKernelGGL(bwd_finalize_rows_kernel, dim3((C + NT / 64 - 1) / (NT / 64)), dim3(NT), 0, st, part, blocks,
                      invstd, gamma, coef, dgamma, dbeta, rows, C);
   NA_LAUNCH(bwd_apply_kernel, grid_for(rows, C, apply_cap()), st, act, dz, z, y, res, mean, coef, scale, shift, rscale, rshift,

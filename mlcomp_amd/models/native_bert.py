@@ -32,6 +32,7 @@ from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops import transformer as Tx
 from mlcomp_amd.ops.layers import NativeContext
 from .bert import BertForSequenceClassification
+from mlcomp_amd.train.native_spec import NativeUnsupported
 
 # MLC_GELU_DERIV=1 (default): the FFN's first GEMM stores gelu'(pre-activation) instead of
 # the pre-activation, so the input-gradient GEMM of the second only multiplies by it (no erf
@@ -334,10 +335,25 @@ class _HeadFn(torch.autograd.Function):
         return dh.view(net.B * net.S, -1), None, None, None
 
 
+def native_bert_unsupported(c, seq_len: int = 1):
+    """Why the native BERT engine cannot train config ``c`` (None when it can): GEMM rows
+    in 16-byte chunks (hidden / intermediate % 8) and the fused attention's head dims
+    (<= 128, :func:`mlcomp_amd.ops.transformer.attn_supported`)."""
+    if c.hidden % 8 or c.intermediate % 8:
+        return f'hidden {c.hidden} / intermediate {c.intermediate}: the native GEMMs need multiples of 8'
+    if c.hidden % c.heads:
+        return f'hidden {c.hidden} is not a multiple of heads {c.heads}'
+    if seq_len < 1 or not Tx.attn_supported(seq_len, c.head_dim):
+        return f'head_dim {c.head_dim} (seq_len {seq_len}): the fused attention takes head dims <= 128'
+    return None
+
+
 class NativeBert:
     def __init__(self, model: BertForSequenceClassification, device, batch: int, seq_len: int):
         c = model.config
-        assert c.hidden % 8 == 0 and c.intermediate % 8 == 0 and seq_len >= 1
+        unsupported = native_bert_unsupported(c, seq_len)
+        if unsupported:
+            raise NativeUnsupported(unsupported)
         self.model, self.c = model, c
         self.B, self.S = batch, seq_len
         self.p_hidden, self.p_attn = c.hidden_dropout, c.attention_dropout

@@ -46,6 +46,7 @@ import torch.nn.functional as F
 from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops.glayers import (AvgPool, BilinearUp, BNAct, BNParams, ChannelGate, Conv3dAs2d, ConvBNAct, ConvParams,
                                     Frames, GlobalAvgPool, LinearAct, LinearParams, MaxPool, TemporalAs2d, UpCat)
+from mlcomp_amd.ops import gtransformer as GT
 from mlcomp_amd.ops.layers import NativeContext
 from mlcomp_amd.train.native_spec import NativeUnsupported
 
@@ -305,6 +306,13 @@ class _Lowering:
         if u is not None and _act_of(u, self.modules) == (A['relu'], 0.0):
             act = 3                       # the dense epilogue's ReLU code
             chain.append(u)
+        elif u is not None and _act_of(u, self.modules) == (A['gelu'], 0.0):
+            # exact GELU in the GEMM epilogue, gelu' stored for the backward
+            chain.append(u)
+            site = GT.LinearGelu(self.net.ctx, self.net.linear_params(node.target, m))
+            new = self._site_node(chain[-1], site, [node.args[0]])
+            self._replace(chain, new)
+            return
         site = LinearAct(self.net.ctx, self.net.linear_params(node.target, m), act)
         new = self._site_node(chain[-1], site, [node.args[0]])
         self._replace(chain, new)
@@ -395,9 +403,30 @@ class _Lowering:
             g = g.args[0]
         return None
 
+    def _channels(self, n: fx.Node, depth: int = 8):
+        """Channel count of the value ``n`` when a native site (walking back through
+        elementwise activations) says so, else None."""
+        for _ in range(depth):
+            if not isinstance(n, fx.Node):
+                return None
+            m = getattr(self.gm, n.target, None) if n.op == 'call_module' else None
+            if isinstance(m, ConvBNAct):
+                return m.conv.Co
+            if isinstance(m, LinearAct):
+                return m.lin.O
+            if isinstance(m, BNAct):
+                return m.bn.C
+            if isinstance(m, ChannelGate) or _act_of(n, self.modules) is not None:
+                n = n.args[0]
+                continue
+            return None
+        return None
+
     def gate(self, node):
         """``y * g`` where g is computed from y's global average (squeeze-excitation) ->
-        ChannelGate."""
+        ChannelGate.  Only a per-channel gate lowers: g's producing site must output as many
+        channels as y has (a per-sample [N, 1, 1, 1] gate is a valid torch broadcast and
+        stays a torch op)."""
         if len(node.args) != 2 or node.kwargs:
             return
         a, b = node.args
@@ -408,6 +437,9 @@ class _Lowering:
         elif self._gate_source(a) is b:
             y, g = b, a
         else:
+            return
+        cg, cy = self._channels(g), self._channels(y)
+        if cg is None or cg != cy:
             return
         # SE-ResNeXt's block tail: (y * g) + residual -> ReLU in the same pass
         chain = [node]
@@ -420,6 +452,120 @@ class _Lowering:
 
     def avgpool(self, node):
         new = self._site_node(node, GlobalAvgPool(self.net.ctx), [node.args[0]])
+        self._replace([node], new)
+
+    # ------------------------------------------------------------------ transformer blocks
+    @staticmethod
+    def _call_args(node, names):
+        a = dict(zip(names, node.args))
+        a.update(node.kwargs)
+        return a
+
+    def layernorm(self, node):
+        """nn.LayerNorm [over ``a + b`` whose only user it is] -> LayerNormSite (the add
+        fused into the normalisation pass); unsupported configurations stay torch ops."""
+        m = self.modules[node.target]
+        if GT.LNParams.supported(m) is not None or len(node.args) != 1:
+            return
+        x = node.args[0]
+        lp = self.net.ln_params(node.target, m)
+        chain, inputs = [node], [x]
+        if isinstance(x, fx.Node) and len(x.users) == 1:
+            for cand in x.args[:2] if len(x.args) >= 2 else ():
+                r = _residual_of(x, cand) if isinstance(cand, fx.Node) else None
+                if r is not None:
+                    inputs = [cand, r]
+                    chain = [x, node]
+                    break
+        site = GT.LayerNormSite(self.net.ctx, lp, residual=len(inputs) == 2)
+        new = self._site_node(node, site, inputs)
+        self._replace(chain, new)
+
+    def _getitem_users(self, node):
+        """{index: user} of a tuple-returning call whose every user is ``out[i]``; None when
+        some user takes the tuple itself."""
+        out = {}
+        for u in node.users:
+            if not (u.op == 'call_function' and u.target is operator.getitem and isinstance(u.args[1], int)):
+                return None
+            out.setdefault(u.args[1], []).append(u)
+        return out
+
+    def mha(self, node):
+        m = self.modules[node.target]
+        why = GT.mha_supported(m)
+        if why:
+            raise NativeUnsupported(f'{node.target}: {why}')
+        a = self._call_args(node, ('query', 'key', 'value', 'key_padding_mask', 'need_weights', 'attn_mask',
+                                   'average_attn_weights', 'is_causal'))
+        q = a.get('query')
+        if a.get('key') is not q or a.get('value') is not q:
+            raise NativeUnsupported(f'{node.target}: MultiheadAttention lowers for self-attention only (q = k = v)')
+        if a.get('attn_mask') is not None or a.get('is_causal'):
+            raise NativeUnsupported(f'{node.target}: MultiheadAttention attn_mask / is_causal (native: a key-padding '
+                                    'mask only)')
+        users = self._getitem_users(node)
+        if users is None or any(u.users for i, us in users.items() if i != 0 for u in us):
+            raise NativeUnsupported(f'{node.target}: MultiheadAttention attention weights are used (native: the '
+                                    'output only)')
+        kpm = a.get('key_padding_mask')
+        site = GT.MHASite(self.net.ctx, self.net.mha_params(node.target, m))
+        new = self._site_node(node, site, [q] + ([kpm] if kpm is not None else []))
+        for i, us in users.items():
+            for u in us:
+                if i == 0:
+                    u.replace_all_uses_with(new)
+                self.gm.graph.erase_node(u)
+                self.erased.add(u)
+        self.gm.graph.erase_node(node)
+        self.erased.add(node)
+
+    def encoder(self, node, layers, norm):
+        """nn.TransformerEncoderLayer / nn.TransformerEncoder -> EncoderSite."""
+        for i, layer in enumerate(layers):
+            why = GT.encoder_layer_supported(layer)
+            if why:
+                raise NativeUnsupported(f'{node.target}: {why}')
+        names = ('src', 'mask', 'src_key_padding_mask', 'is_causal')
+        a = self._call_args(node, names)
+        if a.get('src_mask') is not None or a.get('mask') is not None or a.get('is_causal'):
+            raise NativeUnsupported(f'{node.target}: an attention mask / is_causal (native: a key-padding mask only)')
+        if norm is not None and GT.LNParams.supported(norm) is not None:
+            raise NativeUnsupported(f'{node.target}: final norm: {GT.LNParams.supported(norm)}')
+        if len({bool(l.self_attn.batch_first) for l in layers}) != 1:
+            raise NativeUnsupported(f'{node.target}: layers disagree on batch_first')
+        single = len(layers) == 1 and isinstance(self.modules[node.target], nn.TransformerEncoderLayer)
+        lps = [self.net.encoder_params(node.target if single else f'{node.target}.layers.{i}', l)
+               for i, l in enumerate(layers)]
+        lnp = self.net.ln_params(f'{node.target}.norm', norm) if norm is not None else None
+        kpm = a.get('src_key_padding_mask')
+        site = GT.EncoderSite(self.net.ctx, lps, lnp)
+        new = self._site_node(node, site, [a['src']] + ([kpm] if kpm is not None else []))
+        self._replace([node], new)
+
+    def sdpa(self, node):
+        a = self._call_args(node, ('query', 'key', 'value', 'attn_mask', 'dropout_p', 'is_causal', 'scale',
+                                   'enable_gqa'))
+        if a.get('attn_mask') is not None or a.get('is_causal') or a.get('enable_gqa'):
+            raise NativeUnsupported(f'{node.name}: scaled_dot_product_attention with a mask / is_causal / GQA '
+                                    '(native: unmasked self-attention)')
+        p, scale = a.get('dropout_p', 0.0), a.get('scale')
+        if isinstance(p, fx.Node) or isinstance(scale, fx.Node):
+            raise NativeUnsupported(f'{node.name}: scaled_dot_product_attention with a traced dropout_p / scale')
+        site = GT.SDPASite(self.net.ctx, float(p or 0.0), None if scale is None else float(scale))
+        new = self._site_node(node, site, [a['query'], a['key'], a['value']])
+        self._replace([node], new)
+
+    def patch_embed(self, node, m):
+        """A conv with stride == kernel and no padding whose kernel is beyond the
+        implicit-GEMM engine (ViT's 16x16/16 patch embedding) -> one dense GEMM."""
+        k = _pair(m.kernel_size, 'kernel_size')
+        if (_pair(m.stride, 'stride') != k or _pair(m.padding, 'padding') != 0 or _pair(m.dilation, 'dilation') != 1
+                or m.groups != 1 or m.padding_mode != 'zeros' or (m.in_channels * k * k) % 8 or m.out_channels % 8):
+            raise NativeUnsupported(f'{node.target}: kernel {m.kernel_size} (native convs take <= 15x15; larger ones '
+                                    'only as a stride = kernel patch embedding)')
+        d = self.net.dense_set(node.target, m.weight, m.bias)
+        new = self._site_node(node, GT.PatchEmbed(self.net.ctx, d, k, m.in_channels), [node.args[0]])
         self._replace([node], new)
 
     def _link_residuals(self):
@@ -590,7 +736,9 @@ class _Lowering:
                 continue
             if node.op == 'call_module':
                 m = self.modules.get(node.target)
-                if isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)):
+                if isinstance(m, nn.Conv2d) and max(m.kernel_size) > 15:
+                    self.patch_embed(node, m)
+                elif isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)):
                     self.conv(node)
                 elif isinstance(m, (nn.Conv3d, nn.Conv1d)):
                     self.conv3d(node)
@@ -607,8 +755,17 @@ class _Lowering:
                 elif isinstance(m, nn.AvgPool2d):
                     self.avgpool2d(node, m.kernel_size, m.stride, m.padding, m.ceil_mode, m.count_include_pad,
                                    m.divisor_override)
+                elif isinstance(m, nn.LayerNorm):
+                    self.layernorm(node)
+                elif isinstance(m, nn.MultiheadAttention):
+                    self.mha(node)
+                elif isinstance(m, nn.TransformerEncoderLayer):
+                    self.encoder(node, [m], None)
+                elif isinstance(m, nn.TransformerEncoder):
+                    self.encoder(node, list(m.layers), m.norm)
                 elif isinstance(m, (nn.ConvTranspose1d, nn.ConvTranspose3d, nn.LSTM, nn.GRU, nn.RNN,
-                                    nn.MultiheadAttention, nn.Bilinear, nn.InstanceNorm2d)):
+                                    nn.TransformerDecoder, nn.TransformerDecoderLayer, nn.Transformer,
+                                    nn.Bilinear, nn.InstanceNorm2d)):
                     raise NativeUnsupported(f'{node.target}: {type(m).__name__} has no native lowering')
             elif node.op == 'call_function':
                 t = node.target
@@ -636,9 +793,10 @@ class _Lowering:
                 elif t is F.adaptive_avg_pool2d and _pair(node.args[1] if len(node.args) > 1
                                                           else node.kwargs['output_size'], 'output_size') == 1:
                     self.avgpool(node)
+                elif t is F.scaled_dot_product_attention:
+                    self.sdpa(node)
                 elif t in (F.conv2d, torch.conv2d, F.linear, torch.matmul, torch.mm, torch.bmm, torch.addmm,
-                           F.batch_norm, torch.einsum, F.conv_transpose2d, F.scaled_dot_product_attention,
-                           operator.matmul):
+                           F.batch_norm, torch.einsum, F.conv_transpose2d, operator.matmul):
                     raise NativeUnsupported(f'{node.name}: functional {getattr(t, "__name__", t)} on module '
                                             'parameters has no native lowering (use the nn modules)')
             elif node.op == 'call_method':
@@ -676,6 +834,7 @@ class GenericNet:
         ctx.wt = Fn.WtTable() if os.environ.get('MLC_GENERIC_WT', '1') == '1' else None
         ctx.grad_prezeroed = True          # the step zeroes the grad arena once
         self._params: Dict[str, object] = {}
+        self._composite: Dict[str, object] = {}    # MHA / encoder-layer groupings of _params
         was = model.training
         model.to(self.device)
         try:
@@ -702,6 +861,9 @@ class GenericNet:
             if isinstance(p, BNParams):
                 p.single_site = uses.get(id(p), 0) == 1
         ctx.finalize(self.device)
+        # dropout seed of the kernels' counter-hash masks (transformer sites), advanced on the
+        # device by every training forward, so captured replays draw fresh masks
+        ctx.seed = torch.zeros(1, device=self.device, dtype=torch.int32)
         # weight gradients as one unjoined side chain, each forked before its site's input
         # gradient (BERT's and the segmentation engines' schedule).  Interleaved A/B on one
         # MI355X (profiles/round5/generic/bench_ab_defer.jsonl): ResNeXt-50 @128 7,451 ->
@@ -741,6 +903,30 @@ class GenericNet:
             self._params[key] = LinearParams(self.ctx, name, m)
         return self._params[key]
 
+    def dense_set(self, name, weight, bias):
+        key = f'dense:{name}'
+        if key not in self._params:
+            self._params[key] = GT.DenseSet(self.ctx, name, weight, bias)
+        return self._params[key]
+
+    def ln_params(self, name, m):
+        key = f'ln:{name}'
+        if key not in self._params:
+            self._params[key] = GT.LNParams(self.ctx, name, m)
+        return self._params[key]
+
+    def mha_params(self, name, m):
+        key = f'mha:{name}'
+        if key not in self._composite:
+            self._composite[key] = GT.MHAParams(self.dense_set, name, m)
+        return self._composite[key]
+
+    def encoder_params(self, name, layer):
+        key = f'encoder:{name}'
+        if key not in self._composite:
+            self._composite[key] = GT.EncoderLayerParams(self.dense_set, self.ln_params, name, layer)
+        return self._composite[key]
+
     def _alias_residual_params(self, model):
         """Parameters no site owns (read by torch ops left in the graph) get arena slots too."""
         owned = set()
@@ -776,7 +962,7 @@ class GenericNet:
     def eval(self):
         return self.train(False)
 
-    def __call__(self, x):
+    def __call__(self, x, *rest):
         gm = self.train_gm if self.training else self.eval_gm
         # torch ops left in the graph as leaf modules (Dropout, Dropout2d, user modules) are
         # the user model's own objects, shared by both graphs: their mode is set here, on
@@ -784,8 +970,10 @@ class GenericNet:
         gm.train(self.training)
         if self.training and self.ctx.wt is not None:
             self.ctx.wt.refresh()          # the weights are fixed until this step's optimizer
+        if self.training and getattr(self.ctx, '_salt', None) is not None:
+            self.ctx.seed.add_(1)          # fresh dropout masks for this step
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.device.type == 'cuda'):
-            return gm(x)
+            return gm(x, *rest)
 
     def logits(self, x):
         return self(x)
@@ -813,6 +1001,7 @@ def lower_or_none(model: nn.Module) -> Optional[str]:
             probe = GenericNet.__new__(GenericNet)
             probe.ctx = NativeContext()
             probe._params = {}
+            probe._composite = {}
             _Lowering(probe, gm).run()
         return None
     except NativeUnsupported as e:

@@ -123,9 +123,17 @@ _SIGS = {
     'mlc_chscale_bwd': [vp] * 7 + [i32] * 3 + [vp],
     'mlc_conv_fwd_ex': [vp] * 4 + [i32] * 13 + [vp],
     'mlc_conv_wgrad_bias': [vp] * 4 + [i32] * 13 + [vp, i64, vp],
+    'mlc_counters_owner': [i32],
+    'mlc_counters_release': [i32],
+    'mlc_counters_in_use': [],
     'mlc_comm_unique_id_bytes': [],
     'mlc_comm_get_unique_id': [vp],
-    'mlc_comm_init': [vp, i32, i32, i32, vp],
+    'mlc_comm_init': [vp, i32, i32, i32, i32, vp],
+    'mlc_comm_async_error': [vp],
+    'mlc_comm_abort': [vp],
+    'mlc_comm_error_string': [i32],
+    'mlc_comm_last_error': [vp],
+    'mlc_comm_set_timeout': [i64],
     'mlc_comm_destroy': [vp],
     'mlc_allreduce': [vp, vp, vp, i64, i32, i32, vp],
     'mlc_broadcast': [vp, vp, vp, i64, i32, i32, vp],
@@ -133,7 +141,9 @@ _SIGS = {
     'mlc_allgather': [vp, vp, vp, i64, i32, vp],
     'mlc_alltoall': [vp, vp, vp, i64, i32, i32, i32, vp],
 }
-_RESTYPE = {'mlc_comm_init': vp, 'mlc_gconv_wb_elems': C.c_long}
+_RESTYPE = {'mlc_comm_init': vp, 'mlc_gconv_wb_elems': C.c_long, 'mlc_counters_owner': None,
+            'mlc_counters_release': C.c_long, 'mlc_counters_in_use': C.c_long,
+            'mlc_comm_error_string': C.c_char_p, 'mlc_comm_last_error': C.c_char_p, 'mlc_comm_set_timeout': None}
 
 
 def lib_path():

@@ -289,19 +289,55 @@ def side_stream(stream):
         _ROLE.side = prev
 
 
+class CounterLease:
+    """The split-K tile-counter regions (``split_counters`` in igemm.hip) that the kernel
+    library hands to launches captured under one owner id.  They are returned to the
+    device's pool when the lease dies, i.e. with the capture store (and so the graph) that
+    holds it: a re-capture (another model, a rebuilt step) reuses them instead of
+    draining the pool."""
+    _next = 0
+
+    def __init__(self, device):
+        CounterLease._next += 1
+        self.owner = CounterLease._next
+        self.device = torch.device(device)
+
+    def release(self):
+        if self.owner and torch.cuda.is_available():
+            from . import _lib
+            with torch.cuda.device(self.device):
+                _lib.load().mlc_counters_release(self.owner)
+        self.owner = 0
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
 @contextlib.contextmanager
 def capture_scope(store: dict):
     """Workspaces requested while a graph is being captured live in ``store`` (owned by the
     graph's owner) instead of the process-wide eager pool.  A captured graph bakes the
     workspace pointers in; eager work on another stream (a second model, a validation pass)
     must never write the slabs a replay may be using at the same time.  The kernel
-    library does the same for its split-K tile counters (``split_counters`` in igemm.hip)."""
+    library does the same for its split-K tile counters: regions handed out during the
+    capture are tagged with a :class:`CounterLease` kept in ``store`` and go back to the
+    pool when ``store`` is dropped."""
     prev = getattr(_ROLE, 'capture', None)
     _ROLE.capture = store
+    lease = None
+    if torch.cuda.is_available():
+        from . import _lib
+        lease = store.setdefault('__counter_lease__', CounterLease(torch.cuda.current_device()))
+        _lib.load().mlc_counters_owner(lease.owner)
     try:
         yield
     finally:
         _ROLE.capture = prev
+        if lease is not None:
+            _lib.load().mlc_counters_owner(0)
 
 
 def workspace_key(device) -> str:

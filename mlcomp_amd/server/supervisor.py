@@ -48,6 +48,9 @@ FATAL_RESTART_MESSAGES = (
     'device-side assert triggered', 'Memory access fault by GPU', 'GPU Hang', 'HW Exception by GPU',
     'hipErrorLaunchFailure', 'ncclUnhandledCudaError', 'ncclSystemError: System call',
     'unhandled system error', 'ncclRemoteError', 'MIOPEN_STATUS_INTERNAL_ERROR',
+    # the framework's own RCCL communicator: a timed-out / failed collective or rendezvous
+    # (parallel/comm.py WATCHDOG_MESSAGE; torch's NCCL watchdog gives the reference the same)
+    'RCCL watchdog:',
     ORPHAN_MESSAGE,
     # a rank whose process died (SIGKILL, OOM killer): worker/daemon.PROCESS_LOST_MESSAGE
     'task process was lost',

@@ -118,9 +118,15 @@ class GraphedStep:
 
     def __call__(self):
         self.calls += 1
+        comm = self.comm
+        watched = comm is not None and hasattr(comm, 'watch_stream')
+        if watched:
+            comm.check()        # a failure the RCCL watchdog saw: raise before replaying
         self.opt.prepare()
         with work_stream(self.device):
             self._call()
+            if watched:         # the watchdog times this step's collectives (MLC_COMM_TIMEOUT)
+                comm.watch_stream()
 
     def _call(self):
         if not self.use_graph:

@@ -109,7 +109,10 @@ def _native_kind(model: nn.Module, device: torch.device) -> Optional[str]:
     if isinstance(model, ResNet) and model.groups == 1 and model.include_top:
         return 'resnet'
     if isinstance(model, BertForSequenceClassification):
-        return 'bert'
+        from mlcomp_amd.models.native_bert import native_bert_unsupported
+        if native_bert_unsupported(model.config) is None:
+            return 'bert'
+        return None
     from mlcomp_amd.contrib.segmentation.deeplab import DeepLab, ResNetBackbone
     from mlcomp_amd.contrib.segmentation.models import FPN, Linknet, PSPNet, Unet
     if isinstance(model, DeepLab):     # dilated-ResNet backbone, sigmoid heads of <= 4 classes
@@ -149,6 +152,10 @@ def _native_kind(model: nn.Module, device: torch.device) -> Optional[str]:
 
 
 def _generic_reason(model: nn.Module) -> Optional[str]:
+    from mlcomp_amd.models.bert import BertForSequenceClassification
+    if isinstance(model, BertForSequenceClassification):
+        from mlcomp_amd.models.native_bert import native_bert_unsupported
+        return native_bert_unsupported(model.config)
     from mlcomp_amd.models.native_generic import lower_or_none
     return lower_or_none(model)
 

@@ -141,3 +141,19 @@ def test_deterministic_embedding_segment_sums_match_index_add():
     got = _segment_sums(ix, rows, 100)                # ids 97..99 never occur: zero rows
     want = torch.zeros(100, 24).index_add_(0, ix, rows)
     assert torch.allclose(got, want, atol=1e-5)
+
+
+def test_head_dim_above_flash_limit_is_native_unsupported():
+    """A head dim the fused attention does not take (> 128) raises NativeUnsupported at
+    build time, and the runner's engine choice sends the model to the torch engine instead
+    of asserting inside the first forward."""
+    from mlcomp_amd.train.native_spec import NativeUnsupported
+    from mlcomp_amd.train.runner import _generic_reason, _native_kind
+    tm = build_model('bert-tiny', num_classes=2, hidden=512, heads=2, intermediate=512)
+    assert tm.config.head_dim == 256
+    with pytest.raises(NativeUnsupported, match='head_dim 256'):
+        NativeBert(tm, 'cpu', 2, 16)
+    assert _native_kind(tm, torch.device('cuda')) is None
+    assert 'head_dim 256' in _generic_reason(tm)
+    ok = build_model('bert-tiny', num_classes=2)
+    assert _native_kind(ok, torch.device('cuda')) == 'bert'

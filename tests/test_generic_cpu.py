@@ -536,6 +536,32 @@ def test_squeeze_excitation_gates_match_fp32_autograd():
         assert _cos(gg, _torch_grad(p, ref)) > 0.98, p.name
 
 
+class _SampleGateNet(nn.Module):
+    """A per-sample gate ([N, 1, 1, 1]) computed from the value's global average: a valid
+    torch broadcast that is not a per-channel gate, so it must stay a torch op."""
+
+    def __init__(self):
+        super().__init__()
+        self.c1 = nn.Conv2d(3, 16, 3, 1, 1)
+        self.fc = nn.Conv2d(16, 1, 1)
+        self.head = nn.Linear(16, 4)
+
+    def forward(self, x):
+        y = torch.relu(self.c1(x))
+        y = y * torch.sigmoid(self.fc(F.adaptive_avg_pool2d(y, 1)))
+        return self.head(F.adaptive_avg_pool2d(y, 1).flatten(1))
+
+
+def test_per_sample_gate_stays_a_torch_op():
+    m, ref = _pair(_SampleGateNet)
+    net = GenericNet(m, 'cpu')
+    kinds = [type(s).__name__ for s in net.train_gm.modules()]
+    assert 'ChannelGate' not in kinds, kinds
+    x = torch.randn(3, 3, 8, 8)
+    out, want = net(x), ref(x)
+    assert _rel(out, want) < 2e-2
+
+
 class _DropPathNet(nn.Module):
     """Residual blocks ending in conv -> BN -> stochastic depth -> + x (EfficientNet's MBConv)."""
 

@@ -14,7 +14,7 @@ def _parse():
     decls = {}
     for f in glob.glob(os.path.join(ROOT, 'csrc', 'kernels', '*.hip')):
         src = open(f).read()
-        for m in re.finditer(r'MLC_EXPORT\s+(?:int|long|void\*)\s+(\w+)\s*\(([^)]*)\)', src):
+        for m in re.finditer(r'MLC_EXPORT\s+(?:int|long|void\*|void|const char\*)\s+(\w+)\s*\(([^)]*)\)', src):
             args = [a.strip() for a in m.group(2).replace('\n', ' ').split(',') if a.strip()]
             kinds = []
             for a in args:
