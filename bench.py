@@ -100,13 +100,20 @@ def main():
     comm = _world1_rccl(device) if (args.comm == 'rccl1' and world == 1 and args.impl == 'native') else None
     is_bert = args.model.startswith('bert')
     is_unet = args.model.split('-')[0] in ('unet', 'linknet', 'fpn', 'pspnet', 'deeplab')
+    # torch.nn-defined transformers (no hand engine): the generic native engine's fx lowering
+    is_generic = args.model.startswith(('transformer-', 'vit-'))
     if args.batch is None:
         # ResNet-50: 512 images per GPU, sized for 288 GB of HBM3E (the reference's preset is 56
         # for 11-16 GB cards). Measured on one MI355X: 256 -> 12.4-12.7k img/s, 512 -> 13.3-13.4k,
         # 768 -> 13.5k; stock PyTorch-ROCm 6.0k / 6.4k at 256 / 512
         # (profiles/round4/resnet50_batch.txt). --batch 256 reproduces the earlier rounds' config.
-        args.batch = 32 if (is_bert or is_unet) else 512
-    if is_unet:
+        args.batch = 32 if (is_bert or is_unet) else 128 if args.model.startswith('vit-') else 512
+    if is_generic:
+        from mlcomp_amd.train.generic import build_generic_step
+        step = build_generic_step(args.model, batch=args.batch, seq_len=args.seq_len, image_size=args.image_size,
+                                  impl=args.impl, device=device, world_size=world,
+                                  use_graph=(args.graph if args.graph >= 0 else None), comm=comm)
+    elif is_unet:
         # U-Net (BASELINE config 3): --model unet[-<encoder>], 256x256 unless --image-size
         from mlcomp_amd.train.segment import build_seg_step
         if args.image_size == 224:
@@ -181,6 +188,21 @@ def main():
             'config': {'model': args.model, 'global_batch': args.batch * world, 'per_gpu_batch': args.batch,
                        'image_size': args.image_size, 'parallelism': f'dp{world}', 'impl': args.impl,
                        'loader_threads': args.loader_threads, 'final_loss': loss}}
+        print(json.dumps(out), flush=True)
+    elif rank == 0 and is_generic:
+        text = args.model.startswith('transformer-')
+        unit = 'sequences/s' if text else 'images/s'
+        out = {
+            'metric': f'{unit.split("/")[0]}/sec (whole node) {args.model} train task (torch.nn model, generic engine)',
+            'value': round(value, 2), 'unit': unit, 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'bf16',
+            'data': (f'synthetic (random token ids, seq_len {args.seq_len}, 2 labels, random-init weights)' if text else
+                     f'synthetic ({args.image_size}x{args.image_size}x3 images, 1000 classes, random-init weights)'),
+            'config': {'model': args.model, 'global_batch': args.batch * world, 'per_gpu_batch': args.batch,
+                       'seq_len': args.seq_len if text else None, 'image_size': None if text else args.image_size,
+                       'parallelism': f'dp{world}', 'impl': args.impl,
+                       'optimizer': 'AdamW wd 0.01, fp32 master weights', 'final_loss': loss}}
         print(json.dumps(out), flush=True)
     elif rank == 0 and is_bert:
         out = {

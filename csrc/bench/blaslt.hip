@@ -1,5 +1,11 @@
-// Library GEMM backend (hipBLASLt) for the plain dense-layer GEMMs, and the per-shape
-// selection between it and the native MFMA kernels (igemm.hip).
+// BENCH-ONLY library GEMM backend (hipBLASLt) for the plain dense-layer GEMMs, and the
+// per-shape selection between it and the native MFMA kernels (igemm.hip).
+//
+// Not part of the production kernel library: build.py links it into a separate A/B twin,
+// libmlcomp_kernels_blaslt.so (every kernel object + this file + -lhipblaslt), which the
+// comparison scripts and tests/test_blaslt_gpu.py load through MLC_KERNEL_LIB.  The
+// production libmlcomp_kernels.so exports the same three entry points from
+// csrc/kernels/dense_entry.hip, which call the native kernels only.
 //
 // The dense layers of BERT-base (M = 4096 tokens, K = 768 / 3072) are plain GEMMs with a
 // bias or residual epilogue; on those shapes hipBLASLt's assembly kernels run 25-45 %
@@ -35,7 +41,7 @@
 #include <tuple>
 #include <vector>
 
-#include "common.h"
+#include "../kernels/common.h"
 
 // native launchers (igemm.hip)
 extern "C" int mlc_gemm_bf16_ex_native(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int lda, int ldb,

@@ -1,7 +1,11 @@
 """Build the native parts of mlcomp_amd in-tree.
 
 * ``libmlcomp_kernels.so`` - every ``csrc/kernels/*.hip`` compiled for gfx950 with hipcc
-  (extern "C" launchers, loaded with ctypes by :mod:`mlcomp_amd.ops._lib`).
+  (extern "C" launchers, loaded with ctypes by :mod:`mlcomp_amd.ops._lib`); links RCCL and
+  no vendor GEMM / conv library.
+* ``libmlcomp_kernels_blaslt.so`` - its bench-only A/B twin: the same kernel objects, with
+  ``csrc/bench/blaslt.hip`` (timed per-shape hipBLASLt selection) in place of
+  ``dense_entry.hip``; loaded only through ``MLC_KERNEL_LIB`` by comparison scripts / tests.
 * ``mlcomp-broker`` - the C++17 epoll task-queue daemon (``csrc/broker``), the native
   replacement for the reference's vendored redis-server (`mlcomp/bin/redis-server`,
   launched at `mlcomp/server/__main__.py:66-79`).
@@ -28,6 +32,7 @@ HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('MLC_OFFLOAD_ARCH', 'gfx950')
 
 KERNEL_LIB = os.path.join(OUT, 'libmlcomp_kernels.so')
+BLASLT_LIB = os.path.join(OUT, 'libmlcomp_kernels_blaslt.so')
 BROKER_BIN = os.path.join(OUT, 'mlcomp-broker')
 RUNTIME_LIB = os.path.join(OUT, 'libmlcomp_runtime.so')
 
@@ -48,7 +53,8 @@ def _run(cmd):
 
 def build_kernels(verbose=False, jobs=None):
     os.makedirs(OUT, exist_ok=True)
-    srcs = sorted(glob.glob(os.path.join(ROOT, 'csrc', 'kernels', '*.hip')))
+    bench = sorted(glob.glob(os.path.join(ROOT, 'csrc', 'bench', '*.hip')))
+    srcs = sorted(glob.glob(os.path.join(ROOT, 'csrc', 'kernels', '*.hip'))) + bench
     headers = glob.glob(os.path.join(ROOT, 'csrc', 'kernels', '*.h'))
     objdir = os.path.join(OUT, 'obj')
     os.makedirs(objdir, exist_ok=True)
@@ -65,11 +71,18 @@ def build_kernels(verbose=False, jobs=None):
         futs = [ex.submit(_run, [HIPCC] + flags + ['-c', s, '-o', o]) for s, o in todo]
         for f in futs:
             f.result()
-    if todo or _newer(KERNEL_LIB, objs):
-        _run([HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', '-o', KERNEL_LIB] + objs
+    bench_objs = [os.path.join(objdir, os.path.basename(s) + '.o') for s in bench]
+    entry = os.path.join(objdir, 'dense_entry.hip.o')
+    prod = [o for o in objs if o not in bench_objs]
+    if todo or _newer(KERNEL_LIB, prod):
+        _run([HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', '-o', KERNEL_LIB] + prod
+             + ['-L/opt/rocm/lib', '-lrccl', '-Wl,-rpath,/opt/rocm/lib'])
+    twin = [o for o in prod if o != entry] + bench_objs
+    if bench_objs and (todo or _newer(BLASLT_LIB, twin)):
+        _run([HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', '-o', BLASLT_LIB] + twin
              + ['-L/opt/rocm/lib', '-lrccl', '-lhipblaslt', '-Wl,-rpath,/opt/rocm/lib'])
     if verbose:
-        print(f'[build] kernels: {len(todo)} rebuilt -> {KERNEL_LIB}')
+        print(f'[build] kernels: {len(todo)} rebuilt -> {KERNEL_LIB} (+ bench twin {os.path.basename(BLASLT_LIB)})')
     return KERNEL_LIB
 
 

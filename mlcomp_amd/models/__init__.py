@@ -33,6 +33,6 @@ def _populate():
     from . import resnet as _r
     for v in _r._SPECS:
         MODELS[v] = (lambda v: (lambda **kw: _r.resnet(v, **kw)))(v)
-    from . import zoo, efficientnet, bert, cadene, nas  # noqa: F401  (register more families)
+    from . import zoo, efficientnet, bert, cadene, nas, transformers  # noqa: F401  (register more families)
     import mlcomp_amd.contrib.segmentation  # noqa: F401
     import mlcomp_amd.contrib.video  # noqa: F401

@@ -1,4 +1,5 @@
-"""Per-shape native vs hipBLASLt selection (csrc/kernels/blaslt.hip) on BERT-base's dense
+"""Per-shape native vs hipBLASLt selection (csrc/bench/blaslt.hip; run with
+MLC_KERNEL_LIB=mlcomp_amd/_native/libmlcomp_kernels_blaslt.so) on BERT-base's dense
 GEMMs: every form (bias forward, residual-addend input gradient, plain input gradient,
 weight + bias gradient) is checked against an fp32 reference under both forced modes,
 then the auto mode's timed choice is printed per shape as one JSON line.

@@ -1,9 +1,16 @@
-"""Per-shape native / hipBLASLt selection for the dense GEMMs (csrc/kernels/blaslt.hip):
-both forced modes and the timed auto mode match an fp32 reference for every form the
-models use (bias forward, residual-addend input gradient, weight + bias gradient
-accumulated into fp32), and a HIP graph captured after the eager warm-up replays the
-choice warm-up made (the library path, bitwise equal to its eager output)."""
+"""Per-shape native / hipBLASLt selection for the dense GEMMs (csrc/bench/blaslt.hip), in the
+BENCH-ONLY twin library libmlcomp_kernels_blaslt.so: both forced modes and the timed auto
+mode match an fp32 reference for every form the models use (bias forward, residual-addend
+input gradient, weight + bias gradient accumulated into fp32), and a HIP graph captured
+after the eager warm-up replays the choice warm-up made.
+
+The production library has no library path (dense_entry.hip): mlc_blaslt_mode refuses to
+turn it on.  The twin is loaded through MLC_KERNEL_LIB, so when this module runs inside the
+GPU suite (production library loaded) the library-path tests run in ONE child process."""
 import ctypes
+import os
+import subprocess
+import sys
 
 import pytest
 import torch
@@ -13,10 +20,31 @@ from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops import transformer as Tx
 
 pytestmark = pytest.mark.gpu
+TWIN = os.environ.get('MLC_KERNEL_LIB', '').endswith('_blaslt.so')
+
+
+def test_production_library_refuses_the_library_path():
+    if TWIN:
+        pytest.skip('running inside the twin-library child')
+    assert _lib.load().mlc_blaslt_mode(1) == -1
+    assert _lib.load().mlc_blaslt_mode(-1) == 0
+
+
+def test_twin_library_selection_in_child():
+    if TWIN:
+        pytest.skip('already the child')
+    from mlcomp_amd.build import BLASLT_LIB
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MLC_KERNEL_LIB=BLASLT_LIB, PYTHONPATH=root)
+    r = subprocess.run([sys.executable, '-m', 'pytest', os.path.abspath(__file__), '-x', '-q', '-m', 'gpu',
+                        '-p', 'no:cacheprovider'], env=env, cwd=root, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
 
 
 @pytest.fixture
 def lib():
+    if not TWIN:
+        pytest.skip('library-path tests run in the twin-library child')
     lib = _lib.load()
     old = lib.mlc_blaslt_mode(-1)
     yield lib

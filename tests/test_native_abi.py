@@ -54,3 +54,19 @@ def test_det_copies_floor_matches_kernels():
                          env=dict(os.environ, MLC_DETERMINISTIC='1', MLC_DET_COPIES='8'),
                          capture_output=True, text=True, check=True)
     assert out.stdout.split() == ['32', '32'], out.stdout
+
+
+def test_production_library_links_no_vendor_gemm():
+    """libmlcomp_kernels.so needs RCCL and the HIP runtime, never hipBLASLt / rocBLAS /
+    MIOpen (the library A/B path lives in the bench-only twin, csrc/bench/blaslt.hip)."""
+    import shutil
+    import subprocess
+    from mlcomp_amd.build import BLASLT_LIB, build_kernels
+    path = build_kernels()
+    tool = shutil.which('readelf') or '/opt/rocm/lib/llvm/bin/llvm-readelf'
+    needed = subprocess.run([tool, '-d', path], capture_output=True, text=True, check=True).stdout
+    libs = [ln.split('[')[1].split(']')[0] for ln in needed.splitlines() if 'NEEDED' in ln]
+    assert any('rccl' in n for n in libs), libs
+    assert not [n for n in libs if any(v in n for v in ('blas', 'MIOpen', 'miopen'))], libs
+    twin = subprocess.run([tool, '-d', BLASLT_LIB], capture_output=True, text=True, check=True).stdout
+    assert 'hipblaslt' in twin
