@@ -107,7 +107,8 @@ def main():
         # for 11-16 GB cards). Measured on one MI355X: 256 -> 12.4-12.7k img/s, 512 -> 13.3-13.4k,
         # 768 -> 13.5k; stock PyTorch-ROCm 6.0k / 6.4k at 256 / 512
         # (profiles/round4/resnet50_batch.txt). --batch 256 reproduces the earlier rounds' config.
-        args.batch = 32 if (is_bert or is_unet) else 128 if args.model.startswith('vit-') else 512
+        args.batch = 32 if (is_bert or is_unet or args.model.startswith('transformer-')) else \
+            128 if args.model.startswith('vit-') else 512
     if is_generic:
         from mlcomp_amd.train.generic import build_generic_step
         step = build_generic_step(args.model, batch=args.batch, seq_len=args.seq_len, image_size=args.image_size,

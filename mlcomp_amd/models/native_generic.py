@@ -298,8 +298,33 @@ class _Lowering:
         new = self._site_node(chain[-1], site, [node.args[0]] + ([res] if res is not None else []))
         self._replace(chain, new)
 
+    def _mlp(self, node, m) -> bool:
+        """Linear -> exact GELU -> Linear [-> + residual] (each value used once) -> MlpSite."""
+        g = _only_user(node)
+        if g is None or _act_of(g, self.modules) != (A['gelu'], 0.0):
+            return False
+        n2 = _only_user(g)
+        if n2 is None or not _is_module(n2, self.modules, nn.Linear) or n2.args[0] is not g or len(n2.args) != 1:
+            return False
+        m2 = self.modules[n2.target]
+        if m.out_features % 8 or m.in_features % 8 or m2.out_features % 8 or m2.in_features != m.out_features:
+            return False
+        chain = [node, g, n2]
+        res = None
+        u = _only_user(n2)
+        if u is not None and _residual_of(u, n2) is not None:
+            res = _residual_of(u, n2)
+            chain.append(u)
+        site = GT.MlpSite(self.net.ctx, self.net.linear_params(node.target, m), self.net.linear_params(n2.target, m2),
+                          residual=res is not None)
+        new = self._site_node(chain[-1], site, [node.args[0]] + ([res] if res is not None else []))
+        self._replace(chain, new)
+        return True
+
     def linear(self, node):
         m = self.modules[node.target]
+        if self._mlp(node, m):
+            return
         chain = [node]
         u = _only_user(node)
         act = 0
@@ -313,8 +338,12 @@ class _Lowering:
             new = self._site_node(chain[-1], site, [node.args[0]])
             self._replace(chain, new)
             return
-        site = LinearAct(self.net.ctx, self.net.linear_params(node.target, m), act)
-        new = self._site_node(chain[-1], site, [node.args[0]])
+        res = None
+        if act == 0 and m.out_features % 8 == 0 and u is not None and _residual_of(u, node) is not None:
+            res = _residual_of(u, node)          # y = x W^T + b + r: the add in the epilogue
+            chain.append(u)
+        site = LinearAct(self.net.ctx, self.net.linear_params(node.target, m), act, residual=res is not None)
+        new = self._site_node(chain[-1], site, [node.args[0]] + ([res] if res is not None else []))
         self._replace(chain, new)
 
     def avgpool2d(self, node, k, s, p, ceil=False, cip=True, div=None):
@@ -543,6 +572,34 @@ class _Lowering:
         new = self._site_node(node, site, [a['src']] + ([kpm] if kpm is not None else []))
         self._replace([node], new)
 
+    def _packed_qkv(self, q, k, v):
+        """timm's packed projection ``L.reshape(B, N, 3, H, D).permute(2, 0, 3, 1, 4)`` split
+        into q / k / v (``unbind(0)`` or ``[0] / [1] / [2]``): (L, H, chain nodes) or None."""
+        def split(n):
+            if not (isinstance(n, fx.Node) and n.op == 'call_function' and n.target is operator.getitem
+                    and isinstance(n.args[1], int)):
+                return None
+            src = n.args[0]
+            if src.op in ('call_method', 'call_function') and getattr(src.target, '__name__', src.target) == 'unbind':
+                dim = src.args[1] if len(src.args) > 1 else src.kwargs.get('dim', 0)
+                return (src.args[0], n.args[1], src) if dim == 0 else None
+            return src, n.args[1], None
+        parts = [split(t) for t in (q, k, v)]
+        if any(p is None for p in parts) or [p[1] for p in parts] != [0, 1, 2] or len({id(p[0]) for p in parts}) != 1:
+            return None
+        perm, _, unb = parts[0]
+        if not (perm.op == 'call_method' and perm.target == 'permute'):
+            return None
+        dims = perm.args[1:] if len(perm.args) > 2 else perm.args[1]
+        if tuple(dims) != (2, 0, 3, 1, 4):
+            return None
+        rs = perm.args[0]
+        if not (rs.op == 'call_method' and rs.target in ('reshape', 'view') and len(rs.args) == 6 and rs.args[3] == 3
+                and isinstance(rs.args[4], int)):
+            return None
+        chain = [n for n in (q, k, v)] + ([unb] if unb is not None else []) + [perm, rs]
+        return rs.args[0], int(rs.args[4]), chain
+
     def sdpa(self, node):
         a = self._call_args(node, ('query', 'key', 'value', 'attn_mask', 'dropout_p', 'is_causal', 'scale',
                                    'enable_gqa'))
@@ -552,6 +609,18 @@ class _Lowering:
         p, scale = a.get('dropout_p', 0.0), a.get('scale')
         if isinstance(p, fx.Node) or isinstance(scale, fx.Node):
             raise NativeUnsupported(f'{node.name}: scaled_dot_product_attention with a traced dropout_p / scale')
+        packed = self._packed_qkv(a['query'], a['key'], a['value'])
+        if packed is not None and all(len(n.users) == 1 for n in packed[2][:3]):
+            # zero-copy: the projection's [B, N, 3E] output IS the kernel's qkv layout
+            L, H, chain = packed
+            site = GT.SDPASite(self.net.ctx, float(p or 0.0), None if scale is None else float(scale), heads=H)
+            new = self._site_node(node, site, [L])
+            self._replace([node], new)
+            for n in chain:
+                if not n.users and n not in self.erased:
+                    self.gm.graph.erase_node(n)
+                    self.erased.add(n)
+            return
         site = GT.SDPASite(self.net.ctx, float(p or 0.0), None if scale is None else float(scale))
         new = self._site_node(node, site, [a['query'], a['key'], a['value']])
         self._replace([node], new)
@@ -729,8 +798,34 @@ class _Lowering:
                     todo.append(p)
         return False
 
+    def _prepass(self):
+        """Before pattern matching: p = 0 dropouts and Identity modules are no ops (so they
+        never split a fusable chain); float parameters that torch ops read (class tokens,
+        position embeddings, layer scales) enter the graph in bf16, the engine's compute
+        dtype, as autocast feeds a matmul - so the residual streams they start stay bf16."""
+        g = self.gm.graph
+        for node in list(g.nodes):
+            if node.op == 'call_module':
+                m = self.modules.get(node.target)
+                if isinstance(m, (nn.Dropout, nn.Identity)) and getattr(m, 'p', 0.0) == 0.0 \
+                        and len(node.args) == 1 and not node.kwargs:
+                    node.replace_all_uses_with(node.args[0])
+                    g.erase_node(node)
+            elif node.op == 'get_attr' and os.environ.get('MLC_GENERIC_PARAM_BF16', '1') == '1':
+                try:
+                    t = self.gm.get_parameter(node.target)
+                except AttributeError:
+                    continue
+                if not t.is_floating_point():
+                    continue
+                with g.inserting_after(node):
+                    cast = g.call_method('to', (node, torch.bfloat16))
+                node.replace_all_uses_with(cast)
+                cast.args = (node, torch.bfloat16)
+
     def run(self):
         g = self.gm.graph
+        self._prepass()
         for node in list(g.nodes):
             if node in self.erased:
                 continue

@@ -815,6 +815,12 @@ def linear_wgrad(dout, x, out=None, accumulate=False):
     return g
 
 
+# Dense weight + bias gradients: split-K tiles added into dW with fp32 atomics
+# (MLC_DENSE_WGRAD=atomic) or written to fp32 slabs that a reduction pass sums (=slab, the
+# round-5 default); the conv weight gradients' MLC_WGRAD_SLAB counterpart for dense layers.
+DENSE_WGRAD_ATOMIC = os.environ.get('MLC_DENSE_WGRAD', 'atomic') == 'atomic'
+
+
 def linear_wgrad_bias(dout, x, dw, db):
     """dW [O, I] += dout^T x and db [O] += colsum(dout) in ONE GEMM: the bias gradient is
     summed from dout's tiles as the wgrad kernel stages them (``mlc_linear_wgrad_bias``)."""
@@ -831,9 +837,13 @@ def linear_wgrad_bias(dout, x, dw, db):
         assert dout.is_contiguous() and x.is_contiguous() and x.shape[0] == B
         assert tuple(dw.shape) == (O, I) and dw.is_contiguous() and db.numel() == O
         from .transformer import gemm_workspace
-        ws = gemm_workspace(dout.device, 8 * O * I)   # split-K slabs (<= 8 splits)
+        if DENSE_WGRAD_ATOMIC:       # split-K partial tiles added straight into dW (fp32 atomics)
+            ws, nws = None, 0
+        else:                        # split-K slabs (<= 8 splits) + a reduction pass
+            ws = gemm_workspace(dout.device, 8 * O * I)
+            nws = ws.numel()
         _lib.call('mlc_linear_wgrad_bias', _lib.ptr(dout), _lib.ptr(x), _lib.ptr(dw), _lib.ptr(db), O, I, B, O, I, I,
-                  0, _lib.ptr(ws), ws.numel(), _lib.stream())
+                  0, _lib.ptr(ws), nws, _lib.stream())
         return dw, db
     dw.add_(dout.float().t() @ x.float())
     db.add_(dout.float().sum(0))

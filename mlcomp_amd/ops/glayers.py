@@ -886,17 +886,20 @@ class BNAct(Site):
 
 
 class LinearAct(Site):
-    """x [..., I] -> act(x W^T + b) on the dense GEMM (bias / ReLU in the epilogue)."""
+    """x [..., I] -> act(x W^T + b) [+ r] on the dense GEMM (bias / ReLU / the residual add
+    in the epilogue; a residual only without an activation)."""
 
-    def __init__(self, ctx, lin: LinearParams, act: int = 0):
+    def __init__(self, ctx, lin: LinearParams, act: int = 0, residual: bool = False):
         super().__init__(ctx)
         object.__setattr__(self, 'lin', lin)
         self.act = act            # 0 or 3 (ReLU; the epilogue's code)
+        self.residual = residual
+        assert not (residual and (act or lin.Op != lin.O)), 'a fused residual needs act 0 and an unpadded output'
 
-    def forward(self, x):
-        return _run(self, x)
+    def forward(self, x, r=None):
+        return _run(self, x, r) if r is not None else _run(self, x)
 
-    def fwd(self, x):
+    def fwd(self, x, r=None):
         p = self.lin
         lead = x.shape[:-1]
         x2 = x.reshape(-1, x.shape[-1])
@@ -906,23 +909,32 @@ class LinearAct(Site):
             x2 = torch.nn.functional.pad(x2, (0, p.Ip - p.I))
         x2 = x2.contiguous()
         B = x2.shape[0]
+        r2 = None
+        if r is not None:
+            r2 = r.expand(*lead, p.O).reshape(B, p.O)
+            if r2.dtype != torch.bfloat16:
+                r2 = r2.to(torch.bfloat16)
+            r2 = r2.contiguous()
         if x2.is_cuda:
             from . import _lib
             y = torch.empty(B, p.Op, device=x2.device, dtype=torch.bfloat16)
             _lib.call('mlc_gemm_bf16_ex', _lib.ptr(x2), _lib.ptr(p.w.bf16), _lib.ptr(y), B, p.Op, p.Ip, p.Ip, p.Ip,
-                      p.Op, 0, 1, _lib.ptr(p.b.master if p.b is not None else None), int(self.act), None, None, None,
-                      None, 0, _lib.stream())
+                      p.Op, 0, 1, _lib.ptr(p.b.master if p.b is not None else None), int(self.act), None,
+                      _lib.ptr(r2), None, None, 0, _lib.stream())
         else:
             yf = x2.float() @ p.w.bf16.float().t()
             if p.b is not None:
                 yf = yf + p.b.master
             if self.act == 3:
                 yf = yf.clamp_min(0)
+            if r2 is not None:
+                yf = yf + r2.float()
             y = yf.to(torch.bfloat16)
         out = y[:, :p.O] if p.Op != p.O else y
-        return out.reshape(*lead, p.O), [x2, y], False
+        keep = None if r is None else (tuple(r.shape), r.dtype)
+        return out.reshape(*lead, p.O), [x2, y], keep
 
-    def bwd(self, dout, saved, has_res, needs):
+    def bwd(self, dout, saved, keep, needs):
         p = self.lin
         x2, y = saved
         d = dout.reshape(-1, p.O)
@@ -944,7 +956,11 @@ class LinearAct(Site):
             if p.Ip != p.I:
                 dx = dx[:, :p.I]
             dx = dx.reshape(*dout.shape[:-1], p.I)
-        return [dx]
+        out = [dx]
+        if keep is not None:           # the residual's gradient is the output gradient
+            from .gtransformer import _reduce_to
+            out.append(_reduce_to(dout, keep[0], keep[1]) if needs[1] else None)
+        return out
 
 
 class UpCat(Site):

@@ -91,39 +91,49 @@ class DenseSet:
     def fwd(self, x, act=0, want_preact=False):
         return Tx.dense_fwd(x, self.w.bf16, self.b.master if self.b is not None else None, act, want_preact)
 
-    def _wgrad(self, dy, x):
-        if self.b is not None and dy.shape[1] % 8 == 0 and x.shape[1] % 8 == 0:
-            Fn.linear_wgrad_bias(dy, x, self.w.grad, self.b.grad)
-        else:
-            Fn.linear_wgrad(dy, x, out=self.w.grad, accumulate=True)
-            if self.b is not None:
-                Tx.colsum_acc(dy, self.b.grad) if dy.shape[1] % 8 == 0 else self.b.grad.add_(dy.float().sum(0))
-
     def backward(self, dy, x, dact_u=None, addend=None, dact_is_deriv=False, need_dx=True):
         """dx = dy @ W [* dact_u] [+ addend] (returned); dW += dy^T x, db += colsum(dy)."""
-        ctx = self.ctx
-        side = ctx.wgrad_stream
-        dx = None
-        if side is None:
-            if need_dx:
-                dx = Tx.dense_dgrad(dy, self.w.bf16, dact_u=dact_u, addend=addend, dact_is_deriv=dact_is_deriv)
-            self._wgrad(dy, x)
-        else:
-            main = torch.cuda.current_stream(ctx.device)
-            fork = torch.cuda.Event()
-            fork.record(main)
-            if need_dx:
-                dx = Tx.dense_dgrad(dy, self.w.bf16, dact_u=dact_u, addend=addend, dact_is_deriv=dact_is_deriv)
-            side.wait_event(fork)
-            with Fn.side_stream(side):
-                self._wgrad(dy, x)
-            dy.record_stream(side)
-            x.record_stream(side)
-            if not ctx.wgrad_defer:
-                main.wait_stream(side)
+        dx = dense_backward(self.ctx, self.w, self.b, dy, x, dact_u=dact_u, addend=addend,
+                            dact_is_deriv=dact_is_deriv, need_dx=need_dx)
         if self.uses.bwd_done():
             self.mark_ready()
         return dx
+
+
+def _wgrad(w, b, dy, x):
+    if b is not None and dy.shape[1] % 8 == 0 and x.shape[1] % 8 == 0:
+        Fn.linear_wgrad_bias(dy, x, w.grad, b.grad)
+    else:
+        Fn.linear_wgrad(dy, x, out=w.grad, accumulate=True)
+        if b is not None:
+            Tx.colsum_acc(dy, b.grad) if dy.shape[1] % 8 == 0 else b.grad.add_(dy.float().sum(0))
+
+
+def dense_backward(ctx, w, b, dy, x, dact_u=None, addend=None, dact_is_deriv=False, need_dx=True):
+    """A dense layer's backward with the hand BERT engine's schedule: the input gradient
+    dx = dy @ W [* dact_u] [+ addend] on the main stream first, the weight + bias gradient
+    (one GEMM) forked onto the side stream from the point before it (unjoined with
+    ``ctx.wgrad_defer``: one free-running chain joined before the optimizer)."""
+    side = ctx.wgrad_stream
+    dx = None
+    if side is None:
+        if need_dx:
+            dx = Tx.dense_dgrad(dy, w.bf16, dact_u=dact_u, addend=addend, dact_is_deriv=dact_is_deriv)
+        _wgrad(w, b, dy, x)
+        return dx
+    main = torch.cuda.current_stream(ctx.device)
+    fork = torch.cuda.Event()
+    fork.record(main)
+    if need_dx:
+        dx = Tx.dense_dgrad(dy, w.bf16, dact_u=dact_u, addend=addend, dact_is_deriv=dact_is_deriv)
+    side.wait_event(fork)
+    with Fn.side_stream(side):
+        _wgrad(w, b, dy, x)
+    dy.record_stream(side)
+    x.record_stream(side)
+    if not ctx.wgrad_defer:
+        main.wait_stream(side)
+    return dx
 
 
 class LNParams:
@@ -536,34 +546,49 @@ class EncoderSite(nn.Module):
 
 # ---------------------------------------------------------------------------- SDPA, dense + GELU
 class SDPASite(Site):
-    """``F.scaled_dot_product_attention(q, k, v, dropout_p=p, scale=s)`` with q / k / v
-    [B, H, S, D] (no mask, not causal): packed into the kernel's [B*S, 3*H*D] layout, flash
-    attention forward / backward; the output is a [B, H, S, D] view of the kernel's
-    [B*S, H*D] context rows (so a following ``transpose(1, 2).reshape(B, S, H*D)`` is free)."""
+    """``F.scaled_dot_product_attention(q, k, v, dropout_p=p, scale=s)`` (no mask, not causal)
+    on the flash kernels; the output is a [B, H, S, D] view of the kernel's [B*S, H*D]
+    context rows (so a following ``transpose(1, 2).reshape(B, S, H*D)`` is free).
 
-    def __init__(self, ctx, p: float = 0.0, scale: Optional[float] = None):
+    ``heads`` set (the lowering matched timm's ``qkv(x).reshape(B, N, 3, H, D).permute(2, 0,
+    3, 1, 4)`` split): the single input is the projection output [B, N, 3*H*D], which already
+    is the kernel's packed layout - no copy forward, and the packed gradient is the
+    projection's output gradient - no copy backward.  Otherwise q / k / v [B, H, S, D] are
+    packed with one copy."""
+
+    def __init__(self, ctx, p: float = 0.0, scale: Optional[float] = None, heads: Optional[int] = None):
         super().__init__(ctx)
-        self.p, self.scale = float(p), scale
+        self.p, self.scale, self.heads = float(p), scale, heads
         self.salt = next_salt(ctx)
 
     def params(self):
         return []
 
-    def forward(self, q, k, v):
-        return _run(self, q, k, v)
+    def forward(self, *qkv):
+        return _run(self, *qkv)
 
-    def fwd(self, q, k, v):
-        B, H, S, D = q.shape
-        if tuple(k.shape) != (B, H, S, D) or tuple(v.shape) != (B, H, S, D):
-            raise ValueError(f'SDPA site: q {tuple(q.shape)} k {tuple(k.shape)} v {tuple(v.shape)} (self-attention '
-                             'shapes expected)')
-        qkv = torch.stack([t.to(torch.bfloat16) for t in (q, k, v)], 2)        # [B, H, 3, S, D]
-        qkv = qkv.permute(0, 3, 2, 1, 4).reshape(B * S, 3 * H * D).contiguous()
+    def fwd(self, *inputs):
+        if self.heads is not None:
+            (L,) = inputs
+            B, S, E3 = L.shape
+            H = self.heads
+            D = E3 // (3 * H)
+            qkv = _rows(L)
+            dt = L.dtype
+        else:
+            q, k, v = inputs
+            B, H, S, D = q.shape
+            if tuple(k.shape) != (B, H, S, D) or tuple(v.shape) != (B, H, S, D):
+                raise ValueError(f'SDPA site: q {tuple(q.shape)} k {tuple(k.shape)} v {tuple(v.shape)} '
+                                 '(self-attention shapes expected)')
+            qkv = torch.stack([t.to(torch.bfloat16) for t in (q, k, v)], 2)    # [B, H, 3, S, D]
+            qkv = qkv.permute(0, 3, 2, 1, 4).reshape(B * S, 3 * H * D).contiguous()
+            dt = q.dtype
         scale = self.scale if self.scale is not None else 1.0 / math.sqrt(D)
         p = self.p if self.ctx.training else 0.0
         ctx2, lse = Tx.attn_fwd(qkv, None, B, S, H, scale, p, _seed(self.ctx), self.salt, head_dim=D)
         out = ctx2.view(B, S, H, D).transpose(1, 2)
-        return out, [qkv, lse, ctx2], (B, H, S, D, scale, p, q.dtype)
+        return out, [qkv, lse, ctx2], (B, H, S, D, scale, p, dt)
 
     def bwd(self, dout, saved, keep, needs):
         qkv, lse, ctx2 = saved
@@ -573,6 +598,8 @@ class SDPASite(Site):
             dctx = dctx.to(torch.bfloat16)
         dqkv = Tx.attn_bwd(qkv, None, dctx.contiguous(), lse, B, S, H, scale, p, _seed(self.ctx), self.salt,
                            head_dim=D, ctx=ctx2)
+        if self.heads is not None:
+            return [dqkv.view(B, S, 3 * H * D).to(dt) if needs[0] else None]
         d = dqkv.view(B, S, 3, H, D).permute(2, 0, 3, 1, 4)                   # [3, B, H, S, D]
         return [d[i].to(dt) if needs[i] else None for i in range(3)]
 
@@ -616,6 +643,52 @@ class PatchEmbed(Site):
         if Hp * k != H or Wp * k != W:
             dx = torch.nn.functional.pad(dx, (0, W - Wp * k, 0, H - Hp * k))
         return [dx.to(dt)]
+
+
+class MlpSite(Site):
+    """``fc2(gelu(fc1(x))) [+ r]`` (exact GELU; a transformer MLP, timm's ``Mlp``): fc1's
+    epilogue adds the bias, applies the GELU and stores gelu'(pre-activation); fc2's adds its
+    bias and the residual ``r``; backward multiplies by gelu' inside fc2's input-gradient
+    epilogue, so no elementwise pass is left.  Weight gradients on the side stream."""
+
+    def __init__(self, ctx, fc1, fc2, residual: bool = False):
+        super().__init__(ctx)
+        object.__setattr__(self, 'fc1', fc1)          # glayers.LinearParams, unpadded
+        object.__setattr__(self, 'fc2', fc2)
+        self.residual = residual
+
+    def params(self):
+        return [self.fc1, self.fc2]
+
+    def forward(self, x, r=None):
+        return _run(self, x, r) if r is not None else _run(self, x)
+
+    def fwd(self, x, r=None):
+        p1, p2 = self.fc1, self.fc2
+        lead = x.shape[:-1]
+        x2 = _rows(x)
+        g, m = Tx.dense_fwd(x2, p1.w.bf16, p1.b.master if p1.b is not None else None, act=2, want_preact=True)
+        r2 = _rows(r.expand(*lead, p2.O)) if r is not None else None
+        y, _ = Tx.dense_fwd(g, p2.w.bf16, p2.b.master if p2.b is not None else None, addend=r2)
+        keep = (x.dtype, None if r is None else (r.shape, r.dtype))
+        return y.view(*lead, p2.O), [x2, g, m], keep
+
+    def bwd(self, dout, saved, keep, needs):
+        _db = dense_backward
+        p1, p2 = self.fc1, self.fc2
+        x2, g, m = saved
+        xdt, rkeep = keep
+        d = _rows(dout)
+        du = _db(self.ctx, p2.w, p2.b, d, g, dact_u=m, dact_is_deriv=True)
+        if p2.uses.bwd_done():
+            p2.mark_ready()
+        dx = _db(self.ctx, p1.w, p1.b, du, x2, need_dx=needs[0])
+        if p1.uses.bwd_done():
+            p1.mark_ready()
+        out = [dx.view(*dout.shape[:-1], p1.I).to(xdt) if dx is not None else None]
+        if rkeep is not None:
+            out.append(_reduce_to(dout, rkeep[0], rkeep[1]) if needs[1] else None)
+        return out
 
 
 class LinearGelu(Site):
@@ -663,4 +736,4 @@ class LinearGelu(Site):
 
 
 __all__ = ['DenseSet', 'LNParams', 'LayerNormSite', 'MHAParams', 'MHASite', 'EncoderLayerParams', 'EncoderSite',
-           'SDPASite', 'LinearGelu', 'PatchEmbed', 'encoder_layer_supported', 'mha_supported', 'key_bias_of', 'next_salt']
+           'SDPASite', 'LinearGelu', 'PatchEmbed', 'MlpSite', 'dense_backward', 'encoder_layer_supported', 'mha_supported', 'key_bias_of', 'next_salt']

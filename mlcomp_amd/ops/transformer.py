@@ -363,19 +363,22 @@ def _dgelu(u):
     return 0.5 * (1.0 + torch.erf(u / math.sqrt(2.0))) + u * torch.exp(-0.5 * u * u) / math.sqrt(2 * math.pi)
 
 
-def dense_fwd(x, w, bias=None, act: int = 0, want_preact: bool = False):
-    """y = act(x @ w^T + bias): x [M, K] bf16, w [N, K] bf16, bias fp32 [N].  Returns
-    (y, u) with u the bf16 pre-activation (when ``want_preact``).  ``act`` 1 = exact-erf
-    GELU; 2 = GELU returning u = gelu'(pre-activation) instead, for
-    ``dense_dgrad(..., dact_is_deriv=True)`` (the backward epilogue then only multiplies)."""
+def dense_fwd(x, w, bias=None, act: int = 0, want_preact: bool = False, addend=None):
+    """y = act(x @ w^T + bias) [+ addend]: x [M, K] bf16, w [N, K] bf16, bias fp32 [N],
+    addend bf16 [M, N] (a residual summed in the epilogue).  Returns (y, u) with u the bf16
+    pre-activation (when ``want_preact``).  ``act`` 1 = exact-erf GELU; 2 = GELU returning
+    u = gelu'(pre-activation) instead, for ``dense_dgrad(..., dact_is_deriv=True)`` (the
+    backward epilogue then only multiplies)."""
     M, K = x.shape
     N = w.shape[0]
     if _cuda(x):
         y = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
         u = torch.empty_like(y) if want_preact else None
+        if addend is not None:
+            assert addend.dtype == torch.bfloat16 and addend.is_contiguous() and tuple(addend.shape) == (M, N)
         _lib.call('mlc_gemm_bf16_ex', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), M, N, K, K, K, N, 0, 1,
-                  _lib.ptr(bias), act, _lib.ptr(u), None, None, _lib.ptr(gemm_workspace(x.device, 4 * M * N)),
-                  4 * M * N, _lib.stream())
+                  _lib.ptr(bias), act, _lib.ptr(u), _lib.ptr(addend), None,
+                  _lib.ptr(gemm_workspace(x.device, 4 * M * N)), 4 * M * N, _lib.stream())
         return y, u
     z = x.float() @ w.float().t()
     if bias is not None:
@@ -386,6 +389,8 @@ def dense_fwd(x, w, bias=None, act: int = 0, want_preact: bool = False):
         u = z.to(torch.bfloat16) if want_preact else None
     if act in (1, 2):
         z = _gelu(z)
+    if addend is not None:
+        z = z + addend.float()
     return z.to(torch.bfloat16), u
 
 

@@ -204,9 +204,27 @@ class _ViT(nn.Module):
 
 def test_vit_style_model_lowers_and_matches_autograd():
     net = _check(_ViT, lambda: torch.randn(2, 3, 64, 64),
-                 {'PatchEmbed': 1, 'SDPASite': 2, 'LayerNormSite': 5, 'LinearGelu': 2})
+                 {'PatchEmbed': 1, 'SDPASite': 2, 'LayerNormSite': 5, 'MlpSite': 2})
+    res = [s for s in net.train_gm.modules() if type(s).__name__ == 'LinearAct' and s.residual]
+    assert len(res) == 2                      # attention projections with the residual add fused
     # the position embedding and class token stay torch ops on arena-aliased parameters
     assert any(n.op == 'call_function' and n.target is torch.cat for n in net.train_gm.graph.nodes)
+
+
+class _GeluHead(nn.Module):
+    """Linear -> GELU not followed by a Linear: the GELU epilogue site."""
+
+    def __init__(self):
+        super().__init__()
+        self.fc = nn.Linear(24, 32)
+        self.act = nn.GELU()
+
+    def forward(self, x):
+        return self.act(self.fc(x)).mean(1)
+
+
+def test_linear_gelu_epilogue():
+    _check(_GeluHead, lambda: torch.randn(6, 5, 24), {'LinearGelu': 1})
 
 
 def test_transformer_models_choose_the_native_engine():
