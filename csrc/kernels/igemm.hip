@@ -721,6 +721,13 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
   // of an activation (act 1/2 = exact-erf GELU; act 4: dact holds the derivative)
   const float* bias = nullptr; int act = 0; bf16* preact = nullptr; const bf16* dact = nullptr;
   int ncopy = NSTAT;   // copies of sum / sumsq (g_mlc_ncopy at launch)
+  // the persistent kernel runs this epilogue while the next tile's LDS-DMA copies are in
+  // flight: its barriers must then be raw s_barriers (a full barrier would wait vmcnt(0))
+  bool raw_sync = false;
+  __device__ __forceinline__ void esync() const {
+    if (raw_sync) lds_barrier();
+    else __syncthreads();
+  }
   template <int BM, int BN, int MI, int NI>
   __device__ void apply(f32x16 (&acc)[MI][NI], char* lds, int m0, int n0, int M, int N,
                         int wm, int wn, int lane, int tid) const {
@@ -745,7 +752,7 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
     }
     // stage the BMxBN tile through LDS as bf16 rows of (BN+8)*2 B, then 16 B/lane stores
     constexpr int RS = (BN + 8) * 2;
-    __syncthreads();
+    esync();
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -756,7 +763,7 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
           const int n = wn * 32 * NI + 32 * j + (lane & 31);
           *reinterpret_cast<bf16*>(lds + m * RS + n * 2) = (bf16)acc[i][j][r];
         }
-    __syncthreads();
+    esync();
     constexpr int CPR = BN / 8;              // 16 B chunks per row
     constexpr int RPI = NTHR / CPR;          // rows per iteration
     // three-wide tiles: CPR does not divide the block (12 / 24 / 36 chunks per row), so
@@ -893,14 +900,14 @@ struct EpiBF16 {  // bf16 [M][ld] store (+ addend), optional per-column sum / su
       // combine the RPI threads that own the same 8 columns, then one atomic per
       // column and quantity into this block's copy slot
       float* rb = reinterpret_cast<float*>(lds);     // [NTHR][24]
-      __syncthreads();
+      esync();
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         rb[tid * 24 + e] = s1[e];
         rb[tid * 24 + 8 + e] = s2[e];
         rb[tid * 24 + 16 + e] = t2[e];
       }
-      __syncthreads();
+      esync();
       if (tid < BN) {
         const int col = tid, cc = col >> 3, e = col & 7, n = n0 + col;
         float a = 0.f, b = 0.f, d = 0.f;

@@ -92,8 +92,14 @@ class TimerCallback(Callback):
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() != state.world_size:
             return fps * state.world_size
         dev = getattr(getattr(state, 'runner', None), 'device', None)
-        on_gpu = dist.get_backend() == 'nccl' and dev is not None and dev.type == 'cuda'
-        t = torch.tensor([fps], dtype=torch.float64, device=dev if on_gpu else 'cpu')
+        if dist.get_backend() == 'nccl':
+            # an NCCL (= RCCL) group only reduces device tensors: the runner's device, else
+            # the process's current one
+            if dev is None or dev.type != 'cuda':
+                dev = torch.device('cuda', torch.cuda.current_device())
+        else:
+            dev = torch.device('cpu')
+        t = torch.tensor([fps], dtype=torch.float64, device=dev)
         dist.all_reduce(t)
         return float(t.item())
 

@@ -160,11 +160,13 @@ class WorkerPool:
             session.expire_all()
             tp = TaskProvider(session)
             t = tp.by_id(task_id)
-            if t is None or t.status != TaskStatus.InProgress.value:
+            # only a task still InProgress is failed here.  A straggler rank the scheduler
+            # stops on purpose is set Success before its kill (supervisor: parent finished),
+            # so the status test already covers it; the killed_by_supervisor mark is checked
+            # first anyway, so a kill that races the status write is never reported as lost
+            info = yaml_load(t.additional_info) or {} if t is not None else {}
+            if t is None or info.get('killed_by_supervisor') or t.status != TaskStatus.InProgress.value:
                 return
-            info = yaml_load(t.additional_info) or {}
-            if info.get('killed_by_supervisor'):
-                return     # a straggler rank the scheduler stopped on purpose
             for pid in info.get('child_processes', []):
                 kill_pid(pid)
             create_logger(session, 'WorkerPool', console=False).error(
