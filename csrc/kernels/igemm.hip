@@ -1292,6 +1292,122 @@ gemm_kernel(const LA la, const LB lb, const EPI epi, int M, int N, int K, int kt
   epi.template apply<BM, BN, MI, NI>(acc, smem, m0, n0, M, N, wm, wn, lane, tid);
 }
 
+// Persistent variant of the LDS-DMA main loop for short-K GEMMs (1x1 convs over <= a few
+// hundred channels: 1-8 K-tiles per output tile).  The non-persistent kernel pays, per
+// output tile, a cold prologue (first DMA round trip with nothing to overlap) and an
+// epilogue (LDS staging + stores) with nothing in flight; with only 1-4 K-tiles that is
+// most of a tile's life (the channel-expanding ResNet 1x1 convs ran at 1.7-4.5 TB/s,
+// profiles/round6/roofline_resnet50_b512.txt).  Here one block per CU walks a sequence of
+// tiles and the DMA ring runs ACROSS tile boundaries: the copies of the next tile's first
+// K-tiles are in flight while this tile's last MFMAs and its epilogue run.
+//   * NBUF operand stages in a ring + a separate epilogue staging region, so the epilogue
+//     never waits for the ring;
+//   * the epilogue's barriers are raw s_barriers (EpiBF16::raw_sync), never a full
+//     __syncthreads() that would drain vmcnt;
+//   * tiles are split into 8 contiguous ranges of the grouped tile order, one per XCD
+//     (blockIdx.x % 8), whose blocks stride through it: the tiles one XCD holds at a time
+//     are neighbours, so the A rows / B columns they share stay in that XCD's L2.
+template <class E> struct IsEpiBF16 { static constexpr bool value = false; };
+template <class RM, bool D> struct IsEpiBF16<EpiBF16<RM, D>> { static constexpr bool value = true; };
+
+template <int BM, int BN, class LA, class LB, class EPI, int NBUF>
+__global__ void __launch_bounds__(NTHR, 1)
+gemm_persist_kernel(const LA la, const LB lb, EPI epi, int M, int N, int K) {
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int MI = TileCfg<BM, BN>::MI, NI = TileCfg<BM, BN>::NI;
+  constexpr int WN = BN / (32 * NI);
+  constexpr int EPI_BYTES = BM * (BN + 8) * 2;
+  constexpr int NDMA = BM / 32 + BN / 32;
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE + EPI_BYTES];
+  char* const elds = smem + NBUF * STAGE;
+  epi.raw_sync = true;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int nt = (K + BK - 1) / BK;
+  // this XCD's contiguous range of tile ids and this block's stride through it
+  const int G = gridDim.x;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  const int gx = (G >> 3) + (xcd < (G & 7) ? 1 : 0);
+  const int q8 = ntiles >> 3, r8 = ntiles & 7;
+  const int t_begin = xcd * q8 + (xcd < r8 ? xcd : r8);
+  const int t_count = q8 + (xcd < r8 ? 1 : 0);
+  const int mine = loc < t_count ? (t_count - loc + gx - 1) / gx : 0;
+  const int Q = mine * nt;                  // (tile, K-tile) work items of this block
+  auto tile_mn = [&](int j, int& m0, int& n0) {
+    const int id = t_begin + loc + j * gx;
+    constexpr int GM = 8;
+    const int group = id / (GM * tiles_n);
+    const int first_m = group * GM;
+    const int gsize = min(tiles_m - first_m, GM);
+    const int in_g = id % (GM * tiles_n);
+    m0 = (first_m + in_g % gsize) * BM;
+    n0 = (in_g / gsize) * BN;
+  };
+  typename LA::St sa;
+  typename LB::St sb;
+  int issue_tile = -1;
+  auto issue = [&](int q) {
+    const int j = q / nt, t = q - j * nt;
+    if (j != issue_tile) {
+      int m0, n0;
+      tile_mn(j, m0, n0);
+      la.init(sa, m0, tid);
+      lb.init(sb, n0, tid);
+      issue_tile = j;
+    }
+    char* buf = smem + (q % NBUF) * STAGE;
+    la.dma(sa, t, tid, buf);
+    lb.dma(sb, t, tid, buf + A_BYTES);
+  };
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  for (int q = 0; q < NBUF - 1 && q < Q; ++q) issue(q);
+  int cm0 = 0, cn0 = 0;
+  if (Q > 0) tile_mn(0, cm0, cn0);
+  for (int q = 0; q < Q; ++q) {
+    if (q + NBUF - 1 < Q) {
+      issue(q + NBUF - 1);
+      vmwait<(NBUF - 1) * NDMA>();           // this wave's copies of item q landed
+    } else {
+      vmwait<0>();
+    }
+    lds_barrier();                           // every wave's copies of item q landed
+    const char* cur = smem + (q % NBUF) * STAGE;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 a[MI], b[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = read_frag<LA::KC, BM>(cur, wm * 32 * MI + 32 * i, s, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b[j] = read_frag<LB::KC, BN>(cur + A_BYTES, wn * 32 * NI + 32 * j, s, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if ((q + 1) % nt == 0) {                 // the tile's last K-tile: epilogue, next tile
+      epi.template apply<BM, BN, MI, NI>(acc, elds, cm0, cn0, M, N, wm, wn, lane, tid);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      if (q + 1 < Q) tile_mn((q + 1) / nt, cm0, cn0);
+    }
+    lds_barrier();                           // stage q % NBUF is free for item q + NBUF
+  }
+}
+
 // K-tile prefetch depth of the main loop (1 = next tile, 2 = two tiles ahead, used for the
 // 128x128 tile when a split has at least 4 K-tiles); mlc_gemm_config switches it for A/B
 // measurements
@@ -1332,12 +1448,49 @@ static int g_dense_bf16_split_target = 0;
 // A/B knob 8; -1: read MLC_GEMM_DMA on first use (default 1: ResNet-50 +1.2 %, U-Net
 // +3.2 %, BERT +0.8 %, profiles/round2_ab/gemm_dma)
 static int g_gemm_dma = -1;
+// persistent short-K kernel (gemm_persist_kernel): 0 off, 1 for epilogues without global
+// loads (forward convs + BN statistics), 2 also epilogues that load (residual addend, BN
+// backward operands, bias); MLC_GEMM_PERSIST, read on first use.  g_persist_kt: most
+// K-tiles per output tile it takes (MLC_GEMM_PERSIST_KT); g_persist_nbuf: ring depth 2 / 3.
+static int g_persist = -1;
+static int g_persist_kt = 8;
+static int g_persist_nbuf = 3;
+static int g_num_cus = 0;
+
+template <class EPI>
+static bool epi_loads(const EPI& e) {
+  if constexpr (IsEpiBF16<EPI>::value) return e.addend || e.bn.y0 || e.dact || e.bias || e.preact;
+  return true;
+}
 
 template <int BM, int BN, class LA, class LB, class EPI>
 static hipError_t launch(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K,
                          int splits, hipStream_t st) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const int ktiles = (K + BK - 1) / BK;
+  if constexpr (BM == 128 && BN == 128 && HasDma<LA>::value && HasDma<LB>::value && IsEpiBF16<EPI>::value) {
+    if (g_persist < 0) {
+      const char* e = getenv("MLC_GEMM_PERSIST");
+      g_persist = e ? atoi(e) : 0;
+      if (const char* k = getenv("MLC_GEMM_PERSIST_KT")) g_persist_kt = atoi(k);
+      if (const char* b = getenv("MLC_GEMM_PERSIST_NBUF")) g_persist_nbuf = atoi(b);
+      int dev = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (g_num_cus <= 0) g_num_cus = 256;
+    }
+    if (g_persist && splits <= 1 && ktiles >= 1 && ktiles <= g_persist_kt && tiles >= 2 * g_num_cus &&
+        (g_persist >= 2 || !epi_loads(epi))) {
+      const int grid = g_num_cus;            // one block per CU (the LDS ring + staging region)
+      if (g_persist_nbuf == 2)
+        hipLaunchKernelGGL((gemm_persist_kernel<BM, BN, LA, LB, EPI, 2>), dim3(grid), dim3(NTHR), 0, st, la, lb, epi,
+                           M, N, K);
+      else
+        hipLaunchKernelGGL((gemm_persist_kernel<BM, BN, LA, LB, EPI, 3>), dim3(grid), dim3(NTHR), 0, st, la, lb, epi,
+                           M, N, K);
+      return hipGetLastError();
+    }
+  }
   if (splits < 1) splits = 1;
   if (splits > ktiles) splits = ktiles > 0 ? ktiles : 1;
   const int per = ktiles > 0 ? (ktiles + splits - 1) / splits : 0;
@@ -1609,8 +1762,18 @@ MLC_EXPORT int mlc_gemm_get_set(int key, int value) {
           : key == 6 ? &igemm::g_splitk_fused : key == 7 ? &igemm::g_dense_narrow
           : key == 8 ? &igemm::g_gemm_dma : key == 9 ? &igemm::g_split_target_dense
           : key == 10 ? &igemm::g_dense_tile : key == 11 ? &igemm::g_dense_split
-          : key == 12 ? &igemm::g_dense_bf16_split_target : key == 13 ? &igemm::g_single_stage_kt : nullptr;
+          : key == 12 ? &igemm::g_dense_bf16_split_target : key == 13 ? &igemm::g_single_stage_kt
+          : key == 14 ? &igemm::g_persist : key == 15 ? &igemm::g_persist_nbuf : key == 16 ? &igemm::g_persist_kt
+          : nullptr;
   if (!k) return -1;
+  if (key == 14 && igemm::g_persist < 0) {   // resolve the env defaults (CU count) first
+    const char* e = getenv("MLC_GEMM_PERSIST");
+    igemm::g_persist = e ? atoi(e) : 0;
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&igemm::g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (igemm::g_num_cus <= 0) igemm::g_num_cus = 256;
+  }
   if (key == 10 || key == 11) {   // resolve the env defaults before the first override
     int sp = 1;
     (void)igemm::pick_dense_tile(4096, 768, 768, sp);

@@ -45,7 +45,7 @@ import torch.nn.functional as F
 
 from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops.glayers import (AvgPool, BilinearUp, BNAct, BNParams, ChannelGate, Conv3dAs2d, ConvBNAct, ConvParams,
-                                    Frames, GlobalAvgPool, LinearAct, LinearParams, MaxPool, TemporalAs2d, UpCat)
+                                    Frames, GlobalAvgPool, LinearAct, LinearParams, MaxPool, TemporalAs2d, UpCat, VolumePool)
 from mlcomp_amd.ops import gtransformer as GT
 from mlcomp_amd.ops.layers import NativeContext
 from mlcomp_amd.train.native_spec import NativeUnsupported
@@ -483,6 +483,22 @@ class _Lowering:
         new = self._site_node(node, GlobalAvgPool(self.net.ctx), [node.args[0]])
         self._replace([node], new)
 
+    def volume_pool(self, node, m):
+        """AdaptiveAvgPool3d(1) / AdaptiveAvgPool1d(1) -> VolumePool; AdaptiveAvgPool1d(K) of
+        ``x.reshape(N, 1, -1)`` (the ResNeXt3D head) -> VolumePool(flat_bins=K) on x."""
+        out = m.output_size
+        sizes = tuple(out) if isinstance(out, (tuple, list)) else (out,)
+        src = node.args[0]
+        if all(v == 1 for v in sizes):
+            new = self._site_node(node, VolumePool(self.net.ctx), [src])
+            self._replace([node], new)
+            return
+        if (isinstance(m, nn.AdaptiveAvgPool1d) and isinstance(src, fx.Node) and src.op == 'call_method'
+                and src.target in ('reshape', 'view') and len(src.args) == 4 and src.args[2] == 1
+                and src.args[3] == -1 and len(src.users) == 1):
+            new = self._site_node(node, VolumePool(self.net.ctx, flat_bins=int(sizes[0])), [src.args[0]])
+            self._replace([src, node], new)
+
     # ------------------------------------------------------------------ transformer blocks
     @staticmethod
     def _call_args(node, names):
@@ -850,6 +866,8 @@ class _Lowering:
                 elif isinstance(m, nn.AvgPool2d):
                     self.avgpool2d(node, m.kernel_size, m.stride, m.padding, m.ceil_mode, m.count_include_pad,
                                    m.divisor_override)
+                elif isinstance(m, (nn.AdaptiveAvgPool3d, nn.AdaptiveAvgPool1d)):
+                    self.volume_pool(node, m)
                 elif isinstance(m, nn.LayerNorm):
                     self.layernorm(node)
                 elif isinstance(m, nn.MultiheadAttention):

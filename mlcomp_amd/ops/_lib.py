@@ -123,6 +123,8 @@ _SIGS = {
     'mlc_chscale_bwd': [vp] * 7 + [i32] * 3 + [vp],
     'mlc_conv_fwd_ex': [vp] * 4 + [i32] * 13 + [vp],
     'mlc_conv_wgrad_bias': [vp] * 4 + [i32] * 13 + [vp, i64, vp],
+    'mlc_temporal_unfold': [vp, vp] + [i32] * 9 + [vp],
+    'mlc_temporal_fold': [vp, vp] + [i32] * 9 + [vp],
     'mlc_counters_owner': [i32],
     'mlc_counters_release': [i32],
     'mlc_counters_in_use': [],
@@ -172,7 +174,8 @@ def load():
         # A/B knobs of the GEMM engine (tile policy / min blocks for the wide-wave tiles)
         for key, env in ((1, 'MLC_SPLIT_TARGET'), (2, 'MLC_SPLIT_TARGET_MAT'), (3, 'MLC_GEMM_BIG'),
                          (4, 'MLC_GEMM_BIG_MIN'), (5, 'MLC_GEMM_SINGLE_STAGE'), (6, 'MLC_SPLITK_FUSED'),
-                         (9, 'MLC_SPLIT_TARGET_DENSE'), (12, 'MLC_DENSE_SPLIT_TARGET'), (13, 'MLC_SINGLE_STAGE_KT')):
+                         (9, 'MLC_SPLIT_TARGET_DENSE'), (12, 'MLC_DENSE_SPLIT_TARGET'), (13, 'MLC_SINGLE_STAGE_KT'),
+                         (15, 'MLC_GEMM_PERSIST_NBUF'), (16, 'MLC_GEMM_PERSIST_KT')):
             if os.environ.get(env):
                 lib.mlc_gemm_get_set(key, int(os.environ[env]))
         for key, env in ((0, 'MLC_BN_UNROLL'), (1, 'MLC_BN_BLOCKS')):   # BN elementwise passes

@@ -105,7 +105,9 @@ class Conv3dAs2d:
 
     def unfold(self, x: torch.Tensor) -> torch.Tensor:
         """Logical [N, C, T, H, W] (or [N, C, L]) -> the frames [N*To, C*kt, H, W] the 2D
-        conv reads (torch gather / pad ops: autograd folds the gradient back)."""
+        conv reads.  On the GPU (C % 8 == 0, kt <= 8) the native unfold / fold kernels
+        (``csrc/kernels/video.hip``) build it from the channels_last_3d activation and fold
+        the gradient back; elsewhere torch gather / pad ops (autograd folds the gradient)."""
         if x.dim() == 3:
             x = x[:, :, :, None, None]
         N, C, T, H, W = x.shape
@@ -113,6 +115,8 @@ class Conv3dAs2d:
         if kt == 1 and st == 1 and pt == 0:
             return frames_of(x)
         To = (T + 2 * pt - dt * (kt - 1) - 1) // st + 1
+        if x.is_cuda and C % 8 == 0 and kt <= 8:
+            return _TemporalUnfold.apply(x, kt, st, pt, dt, To)
         if pt:
             x = torch.nn.functional.pad(x, (0, 0, 0, 0, pt, pt))
         idx = (torch.arange(To, device=x.device)[:, None] * st + torch.arange(kt, device=x.device)[None] * dt)
@@ -127,6 +131,46 @@ class Conv3dAs2d:
     def frames_like_out(self, r: torch.Tensor) -> torch.Tensor:
         """A tensor of the conv's output shape (a residual) as output frames."""
         return frames_of(r[:, :, :, None, None] if r.dim() == 3 else r)
+
+
+def temporal_unfold(x5: torch.Tensor, kt: int, st: int, pt: int, dt: int, To: int) -> torch.Tensor:
+    """[N, C, T, H, W] (any layout; channels_last_3d is free) -> frames [N*To, C*kt, H, W]
+    (channels_last) on the native unfold kernel."""
+    from . import _lib
+    N, C, T, H, W = x5.shape
+    xm = x5.permute(0, 2, 3, 4, 1)
+    if xm.dtype != torch.bfloat16:
+        xm = xm.to(torch.bfloat16)
+    xm = xm.contiguous()
+    out = torch.empty(N * To, H, W, C * kt, device=x5.device, dtype=torch.bfloat16)
+    _lib.call('mlc_temporal_unfold', _lib.ptr(xm), _lib.ptr(out), N, T, H * W, C, kt, st, pt, dt, To, _lib.stream())
+    return out.permute(0, 3, 1, 2)
+
+
+def temporal_fold(dcol: torch.Tensor, N: int, C: int, T: int, H: int, W: int, kt: int, st: int, pt: int, dt: int,
+                  To: int) -> torch.Tensor:
+    """Gradient of :func:`temporal_unfold`: frames-gradient [N*To, C*kt, H, W] -> [N, C, T, H, W]
+    (channels_last_3d), a gather over the taps (no atomics)."""
+    from . import _lib
+    dm = dcol.permute(0, 2, 3, 1)
+    if dm.dtype != torch.bfloat16:
+        dm = dm.to(torch.bfloat16)
+    dm = dm.contiguous()
+    dx = torch.empty(N, T, H, W, C, device=dcol.device, dtype=torch.bfloat16)
+    _lib.call('mlc_temporal_fold', _lib.ptr(dm), _lib.ptr(dx), N, T, H * W, C, kt, st, pt, dt, To, _lib.stream())
+    return dx.permute(0, 4, 1, 2, 3)
+
+
+class _TemporalUnfold(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kt, st, pt, dt, To):
+        ctx.geom = (tuple(x.shape), kt, st, pt, dt, To, x.dtype)
+        return temporal_unfold(x, kt, st, pt, dt, To)
+
+    @staticmethod
+    def backward(ctx, g):
+        (N, C, T, H, W), kt, st, pt, dt, To, dtype = ctx.geom
+        return temporal_fold(g, N, C, T, H, W, kt, st, pt, dt, To).to(dtype), None, None, None, None, None
 
 
 class TemporalAs2d:
@@ -1136,5 +1180,32 @@ class GlobalAvgPool(Site):
         return [from_nhwc(dx, C)]
 
 
+class VolumePool(nn.Module):
+    """Global average pooling of a [N, C, *spatial] tensor (video / 1-D) on the native pooling
+    kernel: the channels_last(_3d) activation viewed as the image [N, C, prod(spatial), 1]
+    (a view, no copy).
+
+    * ``flat_bins=None``: ``AdaptiveAvgPool3d(1)`` / ``AdaptiveAvgPool1d(1)`` ->
+      [N, C, 1, ...];
+    * ``flat_bins=K``: the ResNeXt3D head's ``AdaptiveAvgPool1d(K)`` over ``x.reshape(N, 1,
+      -1)`` (`mlcomp/contrib/model/video/resnext3d/resnext3d.py`): with C == K every bin is
+      exactly one channel's T*H*W values, i.e. a global average pool -> [N, 1, K]; other
+      sizes run the torch ops."""
+
+    def __init__(self, ctx, flat_bins=None):
+        super().__init__()
+        self.gap = GlobalAvgPool(ctx)
+        self.flat_bins = flat_bins
+
+    def forward(self, x):
+        N, C = x.shape[:2]
+        if self.flat_bins is not None and C != self.flat_bins:
+            return torch.nn.functional.adaptive_avg_pool1d(x.reshape(N, 1, -1), self.flat_bins)
+        y = self.gap(x.flatten(2).unsqueeze(-1))            # [N, C, 1, 1]
+        if self.flat_bins is not None:
+            return y.reshape(N, 1, C)
+        return y.reshape(N, C, *([1] * (x.dim() - 2)))
+
+
 __all__ = ['ConvParams', 'BNParams', 'LinearParams', 'ConvBNAct', 'BNAct', 'LinearAct', 'MaxPool',
-           'GlobalAvgPool', 'to_nhwc', 'from_nhwc', 'ceil8']
+           'GlobalAvgPool', 'VolumePool', 'to_nhwc', 'from_nhwc', 'ceil8']

@@ -631,8 +631,10 @@ def test_video_resnext3d_lowers_and_matches_fp32_autograd(kw):
     assert lower_or_none(m) is None
     net = GenericNet(m, 'cpu')
     left = [type(mod).__name__ for mod in net.train_gm.modules()
-            if isinstance(mod, (nn.Conv3d, nn.BatchNorm3d, nn.MaxPool3d, nn.Linear))]
+            if isinstance(mod, (nn.Conv3d, nn.BatchNorm3d, nn.MaxPool3d, nn.Linear, nn.AdaptiveAvgPool1d))]
     assert not left, left
+    # the head's AdaptiveAvgPool1d over the flattened [N, 1, C*T*H*W] is a global pool per channel
+    assert any(type(mod).__name__ == 'VolumePool' for mod in net.train_gm.modules())
     x = torch.randn(4, 3, 4, 16, 16)
     y = torch.randint(0, 5, (4,))
     out = net(x)

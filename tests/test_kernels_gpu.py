@@ -628,3 +628,56 @@ def test_linear_lds_dma(B, I, O, gemm_dma):
     torch.cuda.synchronize()
     assert rel_err(dg, dr) < 1e-2
 
+
+
+@pytest.mark.parametrize('kt,st,pt,dt', [(3, 1, 1, 1), (3, 2, 1, 1), (5, 1, 2, 1), (3, 1, 2, 2), (2, 2, 0, 1)])
+def test_temporal_unfold_fold_match_torch(kt, st, pt, dt):
+    """Native temporal unfold (Conv3d taps -> channels of the frame tensor) and its gradient
+    fold (a gather over taps, csrc/kernels/video.hip) against the torch pad / index_select
+    reference and its autograd gradient (fp32)."""
+    from mlcomp_amd.ops.glayers import Conv3dAs2d
+    conv = torch.nn.Conv3d(16, 8, (kt, 3, 3), (st, 1, 1), (pt, 1, 1), (dt, 1, 1))
+    c = Conv3dAs2d(conv)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 16, 7, 5, 6, generator=g).to(torch.bfloat16)
+    xg = x.cuda().contiguous(memory_format=torch.channels_last_3d).requires_grad_()
+    got = c.unfold(xg)
+    xr = x.float().requires_grad_()
+    want = c.unfold(xr)                             # CPU: the torch gather path
+    assert got.shape == want.shape
+    assert torch.equal(got.float().cpu(), want.to(torch.bfloat16).float())
+    dg = torch.randn(want.shape, generator=g).to(torch.bfloat16)
+    got.backward(dg.cuda())
+    want.backward(dg.float())
+    err = (xg.grad.float().cpu() - xr.grad).abs().max() / xr.grad.abs().max()
+    assert err < 1e-2, err
+
+
+@pytest.mark.parametrize('M,C,Co,S', [(8 * 28 * 28, 128, 512, 1), (3 * 56 * 56 + 5, 64, 256, 1), (4 * 14 * 14, 256, 1024, 2)])
+def test_persistent_short_k_gemm_matches_tile_kernel(M, C, Co, S):
+    """The persistent short-K GEMM (knob 14, igemm.hip gemm_persist_kernel: a DMA ring across
+    output tiles, raw-barrier epilogue) gives the per-tile kernel's output and BN statistics
+    on 1x1 convs (partial last tile, stride 2), and both match the fp32 reference."""
+    from mlcomp_amd.ops import _lib
+    lib = _lib.load()
+    H = 28 if S == 1 else 28
+    N = max(1, M // (H * H))
+    g = torch.Generator(device='cuda').manual_seed(0)
+    x = torch.randn(N, H, H, C, device='cuda', generator=g).to(torch.bfloat16)
+    w = (torch.randn(Co, 1, 1, C, device='cuda', generator=g) * C ** -0.5).to(torch.bfloat16)
+    outs = []
+    old = lib.mlc_gemm_get_set(14, -1)
+    try:
+        for p in (0, 1):
+            lib.mlc_gemm_get_set(14, p)
+            st = torch.zeros(2, Fn.NSTAT * Co, device='cuda')
+            y = Fn.conv2d_fwd(x, w, S, 0, 1, stats=(st[0], st[1]))
+            torch.cuda.synchronize()
+            outs.append((y.float(), st.view(2, Fn.NSTAT, Co).sum(1)))
+    finally:
+        lib.mlc_gemm_get_set(14, max(old, 0))
+    want = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=S)
+    want = want.permute(0, 2, 3, 1)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert (outs[1][0] - want).abs().max() <= 2e-2 * want.abs().max()
+    assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-2)
