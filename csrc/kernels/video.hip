@@ -12,7 +12,8 @@
 //           kt 16-byte stores of the contiguous 8*kt-element output chunk;
 //   fold:   one thread per (input row, 8-channel group), a GATHER over the kt taps that read
 //           it (no atomics, deterministic): for each tap j with (ti + pad - j*dil) a multiple
-//           of st inside [0, To*st), the tap's chunk is loaded and its 8 values summed in fp32.
+//           of st inside [0, To*st), the tap's chunk (kt 16-byte loads, shared through L2 with
+//           the neighbouring frames' threads) is loaded and its 8 values summed in fp32.
 //
 // Both are streaming passes (bandwidth bound); C % 8 == 0, kt <= 8.
 #include "common.h"
@@ -57,9 +58,10 @@ temporal_unfold_kernel(const bf16* __restrict__ x, bf16* __restrict__ out, int N
   }
 }
 
+template <int KT>
 __global__ void __launch_bounds__(NT)
-temporal_fold_kernel(const bf16* __restrict__ dcol, bf16* __restrict__ dx, int N, int T, int HW, int C, int kt,
-                     int st, int pad, int dil, int To) {
+temporal_fold_kernel(const bf16* __restrict__ dcol, bf16* __restrict__ dx, int N, int T, int HW, int C, int st,
+                     int pad, int dil, int To) {
   const int G = C >> 3;
   const long total = (long)N * T * HW * G;
   for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
@@ -71,15 +73,20 @@ temporal_fold_kernel(const bf16* __restrict__ dcol, bf16* __restrict__ dx, int N
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-    for (int j = 0; j < kt; ++j) {
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
       const int num = ti + pad - j * dil;
       if (num < 0 || num % st) continue;
       const int to = num / st;
       if (to >= To) continue;
-      const bf16* src = dcol + ((((long)n * To + to) * HW + p) * C + (long)g * 8) * kt;
-      // element c*kt + j of the chunk for the 8 channels (stride kt)
+      // the tap's 8*KT-element chunk (KT 16-byte loads), element c*KT + j for the 8 channels
+      const uint4* src = reinterpret_cast<const uint4*>(dcol + ((((long)n * To + to) * HW + p) * C + (long)g * 8) * KT);
+      uint4 u[KT];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += (float)src[e * kt + j];
+      for (int q = 0; q < KT; ++q) u[q] = src[q];
+      const bf16* b = reinterpret_cast<const bf16*>(u);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += (float)b[e * KT + j];
     }
     bf16 o[8];
 #pragma unroll
@@ -121,7 +128,19 @@ MLC_EXPORT int mlc_temporal_unfold(const bf16* x, bf16* out, int N, int T, int H
 MLC_EXPORT int mlc_temporal_fold(const bf16* dcol, bf16* dx, int N, int T, int HW, int C, int kt, int st, int pad,
                                  int dil, int To, hipStream_t stream) {
   if (C % 8 || kt < 1 || kt > KTMAX || st < 1 || dil < 1 || To < 1) return -1;
-  hipLaunchKernelGGL(temporal_fold_kernel, dim3(grid_of((long)N * T * HW * (C / 8))), dim3(NT), 0, stream, dcol, dx,
-                     N, T, HW, C, kt, st, pad, dil, To);
+  const dim3 grid(grid_of((long)N * T * HW * (C / 8)));
+#define MLC_FOLD(K) hipLaunchKernelGGL(temporal_fold_kernel<K>, grid, dim3(NT), 0, stream, dcol, dx, N, T, HW, C, st, \
+                                       pad, dil, To)
+  switch (kt) {
+    case 1: MLC_FOLD(1); break;
+    case 2: MLC_FOLD(2); break;
+    case 3: MLC_FOLD(3); break;
+    case 4: MLC_FOLD(4); break;
+    case 5: MLC_FOLD(5); break;
+    case 6: MLC_FOLD(6); break;
+    case 7: MLC_FOLD(7); break;
+    default: MLC_FOLD(8); break;
+  }
+#undef MLC_FOLD
   return hipGetLastError();
 }

@@ -815,10 +815,12 @@ def linear_wgrad(dout, x, out=None, accumulate=False):
     return g
 
 
-# Dense weight + bias gradients: split-K tiles added into dW with fp32 atomics
-# (MLC_DENSE_WGRAD=atomic) or written to fp32 slabs that a reduction pass sums (=slab, the
-# round-5 default); the conv weight gradients' MLC_WGRAD_SLAB counterpart for dense layers.
-DENSE_WGRAD_ATOMIC = os.environ.get('MLC_DENSE_WGRAD', 'atomic') == 'atomic'
+# Dense weight + bias gradients: split-K tiles written to fp32 slabs that a reduction pass
+# sums (MLC_DENSE_WGRAD=slab, default) or added into dW with fp32 atomics (=atomic); the conv
+# weight gradients' MLC_WGRAD_SLAB counterpart for dense layers.  Interleaved A/B on one
+# MI355X (profiles/round6/dense_wgrad_ab.jsonl): BERT-base slab 5,711 / 5,708 seq/s vs atomic
+# 5,568 / 5,563; ViT-B/16 5,136 / 5,151 vs 5,166 / 5,165 img/s.
+DENSE_WGRAD_ATOMIC = os.environ.get('MLC_DENSE_WGRAD', 'slab') == 'atomic'
 
 
 def linear_wgrad_bias(dout, x, dw, db):

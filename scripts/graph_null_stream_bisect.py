@@ -9,12 +9,14 @@ corruption that stays finite shows up there).
     python scripts/graph_null_stream_bisect.py MODEL MODE
 
 MODEL: mlp (Linear+ReLU: hipBLASLt GEMMs + elementwise), conv (Conv2d+ReLU, no BN: MIOpen
-convolutions), bn (Conv2d+BatchNorm2d+ReLU: MIOpen BN), effnet (EfficientNet-b0 from the
+convolutions), bn (Conv2d+BatchNorm2d+ReLU: MIOpen BN), dw (a depthwise conv between BNs),
+silu (conv+BN+SiLU), se (a squeeze-excitation gate), effnet (EfficientNet-b0 from the
 generic-engine test models).
 MODE: null (baseline), estream (eager twin on a created stream), sharedpool (the capture
 shares a pool handle made up front), nocache (run under PYTORCH_NO_HIP_MEMORY_CACHING=1, set
 by the caller), noeager (no eager twin at all: the graph alone), evalnull (the eager twin
-runs forward only, no_grad, on the NULL stream)."""
+runs forward only, no_grad, on the NULL stream), nomiopen / nomiopen_eval (null / evalnull
+with MIOpen disabled: torch.backends.cudnn.enabled = False, PyTorch's own conv kernels)."""
 import json
 import math
 import os
@@ -29,6 +31,12 @@ sys.path[:0] = [root, os.path.join(root, 'tests')]
 
 name = sys.argv[1] if len(sys.argv) > 1 else 'mlp'
 mode = sys.argv[2] if len(sys.argv) > 2 else 'null'
+if mode.startswith('nomiopen'):
+    torch.backends.cudnn.enabled = False
+    mode = 'null' if mode == 'nomiopen' else 'evalnull'
+    tag = 'nomiopen'
+else:
+    tag = ''
 STEPS = 20
 
 
@@ -42,6 +50,26 @@ def make():
     if name == 'bn':
         return nn.Sequential(nn.Conv2d(3, 64, 3, 1, 1), nn.BatchNorm2d(64), nn.ReLU(), nn.Conv2d(64, 64, 3, 2, 1),
                              nn.BatchNorm2d(64), nn.ReLU(), nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(64, 10))
+    if name == 'dw':        # depthwise conv + BN + ReLU (EfficientNet's MBConv core, MIOpen grouped conv)
+        return nn.Sequential(nn.Conv2d(3, 64, 3, 1, 1), nn.BatchNorm2d(64), nn.ReLU(),
+                             nn.Conv2d(64, 64, 3, 1, 1, groups=64), nn.BatchNorm2d(64), nn.ReLU(),
+                             nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(64, 10))
+    if name == 'silu':      # the same without the depthwise conv, SiLU activations
+        return nn.Sequential(nn.Conv2d(3, 64, 3, 1, 1), nn.BatchNorm2d(64), nn.SiLU(), nn.Conv2d(64, 64, 3, 1, 1),
+                             nn.BatchNorm2d(64), nn.SiLU(), nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(64, 10))
+    if name == 'se':        # a squeeze-excitation gate (global pool, 1x1 convs, sigmoid, multiply)
+        class SE(nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.c = nn.Sequential(nn.Conv2d(3, 64, 3, 1, 1), nn.BatchNorm2d(64), nn.ReLU())
+                self.g = nn.Sequential(nn.AdaptiveAvgPool2d(1), nn.Conv2d(64, 16, 1), nn.ReLU(), nn.Conv2d(16, 64, 1),
+                                       nn.Sigmoid())
+                self.h = nn.Sequential(nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(64, 10))
+
+            def forward(self, x):
+                y = self.c(x)
+                return self.h(y * self.g(y))
+        return SE()
     from test_generic_gpu import _models, _no_stochastic
     mk, _, _ = _models()['efficientnet-b0']
     return _no_stochastic(mk())
@@ -95,7 +123,7 @@ try:
         body(1)
     torch.cuda.synchronize()
 except Exception as e:        # e.g. PYTORCH_NO_HIP_MEMORY_CACHING=1: hipMalloc inside the capture
-    print(json.dumps({'model': name, 'mode': mode, 'nocache_env': os.environ.get('PYTORCH_NO_HIP_MEMORY_CACHING'),
+    print(json.dumps({'model': name, 'mode': mode + (f'+{tag}' if tag else ''), 'nocache_env': os.environ.get('PYTORCH_NO_HIP_MEMORY_CACHING'),
                       'capture_error': str(e).splitlines()[0][:160]}), flush=True)
     sys.exit(0)
 es = torch.cuda.Stream() if mode == 'estream' else None
@@ -118,7 +146,7 @@ for i in range(STEPS):
         if bad[k] is None and losses[k] and not math.isfinite(losses[k][-1]):
             bad[k] = i
 dev = max(abs(a - b) / max(abs(b), 1e-6) for a, b in zip(losses[1], ref))
-print(json.dumps({'model': name, 'mode': mode, 'nocache_env': os.environ.get('PYTORCH_NO_HIP_MEMORY_CACHING'),
+print(json.dumps({'model': name, 'mode': mode + (f'+{tag}' if tag else ''), 'nocache_env': os.environ.get('PYTORCH_NO_HIP_MEMORY_CACHING'),
                   'first_nonfinite_eager': bad[0], 'first_nonfinite_graph': bad[1],
                   'graph_vs_eager_ref_max_rel': round(dev, 5),
                   'graph_losses': [round(v, 4) for v in losses[1][:8]], 'ref_losses': [round(v, 4) for v in ref[:8]]}),
