@@ -254,6 +254,10 @@ class RcclComm(Watched):
         self.device = torch.device(device)
         self.timeout = COMM_TIMEOUT if timeout is None else float(timeout)
         self._h = None
+        # the handle is read by the watchdog thread (async-error polls) and torn down by
+        # abort / close: every RCCL call that takes it runs under this lock, so no call ever
+        # sees a communicator that another thread has already freed
+        self._hlock = threading.RLock()
         lib = _lib.load()
         lib.mlc_comm_set_timeout(int(self.timeout * 1000))
         nbytes = lib.mlc_comm_unique_id_bytes()
@@ -301,29 +305,35 @@ class RcclComm(Watched):
 
     # ---- Watched
     def _async_error(self) -> int:
-        if self._h is None:
-            return 0
-        return int(_lib.load().mlc_comm_async_error(C.c_void_p(self._h)))
+        with self._hlock:
+            if self._h is None:
+                return 0
+            return int(_lib.load().mlc_comm_async_error(C.c_void_p(self._h)))
 
     def _abort(self):
-        if self._h is not None:
-            _lib.load().mlc_comm_abort(C.c_void_p(self._h))
-            self._h = None
+        with self._hlock:
+            h, self._h = self._h, None
+            if h is not None:
+                _lib.load().mlc_comm_abort(C.c_void_p(h))
+        if h is not None:
             WATCHDOG.unregister(self)
 
     def _error_name(self, code: int) -> str:
         lib = _lib.load()
         s = (lib.mlc_comm_error_string(int(code)) or b'').decode(errors='replace')
         last = ''
-        if self._h is not None and code not in (0, _TIMED_OUT):
-            last = (lib.mlc_comm_last_error(C.c_void_p(self._h)) or b'').decode(errors='replace')
+        with self._hlock:
+            if self._h is not None and code not in (0, _TIMED_OUT):
+                last = (lib.mlc_comm_last_error(C.c_void_p(self._h)) or b'').decode(errors='replace')
         return f'{s} ({code})' + (f': {last}' if last else '')
 
     def _call(self, name, *args):
         self.check()
-        if self._h is None:
-            raise CommError(f'{WATCHDOG_MESSAGE} {name} on a closed communicator (rank {self.rank} of {self.world})')
-        rc = int(getattr(_lib.load(), name)(C.c_void_p(self._h), *args))
+        with self._hlock:
+            if self._h is None:
+                raise CommError(f'{WATCHDOG_MESSAGE} {name} on a closed communicator (rank {self.rank} of '
+                                f'{self.world})')
+            rc = int(getattr(_lib.load(), name)(C.c_void_p(self._h), *args))
         if rc == 0:
             return
         if rc == _TIMED_OUT:
@@ -373,10 +383,13 @@ class RcclComm(Watched):
         self.watch(ev.query, what)
 
     def close(self):
-        if getattr(self, '_h', None):
-            WATCHDOG.unregister(self)
-            _lib.load().mlc_comm_destroy(C.c_void_p(self._h))
-            self._h = None
+        if getattr(self, '_h', None) is None or not hasattr(self, '_hlock'):
+            return
+        WATCHDOG.unregister(self)
+        with self._hlock:
+            h, self._h = self._h, None
+            if h is not None:
+                _lib.load().mlc_comm_destroy(C.c_void_p(h))
 
     def __del__(self):
         try:

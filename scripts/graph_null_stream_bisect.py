@@ -104,9 +104,10 @@ def body(k, train=True):
 ref = []
 s0 = torch.cuda.Stream()
 with torch.cuda.stream(s0):
-    for _ in range(3 + STEPS):
+    for i in range(3 + STEPS):
         body(2)
         ref.append(loss_buf[2])
+        print(f'reference step {i}', file=sys.stderr, flush=True)   # progress (slow without MIOpen)
 torch.cuda.synchronize()
 ref = [float(v.item()) for v in ref][3:]
 
@@ -142,6 +143,7 @@ for i in range(STEPS):
             losses[0].append(float(loss_buf[0].item()))
     g.replay()
     losses[1].append(float(loss_buf[1].item()))
+    print(f'step {i}: graph loss {losses[1][-1]:.4f}', file=sys.stderr, flush=True)   # progress
     for k in range(2):
         if bad[k] is None and losses[k] and not math.isfinite(losses[k][-1]):
             bad[k] = i
