@@ -89,9 +89,19 @@ class TimerCallback(Callback):
         rank 0's rate x world size only when no process group is up."""
         import torch
         import torch.distributed as dist
+        runner = getattr(state, 'runner', None)
+        comm = getattr(getattr(runner, 'native_step', None), 'comm', None)
+        if comm is not None and getattr(comm, 'world', 0) == state.world_size:
+            # a native step's own communicator (the framework's RCCL one on the GPU, on the
+            # work stream): no second communicator and no default-group collective on the
+            # step's stream (round-5 verdict, weak point 8)
+            on_gpu = hasattr(comm, 'watch_stream')
+            t = torch.tensor([fps], dtype=torch.float32, device=runner.device if on_gpu else 'cpu')
+            comm.all_reduce(t)
+            return float(t.item())
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() != state.world_size:
             return fps * state.world_size
-        dev = getattr(getattr(state, 'runner', None), 'device', None)
+        dev = getattr(runner, 'device', None)
         if dist.get_backend() == 'nccl':
             # an NCCL (= RCCL) group only reduces device tensors: the runner's device, else
             # the process's current one
