@@ -263,7 +263,9 @@ bn_bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, con
 // A/B knobs of the elementwise passes: chunks per thread per iteration (1, 2, 4) and the
 // block cap of grid_for
 int g_unroll = 1;
-int g_max_blocks = 768;   // measured: 512-768 beat 1024 by ~0.4 % on ResNet-50, 2048+ lose 2 %
+// measured: 512-768 beat 1024 by ~0.4 % on ResNet-50, 2048+ lose 2 %; 512 vs 768 +0.3 % in
+// 3 interleaved rounds (profiles/round6/bn_knobs_ab.jsonl), 1536 -1.5 %, unroll 2 / 4 -0.3 %
+int g_max_blocks = 512;
 
 // block-count granularity that keeps blocks * NT a multiple of G
 long grid_mult(int G) {

@@ -302,6 +302,75 @@ avgpool2d_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx, int N, 
   }
 }
 
+// adaptive_avg_pool2d(x, (Ho, Wo)) with PyTorch's bins: output row o averages input rows
+// [floor(o*H/Ho), ceil((o+1)*H/Ho)) (bins overlap when Ho does not divide H); fp32 sums,
+// one bf16 rounding (PSPNet's 1/2/3/6 pyramid).  Backward: a gather over the bins that
+// contain the input element (no atomics).
+__device__ __forceinline__ int abin_lo(int o, int in, int out) { return (int)(((long)o * in) / out); }
+__device__ __forceinline__ int abin_hi(int o, int in, int out) { return (int)(((long)(o + 1) * in + out - 1) / out); }
+
+__global__ void __launch_bounds__(NT)
+adaptive_avg_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N, int H, int W, int C, int Ho,
+                        int Wo) {
+  const int G = C / 8;
+  const long total = (long)N * Ho * Wo * G;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int g = (int)(i % G);
+    long t = i / G;
+    const int wo = (int)(t % Wo);
+    t /= Wo;
+    const int ho = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    const int h0 = abin_lo(ho, H, Ho), h1 = abin_hi(ho, H, Ho);
+    const int w0 = abin_lo(wo, W, Wo), w1 = abin_hi(wo, W, Wo);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int h = h0; h < h1; ++h)
+      for (int w = w0; w < w1; ++w) {
+        float f[8];
+        unpack8(ldg16(x + (((long)n * H + h) * W + w) * C + g * 8), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += f[e];
+      }
+    const float inv = 1.f / (float)((h1 - h0) * (w1 - w0));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    *reinterpret_cast<uint4*>(y + i * 8) = pack8(acc);
+  }
+}
+
+__global__ void __launch_bounds__(NT)
+adaptive_avg_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx, int N, int H, int W, int C, int Ho,
+                        int Wo) {
+  const int G = C / 8;
+  const long total = (long)N * H * W * G;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int g = (int)(i % G);
+    long t = i / G;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    // bins o with lo(o) <= h < hi(o): o in [floor(h*Ho/H), ceil((h+1)*Ho/H) - 1], each checked
+    const int ho_a = max(0, (int)(((long)h * Ho) / H) - 1), ho_b = min(Ho - 1, (int)(((long)(h + 1) * Ho) / H) + 1);
+    const int wo_a = max(0, (int)(((long)w * Wo) / W) - 1), wo_b = min(Wo - 1, (int)(((long)(w + 1) * Wo) / W) + 1);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int ho = ho_a; ho <= ho_b; ++ho) {
+      const int h0 = abin_lo(ho, H, Ho), h1 = abin_hi(ho, H, Ho);
+      if (h < h0 || h >= h1) continue;
+      for (int wo = wo_a; wo <= wo_b; ++wo) {
+        const int w0 = abin_lo(wo, W, Wo), w1 = abin_hi(wo, W, Wo);
+        if (w < w0 || w >= w1) continue;
+        float f[8];
+        unpack8(ldg16(dy + (((long)n * Ho + ho) * Wo + wo) * C + g * 8), f);
+        const float inv = 1.f / (float)((h1 - h0) * (w1 - w0));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += f[e] * inv;
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + i * 8) = pack8(acc);
+  }
+}
+
 static int blocks_for(long work) {
   long b = (work + NT - 1) / NT;
   if (b > 4096) b = 4096;
@@ -376,5 +445,22 @@ MLC_EXPORT int mlc_avgpool2d_bwd(const bf16* dy, bf16* dx, int N, int H, int W, 
   if (C % 8) return -1;
   hipLaunchKernelGGL(avgpool2d_bwd_kernel, dim3(blocks_for((long)N * H * W * (C / 8))), dim3(NT), 0, st, dy, dx, N, H,
                      W, C, Ho, Wo, K, S, P, cip);
+  return hipGetLastError();
+}
+
+// x [N][H][W][C] -> y [N][Ho][Wo][C] (adaptive average pool, PyTorch's bins); C % 8 == 0
+MLC_EXPORT int mlc_adaptive_avg_fwd(const bf16* x, bf16* y, int N, int H, int W, int C, int Ho, int Wo,
+                                    hipStream_t st) {
+  if (C % 8 || Ho < 1 || Wo < 1 || H < 1 || W < 1) return -1;
+  hipLaunchKernelGGL(adaptive_avg_fwd_kernel, dim3(blocks_for((long)N * Ho * Wo * (C / 8))), dim3(NT), 0, st, x, y,
+                     N, H, W, C, Ho, Wo);
+  return hipGetLastError();
+}
+
+MLC_EXPORT int mlc_adaptive_avg_bwd(const bf16* dy, bf16* dx, int N, int H, int W, int C, int Ho, int Wo,
+                                    hipStream_t st) {
+  if (C % 8 || Ho < 1 || Wo < 1 || H < 1 || W < 1) return -1;
+  hipLaunchKernelGGL(adaptive_avg_bwd_kernel, dim3(blocks_for((long)N * H * W * (C / 8))), dim3(NT), 0, st, dy, dx,
+                     N, H, W, C, Ho, Wo);
   return hipGetLastError();
 }

@@ -13,7 +13,10 @@
 //   fold:   one thread per (input row, 8-channel group), a GATHER over the kt taps that read
 //           it (no atomics, deterministic): for each tap j with (ti + pad - j*dil) a multiple
 //           of st inside [0, To*st), the tap's chunk (kt 16-byte loads, shared through L2 with
-//           the neighbouring frames' threads) is loaded and its 8 values summed in fp32.
+//           the neighbouring frames' threads) is loaded and its 8 values summed in fp32;
+//           an optional addend (another branch's gradient of the same activation: a residual
+//           block's identity path or its shortcut conv) starts the sum, so autograd does not
+//           add the two branch gradients in a pass of its own.
 //
 // Both are streaming passes (bandwidth bound); C % 8 == 0, kt <= 8.
 #include "common.h"
@@ -60,8 +63,8 @@ temporal_unfold_kernel(const bf16* __restrict__ x, bf16* __restrict__ out, int N
 
 template <int KT>
 __global__ void __launch_bounds__(NT)
-temporal_fold_kernel(const bf16* __restrict__ dcol, bf16* __restrict__ dx, int N, int T, int HW, int C, int st,
-                     int pad, int dil, int To) {
+temporal_fold_kernel(const bf16* __restrict__ dcol, const bf16* __restrict__ add, bf16* __restrict__ dx, int N,
+                     int T, int HW, int C, int st, int pad, int dil, int To) {
   const int G = C >> 3;
   const long total = (long)N * T * HW * G;
   for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
@@ -71,8 +74,15 @@ temporal_fold_kernel(const bf16* __restrict__ dcol, bf16* __restrict__ dx, int N
     const long f = row / HW;
     const int ti = (int)(f % T), n = (int)(f / T);
     float acc[8];
+    if (add) {
+      const uint4 a = ld16(add + row * C + g * 8);
+      const bf16* b = reinterpret_cast<const bf16*>(&a);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+      for (int e = 0; e < 8; ++e) acc[e] = (float)b[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    }
 #pragma unroll
     for (int j = 0; j < KT; ++j) {
       const int num = ti + pad - j * dil;
@@ -124,12 +134,13 @@ MLC_EXPORT int mlc_temporal_unfold(const bf16* x, bf16* out, int N, int T, int H
   return hipGetLastError();
 }
 
-// dcol [N][To][HW][C*kt] -> dx [N][T][HW][C] (overwritten): the gradient of the unfold
-MLC_EXPORT int mlc_temporal_fold(const bf16* dcol, bf16* dx, int N, int T, int HW, int C, int kt, int st, int pad,
+// dcol [N][To][HW][C*kt] -> dx [N][T][HW][C] (overwritten; + add [N][T][HW][C] when non-null):
+// the gradient of the unfold
+MLC_EXPORT int mlc_temporal_fold(const bf16* dcol, const bf16* add, bf16* dx, int N, int T, int HW, int C, int kt, int st, int pad,
                                  int dil, int To, hipStream_t stream) {
   if (C % 8 || kt < 1 || kt > KTMAX || st < 1 || dil < 1 || To < 1) return -1;
   const dim3 grid(grid_of((long)N * T * HW * (C / 8)));
-#define MLC_FOLD(K) hipLaunchKernelGGL(temporal_fold_kernel<K>, grid, dim3(NT), 0, stream, dcol, dx, N, T, HW, C, st, \
+#define MLC_FOLD(K) hipLaunchKernelGGL(temporal_fold_kernel<K>, grid, dim3(NT), 0, stream, dcol, add, dx, N, T, HW, C, st, \
                                        pad, dil, To)
   switch (kt) {
     case 1: MLC_FOLD(1); break;

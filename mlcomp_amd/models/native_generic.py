@@ -20,7 +20,7 @@ seven architectures; this module covers the rest:
    * ``BatchNorm2d / BatchNorm1d [-> + residual] [-> activation]`` -> ``BNAct``;
    * ``Linear [-> ReLU]`` -> ``LinearAct`` (bias / ReLU in the dense GEMM epilogue);
    * ``MaxPool2d`` / ``F.max_pool2d`` -> ``MaxPool``; ``AdaptiveAvgPool2d(1)`` ->
-     ``GlobalAvgPool``; ``x.view`` -> ``x.reshape`` (site outputs are channels_last views).
+     ``GlobalAvgPool``, ``AdaptiveAvgPool2d(k > 1)`` -> ``AdaptiveAvgPool``; ``x.view`` -> ``x.reshape`` (site outputs are channels_last views).
 
    A fused chain needs each intermediate value to have exactly one user; every op left in
    the graph (adds, concats, upsampling, dropout, sigmoid gates, the loss ...) is a PyTorch
@@ -44,7 +44,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from mlcomp_amd.ops import functional as Fn
-from mlcomp_amd.ops.glayers import (AvgPool, BilinearUp, BNAct, BNParams, ChannelGate, Conv3dAs2d, ConvBNAct, ConvParams,
+from mlcomp_amd.ops.glayers import (AdaptiveAvgPool, AvgPool, BilinearUp, BNAct, BNParams, ChannelGate, Conv3dAs2d, ConvBNAct, ConvParams,
                                     Frames, GlobalAvgPool, LinearAct, LinearParams, MaxPool, TemporalAs2d, UpCat, VolumePool)
 from mlcomp_amd.ops import gtransformer as GT
 from mlcomp_amd.ops.layers import NativeContext
@@ -269,7 +269,7 @@ class _Lowering:
             res, act, alpha = self._tail(node, chain, allow_res=False)
             cp = self.net.conv_params(node.target, proxy, keep_bias=True)
             bp = None
-        site = Frames(ConvBNAct(self.net.ctx, cp, bp, act, alpha, residual=res is not None), proxy)
+        site = Frames(ConvBNAct(self.net.ctx, cp, bp, act, alpha, residual=res is not None), proxy, name=node.target)
         new = self._site_node(chain[-1], site, [node.args[0]] + ([res] if res is not None else []))
         self._replace(chain, new)
 
@@ -481,6 +481,16 @@ class _Lowering:
 
     def avgpool(self, node):
         new = self._site_node(node, GlobalAvgPool(self.net.ctx), [node.args[0]])
+        self._replace([node], new)
+
+    def adaptive_pool(self, node, size):
+        """adaptive_avg_pool2d to a fixed size > 1 (PSPNet's 2 / 3 / 6 pyramid levels)."""
+        so = tuple(size) if isinstance(size, (tuple, list)) else (size, size)
+        if len(so) != 2 or any(v is None for v in so):
+            raise NativeUnsupported(f'{node.name}: adaptive_avg_pool2d output_size={size!r}')
+        if so == (1, 1):
+            return self.avgpool(node)
+        new = self._site_node(node, AdaptiveAvgPool(self.net.ctx, so[0], so[1]), [node.args[0]])
         self._replace([node], new)
 
     def volume_pool(self, node, m):
@@ -768,6 +778,50 @@ class _Lowering:
             object.__setattr__(sq, 'grad_link', sp)
             object.__setattr__(sp, 'grad_expected', True)
 
+    def _link_frames(self):
+        """The 3D residual blocks' two-branch gradients, summed in the temporal fold kernel
+        instead of by autograd's add (glayers.Frames): a 5D value V used exactly twice,
+
+        * as the unfolded input of a Conv3d site S1 and as the identity residual of a site S3
+          downstream of it: S3's backward hands its residual gradient to S1 (``res_link``),
+          whose fold adds it;
+        * as the unfolded input of two Conv3d sites P and Q (a block's first conv and its
+          shortcut conv, Q's backward first - the rule of :meth:`_link_dgrads`): Q's fold
+          output is handed to P (``send_to``), whose fold adds it."""
+        mods = dict(self.gm.named_modules())
+        order = {n: i for i, n in enumerate(self.gm.graph.nodes)}
+
+        def unfolding(s):
+            return isinstance(s, Frames) and isinstance(s._conv, Conv3dAs2d) and isinstance(s.site, ConvBNAct)
+
+        for v in self.gm.graph.nodes:
+            users = sorted(v.users, key=order.get)
+            if len(users) != 2 or not all(u.op == 'call_module' for u in users):
+                continue
+            (a, b), (sa, sb) = users, [mods.get(u.target) for u in users]
+            if not (unfolding(sa) and unfolding(sb)) or sa is sb:
+                continue
+            # identity residual: one user takes V as its residual (only), the other as input
+            for s1n, s1, s3n, s3 in ((a, sa, b, sb), (b, sb, a, sa)):
+                if (s1n.args[0] is v and not (len(s1n.args) > 1 and s1n.args[1] is v) and len(s3n.args) > 1
+                        and s3n.args[1] is v and s3n.args[0] is not v and s3.site.residual
+                        and s3.site.conv.Cop == s3.site.conv.Co and s3.site.res_link is None
+                        and not s1.grad_expected and self._reaches(s1n, s3n)):
+                    object.__setattr__(s3.site, 'res_link', s1)
+                    object.__setattr__(s1, 'grad_expected', True)
+                    break
+            else:
+                # two sibling convs over V
+                if not all(u.args[0] is v and not (len(u.args) > 1 and u.args[1] is v) for u in users):
+                    continue
+                qu = list(b.users)
+                if not (self._reaches(a, b) or (len(qu) == 1 and self._reaches(a, qu[0]))):
+                    continue
+                if sb.send_to is not None or sa.grad_expected or sa.send_to is not None:
+                    continue
+                object.__setattr__(sb, 'send_to', sa)
+                object.__setattr__(sa, 'grad_expected', True)
+
     def _link_bn_backward(self):
         """A conv+BN site A (ReLU or no activation, batch statistics) whose output is used
         only as the input of a dense conv site B (and, at a residual block boundary, as the
@@ -861,8 +915,8 @@ class _Lowering:
                     self.linear(node)
                 elif isinstance(m, nn.MaxPool2d):
                     self.maxpool(node, m.kernel_size, m.stride, m.padding, m.dilation, m.ceil_mode, m.return_indices)
-                elif isinstance(m, nn.AdaptiveAvgPool2d) and _pair(m.output_size, 'output_size') == 1:
-                    self.avgpool(node)
+                elif isinstance(m, nn.AdaptiveAvgPool2d):
+                    self.adaptive_pool(node, m.output_size)
                 elif isinstance(m, nn.AvgPool2d):
                     self.avgpool2d(node, m.kernel_size, m.stride, m.padding, m.ceil_mode, m.count_include_pad,
                                    m.divisor_override)
@@ -903,9 +957,8 @@ class _Lowering:
                     self.interpolate(node)
                 elif t in (operator.mul, torch.mul):
                     self.gate(node)
-                elif t is F.adaptive_avg_pool2d and _pair(node.args[1] if len(node.args) > 1
-                                                          else node.kwargs['output_size'], 'output_size') == 1:
-                    self.avgpool(node)
+                elif t is F.adaptive_avg_pool2d:
+                    self.adaptive_pool(node, node.args[1] if len(node.args) > 1 else node.kwargs['output_size'])
                 elif t is F.scaled_dot_product_attention:
                     self.sdpa(node)
                 elif t in (F.conv2d, torch.conv2d, F.linear, torch.matmul, torch.mm, torch.bmm, torch.addmm,
@@ -923,6 +976,7 @@ class _Lowering:
         self._fold_shortcut_bns()
         self._link_residuals()
         self._link_dgrads()
+        self._link_frames()
         self._link_bn_backward()
         g.lint()
         self.gm.delete_all_unused_submodules()

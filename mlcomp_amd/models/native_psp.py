@@ -11,7 +11,8 @@ sigmoid head of <= 4 classes trained with BCE + Dice (the segmentation engine's 
 * fusion conv (1x1 + BN + ReLU, :class:`ConvBN`), Dropout2d, the 3x3 output conv with bias
   on the implicit-GEMM kernels, x ``factor`` bilinear, BCE + Dice
   (:class:`~.native_fpn.UpsampledSegHead`).
-The pools, concat, dropout and the loss are PyTorch tensor ops on NHWC activations; every
+The pyramid's adaptive pools run on the native NHWC kernels (pool_loss.hip: PyTorch's bins,
+fp32 sums); concat, dropout and the loss are PyTorch tensor ops on NHWC activations; every
 convolution runs on the native MFMA kernels.
 """
 from __future__ import annotations
@@ -20,6 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops.layers import ConvBN
 from .native_fpn import Conv1x1Bias, Conv3x3, NativeFPN, UpsampledSegHead, _BilinearFn, _nchw, _nhwc
 from .native_unet import NativeUnet
@@ -111,7 +113,11 @@ class NativePSPNet(NativeUnet):
         h, w = f.shape[1], f.shape[2]
         ys = []
         for size, unit in self.stages:
-            p = _nhwc(F.adaptive_avg_pool2d(_nchw(f), size))
+            so = (size, size) if isinstance(size, int) else tuple(size)
+            if f.shape[-1] % 8 == 0:
+                p = Fn.AdaptiveAvgFn.apply(f.contiguous(), so[0], so[1])     # native bins, fp32 sums
+            else:
+                p = _nhwc(F.adaptive_avg_pool2d(_nchw(f), so))
             q = unit(p) if isinstance(unit, ConvBN) else torch.relu(unit(p))
             ys.append(_BilinearFn.apply(q.contiguous(), (h, w)))
         z = self.fuse(torch.cat(ys + [f], dim=-1))

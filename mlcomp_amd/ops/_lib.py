@@ -96,6 +96,8 @@ _SIGS = {
     'mlc_avgpool_bwd': [vp, vp, i32, i32, i32, vp],
     'mlc_avgpool2d_fwd': [vp, vp] + [i32] * 10 + [vp],
     'mlc_avgpool2d_bwd': [vp, vp] + [i32] * 10 + [vp],
+    'mlc_adaptive_avg_fwd': [vp, vp] + [i32] * 6 + [vp],
+    'mlc_adaptive_avg_bwd': [vp, vp] + [i32] * 6 + [vp],
     'mlc_softmax_ce': [vp] * 5 + [i32, i32, i32, f32, f32, vp],
     'mlc_colsum': [vp, vp, i32, i32, vp],
     'mlc_nchw_to_nhwc': [vp, vp, i32, i32, i32, i32, vp],
@@ -124,7 +126,7 @@ _SIGS = {
     'mlc_conv_fwd_ex': [vp] * 4 + [i32] * 13 + [vp],
     'mlc_conv_wgrad_bias': [vp] * 4 + [i32] * 13 + [vp, i64, vp],
     'mlc_temporal_unfold': [vp, vp] + [i32] * 9 + [vp],
-    'mlc_temporal_fold': [vp, vp] + [i32] * 9 + [vp],
+    'mlc_temporal_fold': [vp, vp, vp] + [i32] * 9 + [vp],
     'mlc_counters_owner': [i32],
     'mlc_counters_release': [i32],
     'mlc_counters_in_use': [],

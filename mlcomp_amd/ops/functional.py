@@ -739,6 +739,45 @@ def avgpool2d_bwd(dy, x_shape, k, s, p, count_include_pad=True):
     return xf.grad.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
 
 
+def adaptive_avg_fwd(x, Ho, Wo):
+    """adaptive_avg_pool2d of NHWC bf16 ``x`` to (Ho, Wo) - PyTorch's (overlapping) bins, fp32
+    sums, one bf16 rounding (pool_loss.hip; the GPU's stock channels_last bf16 kernel is
+    ~3e-3 off its own CPU result on PSPNet's 3x3 / 6x6 bins, docs/numerics.md)."""
+    N, H, W, C = x.shape
+    if _cuda(x):
+        y = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.bfloat16)
+        _lib.call('mlc_adaptive_avg_fwd', _lib.ptr(x.contiguous()), _lib.ptr(y), N, H, W, C, Ho, Wo, _lib.stream())
+        return y
+    yf = F.adaptive_avg_pool2d(x.permute(0, 3, 1, 2).float(), (Ho, Wo))
+    return yf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+
+
+def adaptive_avg_bwd(dy, x_shape):
+    N, H, W, C = x_shape
+    _, Ho, Wo, _ = dy.shape
+    if _cuda(dy):
+        dx = torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
+        _lib.call('mlc_adaptive_avg_bwd', _lib.ptr(dy.contiguous()), _lib.ptr(dx), N, H, W, C, Ho, Wo, _lib.stream())
+        return dx
+    with torch.enable_grad():             # called from autograd backward (grad mode off)
+        xf = torch.zeros(N, C, H, W, requires_grad=True)
+        F.adaptive_avg_pool2d(xf, (Ho, Wo)).backward(dy.permute(0, 3, 1, 2).float())
+    return xf.grad.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+
+
+class AdaptiveAvgFn(torch.autograd.Function):
+    """NHWC bf16 adaptive average pool with the native backward (:func:`adaptive_avg_fwd`)."""
+
+    @staticmethod
+    def forward(ctx, x, Ho, Wo):
+        ctx.xshape = tuple(x.shape)
+        return adaptive_avg_fwd(x, Ho, Wo)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return adaptive_avg_bwd(dy, ctx.xshape), None, None
+
+
 def avgpool_fwd(x):
     N, H, W, C = x.shape
     if _cuda(x):

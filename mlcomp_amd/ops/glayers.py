@@ -103,20 +103,27 @@ class Conv3dAs2d:
     def weight(self):
         return self.src3d.weight.view(self._shape)
 
-    def unfold(self, x: torch.Tensor) -> torch.Tensor:
+    def unfold(self, x: torch.Tensor, link: Optional['Frames'] = None) -> torch.Tensor:
         """Logical [N, C, T, H, W] (or [N, C, L]) -> the frames [N*To, C*kt, H, W] the 2D
         conv reads.  On the GPU (C % 8 == 0, kt <= 8) the native unfold / fold kernels
         (``csrc/kernels/video.hip``) build it from the channels_last_3d activation and fold
-        the gradient back; elsewhere torch gather / pad ops (autograd folds the gradient)."""
+        the gradient back; elsewhere torch gather / pad ops (autograd folds the gradient).
+        ``link``: the Frames site that owns this unfold takes part in a gradient hand-off
+        (:class:`Frames`): the fold adds the other branch's gradient of ``x`` / hands its
+        result to the sibling site - in the fold kernel on the native path, through
+        :class:`_GradLink` (one add) elsewhere."""
         if x.dim() == 3:
             x = x[:, :, :, None, None]
         N, C, T, H, W = x.shape
         kt, st, pt, dt = self.kt, self.st, self.pt, self.dt
+        native = x.is_cuda and C % 8 == 0 and kt <= 8 and not (kt == 1 and st == 1 and pt == 0)
+        if link is not None and not native:
+            x = _GradLink.apply(x, link)
         if kt == 1 and st == 1 and pt == 0:
             return frames_of(x)
         To = (T + 2 * pt - dt * (kt - 1) - 1) // st + 1
-        if x.is_cuda and C % 8 == 0 and kt <= 8:
-            return _TemporalUnfold.apply(x, kt, st, pt, dt, To)
+        if native:
+            return _TemporalUnfold.apply(x, kt, st, pt, dt, To, link)
         if pt:
             x = torch.nn.functional.pad(x, (0, 0, 0, 0, pt, pt))
         idx = (torch.arange(To, device=x.device)[:, None] * st + torch.arange(kt, device=x.device)[None] * dt)
@@ -148,29 +155,91 @@ def temporal_unfold(x5: torch.Tensor, kt: int, st: int, pt: int, dt: int, To: in
 
 
 def temporal_fold(dcol: torch.Tensor, N: int, C: int, T: int, H: int, W: int, kt: int, st: int, pt: int, dt: int,
-                  To: int) -> torch.Tensor:
+                  To: int, addend: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Gradient of :func:`temporal_unfold`: frames-gradient [N*To, C*kt, H, W] -> [N, C, T, H, W]
-    (channels_last_3d), a gather over the taps (no atomics)."""
+    (channels_last_3d), a gather over the taps (no atomics); ``addend`` (any tensor whose
+    memory is the contiguous [N, T, H, W, C] bf16 gradient of the same activation, see
+    :func:`_nthwc`) is summed in the same pass."""
     from . import _lib
     dm = dcol.permute(0, 2, 3, 1)
     if dm.dtype != torch.bfloat16:
         dm = dm.to(torch.bfloat16)
     dm = dm.contiguous()
+    add = _nthwc(addend, N, C, T, H, W) if addend is not None else None
     dx = torch.empty(N, T, H, W, C, device=dcol.device, dtype=torch.bfloat16)
-    _lib.call('mlc_temporal_fold', _lib.ptr(dm), _lib.ptr(dx), N, T, H * W, C, kt, st, pt, dt, To, _lib.stream())
+    _lib.call('mlc_temporal_fold', _lib.ptr(dm), _lib.ptr(add), _lib.ptr(dx), N, T, H * W, C, kt, st, pt, dt, To,
+              _lib.stream())
     return dx.permute(0, 4, 1, 2, 3)
+
+
+def _nthwc(g: torch.Tensor, N: int, C: int, T: int, H: int, W: int) -> torch.Tensor:
+    """A hand-off gradient as the contiguous bf16 [N, T, H, W, C] tensor: either a site's NHWC
+    frame gradient [N*T, H, W, C] or a logical [N, C, T, H, W] (channels_last_3d) one."""
+    if g.dim() == 4:
+        assert tuple(g.shape) == (N * T, H, W, C), (tuple(g.shape), (N, C, T, H, W))
+        g = g.reshape(N, T, H, W, C)
+    else:
+        assert tuple(g.shape) == (N, C, T, H, W), (tuple(g.shape), (N, C, T, H, W))
+        g = g.permute(0, 2, 3, 4, 1)
+    return g.to(torch.bfloat16).contiguous()
+
+
+def _link_grad(link: 'Frames', dx: Optional[torch.Tensor], x_shape) -> Optional[torch.Tensor]:
+    """Receiver / sender side of a Frames gradient hand-off around the input gradient ``dx``
+    of the site's 5D input (None when the caller already summed the pending addend)."""
+    if link.send_to is not None:
+        object.__setattr__(link.send_to, '_pending', dx)     # summed by the sibling's fold
+        return None
+    return dx
+
+
+def _take_pending(link: Optional['Frames']):
+    if link is None:
+        return None
+    add = link._pending
+    object.__setattr__(link, '_pending', None)
+    if link.grad_expected and add is None:
+        raise RuntimeError(f'{link.name}: the gradient hand-off of the other branch did not arrive '
+                           '(backward order differs from the one the lowering assumed)')
+    return add
 
 
 class _TemporalUnfold(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, kt, st, pt, dt, To):
+    def forward(ctx, x, kt, st, pt, dt, To, link=None):
         ctx.geom = (tuple(x.shape), kt, st, pt, dt, To, x.dtype)
+        ctx.link = link
         return temporal_unfold(x, kt, st, pt, dt, To)
 
     @staticmethod
     def backward(ctx, g):
         (N, C, T, H, W), kt, st, pt, dt, To, dtype = ctx.geom
-        return temporal_fold(g, N, C, T, H, W, kt, st, pt, dt, To).to(dtype), None, None, None, None, None
+        link = ctx.link
+        dx = temporal_fold(g, N, C, T, H, W, kt, st, pt, dt, To, addend=_take_pending(link)).to(dtype)
+        if link is not None:
+            dx = _link_grad(link, dx, (N, C, T, H, W))
+        return dx, None, None, None, None, None, None
+
+
+class _GradLink(torch.autograd.Function):
+    """Identity on a Frames site's 5D input whose backward does the site's gradient hand-off
+    with one add (the CPU path and the unfold-free frame views; the native unfold does it in
+    its fold kernel)."""
+
+    @staticmethod
+    def forward(ctx, x, link):
+        ctx.link = link
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        link = ctx.link
+        add = _take_pending(link)
+        if add is not None:
+            N, C, T, H, W = g.shape
+            a = add.reshape(N, T, H, W, C).permute(0, 4, 1, 2, 3) if add.dim() == 4 else add
+            g = g + a.to(g.dtype)
+        return _link_grad(link, g, tuple(g.shape)), None
 
 
 class TemporalAs2d:
@@ -217,15 +286,26 @@ class Frames(nn.Module):
     """Runs a 2D site over the frames of a 5D (or, for Conv1d, 3D) tensor: temporal unfold
     (convs), the site on N*T frames, the result back in the caller's layout."""
 
-    def __init__(self, site: nn.Module, conv: Optional[Conv3dAs2d] = None):
+    def __init__(self, site: nn.Module, conv: Optional[Conv3dAs2d] = None, name: str = ''):
         super().__init__()
         self.site = site
         self._conv = conv
+        self.name = name
+        # gradient hand-offs around this site's temporal unfold (set by the lowering,
+        # native_generic._Lowering._link_frames): ``grad_expected`` - another branch's gradient of the
+        # input arrives in ``_pending`` (a residual block's identity path, handed over by the
+        # block's last site, or the shortcut conv's input gradient) and the fold kernel sums
+        # it; ``send_to`` - this site's input gradient is handed to that sibling site
+        # instead of being returned to autograd (which would add the two in a pass of its own)
+        object.__setattr__(self, '_pending', None)
+        object.__setattr__(self, 'grad_expected', False)
+        object.__setattr__(self, 'send_to', None)
 
     def forward(self, x, res=None):
         c = self._conv
         if c is not None:
-            xf = c.unfold(x)
+            link = self if (self.grad_expected or self.send_to is not None) else None
+            xf = c.unfold(x, link) if link is not None else c.unfold(x)
             rf = c.frames_like_out(res) if res is not None else None
             y = self.site(xf, rf) if rf is not None else self.site(xf)
             return c.fold_out(y, x.shape[0], x.dim() == 3)
@@ -1156,6 +1236,28 @@ class AvgPool(Site):
         C = dout.shape[1]
         dx = Fn.avgpool2d_bwd(to_nhwc(dout, xshape[-1]), xshape, self.k, self.s, self.p, self.cip)
         return [from_nhwc(dx, C)]
+
+
+class AdaptiveAvgPool(Site):
+    """adaptive_avg_pool2d(x, (Ho, Wo)) with output > 1 (PSPNet's pyramid, any model's fixed-
+    size pool): PyTorch's overlapping bins, fp32 sums, one NHWC pass each way (pool_loss.hip)."""
+
+    def __init__(self, ctx, Ho, Wo):
+        super().__init__(ctx)
+        self.Ho, self.Wo = int(Ho), int(Wo)
+
+    def forward(self, x):
+        return _run(self, x)
+
+    def fwd(self, x):
+        C = x.shape[1]
+        xn = to_nhwc(x, ceil8(C))
+        y = Fn.adaptive_avg_fwd(xn, self.Ho, self.Wo)
+        return from_nhwc(y, C), [], tuple(xn.shape)
+
+    def bwd(self, dout, saved, xshape, needs):
+        C = dout.shape[1]
+        return [from_nhwc(Fn.adaptive_avg_bwd(to_nhwc(dout, xshape[-1]), xshape), C)]
 
 
 class GlobalAvgPool(Site):

@@ -7,10 +7,14 @@ error and the distribution of per-slot relative gradient errors ||g_gpu - g_cpu|
 
     MLC_DETERMINISTIC=1 python scripts/engines_det_compare.py [--noise] [kind ...]
 
-``--noise``: also run the CPU step with every weight perturbed by ~one bf16 ulp
-(x (1 + 2^-9 n)) and report the per-slot errors that perturbation causes (the measured
-sensitivity of the step: a segmentation loss's pixel-sum gradients cancel strongly, so
-their per-slot relative error is large even for one-ulp changes).
+``--noise``: also run the CPU step with every fp32 master weight moved by about one fp32 ulp
+(x (1 + eps n), eps = DET_NOISE_EPS, default 2^-24; this flips the bf16 rounding of ~0.003 %
+of the weights) in DET_NOISE_DRAWS independent draws (default 2), and report the per-slot
+errors that causes: the step's sensitivity to a change far below anything the GPU kernels
+could introduce on purpose.  Batch-normalised networks at random init amplify such changes
+enormously (docs/numerics.md: stock PyTorch bf16 autocast moves ResNeXt-50 slot gradients by
+~100 % for the same perturbation), so this floor, not a fixed tolerance, is what a bf16 GPU
+step can be held to.  ``noise_per_slot`` is the per-slot maximum over the draws.
 """
 import json
 import os
@@ -22,6 +26,8 @@ root = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..')
 sys.path[:0] = [root, os.path.join(root, 'tests')]
 
 B, R = int(os.environ.get('DET_BATCH', 8)), int(os.environ.get('DET_RES', 128))
+NOISE_EPS = float(os.environ.get('DET_NOISE_EPS', 2.0 ** -24))
+NOISE_DRAWS = int(os.environ.get('DET_NOISE_DRAWS', 2))
 
 
 def make(kind, device):
@@ -102,20 +108,30 @@ def main():
                'grad_rel_max': v[-1], 'grad_rel_p90': v[int(0.9 * (len(v) - 1))], 'grad_rel_median': v[len(v) // 2],
                'worst': [(n, round(e, 4)) for n, e in worst], 'per_slot': rel}
         if noise:
-            per = make(kind, 'cpu')
-            copy_inputs(per, cpu)
-            gen = torch.Generator().manual_seed(1)
-            with torch.no_grad():
-                for a in per.net.arena.arenas():
-                    a.master.mul_(1 + 2 ** -9 * torch.randn(a.master.shape, generator=gen))
-                per.net.arena.decay.refresh_mirror()
-            l_p, g_p = grads(per)
-            out['noise_per_slot'] = {n: float((g_p[n] - g_c[n]).norm() / (g_c[n].norm() + 1e-20)) for n in g_c
-                                     if n in g_p}
-            vn = sorted(out['noise_per_slot'].values())
+            env, draws, lrel = {}, [], 0.0
+            for d in range(NOISE_DRAWS):
+                per = make(kind, 'cpu')
+                copy_inputs(per, cpu)
+                gen = torch.Generator().manual_seed(1 + d)
+                with torch.no_grad():
+                    for a in per.net.arena.arenas():
+                        a.master.mul_(1 + NOISE_EPS * torch.randn(a.master.shape, generator=gen))
+                        a.refresh_mirror()
+                l_p, g_p = grads(per)
+                one = {n: float((g_p[n] - g_c[n]).norm() / (g_c[n].norm() + 1e-20)) for n in g_c if n in g_p}
+                for n, e in one.items():
+                    env[n] = max(env.get(n, 0.0), e)
+                vd = sorted(one.values())
+                draws.append(vd[len(vd) // 2])
+                lrel = max(lrel, abs(l_p - l_c) / abs(l_c))
+                del per
+            out['noise_eps'], out['noise_draw_medians'] = NOISE_EPS, draws
+            out['noise_per_slot'] = env
+            vn = sorted(env.values())
             out['noise_median'], out['noise_max'] = vn[len(vn) // 2], vn[-1]
-            out['noise_loss_rel'] = abs(l_p - l_c) / abs(l_c)
-            del per
+            out['noise_loss_rel'] = lrel
+            out['ratio_median'] = out['grad_rel_median'] / max(out['noise_median'], 1e-20)
+            out['ratio_slot_max'] = max(rel[n] / max(env.get(n, 0.0), 1e-20) for n in rel)
         print(json.dumps(out), flush=True)
         del cpu, gpu
         torch.cuda.empty_cache()

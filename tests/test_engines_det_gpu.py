@@ -1,19 +1,26 @@
-"""GPU step vs CPU step of the native engines in deterministic mode (round-4 verdict item 4).
+"""GPU step vs CPU step of the native engines in deterministic mode (docs/numerics.md).
 
 The deterministic mode (MLC_DETERMINISTIC=1: ordered reductions, unsplit GEMMs) is
 process-wide, so the comparison runs in a child process (scripts/engines_det_compare.py):
 one lr-0 step at batch 8 @ 128x128 of every hand engine and three generic models, on the
 CPU path of the native ops and on the GPU kernels, same weights and batch.
 
-* Classification / BERT steps (gradients that are coherent sums): every parameter slot's
-  relative gradient error <= 5e-2, the median <= 3e-2, the loss within 1e-3.
-* Segmentation steps and EfficientNet (pixel-sum gradients that cancel strongly, so one-ulp
-  changes move them by tens of percent): the bound is the step's own measured
-  sensitivity - the CPU step re-run with every weight perturbed by ~one bf16 ulp - per slot
-  1.5 x that + 0.02, and the median within 1.25 x the perturbation's median (round 4 used
-  3 x + 0.05).  A wrong kernel moves its slots far past either bound: with DeepLab's
-  dropout left on (CPU and GPU draw different masks) 109 of 110 slots fail it.
-The measured table is kept in profiles/round5/engines_det.jsonl."""
+The bound is each step's own sensitivity to moving every fp32 master weight by one fp32 ulp
+(x (1 + 2^-24 n), 3 draws, per-slot maximum): the GPU kernels differ from the CPU path only
+in fp32 accumulation order, a perturbation of the same size, and batch-normalised networks
+at init amplify such perturbations by orders of magnitude in bf16 (stock PyTorch moves
+ResNeXt-50's slot gradients by up to 4 % with zero-init residuals and ~100 % without), so no
+fixed tolerance is meaningful for every engine.  Per engine:
+
+* loss within max(1e-3, 3 x the perturbed loss change);
+* median slot error <= 2 x the noise median;
+* every slot <= 2.5 x its own noise envelope + 2e-3 (a conv bias before a train-mode BN has a
+  zero true gradient: only cancellation noise);
+* classification / BERT engines additionally every slot <= 5e-2.
+
+A wrong kernel lands far outside: stock PyTorch's own channels_last bf16 adaptive pool put
+PSPNet at 5.3 x its floor (median) before the pyramid moved to the native kernel.  The
+measured tables are kept in profiles/round6/anchor/."""
 import json
 import os
 import subprocess
@@ -24,14 +31,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 COHERENT = ('resnet50', 'bert', 'resnext50')
-CANCELLING = ('unet', 'linknet', 'fpn', 'pspnet', 'deeplab', 'efficientnet-b0', 'unet-resnext50')
+OTHERS = ('unet', 'linknet', 'fpn', 'pspnet', 'deeplab', 'efficientnet-b0', 'unet-resnext50')
 
 
 @pytest.fixture(scope='module')
 def results():
-    env = dict(os.environ, MLC_DETERMINISTIC='1', PYTHONPATH=ROOT)
+    env = dict(os.environ, MLC_DETERMINISTIC='1', PYTHONPATH=ROOT, DET_NOISE_DRAWS='3')
     r = subprocess.run([sys.executable, os.path.join(ROOT, 'scripts', 'engines_det_compare.py'), '--noise',
-                        *COHERENT, *CANCELLING], env=env, cwd=ROOT, capture_output=True, text=True, timeout=900)
+                        *COHERENT, *OTHERS], env=env, cwd=ROOT, capture_output=True, text=True, timeout=1200)
     assert r.returncode == 0, r.stderr[-4000:]
     out = {}
     for line in r.stdout.splitlines():
@@ -41,21 +48,15 @@ def results():
     return out
 
 
-@pytest.mark.parametrize('kind', COHERENT)
-def test_coherent_engines_match_cpu_per_slot(results, kind):
+@pytest.mark.parametrize('kind', COHERENT + OTHERS)
+def test_engine_within_its_fp32_ulp_floor(results, kind):
     d = results[kind]
     assert d['deterministic'] and not d['missing'], d['missing']
-    assert d['loss_rel_err'] <= 1e-3, d['loss_rel_err']
-    assert d['grad_rel_max'] <= 5e-2, d['worst']
-    assert d['grad_rel_median'] <= 3e-2, d['grad_rel_median']
-
-
-@pytest.mark.parametrize('kind', CANCELLING)
-def test_cancelling_engines_within_measured_sensitivity(results, kind):
-    d = results[kind]
-    assert d['deterministic'] and not d['missing'], d['missing']
-    assert d['loss_rel_err'] <= max(2e-3, 2 * d['noise_loss_rel']), (d['loss_rel_err'], d['noise_loss_rel'])
+    assert d['noise_eps'] == 2.0 ** -24
+    assert d['loss_rel_err'] <= max(1e-3, 3 * d['noise_loss_rel']), (d['loss_rel_err'], d['noise_loss_rel'])
+    assert d['grad_rel_median'] <= 2 * d['noise_median'], (d['grad_rel_median'], d['noise_median'])
     g, n = d['per_slot'], d['noise_per_slot']
-    bad = {k: (round(g[k], 4), round(n[k], 4)) for k in g if g[k] > 1.5 * n[k] + 0.02}
+    bad = {k: (round(g[k], 4), round(n[k], 4)) for k in g if g[k] > 2.5 * n[k] + 2e-3}
     assert not bad, bad
-    assert d['grad_rel_median'] <= 1.25 * d['noise_median'] + 1e-3, (d['grad_rel_median'], d['noise_median'])
+    if kind in COHERENT:
+        assert d['grad_rel_max'] <= 5e-2, d['worst']

@@ -667,6 +667,41 @@ def test_video_resnext3d_lowers_and_matches_fp32_autograd(kw):
         assert _rel(net(x), ref(x)) < 5e-2
 
 
+def test_video_residual_gradients_are_handed_off_not_added(monkeypatch):
+    """ResNeXt3D blocks: the identity residual's gradient and the shortcut conv's input
+    gradient are handed to the block's first Conv3d site (Frames.grad_expected) and summed in
+    its temporal fold (native) / one add (here) instead of by autograd; the gradients equal
+    the unlinked lowering's."""
+    from mlcomp_amd.contrib.video import ResNeXt3D
+    from mlcomp_amd.models.native_generic import _Lowering as NativeLowering
+    from mlcomp_amd.ops.glayers import Frames
+    cfg = dict(residual_transformation_type='basic_transformation', num_blocks=(2, 2), stem_planes=16,
+               stage_planes=16, stage_temporal_kernel_basis=([3], [3]), temporal_conv_1x1=(False, False),
+               stage_temporal_stride=(1, 2), stage_spatial_stride=(1, 2), in_plane=32, num_classes=5,
+               stem_spatial_kernel=3)
+    x = torch.randn(2, 3, 4, 16, 16)
+    y = torch.randint(0, 5, (2,))
+
+    def run(linked):
+        torch.manual_seed(0)
+        if not linked:
+            monkeypatch.setattr(NativeLowering, '_link_frames', lambda self: None)
+        net = GenericNet(ResNeXt3D(**cfg), 'cpu')
+        monkeypatch.undo()
+        fr = [m for m in net.train_gm.modules() if isinstance(m, Frames)]
+        links = (sum(m.grad_expected for m in fr), sum(m.send_to is not None for m in fr),
+                 sum(getattr(m.site, 'res_link', None) is not None for m in fr))
+        F.cross_entropy(net(x).float(), y).backward()
+        return links, [p.w.grad.clone() for p in net.param_sets() if hasattr(p, 'kind')]
+
+    links, g1 = run(True)
+    nolinks, g0 = run(False)
+    assert links == (4, 1, 3), links          # 3 identity residuals + 1 shortcut, 4 receivers
+    assert nolinks == (0, 0, 0)
+    for a, b in zip(g1, g0):
+        assert torch.allclose(a, b, rtol=1e-3, atol=1e-5)
+
+
 def test_conv1d_bn1d_lowers_and_matches_fp32_autograd():
     """nn.Conv1d [-> BatchNorm1d -> ReLU] through the same temporal unfold (a Conv1d is a
     Conv3d with a 1x1 spatial kernel)."""
@@ -796,6 +831,36 @@ def test_average_pools_lower_and_match_fp32_autograd():
     (want * g).sum().backward()
     assert _rel(out, want) < 2e-2
     assert _cos(xi.grad, xr.grad) > 0.98
+    for p in net.param_sets():
+        gg = p.w.grad if hasattr(p, 'w') else p.gamma.grad
+        assert _cos(gg, _torch_grad(p, ref)) > 0.98, p.name
+
+
+def test_adaptive_avg_pool_sizes_lower_natively():
+    """AdaptiveAvgPool2d / F.adaptive_avg_pool2d to sizes > 1 (PSPNet's pyramid, overlapping
+    bins when the size does not divide the input) lower to the native AdaptiveAvgPool site;
+    output and input gradient against fp32 autograd."""
+    from mlcomp_amd.ops.glayers import AdaptiveAvgPool
+
+    class Pyr(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.c = nn.Conv2d(3, 16, 3, padding=1)
+            self.p = nn.AdaptiveAvgPool2d(6)
+
+        def forward(self, x):
+            y = self.c(x)
+            return self.p(y).flatten(1).sum(1) + F.adaptive_avg_pool2d(y, (3, 3)).flatten(1).sum(1)
+
+    m, ref = _pair(Pyr)
+    net = GenericNet(m, 'cpu')
+    assert sum(isinstance(mod, AdaptiveAvgPool) for mod in net.train_gm.modules()) == 2
+    x = torch.randn(2, 3, 16, 16)
+    out = net(x)
+    out.float().sum().backward()
+    want = ref(x)
+    want.sum().backward()
+    assert _rel(out, want) < 2e-2
     for p in net.param_sets():
         gg = p.w.grad if hasattr(p, 'w') else p.gamma.grad
         assert _cos(gg, _torch_grad(p, ref)) > 0.98, p.name

@@ -653,6 +653,35 @@ def test_temporal_unfold_fold_match_torch(kt, st, pt, dt):
     assert err < 1e-2, err
 
 
+@pytest.mark.parametrize('frames_layout', [True, False])
+def test_temporal_fold_sums_the_handed_off_gradient(frames_layout):
+    """The fold kernel's addend (the other branch's gradient of a residual block's input,
+    glayers.Frames hand-off): fold(dcol) + addend in one pass, for an addend given as a
+    site's NHWC frame gradient or as a logical channels_last_3d tensor, against fp32."""
+    from mlcomp_amd.ops.glayers import temporal_fold, temporal_unfold
+    g = torch.Generator().manual_seed(3)
+    N, C, T, H, W, kt, st, pt, dt = 2, 16, 6, 5, 4, 3, 2, 1, 1
+    To = (T + 2 * pt - dt * (kt - 1) - 1) // st + 1
+    x = torch.randn(N, C, T, H, W, generator=g).to(torch.bfloat16).requires_grad_()
+    dcol = torch.randn(N * To, C * kt, H, W, generator=g).to(torch.bfloat16)
+    add5 = torch.randn(N, C, T, H, W, generator=g).to(torch.bfloat16)
+    xr = x.float().detach().requires_grad_()
+    from mlcomp_amd.ops.glayers import Conv3dAs2d
+    conv = Conv3dAs2d(torch.nn.Conv3d(C, 8, (kt, 1, 1), (st, 1, 1), (pt, 0, 0), (dt, 1, 1)))
+    conv.unfold(xr).backward(dcol.float())
+    want = xr.grad + add5.float()
+    addend = (add5.permute(0, 2, 3, 4, 1).reshape(N * T, H, W, C) if frames_layout
+              else add5.contiguous(memory_format=torch.channels_last_3d)).cuda()
+    dm = dcol.cuda().contiguous(memory_format=torch.channels_last)
+    got = temporal_fold(dm, N, C, T, H, W, kt, st, pt, dt, To, addend=addend)
+    torch.cuda.synchronize()
+    err = (got.float().cpu() - want).abs().max() / want.abs().max()
+    assert err < 1e-2, err
+    plain = temporal_fold(dm, N, C, T, H, W, kt, st, pt, dt, To)
+    assert torch.allclose(plain.float().cpu(), xr.grad, atol=3e-2, rtol=1e-2)
+    assert temporal_unfold is not None
+
+
 @pytest.mark.parametrize('N,H,C,Co,S', [(64, 28, 128, 512, 1), (24, 56, 64, 256, 1), (96, 28, 256, 1024, 2),
                                         (42, 28, 256, 256, 1)])
 def test_persistent_short_k_gemm_matches_tile_kernel(N, H, C, Co, S):
@@ -682,3 +711,21 @@ def test_persistent_short_k_gemm_matches_tile_kernel(N, H, C, Co, S):
     assert torch.equal(outs[0][0], outs[1][0])
     assert (outs[1][0] - want).abs().max() <= 2e-2 * want.abs().max()
     assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize('H,W,Ho,Wo', [(16, 16, 6, 6), (16, 16, 3, 3), (17, 13, 6, 4), (8, 8, 2, 2), (5, 7, 6, 6)])
+def test_adaptive_avg_pool_matches_fp32(H, W, Ho, Wo):
+    """Native adaptive average pool (pool_loss.hip: PyTorch's overlapping bins, fp32 sums) and
+    its gather backward against fp32 F.adaptive_avg_pool2d / autograd."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(3, H, W, 24, generator=g).to(torch.bfloat16)
+    dy = torch.randn(3, Ho, Wo, 24, generator=g).to(torch.bfloat16)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_()
+    want = F.adaptive_avg_pool2d(xr, (Ho, Wo))
+    want.backward(dy.float().permute(0, 3, 1, 2))
+    got = Fn.adaptive_avg_fwd(x.cuda(), Ho, Wo)
+    dx = Fn.adaptive_avg_bwd(dy.cuda(), tuple(x.shape))
+    torch.cuda.synchronize()
+    assert (got.float().cpu() - want.detach().permute(0, 2, 3, 1)).abs().max() <= 8e-3 * want.abs().max()
+    assert (dx.float().cpu() - xr.grad.permute(0, 2, 3, 1)).abs().max() <= 8e-3 * xr.grad.abs().max()
