@@ -260,12 +260,182 @@ bn_bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, con
   }
 }
 
+// ---- finalize folded into the apply pass (one launch per BN instead of two) -------------
+// The per-channel finalize kernels sat on the critical path between a GEMM and its apply
+// pass, 53 + 53 of them per ResNet-50 step (~5 us each with the dependency gap).  Here each
+// block first reduces the NSTAT partial copies for the channels it touches into LDS: a block
+// owns a slice of FG <= 32 channel groups (<= 256 channels, 64 KB of partial sums read from
+// L2) and strides over the rows; blocks of row-part 0 also publish the per-channel outputs
+// (batch mean / invstd, scale / shift, running statistics - or dgamma / dbeta), so those
+// are written once.  Not used in deterministic mode (one copy per contributing block).
+constexpr int FG = 32;
+
+__device__ __forceinline__ void fused_geom(int G, int& gb, int& nslices) {
+  gb = G < FG ? G : FG;
+  nslices = G / gb;
+}
+
+// red[0][c], red[1][c] (c < nch) = sum over the ncopy copies of a[k*stride + c0 + c] and
+// b[k*stride + c0 + c]: the block's threads split the copies (P = NT / nch phases, each
+// thread's loads all issued before they are summed), then one LDS pass folds the phases
+__device__ __forceinline__ void fused_reduce(const float* __restrict__ a, const float* __restrict__ b, long stride,
+                                             int ncopy, int c0, int nch, int t, float (&red)[2][NT]) {
+  const int P = NT / nch, p = t / nch, cl = t % nch;
+  float x = 0.f, y = 0.f;
+  if (p < P) {
+#pragma unroll 16
+    for (int k = p; k < ncopy; k += P) { x += a[k * stride + c0 + cl]; y += b[k * stride + c0 + cl]; }
+  }
+  red[0][t] = x;
+  red[1][t] = y;
+  __syncthreads();
+  if (t < nch) {
+    for (int q = 1; q < P; ++q) { x += red[0][q * nch + t]; y += red[1][q * nch + t]; }
+  }
+  __syncthreads();
+  if (t < nch) { red[0][t] = x; red[1][t] = y; }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(NT)
+bn_fwd_fused_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf16* __restrict__ z,
+                    const float* __restrict__ sum, const float* __restrict__ sumsq, int ncopy,
+                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                    float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                    float* __restrict__ scale_out, float* __restrict__ shift_out,
+                    float* __restrict__ run_mean, float* __restrict__ run_var,
+                    const float* __restrict__ rscale_, const float* __restrict__ rshift_,
+                    long rows, int C, float eps, float momentum, int relu) {
+  __shared__ float lsc[FG * 8], lsh[FG * 8], red[2][NT];
+  const int G = C >> 3;
+  int gb, nslices;
+  fused_geom(G, gb, nslices);
+  const int slice = blockIdx.x % nslices, part = blockIdx.x / nslices, nparts = gridDim.x / nslices;
+  const int t = threadIdx.x, nch = gb * 8, c0 = slice * nch;
+  fused_reduce(sum, sumsq, (long)C, ncopy, c0, nch, t, red);
+  if (t < nch) {
+    const int c = c0 + t;
+    const float s1 = red[0][t], s2 = red[1][t];
+    const float inv_count = 1.f / (float)rows;
+    const float mean = s1 * inv_count;
+    const float var = fmaxf(s2 * inv_count - mean * mean, 0.f);
+    const float inv = rsqrtf(var + eps);
+    const float g = gamma[c] * inv, h = beta[c] - mean * g;
+    lsc[t] = g;
+    lsh[t] = h;
+    if (part == 0) {
+      save_mean[c] = mean;
+      save_invstd[c] = inv;
+      scale_out[c] = g;
+      shift_out[c] = h;
+      if (run_mean) {
+        const float unbiased = rows > 1 ? var * (float)rows / (float)(rows - 1) : var;
+        run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+        run_var[c] = (1.f - momentum) * run_var[c] + momentum * unbiased;
+      }
+    }
+  }
+  __syncthreads();
+  const int rpi = NT / gb;                          // rows per block iteration
+  if (t >= rpi * gb) return;
+  const int g = t % gb, cg = slice * gb + g;
+  float sc[8], sh[8], rsc[8], rsh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = lsc[g * 8 + j];
+    sh[j] = lsh[g * 8 + j];
+    rsc[j] = rscale_ ? rscale_[cg * 8 + j] : 1.f;
+    rsh[j] = rscale_ ? rshift_[cg * 8 + j] : 0.f;
+  }
+  for (long r = (long)part * rpi + t / gb; r < rows; r += (long)nparts * rpi) {
+    const long i = r * G + cg;
+    // both loads issued before either is used (one round trip per chunk, not two)
+    const uint4 yv = ldg16(y + i * 8);
+    const uint4 rv = res ? ldg16(res + i * 8) : make_uint4(0u, 0u, 0u, 0u);
+    float f[8];
+    unpack8(yv, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[j] + sh[j];
+    if (res) {
+      float q[8];
+      unpack8(rv, q);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += q[j] * rsc[j] + rsh[j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    }
+    *reinterpret_cast<uint4*>(z + i * 8) = pack8(f);
+  }
+}
+
+// dy = k1*dU + k2 + k3*(y-mean) with (k1, k2, k3) from the reduction copies (sums [ncopy][2][C])
+// folded in; dres = dU (optional); z != null applies the ReLU mask z > 0 to dz
+__global__ void __launch_bounds__(NT)
+bn_bwd_fused_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const bf16* __restrict__ y,
+                    const float* __restrict__ mean, const float* __restrict__ sums, int ncopy,
+                    const float* __restrict__ invstd, const float* __restrict__ gamma,
+                    float* __restrict__ dgamma, float* __restrict__ dbeta, bf16* __restrict__ dy,
+                    bf16* __restrict__ dres, long rows, int C) {
+  __shared__ float lk[3][FG * 8], lmu[FG * 8], red[2][NT];
+  const int G = C >> 3;
+  int gb, nslices;
+  fused_geom(G, gb, nslices);
+  const int slice = blockIdx.x % nslices, part = blockIdx.x / nslices, nparts = gridDim.x / nslices;
+  const int t = threadIdx.x, nch = gb * 8, c0 = slice * nch;
+  fused_reduce(sums, sums + C, 2L * C, ncopy, c0, nch, t, red);
+  if (t < nch) {
+    const int c = c0 + t;
+    const float S1 = red[0][t], S2 = red[1][t];
+    const float invM = 1.f / (float)rows;
+    const float is = invstd[c];
+    const float k1 = gamma[c] * is;
+    lk[0][t] = k1;
+    lk[1][t] = -k1 * S1 * invM;
+    lk[2][t] = -k1 * is * is * S2 * invM;
+    lmu[t] = mean[c];
+    if (part == 0 && dgamma) { dgamma[c] = S2 * is; dbeta[c] = S1; }
+  }
+  __syncthreads();
+  const int rpi = NT / gb;
+  if (t >= rpi * gb) return;
+  const int g = t % gb, cg = slice * gb + g;
+  float k1[8], k2[8], k3[8], mu[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    k1[j] = lk[0][g * 8 + j];
+    k2[j] = lk[1][g * 8 + j];
+    k3[j] = lk[2][g * 8 + j];
+    mu[j] = lmu[g * 8 + j];
+  }
+  for (long r = (long)part * rpi + t / gb; r < rows; r += (long)nparts * rpi) {
+    const long i = r * G + cg;
+    const uint4 dv = ldg16(dz + i * 8), yv = ldg16(y + i * 8);
+    const uint4 zv = z ? ldg16(z + i * 8) : make_uint4(0u, 0u, 0u, 0u);
+    float d[8], yy[8], o[8];
+    unpack8(dv, d);
+    unpack8(yv, yy);
+    if (z) {
+      float zz[8];
+      unpack8(zv, zz);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = zz[j] > 0.f ? d[j] : 0.f;
+    }
+    if (dres) *reinterpret_cast<uint4*>(dres + i * 8) = pack8(d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = k1[j] * d[j] + k2[j] + k3[j] * (yy[j] - mu[j]);
+    *reinterpret_cast<uint4*>(dy + i * 8) = pack8(o);
+  }
+}
+
 // A/B knobs of the elementwise passes: chunks per thread per iteration (1, 2, 4) and the
 // block cap of grid_for
 int g_unroll = 1;
 // measured: 512-768 beat 1024 by ~0.4 % on ResNet-50, 2048+ lose 2 %; 512 vs 768 +0.3 % in
 // 3 interleaved rounds (profiles/round6/bn_knobs_ab.jsonl), 1536 -1.5 %, unroll 2 / 4 -0.3 %
 int g_max_blocks = 512;
+int g_fused = 1;
 
 // block-count granularity that keeps blocks * NT a multiple of G
 long grid_mult(int G) {
@@ -289,6 +459,25 @@ int grid_for(long rows, int C) {
   const long m = grid_mult(G);
   blocks = ((blocks + m - 1) / m) * m;
   return (int)blocks;
+}
+
+// grid of the fused passes: ~g_max_blocks blocks, a multiple of the channel slices
+int fused_grid(long rows, int C) {
+  const int G = C >> 3;
+  const int gb = G < FG ? G : FG, nslices = G / gb;
+  const int rpi = NT / gb;
+  long parts = (rows + (long)rpi * 4 - 1) / ((long)rpi * 4);   // ~4 rows per thread at least
+  long cap = g_max_blocks / nslices;
+  if (cap < 1) cap = 1;
+  if (parts > cap) parts = cap;
+  if (parts < 1) parts = 1;
+  return (int)(parts * nslices);
+}
+
+bool fused_ok(int C, int ncopy) {
+  const int G = C >> 3;
+  if (g_fused != 1 || C % 8 || ncopy < 1 || ncopy > 64) return false;   // deterministic copies: the finalize kernel
+  return G <= FG || G % FG == 0;
 }
 
 bool shape_ok(int C) {
@@ -374,6 +563,30 @@ MLC_EXPORT int mlc_bn_bwd_finalize(const float* sums, const float* invstd, const
   return hipGetLastError();
 }
 
+// finalize + apply in one launch (bn_fwd_fused_kernel); returns -1 when the shape / copy
+// count does not fit (the caller then runs mlc_bn_finalize + mlc_bn_fwd_apply2)
+MLC_EXPORT int mlc_bn_fwd_fused(const bf16* y, const bf16* res, bf16* z, const float* sum, const float* sumsq,
+                                int ncopy, const float* gamma, const float* beta, float* save_mean,
+                                float* save_invstd, float* scale, float* shift, float* run_mean, float* run_var,
+                                const float* rscale, const float* rshift, long rows, int C, float eps,
+                                float momentum, int relu, hipStream_t st) {
+  if (!fused_ok(C, ncopy) || (rscale && !rshift) || rows < 1) return -1;
+  hipLaunchKernelGGL(bn_fwd_fused_kernel, dim3(fused_grid(rows, C)), dim3(NT), 0, st, y, res, z, sum, sumsq, ncopy,
+                     gamma, beta, save_mean, save_invstd, scale, shift, run_mean, run_var, rscale, rshift, rows, C,
+                     eps, momentum, relu);
+  return hipGetLastError();
+}
+
+// backward finalize + apply in one launch (bn_bwd_fused_kernel); -1: not applicable
+MLC_EXPORT int mlc_bn_bwd_fused(const bf16* dz, const bf16* z, const bf16* y, const float* mean, const float* sums,
+                                int ncopy, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
+                                bf16* dy, bf16* dres, long rows, int C, hipStream_t st) {
+  if (!fused_ok(C, ncopy) || rows < 1) return -1;
+  hipLaunchKernelGGL(bn_bwd_fused_kernel, dim3(fused_grid(rows, C)), dim3(NT), 0, st, dz, z, y, mean, sums, ncopy,
+                     invstd, gamma, dgamma, dbeta, dy, dres, rows, C);
+  return hipGetLastError();
+}
+
 MLC_EXPORT int mlc_bn_bwd_apply(const bf16* dz, const bf16* z, const bf16* y, const float* mean,
                                 const float* coef, bf16* dy, bf16* dres, long rows, int C,
                                 hipStream_t st) {
@@ -388,10 +601,11 @@ MLC_EXPORT int mlc_bn_bwd_apply(const bf16* dz, const bf16* z, const bf16* y, co
   return hipGetLastError();
 }
 
-// A/B knobs: key 0 = chunks per thread of the apply passes, 1 = block cap; value < 0 only
-// reads.  Returns the previous value.
+// A/B knobs: key 0 = chunks per thread of the apply passes, 1 = block cap, 2 = finalize
+// folded into the apply passes (1 on, 2 off; mlc_bn_{fwd,bwd}_fused return -1 when off);
+// value < 0 only reads.  Returns the previous value.
 MLC_EXPORT int mlc_bn_get_set(int key, int value) {
-  int* k = key == 0 ? &g_unroll : key == 1 ? &g_max_blocks : nullptr;
+  int* k = key == 0 ? &g_unroll : key == 1 ? &g_max_blocks : key == 2 ? &g_fused : nullptr;
   if (!k) return -1;
   const int old = *k;
   if (value > 0) *k = value;

@@ -415,6 +415,19 @@ def stat_buffers(C, device):
     return b[0], b[1]
 
 
+# finalize folded into the apply passes (batchnorm.hip bn_{fwd,bwd}_fused_kernel): one launch
+# per BatchNorm each way instead of a per-channel finalize kernel + the elementwise pass
+# (MLC_BN_FUSED=1; off by default, see profiles/round6/bn_fused_ab.jsonl).  Not in
+# deterministic mode, whose reductions keep one partial copy per contributing block.
+BN_FUSED = os.environ.get('MLC_BN_FUSED', '0') == '1'
+
+
+def _bn_fused_ok(C, ncopy):
+    G = C // 8
+    return (BN_FUSED and not _lib.DETERMINISTIC and C % 8 == 0 and 1 <= ncopy <= 64
+            and (G <= 32 or G % 32 == 0))
+
+
 def bn_fwd_apply(y, res, s1, s2, gamma, beta, save_mean, save_invstd, run_mean, run_var,
                  eps=1e-5, momentum=0.1, relu=True, out=None, scale=None, shift=None,
                  res_affine=None, apply=True):
@@ -430,6 +443,14 @@ def bn_fwd_apply(y, res, s1, s2, gamma, beta, save_mean, save_invstd, run_mean, 
         if scale is None:
             scale = torch.empty(2, C, device=y.device, dtype=torch.float32)
             scale, shift = scale[0], scale[1]
+        if apply and _bn_fused_ok(C, ncopy):
+            z = out if out is not None else torch.empty_like(y)
+            rs, rh = res_affine if res_affine is not None else (None, None)
+            _lib.call('mlc_bn_fwd_fused', _lib.ptr(y), _lib.ptr(res), _lib.ptr(z), _lib.ptr(s1), _lib.ptr(s2), ncopy,
+                      _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(save_mean), _lib.ptr(save_invstd), _lib.ptr(scale),
+                      _lib.ptr(shift), _lib.ptr(run_mean), _lib.ptr(run_var), _lib.ptr(rs), _lib.ptr(rh), rows, C,
+                      float(eps), float(momentum), int(relu), _lib.stream())
+            return z
         _lib.call('mlc_bn_finalize', _lib.ptr(s1), _lib.ptr(s2), ncopy, _lib.ptr(gamma), _lib.ptr(beta),
                   _lib.ptr(save_mean), _lib.ptr(save_invstd), _lib.ptr(scale), _lib.ptr(shift),
                   _lib.ptr(run_mean), _lib.ptr(run_var), rows, C, float(eps), float(momentum),
@@ -517,6 +538,16 @@ def bn_bwd(dz, z, y, mean, invstd, gamma, want_dres=False, dgamma=None, dbeta=No
         if not prereduced:
             _lib.call('mlc_bn_bwd_reduce', _lib.ptr(dz), _lib.ptr(z), _lib.ptr(y), _lib.ptr(mean),
                       _lib.ptr(sums), rows, C, _lib.stream())
+        ncopy = NSTAT
+        if _bn_fused_ok(C, ncopy):
+            dy = torch.empty_like(y)
+            dres = None
+            if want_dres:
+                dres = dz if prereduced else torch.empty_like(y)
+            _lib.call('mlc_bn_bwd_fused', _lib.ptr(dz), _lib.ptr(z), _lib.ptr(y), _lib.ptr(mean), _lib.ptr(sums),
+                      ncopy, _lib.ptr(invstd), _lib.ptr(gamma), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(dy),
+                      _lib.ptr(None if prereduced else dres), rows, C, _lib.stream())
+            return dy, dres
         _lib.call('mlc_bn_bwd_finalize', _lib.ptr(sums), _lib.ptr(invstd), _lib.ptr(gamma), _lib.ptr(coef),
                   _lib.ptr(dgamma), _lib.ptr(dbeta), rows, C, _lib.stream())
         dy = torch.empty_like(y)

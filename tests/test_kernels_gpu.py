@@ -185,10 +185,18 @@ def bn_unroll(request):
     lib.mlc_bn_get_set(0, old)
 
 
+@pytest.fixture(params=[True, False], ids=['bn-fused', 'bn-2pass'])
+def bn_fused(request, monkeypatch):
+    """The BN passes with the per-channel finalize folded into the apply launch
+    (bn_{fwd,bwd}_fused_kernel) and as separate finalize + apply launches."""
+    monkeypatch.setattr(Fn, 'BN_FUSED', request.param)
+    yield request.param
+
+
 @pytest.mark.parametrize('relu,res', [(True, True), (True, False), (False, False)])
 @pytest.mark.parametrize('C,shape', [(64, (4, 5, 3)), (256, (4, 5, 3)), (2048, (4, 5, 3)), (256, (4, 50, 31)),
-                                     (48, (4, 9, 7)), (768, (4, 50, 31))])   # channel groups not dividing 256
-def test_bn_fwd_bwd(relu, res, C, shape, bn_unroll):
+                                     (48, (4, 9, 7)), (768, (4, 50, 31)), (320, (2, 9, 7))])
+def test_bn_fwd_bwd(relu, res, C, shape, bn_unroll, bn_fused):
     rows_shape = (*shape, C)
     y = _bf(*rows_shape, scale=2.0, seed=7) + 0.5
     r = _bf(*rows_shape, seed=8) if res else None
@@ -217,6 +225,46 @@ def test_bn_fwd_bwd(relu, res, C, shape, bn_unroll):
             assert a is None
             continue
         assert rel_err(a, b) < 1e-2
+
+
+@pytest.mark.parametrize('C', [64, 512, 1024])
+def test_bn_fused_matches_two_pass_with_residual_affine(C, monkeypatch):
+    """Folded finalize + apply (one launch each way) gives the two-launch form's outputs, with
+    the downsample branch's BN folded in as the residual's affine and the prereduced
+    backward (sums from a dgrad epilogue)."""
+    rows_shape = (3, 11, 13, C)
+    y = (_bf(*rows_shape, scale=2.0, seed=21) + 0.5).to(DEV)
+    r = _bf(*rows_shape, seed=22).to(DEV)
+    g = torch.Generator().manual_seed(23)
+    gamma, beta = (torch.rand(C, generator=g) + 0.5).to(DEV), (torch.randn(C, generator=g) * 0.1).to(DEV)
+    rs, rh = (torch.rand(C, generator=g) + 0.5).to(DEV), (torch.randn(C, generator=g) * 0.1).to(DEV)
+    yf = y.float().reshape(-1, C)
+    s1, s2 = Fn.stat_buffers(C, DEV)
+    s1[:C], s2[:C] = yf.sum(0), (yf * yf).sum(0)
+    dz = _bf(*rows_shape, seed=24).to(DEV)
+
+    def run(fused):
+        monkeypatch.setattr(Fn, 'BN_FUSED', fused)
+        sm, si, rm, rv = (torch.zeros(C, device=DEV) for _ in range(4))
+        sc, sh = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        z = Fn.bn_fwd_apply(y, r, s1, s2, gamma, beta, sm, si, rm, rv, relu=True, scale=sc, shift=sh,
+                            res_affine=(rs, rh))
+        d = dz * (z > 0)
+        sums = torch.zeros(Fn.NSTAT * 2 * C, device=DEV)
+        df = d.float().reshape(-1, C)
+        sums[:C] = df.sum(0)
+        sums[C:2 * C] = (df * (yf - sm)).sum(0)
+        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        dy, dres = Fn.bn_bwd(d, None, y, sm, si, gamma, want_dres=True, dgamma=dg, dbeta=db, sums=sums,
+                             prereduced=True)
+        torch.cuda.synchronize()
+        return [z, sm, si, rm, rv, sc, sh, dy, dres, dg, db]
+
+    for a, b in zip(run(True), run(False)):
+        # fp32 statistics: summation order only; bf16 tensors: an fp32-ulp change of a
+        # coefficient may flip an element's bf16 rounding
+        tol = 1e-5 if a.dtype == torch.float32 else 5e-3
+        assert rel_err(a, b) < tol, (a.shape, a.dtype, rel_err(a, b))
 
 
 def test_maxpool():
