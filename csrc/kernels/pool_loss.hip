@@ -272,8 +272,8 @@ avgpool2d_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N, in
 }
 
 __global__ void __launch_bounds__(NT)
-avgpool2d_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx, int N, int H, int W, int C, int Ho,
-                     int Wo, int K, int S, int P, int cip) {
+avgpool2d_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ add, bf16* __restrict__ dx, int N, int H,
+                     int W, int C, int Ho, int Wo, int K, int S, int P, int cip) {
   const int G = C / 8;
   const long total = (long)N * H * W * G;
   for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
@@ -287,6 +287,7 @@ avgpool2d_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx, int N, 
     const int ho_lo = max(0, (h + P - K + S) / S), ho_hi = min(Ho - 1, (h + P) / S);
     const int wo_lo = max(0, (w + P - K + S) / S), wo_hi = min(Wo - 1, (w + P) / S);
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (add) unpack8(ldg16(add + i * 8), acc);      // another consumer's gradient of x
     for (int ho = ho_lo; ho <= ho_hi; ++ho) {
       if (h + P - ho * S >= K || h + P - ho * S < 0) continue;
       for (int wo = wo_lo; wo <= wo_hi; ++wo) {
@@ -440,10 +441,11 @@ MLC_EXPORT int mlc_avgpool2d_fwd(const bf16* x, bf16* y, int N, int H, int W, in
   return hipGetLastError();
 }
 
-MLC_EXPORT int mlc_avgpool2d_bwd(const bf16* dy, bf16* dx, int N, int H, int W, int C, int Ho, int Wo, int K, int S,
-                                 int P, int cip, hipStream_t st) {
+// dx = avg-pool backward of dy (+ add, the other consumers' gradient of x, when non-null)
+MLC_EXPORT int mlc_avgpool2d_bwd(const bf16* dy, const bf16* add, bf16* dx, int N, int H, int W, int C, int Ho,
+                                 int Wo, int K, int S, int P, int cip, hipStream_t st) {
   if (C % 8) return -1;
-  hipLaunchKernelGGL(avgpool2d_bwd_kernel, dim3(blocks_for((long)N * H * W * (C / 8))), dim3(NT), 0, st, dy, dx, N, H,
+  hipLaunchKernelGGL(avgpool2d_bwd_kernel, dim3(blocks_for((long)N * H * W * (C / 8))), dim3(NT), 0, st, dy, add, dx, N, H,
                      W, C, Ho, Wo, K, S, P, cip);
   return hipGetLastError();
 }

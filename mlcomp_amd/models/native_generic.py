@@ -44,7 +44,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from mlcomp_amd.ops import functional as Fn
-from mlcomp_amd.ops.glayers import (AdaptiveAvgPool, AvgPool, BilinearUp, BNAct, BNParams, ChannelGate, Conv3dAs2d, ConvBNAct, ConvParams,
+from mlcomp_amd.ops.glayers import (AdaptiveAvgPool, AvgPool, BilinearUp, GradAcc, BNAct, BNParams, ChannelGate, Conv3dAs2d, ConvBNAct, ConvParams,
                                     Frames, GlobalAvgPool, LinearAct, LinearParams, MaxPool, TemporalAs2d, UpCat, VolumePool)
 from mlcomp_amd.ops import gtransformer as GT
 from mlcomp_amd.ops.layers import NativeContext
@@ -822,6 +822,43 @@ class _Lowering:
                 object.__setattr__(sb, 'send_to', sa)
                 object.__setattr__(sa, 'grad_expected', True)
 
+    def _link_fanout(self):
+        """A value consumed (as their only / first input) by two or more sites that take an
+        addend in their backward kernels - conv sites (dgrad epilogue) and average pools -
+        and not already in a two-site hand-off: they share a :class:`GradAcc`, so the value's
+        gradient is summed inside those kernels in any backward order (Inception's branch
+        points: three convs and a pool per block); other users' gradients are still added by
+        autograd."""
+        mods = dict(self.gm.named_modules())
+        res_targets = {id(getattr(m, 'res_link', None)) for m in mods.values() if getattr(m, 'res_link', None) is not None}
+        for v in self.gm.graph.nodes:
+            members = []
+            for u in v.users:
+                s = mods.get(u.target) if u.op == 'call_module' else None
+                if not u.args or u.args[0] is not v or any(a is v for a in u.args[1:]):
+                    continue
+                if isinstance(s, ConvBNAct):
+                    if (s.grad_link is not None or s.grad_expected or id(s) in res_targets
+                            or s.acc is not None):
+                        members = None
+                        break
+                    members.append(s)
+                elif isinstance(s, AvgPool) and s.acc is None:
+                    members.append(s)
+            if not members or len(members) < 2:
+                continue
+            cps = {m.conv.Cip for m in members if isinstance(m, ConvBNAct)}
+            if any(isinstance(m, AvgPool) for m in members):
+                # the pool pads channels to a multiple of 8: the convs' input width says how many
+                cis = {m.conv.Ci for m in members if isinstance(m, ConvBNAct)}
+                c = self._channels(v) if not cis else (cis.pop() if len(cis) == 1 else None)
+                cps.add(None if c is None else -(-c // 8) * 8)
+            if len(cps) != 1 or None in cps:       # one NHWC layout for the running sum
+                continue
+            acc = GradAcc(v.name)
+            for m in members:
+                object.__setattr__(m, 'acc', acc)
+
     def _link_bn_backward(self):
         """A conv+BN site A (ReLU or no activation, batch statistics) whose output is used
         only as the input of a dense conv site B (and, at a residual block boundary, as the
@@ -977,6 +1014,7 @@ class _Lowering:
         self._link_residuals()
         self._link_dgrads()
         self._link_frames()
+        self._link_fanout()
         self._link_bn_backward()
         g.lint()
         self.gm.delete_all_unused_submodules()

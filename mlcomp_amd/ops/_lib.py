@@ -97,7 +97,7 @@ _SIGS = {
     'mlc_avgpool_fwd': [vp, vp, i32, i32, i32, vp],
     'mlc_avgpool_bwd': [vp, vp, i32, i32, i32, vp],
     'mlc_avgpool2d_fwd': [vp, vp] + [i32] * 10 + [vp],
-    'mlc_avgpool2d_bwd': [vp, vp] + [i32] * 10 + [vp],
+    'mlc_avgpool2d_bwd': [vp, vp, vp] + [i32] * 10 + [vp],
     'mlc_adaptive_avg_fwd': [vp, vp] + [i32] * 6 + [vp],
     'mlc_adaptive_avg_bwd': [vp, vp] + [i32] * 6 + [vp],
     'mlc_softmax_ce': [vp] * 5 + [i32, i32, i32, f32, f32, vp],

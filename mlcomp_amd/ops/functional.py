@@ -417,9 +417,10 @@ def stat_buffers(C, device):
 
 # finalize folded into the apply passes (batchnorm.hip bn_{fwd,bwd}_fused_kernel): one launch
 # per BatchNorm each way instead of a per-channel finalize kernel + the elementwise pass
-# (MLC_BN_FUSED=1; off by default, see profiles/round6/bn_fused_ab.jsonl).  Not in
-# deterministic mode, whose reductions keep one partial copy per contributing block.
-BN_FUSED = os.environ.get('MLC_BN_FUSED', '0') == '1'
+# (MLC_BN_FUSED=0: the two-launch form; ResNet-50 +0.9 %, 402 -> 302 dispatches per step,
+# profiles/round6/bn_fused_ab.jsonl).  Not in deterministic mode, whose reductions keep one
+# partial copy per contributing block.
+BN_FUSED = os.environ.get('MLC_BN_FUSED', '1') == '1'
 
 
 def _bn_fused_ok(C, ncopy):
@@ -756,18 +757,25 @@ def avgpool2d_fwd(x, k, s, p, count_include_pad=True):
     return yf.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
 
 
-def avgpool2d_bwd(dy, x_shape, k, s, p, count_include_pad=True):
+def avgpool2d_bwd(dy, x_shape, k, s, p, count_include_pad=True, addend=None):
+    """Input gradient of :func:`avgpool2d_fwd` (+ ``addend``, NHWC bf16 of ``x_shape``: the other
+    consumers' gradient of the pool's input, summed in the same pass)."""
     N, H, W, C = x_shape
     _, Ho, Wo, _ = dy.shape
+    if addend is not None:
+        assert tuple(addend.shape) == tuple(x_shape) and addend.is_contiguous(), (addend.shape, x_shape)
     if _cuda(dy):
         dx = torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
-        _lib.call('mlc_avgpool2d_bwd', _lib.ptr(dy.contiguous()), _lib.ptr(dx), N, H, W, C, Ho, Wo, k, s, p,
-                  int(count_include_pad), _lib.stream())
+        _lib.call('mlc_avgpool2d_bwd', _lib.ptr(dy.contiguous()), _lib.ptr(addend), _lib.ptr(dx), N, H, W, C, Ho,
+                  Wo, k, s, p, int(count_include_pad), _lib.stream())
         return dx
     with torch.enable_grad():             # called from autograd backward (grad mode off)
         xf = torch.zeros(N, C, H, W, requires_grad=True)
         F.avg_pool2d(xf, k, s, p, count_include_pad=count_include_pad).backward(_nchw(dy))
-    return xf.grad.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+    g = xf.grad.permute(0, 2, 3, 1)
+    if addend is not None:
+        g = g + addend.float()
+    return g.to(torch.bfloat16).contiguous()
 
 
 def adaptive_avg_fwd(x, Ho, Wo):

@@ -667,6 +667,31 @@ class LinearParams:
 
 
 # ---------------------------------------------------------------------------- sites
+class GradAcc:
+    """One activation's input gradient summed across its N consumer sites in their own
+    backward kernels, in whatever order autograd runs them (set by the lowering,
+    ``_link_fanout``: an Inception block input feeding three convs and an average pool).
+    Each consumer's backward passes the running sum as its kernel's addend (dgrad epilogue
+    / pool-backward) and hands its output on; the last one returns the total to autograd,
+    the others return no gradient - instead of autograd adding N gradients in N - 1 passes.
+    ``left`` counts the consumers' gradient-tracking forwards of this step."""
+
+    def __init__(self, name: str):
+        self.name, self.left, self.buf = name, 0, None
+
+    def enter(self, x):
+        if torch.is_grad_enabled() and isinstance(x, torch.Tensor) and x.requires_grad:
+            self.left += 1
+
+    def give(self, dx):
+        self.left -= 1
+        if self.left <= 0:
+            self.left, self.buf = 0, None
+            return dx
+        self.buf = dx
+        return None
+
+
 class Site(nn.Module):
     """A lowered call site: forward() runs the site's autograd Function.  Holds no
     nn.Parameters (the arena owns the weights)."""
@@ -674,6 +699,7 @@ class Site(nn.Module):
     def __init__(self, ctx: NativeContext):
         super().__init__()
         object.__setattr__(self, 'ctx', ctx)   # not a submodule / not in state_dict
+        object.__setattr__(self, 'acc', None)  # a GradAcc over its first input (the lowering)
 
     def _direct_bn_grads(self) -> bool:
         return bool(getattr(self.bn, 'single_site', False)) and bool(getattr(self.ctx, 'grad_prezeroed', False))
@@ -705,6 +731,8 @@ class _SiteFn(torch.autograd.Function):
 def _run(site, *inputs):
     anchor = site.ctx.anchor
     if torch.is_grad_enabled() and site.ctx.training:
+        if site.acc is not None:      # counted out here: inside Function.forward grad mode is off
+            site.acc.enter(inputs[0])
         return _SiteFn.apply(anchor, site, *inputs)
     with torch.no_grad():
         return site.fwd(*inputs)[0]
@@ -865,6 +893,8 @@ class ConvBNAct(Site):
                 c.b.grad.add_(dy.float().sum(dim=(0, 1, 2)))
         addend = self._pending                 # another site's gradient of our input
         object.__setattr__(self, '_pending', None)
+        if self.acc is not None:
+            addend = self.acc.buf              # the other consumers' running sum
         if self.grad_expected and needs[0] and addend is None:
             raise RuntimeError(f'{c.name}: the input-gradient hand-off of its sibling conv site did not arrive '
                                '(backward order differs from the one the lowering assumed)')
@@ -914,6 +944,8 @@ class ConvBNAct(Site):
         if dx is not None and self.grad_link is not None:
             object.__setattr__(self.grad_link, '_pending', dx)       # summed by the sibling's dgrad
             dx = None
+        if dx is not None and self.acc is not None:
+            dx = self.acc.give(dx)
         out = [from_nhwc(dx, c.Ci) if dx is not None else None]
         if has_res:
             if needs[1] and self.res_link is not None:
@@ -1234,8 +1266,11 @@ class AvgPool(Site):
 
     def bwd(self, dout, saved, xshape, needs):
         C = dout.shape[1]
-        dx = Fn.avgpool2d_bwd(to_nhwc(dout, xshape[-1]), xshape, self.k, self.s, self.p, self.cip)
-        return [from_nhwc(dx, C)]
+        addend = self.acc.buf if self.acc is not None else None
+        dx = Fn.avgpool2d_bwd(to_nhwc(dout, xshape[-1]), xshape, self.k, self.s, self.p, self.cip, addend=addend)
+        if self.acc is not None:
+            dx = self.acc.give(dx)
+        return [from_nhwc(dx, C) if dx is not None else None]
 
 
 class AdaptiveAvgPool(Site):

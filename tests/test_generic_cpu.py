@@ -864,3 +864,60 @@ def test_adaptive_avg_pool_sizes_lower_natively():
     for p in net.param_sets():
         gg = p.w.grad if hasattr(p, 'w') else p.gamma.grad
         assert _cos(gg, _torch_grad(p, ref)) > 0.98, p.name
+
+
+def test_branch_point_gradients_summed_in_the_consumers(monkeypatch):
+    """An Inception-style branch point (one activation feeding three convs and an average
+    pool) shares a GradAcc: the running sum of the input gradient passes through the
+    consumers' dgrad epilogues / pool backward in whatever order autograd runs them, and the
+    result equals the unlinked lowering's (autograd's adds) and fp32 autograd's direction."""
+    from mlcomp_amd.models.native_generic import _Lowering
+    from mlcomp_amd.ops.glayers import GradAcc
+
+    class Block(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.stem = nn.Sequential(nn.Conv2d(3, 16, 3, padding=1, bias=False), nn.BatchNorm2d(16), nn.ReLU())
+            self.b1 = nn.Sequential(nn.Conv2d(16, 8, 1, bias=False), nn.BatchNorm2d(8), nn.ReLU())
+            self.b2 = nn.Sequential(nn.Conv2d(16, 8, 1, bias=False), nn.BatchNorm2d(8), nn.ReLU(),
+                                    nn.Conv2d(8, 8, 3, padding=1, bias=False), nn.BatchNorm2d(8), nn.ReLU())
+            self.b3 = nn.Sequential(nn.Conv2d(16, 8, 3, padding=1, bias=False), nn.BatchNorm2d(8), nn.ReLU())
+            self.b4 = nn.Sequential(nn.AvgPool2d(3, 1, 1), nn.Conv2d(16, 8, 1, bias=False), nn.BatchNorm2d(8), nn.ReLU())
+            self.head = nn.Sequential(nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(32, 5))
+
+        def forward(self, x):
+            x = self.stem(x)
+            return self.head(torch.cat([self.b1(x), self.b2(x), self.b3(x), self.b4(x)], 1))
+
+    x = torch.randn(2, 3, 12, 12)
+    y = torch.randint(0, 5, (2,))
+
+    handed = []
+    give = GradAcc.give
+
+    def counting_give(self, dx):
+        r = give(self, dx)
+        handed.append(r is None)
+        return r
+
+    def run(linked):
+        torch.manual_seed(0)
+        if not linked:
+            monkeypatch.setattr(_Lowering, '_link_fanout', lambda self: None)
+        net = GenericNet(Block(), 'cpu')
+        monkeypatch.undo()
+        monkeypatch.setattr(GradAcc, 'give', counting_give)
+        accs = {id(m.acc) for m in net.train_gm.modules() if getattr(m, 'acc', None) is not None}
+        F.cross_entropy(net(x).float(), y).backward()
+        monkeypatch.undo()
+        return len(accs), [p.w.grad.clone() for p in net.param_sets() if hasattr(p, 'kind')]
+
+    n1, g1 = run(True)
+    # three of the four consumers hand their sum on, the last returns it to autograd
+    assert sorted(handed) == [False, True, True, True], handed
+    n0, g0 = run(False)
+    assert (n1, n0) == (1, 0)
+    # the same sum in another association: bf16 roundings of the partial sums differ
+    for a, b in zip(g1, g0):
+        assert _rel(a, b) < 3e-2 and _cos(a, b) > 0.999
+    assert GradAcc('t').give(torch.zeros(1)) is not None     # no forward counted: passes through
