@@ -396,8 +396,8 @@ chscale_fwd_kernel(const bf16* __restrict__ y, const bf16* __restrict__ g, const
 constexpr int CS_ROWS = 128;
 __global__ void __launch_bounds__(NT)
 chscale_bwd_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ y, const bf16* __restrict__ g,
-                   const bf16* __restrict__ z, bf16* __restrict__ dy, bf16* __restrict__ dres, float* __restrict__ dg,
-                   int HW, int G) {
+                   const bf16* __restrict__ z, const bf16* __restrict__ add, bf16* __restrict__ dy,
+                   bf16* __restrict__ dres, float* __restrict__ dg, int HW, int G) {
   __shared__ float part[NT * 8];
   const int n = blockIdx.y;
   const int CT = G < 64 ? G : 64, R = NT / CT;
@@ -443,6 +443,12 @@ chscale_bwd_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ y, co
         for (int e = 0; e < 8; ++e) {
           a[e] += d[e] * f[e];
           d[e] *= s[e];
+        }
+        if (add) {                      // the other consumers' gradient of y (GradAcc)
+          float q[8];
+          unpack8(ldg16(add + i * 8), q);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d[e] += q[e];
         }
         *reinterpret_cast<uint4*>(dy + i * 8) = pack8(d);
       }
@@ -621,13 +627,14 @@ MLC_EXPORT int mlc_chscale_fwd(const bf16* y, const bf16* g, const bf16* res, bf
   return hipGetLastError();
 }
 
-// dg: N*C fp32, zeroed by the caller; z / dres optional (ReLU mask, residual gradient)
-MLC_EXPORT int mlc_chscale_bwd(const bf16* dout, const bf16* y, const bf16* g, const bf16* z, bf16* dy, bf16* dres,
-                               float* dg, int N, int HW, int C, hipStream_t st) {
+// dg: N*C fp32, zeroed by the caller; z / dres optional (ReLU mask, residual gradient);
+// add optional (summed into dy)
+MLC_EXPORT int mlc_chscale_bwd(const bf16* dout, const bf16* y, const bf16* g, const bf16* z, const bf16* add,
+                               bf16* dy, bf16* dres, float* dg, int N, int HW, int C, hipStream_t st) {
   if (C % 8 || N > 65535) return -1;
   const int G = C / 8, CT = G < 64 ? G : 64;
   hipLaunchKernelGGL(chscale_bwd_kernel, dim3((HW + CS_ROWS - 1) / CS_ROWS, N, (G + CT - 1) / CT), dim3(NT), 0, st,
-                     dout, y, g, z, dy, dres, dg, HW, G);
+                     dout, y, g, z, add, dy, dres, dg, HW, G);
   return hipGetLastError();
 }
 

@@ -123,17 +123,25 @@ avgpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int HW, int
 }
 
 __global__ void __launch_bounds__(NT)
-avgpool_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx, int N, int HW, int C) {
+avgpool_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ add, bf16* __restrict__ dx, int N, int HW,
+                   int C) {
   const int G = C >> 3;
   const long total = (long)N * HW * G;
   const float inv = 1.f / (float)HW;
   for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
     const int cg = (int)(i % G);
     const long n = i / G / HW;
+    const uint4 av = add ? ldg16(add + i * 8) : make_uint4(0u, 0u, 0u, 0u);
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(dy + n * C + cg * 8), f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] *= inv;
+    if (add) {                          // the other consumers' gradient of x (GradAcc)
+      float q[8];
+      unpack8(av, q);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += q[j];
+    }
     *reinterpret_cast<uint4*>(dx + i * 8) = pack8(f);
   }
 }
@@ -400,10 +408,10 @@ MLC_EXPORT int mlc_avgpool_fwd(const bf16* x, bf16* y, int N, int HW, int C, hip
   return hipGetLastError();
 }
 
-MLC_EXPORT int mlc_avgpool_bwd(const bf16* dy, bf16* dx, int N, int HW, int C, hipStream_t st) {
+MLC_EXPORT int mlc_avgpool_bwd(const bf16* dy, const bf16* add, bf16* dx, int N, int HW, int C, hipStream_t st) {
   if (C % 8) return -1;
   hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(blocks_for((long)N * HW * (C / 8))), dim3(NT), 0, st,
-                     dy, dx, N, HW, C);
+                     dy, add, dx, N, HW, C);
   return hipGetLastError();
 }
 

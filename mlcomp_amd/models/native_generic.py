@@ -44,8 +44,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from mlcomp_amd.ops import functional as Fn
-from mlcomp_amd.ops.glayers import (AdaptiveAvgPool, AvgPool, BilinearUp, GradAcc, BNAct, BNParams, ChannelGate, Conv3dAs2d, ConvBNAct, ConvParams,
-                                    Frames, GlobalAvgPool, LinearAct, LinearParams, MaxPool, TemporalAs2d, UpCat, VolumePool)
+from mlcomp_amd.ops.glayers import (AdaptiveAvgPool, AvgPool, BilinearUp, BNAct, BNParams, ChannelGate, Conv3dAs2d,
+                                    ConvBNAct, ConvParams, Frames, GlobalAvgPool, GradAcc, LinearAct, LinearParams,
+                                    MaxPool, TemporalAs2d, UpCat, VolumePool)
 from mlcomp_amd.ops import gtransformer as GT
 from mlcomp_amd.ops.layers import NativeContext
 from mlcomp_amd.train.native_spec import NativeUnsupported
@@ -824,10 +825,11 @@ class _Lowering:
 
     def _link_fanout(self):
         """A value consumed (as their only / first input) by two or more sites that take an
-        addend in their backward kernels - conv sites (dgrad epilogue) and average pools -
-        and not already in a two-site hand-off: they share a :class:`GradAcc`, so the value's
-        gradient is summed inside those kernels in any backward order (Inception's branch
-        points: three convs and a pool per block); other users' gradients are still added by
+        addend in their backward kernels - conv sites (dgrad epilogue), average / global
+        pools, squeeze-excitation gates - and not already in a two-site hand-off: they share
+        a :class:`GradAcc`, so the value's gradient is summed inside those kernels in any
+        backward order (Inception's branch points: three convs and a pool per block; an SE
+        block's input: its pool and its gate); other users' gradients are still added by
         autograd."""
         mods = dict(self.gm.named_modules())
         res_targets = {id(getattr(m, 'res_link', None)) for m in mods.values() if getattr(m, 'res_link', None) is not None}
@@ -843,12 +845,12 @@ class _Lowering:
                         members = None
                         break
                     members.append(s)
-                elif isinstance(s, AvgPool) and s.acc is None:
+                elif isinstance(s, (AvgPool, GlobalAvgPool, ChannelGate)) and s.acc is None:
                     members.append(s)
             if not members or len(members) < 2:
                 continue
             cps = {m.conv.Cip for m in members if isinstance(m, ConvBNAct)}
-            if any(isinstance(m, AvgPool) for m in members):
+            if any(isinstance(m, (AvgPool, GlobalAvgPool, ChannelGate)) for m in members):
                 # the pool pads channels to a multiple of 8: the convs' input width says how many
                 cis = {m.conv.Ci for m in members if isinstance(m, ConvBNAct)}
                 c = self._channels(v) if not cis else (cis.pop() if len(cis) == 1 else None)

@@ -95,7 +95,7 @@ _SIGS = {
     'mlc_stem_s2d': [vp, vp] + [i32] * 5 + [vp],
     'mlc_stem_conv_fwd': [vp] * 5 + [i32] * 3 + [vp],
     'mlc_avgpool_fwd': [vp, vp, i32, i32, i32, vp],
-    'mlc_avgpool_bwd': [vp, vp, i32, i32, i32, vp],
+    'mlc_avgpool_bwd': [vp, vp, vp, i32, i32, i32, vp],
     'mlc_avgpool2d_fwd': [vp, vp] + [i32] * 10 + [vp],
     'mlc_avgpool2d_bwd': [vp, vp, vp] + [i32] * 10 + [vp],
     'mlc_adaptive_avg_fwd': [vp, vp] + [i32] * 6 + [vp],
@@ -124,7 +124,7 @@ _SIGS = {
     'mlc_act_fwd': [vp, vp, i64, i32, f32, vp],
     'mlc_act_bwd': [vp] * 4 + [i64, i32, f32, vp],
     'mlc_chscale_fwd': [vp] * 4 + [i32, i64, i32, i32, vp],
-    'mlc_chscale_bwd': [vp] * 7 + [i32] * 3 + [vp],
+    'mlc_chscale_bwd': [vp] * 8 + [i32] * 3 + [vp],
     'mlc_conv_fwd_ex': [vp] * 4 + [i32] * 13 + [vp],
     'mlc_conv_wgrad_bias': [vp] * 4 + [i32] * 13 + [vp, i64, vp],
     'mlc_temporal_unfold': [vp, vp] + [i32] * 9 + [vp],

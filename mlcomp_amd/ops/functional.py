@@ -826,13 +826,19 @@ def avgpool_fwd(x):
     return x.float().mean(dim=(1, 2)).to(torch.bfloat16)
 
 
-def avgpool_bwd(dy, x_shape):
+def avgpool_bwd(dy, x_shape, addend=None):
+    """Input gradient of the global average pool (+ ``addend``, NHWC bf16 of ``x_shape``)."""
     N, H, W, C = x_shape
+    if addend is not None:
+        assert tuple(addend.shape) == tuple(x_shape) and addend.is_contiguous(), (addend.shape, x_shape)
     if _cuda(dy):
         dx = torch.empty(N, H, W, C, device=dy.device, dtype=torch.bfloat16)
-        _lib.call('mlc_avgpool_bwd', _lib.ptr(dy), _lib.ptr(dx), N, H * W, C, _lib.stream())
+        _lib.call('mlc_avgpool_bwd', _lib.ptr(dy), _lib.ptr(addend), _lib.ptr(dx), N, H * W, C, _lib.stream())
         return dx
-    return (dy.float()[:, None, None, :] / (H * W)).expand(N, H, W, C).to(torch.bfloat16).contiguous()
+    g = dy.float()[:, None, None, :] / (H * W)
+    if addend is not None:
+        g = g + addend.float()
+    return g.expand(N, H, W, C).to(torch.bfloat16).contiguous()
 
 
 # ---------------------------------------------------------------- linear
@@ -1411,25 +1417,29 @@ def chscale_fwd(y, g, res=None, relu=False):
     return a.to(torch.bfloat16)
 
 
-def chscale_bwd(dout, y, g, z=None, want_dres=False):
+def chscale_bwd(dout, y, g, z=None, want_dres=False, addend=None):
     """(dy, dg, dres) of :func:`chscale_fwd`: the ReLU mask from its output ``z`` (if it had a
     ReLU), dres = the masked gradient (if it had a residual), dy = that * g, dg [N, C] (fp32)
     = its sum over pixels times y - one pass (float atomics per channel; deterministic mode
     sums in torch)."""
     N, H, W, C = y.shape
+    if addend is not None:
+        assert tuple(addend.shape) == tuple(y.shape) and addend.is_contiguous(), (addend.shape, y.shape)
     if _cuda(y) and C % 8 == 0 and not _lib.DETERMINISTIC:
         dy = torch.empty_like(y)
         dres = torch.empty_like(y) if want_dres else None
         dg = torch.zeros(N, C, device=y.device, dtype=torch.float32)
         _lib.call('mlc_chscale_bwd', _lib.ptr(dout.contiguous()), _lib.ptr(y), _lib.ptr(g.contiguous()), _lib.ptr(z),
-                  _lib.ptr(dy), _lib.ptr(dres), _lib.ptr(dg), N, H * W, C, _lib.stream())
+                  _lib.ptr(addend), _lib.ptr(dy), _lib.ptr(dres), _lib.ptr(dg), N, H * W, C, _lib.stream())
         return dy, dg, dres
     d = dout.float()
     if z is not None:
         d = d * (z.float() > 0)
     dres = d.to(torch.bfloat16) if want_dres else None
-    dy = (d * g.float().view(N, 1, 1, C)).to(torch.bfloat16)
-    return dy, (d * y.float()).sum((1, 2)), dres
+    dyf = d * g.float().view(N, 1, 1, C)
+    if addend is not None:
+        dyf = dyf + addend.float()
+    return dyf.to(torch.bfloat16), (d * y.float()).sum((1, 2)), dres
 
 
 def act_bwd(dy, x, y, act, alpha=0.0):

@@ -1188,10 +1188,13 @@ class ChannelGate(Site):
     def bwd(self, dout, saved, keep, needs):
         yn, gn, z = saved
         C, gdt, has_res = keep
+        addend = self.acc.buf if self.acc is not None and needs[0] else None
         dy, dg, dres = Fn.chscale_bwd(to_nhwc(dout, yn.shape[-1]), yn, gn, z if self.relu else None,
-                                      want_dres=has_res and needs[2])
+                                      want_dres=has_res and needs[2], addend=addend)
+        if self.acc is not None and needs[0]:
+            dy = self.acc.give(dy)
         N = yn.shape[0]
-        out = [from_nhwc(dy, C) if needs[0] else None,
+        out = [from_nhwc(dy, C) if needs[0] and dy is not None else None,
                dg[:, :C].to(gdt).reshape(N, C, 1, 1) if needs[1] else None]
         if has_res:
             out.append(from_nhwc(dres, C) if needs[2] else None)
@@ -1313,8 +1316,11 @@ class GlobalAvgPool(Site):
         d = dout.reshape(N, C).to(torch.bfloat16)
         if Cp != C:
             d = torch.nn.functional.pad(d, (0, Cp - C))
-        dx = Fn.avgpool_bwd(d.contiguous(), xshape)
-        return [from_nhwc(dx, C)]
+        addend = self.acc.buf if self.acc is not None else None
+        dx = Fn.avgpool_bwd(d.contiguous(), xshape, addend=addend)
+        if self.acc is not None:
+            dx = self.acc.give(dx)
+        return [from_nhwc(dx, C) if dx is not None else None]
 
 
 class VolumePool(nn.Module):

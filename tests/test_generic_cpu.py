@@ -921,3 +921,51 @@ def test_branch_point_gradients_summed_in_the_consumers(monkeypatch):
     for a, b in zip(g1, g0):
         assert _rel(a, b) < 3e-2 and _cos(a, b) > 0.999
     assert GradAcc('t').give(torch.zeros(1)) is not None     # no forward counted: passes through
+
+
+def test_se_block_input_gradient_summed_in_pool_and_gate(monkeypatch):
+    """A squeeze-excitation block's input feeds its global pool and its gate multiply: the
+    pool backward and the gate backward kernels share a GradAcc (no autograd add), with the
+    gradients of the unlinked lowering."""
+    from mlcomp_amd.models.native_generic import _Lowering
+    from mlcomp_amd.ops.glayers import GradAcc
+
+    class SE(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.c = nn.Sequential(nn.Conv2d(3, 16, 3, padding=1, bias=False), nn.BatchNorm2d(16), nn.SiLU())
+            self.g = nn.Sequential(nn.AdaptiveAvgPool2d(1), nn.Conv2d(16, 4, 1), nn.SiLU(), nn.Conv2d(4, 16, 1),
+                                   nn.Sigmoid())
+            self.h = nn.Sequential(nn.Conv2d(16, 8, 1, bias=False), nn.BatchNorm2d(8), nn.AdaptiveAvgPool2d(1),
+                                   nn.Flatten(), nn.Linear(8, 5))
+
+        def forward(self, x):
+            y = self.c(x)
+            return self.h(y * self.g(y))
+
+    x = torch.randn(2, 3, 10, 10)
+    t = torch.randint(0, 5, (2,))
+    handed = []
+    give = GradAcc.give
+
+    def counting_give(self, dx):
+        r = give(self, dx)
+        handed.append(r is None)
+        return r
+
+    def run(linked):
+        torch.manual_seed(0)
+        if not linked:
+            monkeypatch.setattr(_Lowering, '_link_fanout', lambda self: None)
+        net = GenericNet(SE(), 'cpu')
+        monkeypatch.undo()
+        monkeypatch.setattr(GradAcc, 'give', counting_give)
+        F.cross_entropy(net(x).float(), t).backward()
+        monkeypatch.undo()
+        return [p.w.grad.clone() for p in net.param_sets() if hasattr(p, 'kind')]
+
+    g1 = run(True)
+    assert sorted(handed) == [False, True], handed
+    g0 = run(False)
+    for a, b in zip(g1, g0):
+        assert _rel(a, b) < 3e-2 and _cos(a, b) > 0.999
