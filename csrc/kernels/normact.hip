@@ -129,6 +129,34 @@ stats_kernel(const bf16* __restrict__ x, float* __restrict__ sum, float* __restr
   }
 }
 
+// z chunk i = act(y*scale + shift [* row scale] [+ res*rscale + rshift]); y and res loads
+// issued together (one round trip per chunk)
+template <int ACT>
+__device__ __forceinline__ void apply_chunk(const bf16* __restrict__ y, const bf16* __restrict__ res,
+                                            bf16* __restrict__ z, long i, int G, const Ch& c, int act, float alpha,
+                                            const RowScale& rsc) {
+  const uint4 yv = ldg16(y + i * 8);
+  const uint4 rv = res ? ldg16(res + i * 8) : make_uint4(0u, 0u, 0u, 0u);
+  float f[8];
+  unpack8(yv, f);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = f[j] * c.sc[j] + c.sh[j];
+  if (rsc.s) {
+    const float m = rsc.s[(i / G) / rsc.hw];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] *= m;
+  }
+  if (res) {
+    float r[8];
+    unpack8(rv, r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] += r[j] * c.rs[j] + c.rh[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = act_f(f[j], act, alpha);
+  *reinterpret_cast<uint4*>(z + i * 8) = pack8(f);
+}
+
 // The elementwise passes are instantiated per activation code (ACT = 0..10: the activation
 // folds to straight-line code, so the loop keeps its loads in flight; a run-time code made
 // the switch of act_f / act_df a per-element branch, which cost EfficientNet's SiLU passes
@@ -146,26 +174,78 @@ apply_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf16* __r
   Ch c;
   load_ch(c, scale, shift, rscale, rshift, c0);
   const long total = rows * G;
-  for (long i = gtid; i < total; i += stride) {
-    float f[8];
-    unpack8(ldg16(y + i * 8), f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = f[j] * c.sc[j] + c.sh[j];
-    if (rsc.s) {
-      const float m = rsc.s[(i / G) / rsc.hw];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] *= m;
+  for (long i = gtid; i < total; i += stride)
+    apply_chunk<ACT>(y, res, z, i, G, c, act, alpha, rsc);
+}
+
+// the fused finalize of batchnorm.hip (bn_fwd_fused_kernel) for the generic engine: each block
+// reduces the conv epilogue's partial statistic copies for its slice of <= 32 channel groups
+// into LDS (scale, shift), row-part-0 blocks publish mean / invstd / scale / shift and the
+// running statistics, then the apply loop over the slice's rows
+constexpr int FG = 32;
+
+template <int ACT>
+__global__ void __launch_bounds__(NT)
+apply_fused_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf16* __restrict__ z,
+                   const float* __restrict__ sum, const float* __restrict__ sumsq, int ncopy,
+                   const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ mean_out,
+                   float* __restrict__ invstd_out, float* __restrict__ scale_out, float* __restrict__ shift_out,
+                   float* __restrict__ run_mean, float* __restrict__ run_var, const float* __restrict__ rscale,
+                   const float* __restrict__ rshift, long rows, int C, float eps, float momentum, int act_,
+                   float alpha, RowScale rsc) {
+  const int act = ACT >= 0 ? ACT : act_;
+  __shared__ float red[2][NT], lsc[FG * 8], lsh[FG * 8];
+  const int G = C >> 3;
+  const int gb = G < FG ? G : FG, nslices = G / gb;
+  const int slice = blockIdx.x % nslices, part = blockIdx.x / nslices, nparts = gridDim.x / nslices;
+  const int t = threadIdx.x, nch = gb * 8, c0 = slice * nch;
+  {
+    const int P = NT / nch, p = t / nch, cl = t % nch;
+    float a = 0.f, b = 0.f;
+    if (p < P) {
+#pragma unroll 16
+      for (int k = p; k < ncopy; k += P) { a += sum[(long)k * C + c0 + cl]; b += sumsq[(long)k * C + c0 + cl]; }
     }
-    if (res) {
-      float r[8];
-      unpack8(ldg16(res + i * 8), r);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += r[j] * c.rs[j] + c.rh[j];
+    red[0][t] = a;
+    red[1][t] = b;
+    __syncthreads();
+    if (t < nch) {
+      for (int q = 1; q < P; ++q) { a += red[0][q * nch + t]; b += red[1][q * nch + t]; }
+      const int ch = c0 + t;
+      const float inv_count = 1.f / (float)rows;
+      const float mean = a * inv_count;
+      const float var = fmaxf(b * inv_count - mean * mean, 0.f);
+      const float inv = rsqrtf(var + eps);
+      const float g = gamma[ch] * inv, h = beta[ch] - mean * g;
+      lsc[t] = g;
+      lsh[t] = h;
+      if (part == 0) {
+        mean_out[ch] = mean;
+        invstd_out[ch] = inv;
+        scale_out[ch] = g;
+        shift_out[ch] = h;
+        if (run_mean) {
+          const float unbiased = rows > 1 ? var * (float)rows / (float)(rows - 1) : var;
+          run_mean[ch] = (1.f - momentum) * run_mean[ch] + momentum * mean;
+          run_var[ch] = (1.f - momentum) * run_var[ch] + momentum * unbiased;
+        }
+      }
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = act_f(f[j], act, alpha);
-    *reinterpret_cast<uint4*>(z + i * 8) = pack8(f);
+    __syncthreads();
   }
+  const int rpi = NT / gb;
+  if (t >= rpi * gb) return;
+  const int gl = t % gb, cg = slice * gb + gl;
+  Ch c;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    c.sc[j] = lsc[gl * 8 + j];
+    c.sh[j] = lsh[gl * 8 + j];
+    c.rs[j] = rscale ? rscale[cg * 8 + j] : 1.f;
+    c.rh[j] = rscale ? rshift[cg * 8 + j] : 0.f;
+  }
+  for (long r = (long)part * rpi + t / gb; r < rows; r += (long)nparts * rpi)
+    apply_chunk<ACT>(y, res, z, r * G + cg, G, c, act, alpha, rsc);
 }
 
 // dU of one chunk: dz * act'(a), a recomputed from y (and res) with the forward's affine
@@ -554,6 +634,29 @@ MLC_EXPORT int mlc_bnact_apply(const bf16* y, const bf16* res, bf16* z, const fl
   const RowScale rsc{row_scale, hw};
   NA_LAUNCH(apply_kernel, grid_for(rows, C, apply_cap()), st, act, y, res, z, scale, shift, rscale, rshift, rows, C, act,
             alpha, rsc);
+  return hipGetLastError();
+}
+
+// finalize (from the conv epilogue's ncopy partial statistic copies) + apply in one launch;
+// -1 when the shape does not fit (the caller then runs mlc_bn_finalize + mlc_bnact_apply)
+MLC_EXPORT int mlc_bnact_fused(const bf16* y, const bf16* res, bf16* z, const float* sum, const float* sumsq,
+                               int ncopy, const float* gamma, const float* beta, float* mean, float* invstd,
+                               float* scale, float* shift, float* run_mean, float* run_var, const float* rscale,
+                               const float* rshift, long rows, int C, float eps, float momentum, int act, float alpha,
+                               const float* row_scale, long hw, hipStream_t st) {
+  const int G = C >> 3;
+  if (C % 8 || (rscale && !rshift) || (row_scale && (act != 0 || hw < 1)) || rows < 1 || ncopy < 1 || ncopy > 64 ||
+      !(G <= FG || G % FG == 0))
+    return -1;
+  const int gb = G < FG ? G : FG, nslices = G / gb, rpi = NT / gb;
+  long parts = (rows + (long)rpi * 4 - 1) / ((long)rpi * 4);
+  long cap = apply_cap() / nslices;
+  if (cap < 1) cap = 1;
+  if (parts > cap) parts = cap;
+  if (parts < 1) parts = 1;
+  const RowScale rsc{row_scale, hw};
+  NA_LAUNCH(apply_fused_kernel, parts * nslices, st, act, y, res, z, sum, sumsq, ncopy, gamma, beta, mean, invstd,
+            scale, shift, run_mean, run_var, rscale, rshift, rows, C, eps, momentum, act, alpha, rsc);
   return hipGetLastError();
 }
 

@@ -1328,6 +1328,25 @@ def bnact_apply(y, res, scale, shift, act=0, alpha=0.0, res_affine=None, row_sca
     return act_ref(a, act, alpha).to(torch.bfloat16)
 
 
+def bnact_fused(y, res, s1, s2, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, eps, momentum, act=0,
+                alpha=0.0, res_affine=None, row_scale=None):
+    """:func:`bn_finalize` + :func:`bnact_apply` in one launch (normact.hip apply_fused_kernel):
+    fills mean / invstd / scale / shift (and the running statistics) from the partial copies
+    ``s1`` / ``s2`` and returns z; None when the shape does not fit (use the two calls)."""
+    C = y.shape[-1]
+    ncopy = s1.numel() // C
+    if not (_cuda(y) and _bn_fused_ok(C, ncopy)):
+        return None
+    rows = y.numel() // C
+    z = torch.empty_like(y)
+    rs, rh = res_affine if res_affine is not None else (None, None)
+    _lib.call('mlc_bnact_fused', _lib.ptr(y), _lib.ptr(res), _lib.ptr(z), _lib.ptr(s1), _lib.ptr(s2), ncopy,
+              _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(mean), _lib.ptr(invstd), _lib.ptr(scale), _lib.ptr(shift),
+              _lib.ptr(run_mean), _lib.ptr(run_var), _lib.ptr(rs), _lib.ptr(rh), rows, C, float(eps), float(momentum),
+              int(act), float(alpha), _lib.ptr(row_scale), rows // y.shape[0], _lib.stream())
+    return z
+
+
 def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0, dgamma=None, dbeta=None,
               sums=None, coef=None, want_dres=False, res_affine=None, row_scale=None):
     """Backward of z = act(BN(y) [* row_scale[n]] [+ res (*rscale + rshift)]) with the forward's

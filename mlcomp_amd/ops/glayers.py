@@ -628,6 +628,24 @@ class BNParams:
             mean.copy_(self.run_mean)
         return scale, shift, mean, inv
 
+    def finalize_apply(self, s1, s2, y, res, act, alpha, res_affine=None, row_scale=None):
+        """:meth:`finalize` and the apply pass in one launch (Fn.bnact_fused) for batch
+        statistics: (z, scale, shift, mean, invstd), or None when it does not apply."""
+        if s1 is None or not self.batch_stats():
+            return None
+        st = torch.empty(4, self.Cp, device=s1.device, dtype=torch.float32)
+        scale, shift, mean, inv = st[0], st[1], st[2], st[3]
+        upd = self.ctx.training and self.track
+        mom = self.momentum if self.momentum is not None else 0.1
+        z = Fn.bnact_fused(y, res, s1, s2, self.gamma.master, self.beta.master, mean, inv, scale, shift,
+                           self.run_mean if upd else None, self.run_var if upd else None, self.eps, mom, act, alpha,
+                           res_affine=res_affine, row_scale=row_scale)
+        if z is None:
+            return None
+        if upd:
+            self.batches = getattr(self, 'batches', 0) + 1
+        return z, scale, shift, mean, inv
+
     def mark_ready(self):
         self.ctx.arena.mark_ready(self.gamma)
         self.ctx.arena.mark_ready(self.beta)
@@ -813,8 +831,21 @@ class ConvBNAct(Site):
                 stats = (st[:n], st[n:])
             y = c.fwd(xn, stats)
             rows = y.numel() // y.shape[-1]
-            scale, shift, mean, inv = bn.finalize(stats[0] if stats else None, stats[1] if stats else None, rows)
             rsh = None
+            rsc = mask.reshape(-1).float() / self.drop_keep if mask is not None else None
+            if not self.pool3 and not self.bn_folded and stats is not None:
+                # one launch: finalize folded into the apply pass (Fn.BN_FUSED)
+                if self.res_bn is not None and rn is not None:
+                    rsh = self.res_bn._fold
+                fused = bn.finalize_apply(stats[0], stats[1], y, rn, self.act, self.alpha, res_affine=rsh,
+                                          row_scale=rsc)
+                if fused is not None:
+                    if rsh is not None:
+                        object.__setattr__(self.res_bn, '_fold', None)
+                    z, scale, shift, mean, inv = fused
+                    return self._bn_out(xn, y, z, rn, scale, shift, mean, inv, rsh, rsc, stats)
+                rsh = None
+            scale, shift, mean, inv = bn.finalize(stats[0] if stats else None, stats[1] if stats else None, rows)
             if self.pool3:
                 out, idx = Fn.stem_pool_fwd(y, scale, shift)
                 return from_nhwc(out, c.Co), [xn, y, idx, y, scale, shift, mean, inv], False
@@ -825,19 +856,8 @@ class ConvBNAct(Site):
                 if self.res_bn is not None and rn is not None:
                     rsh = self.res_bn._fold
                     object.__setattr__(self.res_bn, '_fold', None)
-                rsc = None
-                if mask is not None:
-                    rsc = mask.reshape(-1).float() / self.drop_keep
                 z = Fn.bnact_apply(y, rn, scale, shift, self.act, self.alpha, res_affine=rsh, row_scale=rsc)
-            saved = [xn, y, z, rn if rn is not None else y, scale, shift, mean, inv]
-            if rsh is not None:
-                saved += list(rsh)
-            if mask is not None:
-                saved.append(rsc)
-            if self.bn_prereduced and stats is not None and self.ctx.training:
-                object.__setattr__(self, '_bn_stash', (y, z, mean))   # read by the linked dgrad
-                object.__setattr__(self, '_bn_done', False)
-            return from_nhwc(z, c.Co), saved, rn is not None
+            return self._bn_out(xn, y, z, rn, scale, shift, mean, inv, rsh, rsc, stats)
         y = c.fwd(xn, None, self.epi_act)        # dense: bias (+ ReLU) in the GEMM epilogue
         if c.b is not None and c.kind != 'dense':
             y = (y.float() + c.b.master).to(torch.bfloat16)
@@ -845,6 +865,17 @@ class ConvBNAct(Site):
         z = Fn.act_fwd(a, self.act, self.alpha) if (self.act and not self.epi_act) else a
         # saved: input, pre-activation (the ReLU output when the epilogue applied it), output
         return from_nhwc(z, c.Co), [xn, a, z], rn is not None
+
+    def _bn_out(self, xn, y, z, rn, scale, shift, mean, inv, rsh, rsc, stats):
+        saved = [xn, y, z, rn if rn is not None else y, scale, shift, mean, inv]
+        if rsh is not None:
+            saved += list(rsh)
+        if rsc is not None:
+            saved.append(rsc)
+        if self.bn_prereduced and stats is not None and self.ctx.training:
+            object.__setattr__(self, '_bn_stash', (y, z, mean))   # read by the linked dgrad
+            object.__setattr__(self, '_bn_done', False)
+        return from_nhwc(z, self.conv.Co), saved, rn is not None
 
     def bwd(self, dout, saved, has_res, needs):
         c, bn = self.conv, self.bn

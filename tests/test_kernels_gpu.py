@@ -777,3 +777,36 @@ def test_adaptive_avg_pool_matches_fp32(H, W, Ho, Wo):
     torch.cuda.synchronize()
     assert (got.float().cpu() - want.detach().permute(0, 2, 3, 1)).abs().max() <= 8e-3 * want.abs().max()
     assert (dx.float().cpu() - xr.grad.permute(0, 2, 3, 1)).abs().max() <= 8e-3 * xr.grad.abs().max()
+
+
+@pytest.mark.parametrize('act,res,rowscale', [(1, True, False), (3, False, False), (0, True, True), (8, False, False)])
+@pytest.mark.parametrize('C', [48, 256, 1024])
+def test_bnact_fused_matches_finalize_then_apply(act, res, rowscale, C):
+    """normact.hip apply_fused_kernel (the generic engine's BN finalize folded into its apply
+    pass) gives the outputs of mlc_bn_finalize + mlc_bnact_apply: z, the per-channel
+    mean / invstd / scale / shift and the running statistics."""
+    N, HW = 3, 37
+    y = (_bf(N, HW, 1, C, scale=2.0, seed=41) + 0.5).to(DEV)
+    r = _bf(N, HW, 1, C, seed=42).to(DEV) if res else None
+    g = torch.Generator().manual_seed(43)
+    gamma, beta = (torch.rand(C, generator=g) + 0.5).to(DEV), (torch.randn(C, generator=g) * 0.1).to(DEV)
+    rsc = (torch.rand(N, generator=g) + 0.5).to(DEV) if rowscale else None
+    yf = y.float().reshape(-1, C)
+    s1, s2 = Fn.stat_buffers(C, DEV)
+    s1[:C], s2[:C] = yf.sum(0), (yf * yf).sum(0)
+    outs = []
+    for fused in (True, False):
+        st = torch.zeros(4, C, device=DEV)
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        if fused:
+            z = Fn.bnact_fused(y, r, s1, s2, gamma, beta, st[2], st[3], st[0], st[1], rm, rv, 1e-5, 0.1, act,
+                               0.0, row_scale=rsc)
+            assert z is not None
+        else:
+            Fn.bn_finalize(s1, s2, N * HW, gamma, beta, st[2], st[3], st[0], st[1], rm, rv, 1e-5, 0.1)
+            z = Fn.bnact_apply(y, r, st[0], st[1], act, 0.0, row_scale=rsc)
+        torch.cuda.synchronize()
+        outs.append([z, st, rm, rv])
+    for a, b in zip(*outs):
+        tol = 1e-5 if a.dtype == torch.float32 else 5e-3
+        assert rel_err(a, b) < tol, (a.dtype, rel_err(a, b))
