@@ -82,7 +82,7 @@ __device__ __forceinline__ void load_ch(Ch& c, const float* scale, const float* 
 
 __global__ void __launch_bounds__(NT)
 stats_kernel(const bf16* __restrict__ x, float* __restrict__ sum, float* __restrict__ sumsq, long rows, int C,
-             int ncopy) {
+             int ncopy, int ld) {
   __shared__ float rb[NT][17];
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
@@ -123,8 +123,8 @@ stats_kernel(const bf16* __restrict__ x, float* __restrict__ sum, float* __restr
     const long slot = blockIdx.x % ncopy;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      atomicAdd(sum + slot * C + cg * 8 + e, a[e]);
-      atomicAdd(sumsq + slot * C + cg * 8 + e, b[e]);
+      atomicAdd(sum + slot * ld + cg * 8 + e, a[e]);
+      atomicAdd(sumsq + slot * ld + cg * 8 + e, b[e]);
     }
   }
 }
@@ -623,7 +623,17 @@ MLC_EXPORT int mlc_bn_stats(const bf16* x, float* sum, float* sumsq, long rows, 
   if (C % 8) return -1;
   const int blocks = grid_for(rows, C, reduce_cap());
   if (!det_blocks_ok(blocks)) return -2;
-  hipLaunchKernelGGL(stats_kernel, dim3(blocks), dim3(NT), 0, st, x, sum, sumsq, rows, C, atomic_copies());
+  hipLaunchKernelGGL(stats_kernel, dim3(blocks), dim3(NT), 0, st, x, sum, sumsq, rows, C, atomic_copies(), C);
+  return hipGetLastError();
+}
+
+// the same into copies of row stride ld >= C (a channel slice of a wider BatchNorm's statistics:
+// a DenseNet concat's new segment, its older channels' sums copied from the previous BN)
+MLC_EXPORT int mlc_bn_stats_ld(const bf16* x, float* sum, float* sumsq, long rows, int C, int ld, hipStream_t st) {
+  if (C % 8 || ld < C) return -1;
+  const int blocks = grid_for(rows, C, reduce_cap());
+  if (!det_blocks_ok(blocks)) return -2;
+  hipLaunchKernelGGL(stats_kernel, dim3(blocks), dim3(NT), 0, st, x, sum, sumsq, rows, C, atomic_copies(), ld);
   return hipGetLastError();
 }
 

@@ -861,6 +861,39 @@ class _Lowering:
             for m in members:
                 object.__setattr__(m, 'acc', acc)
 
+    def _link_cat_stats(self):
+        """A BN site over ``torch.cat([a, b], 1)`` where ``a`` is also the input of an earlier
+        BN site A (DenseNet: x_{i+1} = cat(x_i, layer_i(x_i)), layer_i starting with A's BN):
+        the site copies a's per-channel statistics from A and reduces only b (glayers.BNAct
+        .cat_prev) - each layer's statistics pass reads its 32 new channels, not the whole
+        concatenation."""
+        mods = dict(self.gm.named_modules())
+        for n in list(self.gm.graph.nodes):
+            sb = mods.get(n.target) if n.op == 'call_module' else None
+            if not isinstance(sb, BNAct) or len(n.args) != 1 or n.kwargs or sb.residual:
+                continue
+            cat = n.args[0]
+            if not (isinstance(cat, fx.Node) and cat.op == 'call_function' and cat.target is torch.cat):
+                continue
+            parts = cat.args[0] if cat.args else cat.kwargs.get('tensors')
+            dim = cat.args[1] if len(cat.args) > 1 else cat.kwargs.get('dim', 0)
+            if dim != 1 or not isinstance(parts, (list, tuple)) or len(parts) != 2:
+                continue
+            a, b = parts
+            if not (isinstance(a, fx.Node) and isinstance(b, fx.Node)):
+                continue
+            prev = [u for u in a.users if u.op == 'call_module' and isinstance(mods.get(u.target), BNAct)
+                    and u.args and u.args[0] is a and u is not n]
+            if len(prev) != 1:
+                continue
+            sa = mods[prev[0].target]
+            cb = self._channels(b)
+            if (sa.cat_prev is sb or sa.bn.C != sa.bn.Cp or cb is None or cb % 8 or sb.bn.Cp != sa.bn.C + cb
+                    or sb.bn.C != sb.bn.Cp or not self._reaches(prev[0], b)):
+                continue
+            object.__setattr__(sb, 'cat_prev', sa)
+            n.args = (cat, b)
+
     def _link_bn_backward(self):
         """A conv+BN site A (ReLU or no activation, batch statistics) whose output is used
         only as the input of a dense conv site B (and, at a residual block boundary, as the
@@ -1017,6 +1050,7 @@ class _Lowering:
         self._link_dgrads()
         self._link_frames()
         self._link_fanout()
+        self._link_cat_stats()
         self._link_bn_backward()
         g.lint()
         self.gm.delete_all_unused_submodules()

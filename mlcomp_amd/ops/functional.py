@@ -1270,16 +1270,22 @@ def conv2d_wgrad_bias(dy, x, w_shape, dbias, stride=1, pad=0, dil=1, out=None, a
     return conv2d_wgrad(dy, x, w_shape, stride, pad, dil, out=out, accumulate=accumulate)
 
 
-def bn_stats(x, s1, s2):
-    """Per-channel sum / sum of squares of NHWC x into (s1, s2) ([NSTAT*C] fp32 each, added)."""
+def bn_stats(x, s1, s2, ld=None):
+    """Per-channel sum / sum of squares of NHWC x into (s1, s2) ([NSTAT*C] fp32 each, added);
+    ``ld``: the copies' row stride (>= C; s1 / s2 then point at a channel offset of wider
+    statistics buffers)."""
     C = x.shape[-1]
     rows = x.numel() // C
     if _cuda(x):
-        _lib.call('mlc_bn_stats', _lib.ptr(x), _lib.ptr(s1), _lib.ptr(s2), rows, C, _lib.stream())
+        if ld is None:
+            _lib.call('mlc_bn_stats', _lib.ptr(x), _lib.ptr(s1), _lib.ptr(s2), rows, C, _lib.stream())
+        else:
+            _lib.call('mlc_bn_stats_ld', _lib.ptr(x), _lib.ptr(s1), _lib.ptr(s2), rows, C, ld, _lib.stream())
         return
     xf = x.float().reshape(rows, C)
-    s1[:C].add_(xf.sum(0))
-    s2[:C].add_((xf * xf).sum(0))
+    t1, t2 = (s1[0], s2[0]) if s1.dim() == 2 else (s1, s2)     # copy 0 of a strided slice
+    t1[:C].add_(xf.sum(0))
+    t2[:C].add_((xf * xf).sum(0))
 
 
 def bn_finalize(s1, s2, rows, gamma, beta, save_mean, save_invstd, scale, shift, run_mean=None, run_var=None,

@@ -1016,9 +1016,29 @@ class BNAct(Site):
         self.act, self.alpha, self.residual = act, alpha, residual
         self.k_st = ctx.ws.request(f'{bn.name}@{id(self)}.st', 2 * Fn.NSTAT * bn.Cp)
         self.k_bw = ctx.ws.request(f'{bn.name}@{id(self)}.bw', 2 * Fn.NSTAT * bn.Cp)
+        # concat statistics (set by the lowering, _link_cat_stats): this BN's input is
+        # cat([a, tail], 1) and ``cat_prev`` is the BN site over ``a`` (a DenseNet layer's
+        # first BN; it runs earlier in the step): a's per-channel sums are copied from that
+        # site's statistics and only ``tail`` (the new growth channels, passed as the second
+        # input) is reduced - not the whole concatenation again
+        object.__setattr__(self, 'cat_prev', None)
+        object.__setattr__(self, '_last_stats', None)
 
     def forward(self, x, res=None):
         return _run(self, x, res) if res is not None else _run(self, x)
+
+    def _stats(self, yn, tail, s1, s2):
+        A = self.cat_prev
+        prev = A._last_stats if A is not None else None
+        if prev is None or tail is None:
+            Fn.bn_stats(yn, s1, s2)
+            return
+        Cp, Ca = self.bn.Cp, A.bn.Cp
+        tn = to_nhwc(tail, tail.shape[1])
+        s1v, s2v = s1.view(-1, Cp), s2.view(-1, Cp)
+        s1v[:, :Ca].copy_(prev[0].view(-1, Ca))
+        s2v[:, :Ca].copy_(prev[1].view(-1, Ca))
+        Fn.bn_stats(tn, s1v[:, Ca:], s2v[:, Ca:], ld=Cp)
 
     def _to(self, x):
         if x.dim() == 2:              # BatchNorm1d over [N, C] / [N, C, L]
@@ -1039,6 +1059,9 @@ class BNAct(Site):
 
     def fwd(self, x, res=None):
         bn = self.bn
+        tail = None
+        if self.cat_prev is not None:         # the second input is the concat's new segment
+            tail, res = res, None
         yn = self._to(x)
         rn = self._to(res) if res is not None else None
         rows = yn.numel() // yn.shape[-1]
@@ -1047,9 +1070,14 @@ class BNAct(Site):
             st = self.ctx.ws[self.k_st]
             n = Fn.NSTAT * bn.Cp
             stats = (st[:n], st[n:])
-            Fn.bn_stats(yn, *stats)
-        scale, shift, mean, inv = bn.finalize(stats[0] if stats else None, stats[1] if stats else None, rows)
-        z = Fn.bnact_apply(yn, rn, scale, shift, self.act, self.alpha)
+            self._stats(yn, tail, *stats)
+        object.__setattr__(self, '_last_stats', stats)
+        fused = bn.finalize_apply(stats[0], stats[1], yn, rn, self.act, self.alpha) if stats else None
+        if fused is not None:
+            z, scale, shift, mean, inv = fused
+        else:
+            scale, shift, mean, inv = bn.finalize(stats[0] if stats else None, stats[1] if stats else None, rows)
+            z = Fn.bnact_apply(yn, rn, scale, shift, self.act, self.alpha)
         self._dim = x.dim()
         return self._from(z, x), [yn, z, rn if rn is not None else yn, scale, shift, mean, inv], rn is not None
 
@@ -1069,7 +1097,7 @@ class BNAct(Site):
         out = [self._from(dy, like) if needs[0] else None]
         if has_res:
             out.append(self._from(dres, like) if needs[1] else None)
-        return out
+        return out + [None] * (len(needs) - len(out))      # the concat tail: statistics only
 
 
 class LinearAct(Site):

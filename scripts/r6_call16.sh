@@ -5,7 +5,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r6p
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_kernels_gpu.py tests/test_generic_gpu.py tests/test_gate_gpu.py -k "bnact or generic or gate or video or resnext or efficient or inception" > $O/pytest_g.log 2>&1 || exit $?
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_kernels_gpu.py tests/test_generic_gpu.py tests/test_gate_gpu.py -k "bnact or generic or gate or video or resnext or efficient or inception or stats_into or dense" > $O/pytest_g.log 2>&1 || exit $?
 : > $O/generic.jsonl
 for m in resnet50:512:224 resnext50_32x4d:128:224 efficientnet-b0:256:224 se_resnext50_32x4d:64:224 densenet121:64:224 inceptionv3:80:299; do
   IFS=: read name b sz <<< "$m"

@@ -969,3 +969,47 @@ def test_se_block_input_gradient_summed_in_pool_and_gate(monkeypatch):
     g0 = run(False)
     for a, b in zip(g1, g0):
         assert _rel(a, b) < 3e-2 and _cos(a, b) > 0.999
+
+
+def test_dense_block_bn_statistics_reuse_the_previous_layers(monkeypatch):
+    """DenseNet's BN over cat([x_i, f_i]): the site copies x_i's per-channel sums from the
+    previous layer's BN and reduces only the new channels (BNAct.cat_prev); output, running
+    statistics and weight gradients equal the lowering that reduces the whole concatenation."""
+    from mlcomp_amd.contrib.segmentation.encoders import _DenseLayer
+    from mlcomp_amd.models.native_generic import _Lowering
+    from mlcomp_amd.ops.glayers import BNAct
+
+    class Dense(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.stem = nn.Sequential(nn.Conv2d(3, 16, 3, padding=1, bias=False), nn.BatchNorm2d(16), nn.ReLU())
+            self.layers = nn.Sequential(_DenseLayer(16, 8, 2), _DenseLayer(24, 8, 2), _DenseLayer(32, 8, 2))
+            self.final = nn.BatchNorm2d(40)
+            self.head = nn.Sequential(nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(40, 5))
+
+        def forward(self, x):
+            return self.head(torch.relu(self.final(self.layers(self.stem(x)))))
+
+    x = torch.randn(2, 3, 12, 12)
+    y = torch.randint(0, 5, (2,))
+
+    def run(linked):
+        torch.manual_seed(0)
+        if not linked:
+            monkeypatch.setattr(_Lowering, '_link_cat_stats', lambda self: None)
+        net = GenericNet(Dense(), 'cpu')
+        monkeypatch.undo()
+        k = sum(isinstance(m, BNAct) and m.cat_prev is not None for m in net.train_gm.modules())
+        out = net(x)
+        F.cross_entropy(out.float(), y).backward()
+        rv = [m.bn.run_var.clone() for m in net.train_gm.modules() if isinstance(m, BNAct)]
+        return k, out.detach(), rv, [p.w.grad.clone() for p in net.param_sets() if hasattr(p, 'kind')]
+
+    k1, o1, r1, g1 = run(True)
+    k0, o0, r0, g0 = run(False)
+    assert (k1, k0) == (3, 0)          # layers 2, 3 and the final BN
+    assert _rel(o1, o0) < 1e-2
+    for a, b in zip(r1, r0):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-6)
+    for a, b in zip(g1, g0):
+        assert _rel(a, b) < 3e-2 and _cos(a, b) > 0.999

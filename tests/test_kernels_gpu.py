@@ -810,3 +810,18 @@ def test_bnact_fused_matches_finalize_then_apply(act, res, rowscale, C):
     for a, b in zip(*outs):
         tol = 1e-5 if a.dtype == torch.float32 else 5e-3
         assert rel_err(a, b) < tol, (a.dtype, rel_err(a, b))
+
+
+def test_bn_stats_into_a_channel_slice():
+    """mlc_bn_stats_ld: the per-channel sums of a 16-channel tensor land in channels 24..39 of
+    40-wide statistics copies (a DenseNet concat's new segment), equal to the plain reduction."""
+    x = _bf(2, 9, 7, 16, seed=61).to(DEV)
+    s1, s2 = Fn.stat_buffers(40, DEV)
+    Fn.bn_stats(x, s1.view(-1, 40)[:, 24:], s2.view(-1, 40)[:, 24:], ld=40)
+    r1, r2 = Fn.stat_buffers(16, DEV)
+    Fn.bn_stats(x, r1, r2)
+    torch.cuda.synchronize()
+    got1, got2 = s1.view(-1, 40).sum(0), s2.view(-1, 40).sum(0)
+    assert float(got1[:24].abs().max()) == 0.0 and float(got2[:24].abs().max()) == 0.0
+    assert rel_err(got1[24:], r1.view(-1, 16).sum(0)) < 1e-5
+    assert rel_err(got2[24:], r2.view(-1, 16).sum(0)) < 1e-5
