@@ -318,32 +318,48 @@ avgpool2d_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ add, 
 __device__ __forceinline__ int abin_lo(int o, int in, int out) { return (int)(((long)o * in) / out); }
 __device__ __forceinline__ int abin_hi(int o, int in, int out) { return (int)(((long)(o + 1) * in + out - 1) / out); }
 
+// one block per output bin (n, oh, ow): threads split the bin's pixels (lanes) and the 8-channel
+// groups, fp32 partial sums combined in LDS (the layout of avgpool_fwd_kernel) - a thread per
+// output chunk summing a whole bin serially left a 1x1 / 2x2 pyramid level with a few thousand
+// threads on a few CUs
 __global__ void __launch_bounds__(NT)
 adaptive_avg_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N, int H, int W, int C, int Ho,
                         int Wo) {
-  const int G = C / 8;
-  const long total = (long)N * Ho * Wo * G;
-  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-    const int g = (int)(i % G);
-    long t = i / G;
-    const int wo = (int)(t % Wo);
-    t /= Wo;
-    const int ho = (int)(t % Ho);
-    const int n = (int)(t / Ho);
-    const int h0 = abin_lo(ho, H, Ho), h1 = abin_hi(ho, H, Ho);
-    const int w0 = abin_lo(wo, W, Wo), w1 = abin_hi(wo, W, Wo);
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int h = h0; h < h1; ++h)
-      for (int w = w0; w < w1; ++w) {
+  __shared__ float part[NT][8];
+  const int bin = blockIdx.x;
+  const int ow = bin % Wo, oh = (bin / Wo) % Ho, n = bin / (Wo * Ho);
+  const int h0 = abin_lo(oh, H, Ho), h1 = abin_hi(oh, H, Ho);
+  const int w0 = abin_lo(ow, W, Wo), w1 = abin_hi(ow, W, Wo);
+  const int bw = w1 - w0, area = (h1 - h0) * bw;
+  const float inv = 1.f / (float)area;
+  const int G = C >> 3, t = threadIdx.x;
+  const int lanes = G >= NT ? 1 : NT / G;
+  for (int cgb = 0; cgb < G; cgb += NT) {
+    const int cg = cgb + (G >= NT ? t : t % G);
+    const int pl = G >= NT ? 0 : t / G;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    if (cg < G && pl < lanes)
+      for (int p = pl; p < area; p += lanes) {
+        const int h = h0 + p / bw, w = w0 + p % bw;
         float f[8];
-        unpack8(ldg16(x + (((long)n * H + h) * W + w) * C + g * 8), f);
+        unpack8(ldg16(x + (((long)n * H + h) * W + w) * C + cg * 8), f);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += f[e];
+        for (int j = 0; j < 8; ++j) acc[j] += f[j];
       }
-    const float inv = 1.f / (float)((h1 - h0) * (w1 - w0));
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] *= inv;
-    *reinterpret_cast<uint4*>(y + i * 8) = pack8(acc);
+    for (int j = 0; j < 8; ++j) part[t][j] = acc[j];
+    __syncthreads();
+    if (pl == 0 && cg < G) {
+      for (int u = 1; u < lanes; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += part[t + u * G][j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] *= inv;
+      *reinterpret_cast<uint4*>(y + ((long)bin * C) + cg * 8) = pack8(acc);
+    }
+    __syncthreads();
   }
 }
 
@@ -462,8 +478,8 @@ MLC_EXPORT int mlc_avgpool2d_bwd(const bf16* dy, const bf16* add, bf16* dx, int 
 MLC_EXPORT int mlc_adaptive_avg_fwd(const bf16* x, bf16* y, int N, int H, int W, int C, int Ho, int Wo,
                                     hipStream_t st) {
   if (C % 8 || Ho < 1 || Wo < 1 || H < 1 || W < 1) return -1;
-  hipLaunchKernelGGL(adaptive_avg_fwd_kernel, dim3(blocks_for((long)N * Ho * Wo * (C / 8))), dim3(NT), 0, st, x, y,
-                     N, H, W, C, Ho, Wo);
+  hipLaunchKernelGGL(adaptive_avg_fwd_kernel, dim3((unsigned)(N * Ho * Wo)), dim3(NT), 0, st, x, y, N, H, W, C, Ho,
+                     Wo);
   return hipGetLastError();
 }
 
