@@ -351,7 +351,7 @@ bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const 
                  const bf16* __restrict__ res, const float* __restrict__ mean, const float* __restrict__ coef,
                  const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ rscale,
                  const float* __restrict__ rshift, bf16* __restrict__ dy, bf16* __restrict__ dres, long rows, int C,
-                 int act, float alpha, RowScale rsc) {
+                 int act, float alpha, RowScale rsc, const bf16* __restrict__ add, long add_ld) {
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
   const long stride = (long)gridDim.x * NT;
@@ -371,6 +371,8 @@ bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const 
   for (long i = gtid; i < total; i += stride) {
     const uint4 dv = ldg16(dz + i * 8), yv = ldg16(y + i * 8);
     const uint4 zv = z ? ldg16(z + i * 8) : z4, rv = res ? ldg16(res + i * 8) : z4;
+    // another consumer's gradient of y, rows of stride add_ld (a DenseNet concat's slice)
+    const uint4 av = add ? ldg16(add + (i / G) * add_ld + (i % G) * 8) : z4;
     float d[8], yy[8], o[8];
     unpack8(dv, d);
     unpack8(yv, yy);
@@ -383,6 +385,12 @@ bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const 
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = k1[j] * d[j] + k2[j] + k3[j] * (yy[j] - mu[j]);
+    if (add) {
+      float q[8];
+      unpack8(av, q);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += q[j];
+    }
     *reinterpret_cast<uint4*>(dy + i * 8) = pack8(o);
   }
 }
@@ -695,8 +703,9 @@ MLC_EXPORT int mlc_bnact_bwd(const bf16* dz, const bf16* z, const bf16* y, const
                              const float* invstd, const float* gamma,
                              float* part, long part_floats, float* coef, float* dgamma, float* dbeta, bf16* dy,
                              bf16* dres, long rows, int C, int act, float alpha, const float* row_scale, long hw,
-                             hipStream_t st) {
+                             const bf16* add, long add_ld, hipStream_t st) {
   if (row_scale && (act != 0 || hw < 1)) return -1;
+  if (add && (add_ld < C || add_ld % 8)) return -1;
   const RowScale rsc{row_scale, hw};
   const int G = C >> 3;
   if (C % 8 || G > NT || part_floats < 2L * C || (rscale && !rshift)) return -1;
@@ -710,18 +719,18 @@ MLC_EXPORT int mlc_bnact_bwd(const bf16* dz, const bf16* z, const bf16* y, const
   hipLaunchKernelGGL(bwd_finalize_rows_kernel, dim3((C + NT / 64 - 1) / (NT / 64)), dim3(NT), 0, st, part, blocks,
                      invstd, gamma, coef, dgamma, dbeta, rows, C);
   NA_LAUNCH(bwd_apply_kernel, grid_for(rows, C, apply_cap()), st, act, dz, z, y, res, mean, coef, scale, shift, rscale, rshift,
-            dy, dres, rows, C, act, alpha, rsc);
+            dy, dres, rows, C, act, alpha, rsc, add, add_ld);
   return hipGetLastError();
 }
 
 MLC_EXPORT int mlc_bnact_bwd_apply(const bf16* dz, const bf16* z, const bf16* y, const bf16* res, const float* mean,
                                    const float* coef, const float* scale, const float* shift, const float* rscale,
                                    const float* rshift, bf16* dy, bf16* dres, long rows, int C, int act, float alpha,
-                                   const float* row_scale, long hw, hipStream_t st) {
-  if (C % 8 || (row_scale && (act != 0 || hw < 1))) return -1;
+                                   const float* row_scale, long hw, const bf16* add, long add_ld, hipStream_t st) {
+  if (C % 8 || (row_scale && (act != 0 || hw < 1)) || (add && (add_ld < C || add_ld % 8))) return -1;
   const RowScale rsc{row_scale, hw};
   NA_LAUNCH(bwd_apply_kernel, grid_for(rows, C, apply_cap()), st, act, dz, z, y, res, mean, coef, scale, shift, rscale, rshift,
-            dy, dres, rows, C, act, alpha, rsc);
+            dy, dres, rows, C, act, alpha, rsc, add, add_ld);
   return hipGetLastError();
 }
 

@@ -45,7 +45,7 @@ import torch.nn.functional as F
 
 from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops.glayers import (AdaptiveAvgPool, AvgPool, BilinearUp, BNAct, BNParams, ChannelGate, Conv3dAs2d,
-                                    ConvBNAct, ConvParams, Frames, GlobalAvgPool, GradAcc, LinearAct, LinearParams,
+                                    ConvBNAct, ConvParams, DenseCat, Frames, GlobalAvgPool, GradAcc, LinearAct, LinearParams,
                                     MaxPool, TemporalAs2d, UpCat, VolumePool)
 from mlcomp_amd.ops import gtransformer as GT
 from mlcomp_amd.ops.layers import NativeContext
@@ -894,6 +894,35 @@ class _Lowering:
             object.__setattr__(sb, 'cat_prev', sa)
             n.args = (cat, b)
 
+    def _lower_dense_cats(self):
+        """``torch.cat([a, b], 1)`` where ``a``'s only other user is a BN site A that ``b``
+        depends on (a DenseNet layer): a :class:`DenseCat` site, whose backward hands a's
+        gradient slice to A's apply pass instead of autograd adding a strided slice to A's
+        input gradient."""
+        mods = dict(self.gm.named_modules())
+        for cat in list(self.gm.graph.nodes):
+            if cat.op != 'call_function' or cat.target is not torch.cat or cat in self.erased:
+                continue
+            parts = cat.args[0] if cat.args else cat.kwargs.get('tensors')
+            dim = cat.args[1] if len(cat.args) > 1 else cat.kwargs.get('dim', 0)
+            if dim != 1 or not isinstance(parts, (list, tuple)) or len(parts) != 2:
+                continue
+            a, b = parts
+            if not (isinstance(a, fx.Node) and isinstance(b, fx.Node)) or a is b:
+                continue
+            others = [u for u in a.users if u is not cat]
+            if len(others) != 1 or others[0].op != 'call_module':
+                continue
+            sa = mods.get(others[0].target)
+            nargs = 2 if isinstance(sa, BNAct) and sa.cat_prev is not None else 1     # (x, concat tail)
+            if (not isinstance(sa, BNAct) or len(others[0].args) != nargs or others[0].args[0] is not a or sa.residual
+                    or sa.bn.C != sa.bn.Cp or sa.slice_expected or not self._reaches(others[0], b)):
+                continue
+            site = DenseCat(self.net.ctx, sa)
+            new = self._site_node(cat, site, [a, b])
+            self._replace([cat], new)
+            object.__setattr__(sa, 'slice_expected', True)
+
     def _link_bn_backward(self):
         """A conv+BN site A (ReLU or no activation, batch statistics) whose output is used
         only as the input of a dense conv site B (and, at a residual block boundary, as the
@@ -1051,6 +1080,7 @@ class _Lowering:
         self._link_frames()
         self._link_fanout()
         self._link_cat_stats()
+        self._lower_dense_cats()
         self._link_bn_backward()
         g.lint()
         self.gm.delete_all_unused_submodules()

@@ -121,8 +121,8 @@ _SIGS = {
     'mlc_bn_stats_ld': [vp, vp, vp, i64, i32, i32, vp],
     'mlc_bnact_apply': [vp] * 7 + [i64, i32, i32, f32, vp, i64, vp],
     'mlc_bnact_bwd_reduce': [vp] * 10 + [i64, i32, i32, f32, vp, i64, vp],
-    'mlc_bnact_bwd': [vp] * 12 + [i64] + [vp] * 5 + [i64, i32, i32, f32, vp, i64, vp],
-    'mlc_bnact_bwd_apply': [vp] * 12 + [i64, i32, i32, f32, vp, i64, vp],
+    'mlc_bnact_bwd': [vp] * 12 + [i64] + [vp] * 5 + [i64, i32, i32, f32, vp, i64, vp, i64, vp],
+    'mlc_bnact_bwd_apply': [vp] * 12 + [i64, i32, i32, f32, vp, i64, vp, i64, vp],
     'mlc_act_fwd': [vp, vp, i64, i32, f32, vp],
     'mlc_act_bwd': [vp] * 4 + [i64, i32, f32, vp],
     'mlc_chscale_fwd': [vp] * 4 + [i32, i64, i32, i32, vp],

@@ -1354,15 +1354,25 @@ def bnact_fused(y, res, s1, s2, gamma, beta, mean, invstd, scale, shift, run_mea
 
 
 def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0, dgamma=None, dbeta=None,
-              sums=None, coef=None, want_dres=False, res_affine=None, row_scale=None):
+              sums=None, coef=None, want_dres=False, res_affine=None, row_scale=None, addend=None):
     """Backward of z = act(BN(y) [* row_scale[n]] [+ res (*rscale + rshift)]) with the forward's
     (scale, shift): returns (dy, dres or None) and writes dgamma / dbeta; dres is the gradient
     of the residual term (before ``res_affine``, i.e. of a folded shortcut BN's output).
-    ``sums`` (NSTAT*2*C fp32) must be zero on entry."""
+    ``sums`` (NSTAT*2*C fp32) must be zero on entry.  ``addend``: another consumer's gradient of
+    y added to dy in the apply pass - an NHWC tensor whose last dim may be a channel slice of
+    wider rows (a DenseNet concat's gradient, row stride ``addend.stride(-2)``)."""
     C = y.shape[-1]
     rows = y.numel() // C
     hw = rows // y.shape[0]
     rs, rh = res_affine if res_affine is not None else (None, None)
+    add_ld = 0
+    if addend is not None:
+        # rows of C channels at a row stride >= C (the channel slice of a contiguous NHWC tensor)
+        add_ld = addend.stride(-2)
+        want = [1, add_ld]
+        for d in range(addend.dim() - 2, 0, -1):
+            want.append(want[-1] * addend.shape[d])
+        assert addend.shape == y.shape and list(addend.stride()) == want[::-1], (addend.shape, addend.stride())
     if _cuda(dz):
         if coef is None:
             coef = torch.empty(3 * C, device=dz.device, dtype=torch.float32)
@@ -1375,7 +1385,8 @@ def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0
             _lib.call('mlc_bnact_bwd', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
                       _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(rs), _lib.ptr(rh), _lib.ptr(invstd), _lib.ptr(gamma),
                       _lib.ptr(part), part.numel(), _lib.ptr(coef), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(dy),
-                      _lib.ptr(dres), rows, C, int(act), float(alpha), _lib.ptr(row_scale), hw, _lib.stream())
+                      _lib.ptr(dres), rows, C, int(act), float(alpha), _lib.ptr(row_scale), hw, _lib.ptr(addend),
+                      add_ld, _lib.stream())
             return dy, dres
         if sums is None:
             sums = torch.zeros(NSTAT * 2 * C, device=dz.device, dtype=torch.float32)
@@ -1388,7 +1399,8 @@ def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0
         dres = torch.empty_like(y) if want_dres else None
         _lib.call('mlc_bnact_bwd_apply', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
                   _lib.ptr(coef), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(rs), _lib.ptr(rh), _lib.ptr(dy),
-                  _lib.ptr(dres), rows, C, int(act), float(alpha), _lib.ptr(row_scale), hw, _lib.stream())
+                  _lib.ptr(dres), rows, C, int(act), float(alpha), _lib.ptr(row_scale), hw, _lib.ptr(addend), add_ld,
+                  _lib.stream())
         return dy, dres
     rsc = row_scale.repeat_interleave(hw)[:, None] if row_scale is not None else None
     a = y.float().reshape(rows, C) * scale + shift
@@ -1414,6 +1426,8 @@ def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0
         dbeta.copy_(S1)
     k1 = gamma * invstd
     dyf = k1 * d - k1 * S1 / rows - k1 * invstd * invstd * S2 / rows * yc
+    if addend is not None:
+        dyf = dyf + addend.float().reshape(rows, C)
     return dyf.reshape(y.shape).to(torch.bfloat16), dres
 
 

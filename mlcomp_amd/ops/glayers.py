@@ -1023,6 +1023,11 @@ class BNAct(Site):
         # input) is reduced - not the whole concatenation again
         object.__setattr__(self, 'cat_prev', None)
         object.__setattr__(self, '_last_stats', None)
+        # concat-gradient hand-off (set by the lowering, _lower_dense_cats): this site's input
+        # is also the first operand of a DenseCat whose backward runs first and leaves its
+        # gradient slice here; the apply pass adds it (no copy, no autograd add)
+        object.__setattr__(self, 'slice_expected', False)
+        object.__setattr__(self, '_slice_pending', None)
 
     def forward(self, x, res=None):
         return _run(self, x, res) if res is not None else _run(self, x)
@@ -1086,9 +1091,14 @@ class BNAct(Site):
         yn, z, rn, scale, shift, mean, inv = saved
         dz = self._to(dout)
         d = self._direct_bn_grads()
+        addend = self._slice_pending
+        object.__setattr__(self, '_slice_pending', None)
+        if self.slice_expected and needs[0] and addend is None:
+            raise RuntimeError(f'{bn.name}: the concat gradient hand-off did not arrive (backward order differs '
+                               'from the one the lowering assumed)')
         dy, dres = Fn.bnact_bwd(dz, z, yn, rn if has_res else None, mean, scale, shift, inv, bn.gamma.master,
                                 self.act, self.alpha, dgamma=_acc_view(bn.gamma, d), dbeta=_acc_view(bn.beta, d),
-                                sums=self.ctx.ws[self.k_bw], want_dres=has_res)
+                                sums=self.ctx.ws[self.k_bw], want_dres=has_res, addend=addend)
         _acc_commit(bn.gamma, d)
         _acc_commit(bn.beta, d)
         if bn.uses.bwd_done():
@@ -1176,6 +1186,30 @@ class LinearAct(Site):
             from .gtransformer import _reduce_to
             out.append(_reduce_to(dout, keep[0], keep[1]) if needs[1] else None)
         return out
+
+
+class DenseCat(Site):
+    """``torch.cat([a, b], 1)`` of a DenseNet layer (x_{i+1} = cat(x_i, layer_i(x_i))) whose first
+    operand's other consumer is a BN site (``a_site``, the layer's first BN, whose backward runs
+    after this one): the backward leaves a's gradient - a channel slice of the output gradient,
+    no copy - with that site, whose apply pass adds it; autograd adds nothing."""
+
+    def __init__(self, ctx, a_site: 'BNAct'):
+        super().__init__(ctx)
+        object.__setattr__(self, 'a_site', a_site)
+
+    def forward(self, a, b):
+        return _run(self, a, b)
+
+    def fwd(self, a, b):
+        return torch.cat([a, b], 1), [], (a.shape[1], b.shape[1])
+
+    def bwd(self, dout, saved, keep, needs):
+        Ca, Cb = keep
+        g = to_nhwc(dout, Ca + Cb)                 # the channels_last view, no copy
+        if needs[0]:
+            object.__setattr__(self.a_site, '_slice_pending', g[..., :Ca])
+        return [None, from_nhwc(g[..., Ca:], Cb) if needs[1] else None]
 
 
 class UpCat(Site):

@@ -973,11 +973,12 @@ def test_se_block_input_gradient_summed_in_pool_and_gate(monkeypatch):
 
 def test_dense_block_bn_statistics_reuse_the_previous_layers(monkeypatch):
     """DenseNet's BN over cat([x_i, f_i]): the site copies x_i's per-channel sums from the
-    previous layer's BN and reduces only the new channels (BNAct.cat_prev); output, running
-    statistics and weight gradients equal the lowering that reduces the whole concatenation."""
+    previous layer's BN and reduces only the new channels (BNAct.cat_prev), and the concat's
+    backward hands x_i's gradient slice to that BN's apply pass (DenseCat); output, running
+    statistics and weight gradients equal the plain lowering's."""
     from mlcomp_amd.contrib.segmentation.encoders import _DenseLayer
     from mlcomp_amd.models.native_generic import _Lowering
-    from mlcomp_amd.ops.glayers import BNAct
+    from mlcomp_amd.ops.glayers import BNAct, DenseCat
 
     class Dense(nn.Module):
         def __init__(self):
@@ -997,9 +998,11 @@ def test_dense_block_bn_statistics_reuse_the_previous_layers(monkeypatch):
         torch.manual_seed(0)
         if not linked:
             monkeypatch.setattr(_Lowering, '_link_cat_stats', lambda self: None)
+            monkeypatch.setattr(_Lowering, '_lower_dense_cats', lambda self: None)
         net = GenericNet(Dense(), 'cpu')
         monkeypatch.undo()
         k = sum(isinstance(m, BNAct) and m.cat_prev is not None for m in net.train_gm.modules())
+        k += 10 * sum(isinstance(m, DenseCat) for m in net.train_gm.modules())
         out = net(x)
         F.cross_entropy(out.float(), y).backward()
         rv = [m.bn.run_var.clone() for m in net.train_gm.modules() if isinstance(m, BNAct)]
@@ -1007,7 +1010,7 @@ def test_dense_block_bn_statistics_reuse_the_previous_layers(monkeypatch):
 
     k1, o1, r1, g1 = run(True)
     k0, o0, r0, g0 = run(False)
-    assert (k1, k0) == (3, 0)          # layers 2, 3 and the final BN
+    assert (k1, k0) == (33, 0)         # 3 concat-statistics BNs (layers 2, 3, final), 3 DenseCats
     assert _rel(o1, o0) < 1e-2
     for a, b in zip(r1, r0):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-6)

@@ -825,3 +825,33 @@ def test_bn_stats_into_a_channel_slice():
     assert float(got1[:24].abs().max()) == 0.0 and float(got2[:24].abs().max()) == 0.0
     assert rel_err(got1[24:], r1.view(-1, 16).sum(0)) < 1e-5
     assert rel_err(got2[24:], r2.view(-1, 16).sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize('act', [1, 3])
+def test_bnact_bwd_adds_a_strided_channel_slice(act):
+    """normact backward apply with an addend that is a channel slice of a wider NHWC gradient
+    (a DenseNet concat's gradient, row stride 40 for 24 channels): GPU against the fp32 CPU
+    path of the same call."""
+    C, W = 24, 40
+    y = (_bf(2, 5, 6, C, scale=2.0, seed=71) + 0.3)
+    dz = _bf(2, 5, 6, C, seed=72)
+    wide = _bf(2, 5, 6, W, seed=73)
+    g = torch.Generator().manual_seed(74)
+    gamma, beta = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1
+    yf = y.float().reshape(-1, C)
+    mean, var = yf.mean(0), yf.var(0, unbiased=False)
+    inv = torch.rsqrt(var + 1e-5)
+    scale, shift = gamma * inv, beta - mean * gamma * inv
+    z = Fn.bnact_apply(y, None, scale, shift, act)
+
+    def run(dev):
+        t = lambda v: v.to(dev)
+        dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        dy, _ = Fn.bnact_bwd(t(dz), t(z), t(y), None, t(mean), t(scale), t(shift), t(inv), t(gamma), act,
+                             dgamma=dg, dbeta=db, addend=t(wide)[..., :C])
+        return dy, dg, db
+
+    ref, out = run('cpu'), run(DEV)
+    torch.cuda.synchronize()
+    for a, b in zip(out, ref):
+        assert rel_err(a, b) < 1e-2
