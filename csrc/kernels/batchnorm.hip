@@ -271,7 +271,7 @@ bn_bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, con
 constexpr int FG = 32;
 
 __device__ __forceinline__ void fused_geom(int G, int& gb, int& nslices) {
-  gb = G < FG ? G : FG;
+  gb = slice_groups(G, FG);
   nslices = G / gb;
 }
 
@@ -464,7 +464,7 @@ int grid_for(long rows, int C) {
 // grid of the fused passes: ~g_max_blocks blocks, a multiple of the channel slices
 int fused_grid(long rows, int C) {
   const int G = C >> 3;
-  const int gb = G < FG ? G : FG, nslices = G / gb;
+  const int gb = slice_groups(G, FG), nslices = G / gb;
   const int rpi = NT / gb;
   long parts = (rows + (long)rpi * 4 - 1) / ((long)rpi * 4);   // ~4 rows per thread at least
   long cap = g_max_blocks / nslices;
@@ -477,7 +477,7 @@ int fused_grid(long rows, int C) {
 bool fused_ok(int C, int ncopy) {
   const int G = C >> 3;
   if (g_fused != 1 || C % 8 || ncopy < 1 || ncopy > 64) return false;   // deterministic copies: the finalize kernel
-  return G <= FG || G % FG == 0;
+  return G >= 1;
 }
 
 bool shape_ok(int C) {

@@ -32,6 +32,15 @@ static __device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
 static __device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }
 
 // unpack 8 bf16 held in a uint4 into floats
+// channel-group slice of the folded-finalize BN passes (batchnorm.hip / normact.hip *_fused
+// kernels): the largest divisor of G (8-channel groups) not above cap, so every C % 8 == 0
+// splits into equal slices (DenseNet's 36 / 44 / 52 groups, EfficientNet's 40 / 60 / 84)
+static __host__ __device__ __forceinline__ int slice_groups(int G, int cap) {
+  int d = G < cap ? G : cap;
+  while (d > 1 && G % d) --d;
+  return d;
+}
+
 static __device__ __forceinline__ void unpack8(const uint4& u, float* f) {
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll

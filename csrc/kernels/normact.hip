@@ -192,11 +192,12 @@ apply_fused_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf1
                    float* __restrict__ invstd_out, float* __restrict__ scale_out, float* __restrict__ shift_out,
                    float* __restrict__ run_mean, float* __restrict__ run_var, const float* __restrict__ rscale,
                    const float* __restrict__ rshift, long rows, int C, float eps, float momentum, int act_,
-                   float alpha, RowScale rsc) {
+                   float alpha, RowScale rsc, const float* __restrict__ prev_tot, int prev_c,
+                   float* __restrict__ tot_out) {
   const int act = ACT >= 0 ? ACT : act_;
   __shared__ float red[2][NT], lsc[FG * 8], lsh[FG * 8];
   const int G = C >> 3;
-  const int gb = G < FG ? G : FG, nslices = G / gb;
+  const int gb = slice_groups(G, FG), nslices = G / gb;
   const int slice = blockIdx.x % nslices, part = blockIdx.x / nslices, nparts = gridDim.x / nslices;
   const int t = threadIdx.x, nch = gb * 8, c0 = slice * nch;
   {
@@ -212,6 +213,10 @@ apply_fused_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf1
     if (t < nch) {
       for (int q = 1; q < P; ++q) { a += red[0][q * nch + t]; b += red[1][q * nch + t]; }
       const int ch = c0 + t;
+      // channels [0, prev_c): totals published by the previous BN of a DenseNet concat chain
+      // (this BN's own copies hold only the new segment's sums there: zeros)
+      if (prev_tot && ch < prev_c) { a += prev_tot[ch]; b += prev_tot[prev_c + ch]; }
+      if (tot_out && part == 0) { tot_out[ch] = a; tot_out[C + ch] = b; }
       const float inv_count = 1.f / (float)rows;
       const float mean = a * inv_count;
       const float var = fmaxf(b * inv_count - mean * mean, 0.f);
@@ -661,12 +666,13 @@ MLC_EXPORT int mlc_bnact_fused(const bf16* y, const bf16* res, bf16* z, const fl
                                int ncopy, const float* gamma, const float* beta, float* mean, float* invstd,
                                float* scale, float* shift, float* run_mean, float* run_var, const float* rscale,
                                const float* rshift, long rows, int C, float eps, float momentum, int act, float alpha,
-                               const float* row_scale, long hw, hipStream_t st) {
+                               const float* row_scale, long hw, const float* prev_tot, int prev_c, float* tot_out,
+                               hipStream_t st) {
   const int G = C >> 3;
   if (C % 8 || (rscale && !rshift) || (row_scale && (act != 0 || hw < 1)) || rows < 1 || ncopy < 1 || ncopy > 64 ||
-      !(G <= FG || G % FG == 0))
+      G < 1 || prev_c < 0 || prev_c > C)
     return -1;
-  const int gb = G < FG ? G : FG, nslices = G / gb, rpi = NT / gb;
+  const int gb = slice_groups(G, FG), nslices = G / gb, rpi = NT / gb;
   long parts = (rows + (long)rpi * 4 - 1) / ((long)rpi * 4);
   long cap = apply_cap() / nslices;
   if (cap < 1) cap = 1;
@@ -674,7 +680,8 @@ MLC_EXPORT int mlc_bnact_fused(const bf16* y, const bf16* res, bf16* z, const fl
   if (parts < 1) parts = 1;
   const RowScale rsc{row_scale, hw};
   NA_LAUNCH(apply_fused_kernel, parts * nslices, st, act, y, res, z, sum, sumsq, ncopy, gamma, beta, mean, invstd,
-            scale, shift, run_mean, run_var, rscale, rshift, rows, C, eps, momentum, act, alpha, rsc);
+            scale, shift, run_mean, run_var, rscale, rshift, rows, C, eps, momentum, act, alpha, rsc, prev_tot, prev_c,
+            tot_out);
   return hipGetLastError();
 }
 

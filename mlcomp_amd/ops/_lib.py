@@ -85,7 +85,7 @@ _SIGS = {
     'mlc_bn_bwd_finalize': [vp] * 6 + [i64, i32, vp],
     'mlc_bn_fwd_fused': [vp] * 5 + [i32] + [vp] * 10 + [i64, i32, f32, f32, i32, vp],
     'mlc_bn_bwd_fused': [vp] * 5 + [i32] + [vp] * 6 + [i64, i32, vp],
-    'mlc_bnact_fused': [vp] * 5 + [i32] + [vp] * 10 + [i64, i32, f32, f32, i32, f32, vp, i64, vp],
+    'mlc_bnact_fused': [vp] * 5 + [i32] + [vp] * 10 + [i64, i32, f32, f32, i32, f32, vp, i64, vp, i32, vp, vp],
     'mlc_bn_bwd_apply': [vp] * 7 + [i64, i32, vp],
     'mlc_maxpool_fwd': [vp, vp, vp] + [i32] * 9 + [vp],
     'mlc_maxpool_bwd': [vp, vp, vp] + [i32] * 9 + [vp],

@@ -424,9 +424,7 @@ BN_FUSED = os.environ.get('MLC_BN_FUSED', '1') == '1'
 
 
 def _bn_fused_ok(C, ncopy):
-    G = C // 8
-    return (BN_FUSED and not _lib.DETERMINISTIC and C % 8 == 0 and 1 <= ncopy <= 64
-            and (G <= 32 or G % 32 == 0))
+    return BN_FUSED and not _lib.DETERMINISTIC and C % 8 == 0 and C >= 8 and 1 <= ncopy <= 64
 
 
 def bn_fwd_apply(y, res, s1, s2, gamma, beta, save_mean, save_invstd, run_mean, run_var,
@@ -1335,10 +1333,13 @@ def bnact_apply(y, res, scale, shift, act=0, alpha=0.0, res_affine=None, row_sca
 
 
 def bnact_fused(y, res, s1, s2, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, eps, momentum, act=0,
-                alpha=0.0, res_affine=None, row_scale=None):
+                alpha=0.0, res_affine=None, row_scale=None, prev_tot=None, prev_c=0, tot_out=None):
     """:func:`bn_finalize` + :func:`bnact_apply` in one launch (normact.hip apply_fused_kernel):
     fills mean / invstd / scale / shift (and the running statistics) from the partial copies
-    ``s1`` / ``s2`` and returns z; None when the shape does not fit (use the two calls)."""
+    ``s1`` / ``s2`` and returns z; None when the shape does not fit (use the two calls).
+    ``prev_tot`` ([2, prev_c] fp32): per-channel totals of the first ``prev_c`` channels, added
+    to the copies' sums there (a DenseNet concat's older segment); ``tot_out`` ([2, C]): this
+    BN's per-channel totals, published for the next BN of such a chain."""
     C = y.shape[-1]
     ncopy = s1.numel() // C
     if not (_cuda(y) and _bn_fused_ok(C, ncopy)):
@@ -1349,7 +1350,8 @@ def bnact_fused(y, res, s1, s2, gamma, beta, mean, invstd, scale, shift, run_mea
     _lib.call('mlc_bnact_fused', _lib.ptr(y), _lib.ptr(res), _lib.ptr(z), _lib.ptr(s1), _lib.ptr(s2), ncopy,
               _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(mean), _lib.ptr(invstd), _lib.ptr(scale), _lib.ptr(shift),
               _lib.ptr(run_mean), _lib.ptr(run_var), _lib.ptr(rs), _lib.ptr(rh), rows, C, float(eps), float(momentum),
-              int(act), float(alpha), _lib.ptr(row_scale), rows // y.shape[0], _lib.stream())
+              int(act), float(alpha), _lib.ptr(row_scale), rows // y.shape[0], _lib.ptr(prev_tot), int(prev_c),
+              _lib.ptr(tot_out), _lib.stream())
     return z
 
 

@@ -628,7 +628,8 @@ class BNParams:
             mean.copy_(self.run_mean)
         return scale, shift, mean, inv
 
-    def finalize_apply(self, s1, s2, y, res, act, alpha, res_affine=None, row_scale=None):
+    def finalize_apply(self, s1, s2, y, res, act, alpha, res_affine=None, row_scale=None, prev_tot=None, prev_c=0,
+                       tot_out=None):
         """:meth:`finalize` and the apply pass in one launch (Fn.bnact_fused) for batch
         statistics: (z, scale, shift, mean, invstd), or None when it does not apply."""
         if s1 is None or not self.batch_stats():
@@ -639,7 +640,8 @@ class BNParams:
         mom = self.momentum if self.momentum is not None else 0.1
         z = Fn.bnact_fused(y, res, s1, s2, self.gamma.master, self.beta.master, mean, inv, scale, shift,
                            self.run_mean if upd else None, self.run_var if upd else None, self.eps, mom, act, alpha,
-                           res_affine=res_affine, row_scale=row_scale)
+                           res_affine=res_affine, row_scale=row_scale, prev_tot=prev_tot, prev_c=prev_c,
+                           tot_out=tot_out)
         if z is None:
             return None
         if upd:
@@ -1023,6 +1025,10 @@ class BNAct(Site):
         # input) is reduced - not the whole concatenation again
         object.__setattr__(self, 'cat_prev', None)
         object.__setattr__(self, '_last_stats', None)
+        # per-channel totals [2, Cp] published by the folded-finalize apply (read by the next BN
+        # of a concat chain); _tot_ok: this step's forward wrote them
+        self.k_tot = ctx.ws.request(f'{bn.name}@{id(self)}.tot', 2 * bn.Cp)
+        object.__setattr__(self, '_tot_ok', False)
         # concat-gradient hand-off (set by the lowering, _lower_dense_cats): this site's input
         # is also the first operand of a DenseCat whose backward runs first and leaves its
         # gradient slice here; the apply pass adds it (no copy, no autograd add)
@@ -1032,18 +1038,23 @@ class BNAct(Site):
     def forward(self, x, res=None):
         return _run(self, x, res) if res is not None else _run(self, x)
 
-    def _stats(self, yn, tail, s1, s2):
+    def _stats(self, yn, tail, s1, s2, use_tot):
+        """Fill the partial copies; returns (prev_tot, prev_c) when the older segment's sums are
+        to come from the previous BN's published totals instead of copies (folded finalize)."""
         A = self.cat_prev
         prev = A._last_stats if A is not None else None
         if prev is None or tail is None:
             Fn.bn_stats(yn, s1, s2)
-            return
+            return None, 0
         Cp, Ca = self.bn.Cp, A.bn.Cp
         tn = to_nhwc(tail, tail.shape[1])
         s1v, s2v = s1.view(-1, Cp), s2.view(-1, Cp)
+        Fn.bn_stats(tn, s1v[:, Ca:], s2v[:, Ca:], ld=Cp)
+        if use_tot and A._tot_ok:
+            return self.ctx.ws[A.k_tot], Ca
         s1v[:, :Ca].copy_(prev[0].view(-1, Ca))
         s2v[:, :Ca].copy_(prev[1].view(-1, Ca))
-        Fn.bn_stats(tn, s1v[:, Ca:], s2v[:, Ca:], ld=Cp)
+        return None, 0
 
     def _to(self, x):
         if x.dim() == 2:              # BatchNorm1d over [N, C] / [N, C, L]
@@ -1071,14 +1082,21 @@ class BNAct(Site):
         rn = self._to(res) if res is not None else None
         rows = yn.numel() // yn.shape[-1]
         stats = None
+        prev_tot, prev_c = None, 0
+        use_tot = yn.is_cuda and Fn._bn_fused_ok(bn.Cp, Fn.NSTAT)
         if bn.batch_stats():
             st = self.ctx.ws[self.k_st]
             n = Fn.NSTAT * bn.Cp
             stats = (st[:n], st[n:])
-            self._stats(yn, tail, *stats)
+            prev_tot, prev_c = self._stats(yn, tail, *stats, use_tot)
         object.__setattr__(self, '_last_stats', stats)
-        fused = bn.finalize_apply(stats[0], stats[1], yn, rn, self.act, self.alpha) if stats else None
+        object.__setattr__(self, '_tot_ok', False)
+        fused = bn.finalize_apply(stats[0], stats[1], yn, rn, self.act, self.alpha, prev_tot=prev_tot, prev_c=prev_c,
+                                  tot_out=self.ctx.ws[self.k_tot]) if stats else None
+        if prev_tot is not None and fused is None:
+            raise RuntimeError(f'{bn.name}: concat statistics expected the folded-finalize path')
         if fused is not None:
+            object.__setattr__(self, '_tot_ok', True)
             z, scale, shift, mean, inv = fused
         else:
             scale, shift, mean, inv = bn.finalize(stats[0] if stats else None, stats[1] if stats else None, rows)

@@ -165,6 +165,10 @@ def _models():
         'resnext50': (lambda: build_model('resnext50_32x4d', num_classes=10), (8, 3, 96, 96), 10),
         'se_resnext50': (lambda: build_model('se_resnext50_32x4d', num_classes=10), (8, 3, 96, 96), 10),
         'efficientnet-b0': (lambda: build_model('efficientnet-b0', num_classes=10), (8, 3, 96, 96), 10),
+        # concat statistics reuse, DenseCat gradient hand-offs
+        'densenet121': (lambda: build_model('densenet121', num_classes=10), (8, 3, 64, 64), 10),
+        # branch-point GradAccs (three convs and an average pool)
+        'inceptionv3': (lambda: build_model('inceptionv3', num_classes=10), (4, 3, 96, 96), 10),
         'unet-resnext50': (lambda: Unet(encoder_name='resnext50_32x4d', classes=1), (4, 3, 64, 64), None),
         'pspnet21': (lambda: PSPNet(encoder_name='resnet34', classes=21), (4, 3, 64, 64), 21),
         'linknet': (lambda: Linknet(encoder_name='resnet34', classes=1), (4, 3, 64, 64), None),
