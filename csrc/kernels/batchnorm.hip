@@ -297,6 +297,7 @@ __device__ __forceinline__ void fused_reduce(const float* __restrict__ a, const 
   __syncthreads();
 }
 
+template <int U>
 __global__ void __launch_bounds__(NT)
 bn_fwd_fused_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf16* __restrict__ z,
                     const float* __restrict__ sum, const float* __restrict__ sumsq, int ncopy,
@@ -347,31 +348,43 @@ bn_fwd_fused_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf
     rsc[j] = rscale_ ? rscale_[cg * 8 + j] : 1.f;
     rsh[j] = rscale_ ? rshift_[cg * 8 + j] : 0.f;
   }
-  for (long r = (long)part * rpi + t / gb; r < rows; r += (long)nparts * rpi) {
-    const long i = r * G + cg;
-    // both loads issued before either is used (one round trip per chunk, not two)
-    const uint4 yv = ldg16(y + i * 8);
-    const uint4 rv = res ? ldg16(res + i * 8) : make_uint4(0u, 0u, 0u, 0u);
-    float f[8];
-    unpack8(yv, f);
+  // U rows per thread per iteration, every load issued before any use (one round trip per
+  // U chunks; the y and residual loads of a chunk together)
+  const long step = (long)nparts * rpi;
+  for (long r0 = (long)part * rpi + t / gb; r0 < rows; r0 += step * U) {
+    uint4 yv[U], rv[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[j] + sh[j];
-    if (res) {
-      float q[8];
-      unpack8(rv, q);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += q[j] * rsc[j] + rsh[j];
+    for (int u = 0; u < U; ++u) {
+      const long r = min(r0 + u * step, rows - 1);      // clamped: always a valid row
+      yv[u] = ldg16(y + (r * G + cg) * 8);
+      rv[u] = res ? ldg16(res + (r * G + cg) * 8) : make_uint4(0u, 0u, 0u, 0u);
     }
-    if (relu) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    for (int u = 0; u < U; ++u) {
+      const long r = r0 + u * step;
+      if (r >= rows) break;
+      float f[8];
+      unpack8(yv[u], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[j] + sh[j];
+      if (res) {
+        float q[8];
+        unpack8(rv[u], q);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += q[j] * rsc[j] + rsh[j];
+      }
+      if (relu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+      }
+      *reinterpret_cast<uint4*>(z + (r * G + cg) * 8) = pack8(f);
     }
-    *reinterpret_cast<uint4*>(z + i * 8) = pack8(f);
   }
 }
 
 // dy = k1*dU + k2 + k3*(y-mean) with (k1, k2, k3) from the reduction copies (sums [ncopy][2][C])
 // folded in; dres = dU (optional); z != null applies the ReLU mask z > 0 to dz
+template <int U>
 __global__ void __launch_bounds__(NT)
 bn_bwd_fused_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const bf16* __restrict__ y,
                     const float* __restrict__ mean, const float* __restrict__ sums, int ncopy,
@@ -409,23 +422,36 @@ bn_bwd_fused_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, con
     k3[j] = lk[2][g * 8 + j];
     mu[j] = lmu[g * 8 + j];
   }
-  for (long r = (long)part * rpi + t / gb; r < rows; r += (long)nparts * rpi) {
-    const long i = r * G + cg;
-    const uint4 dv = ldg16(dz + i * 8), yv = ldg16(y + i * 8);
-    const uint4 zv = z ? ldg16(z + i * 8) : make_uint4(0u, 0u, 0u, 0u);
-    float d[8], yy[8], o[8];
-    unpack8(dv, d);
-    unpack8(yv, yy);
-    if (z) {
-      float zz[8];
-      unpack8(zv, zz);
+  const long step = (long)nparts * rpi;
+  for (long r0 = (long)part * rpi + t / gb; r0 < rows; r0 += step * U) {
+    uint4 dv[U], yv[U], zv[U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = zz[j] > 0.f ? d[j] : 0.f;
+    for (int u = 0; u < U; ++u) {
+      const long r = min(r0 + u * step, rows - 1);      // clamped: always a valid row
+      const long i = r * G + cg;
+      dv[u] = ldg16(dz + i * 8);
+      yv[u] = ldg16(y + i * 8);
+      zv[u] = z ? ldg16(z + i * 8) : make_uint4(0u, 0u, 0u, 0u);
     }
-    if (dres) *reinterpret_cast<uint4*>(dres + i * 8) = pack8(d);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = k1[j] * d[j] + k2[j] + k3[j] * (yy[j] - mu[j]);
-    *reinterpret_cast<uint4*>(dy + i * 8) = pack8(o);
+    for (int u = 0; u < U; ++u) {
+      const long r = r0 + u * step;
+      if (r >= rows) break;
+      const long i = r * G + cg;
+      float d[8], yy[8], o[8];
+      unpack8(dv[u], d);
+      unpack8(yv[u], yy);
+      if (z) {
+        float zz[8];
+        unpack8(zv[u], zz);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = zz[j] > 0.f ? d[j] : 0.f;
+      }
+      if (dres) *reinterpret_cast<uint4*>(dres + i * 8) = pack8(d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = k1[j] * d[j] + k2[j] + k3[j] * (yy[j] - mu[j]);
+      *reinterpret_cast<uint4*>(dy + i * 8) = pack8(o);
+    }
   }
 }
 
@@ -571,9 +597,11 @@ MLC_EXPORT int mlc_bn_fwd_fused(const bf16* y, const bf16* res, bf16* z, const f
                                 const float* rscale, const float* rshift, long rows, int C, float eps,
                                 float momentum, int relu, hipStream_t st) {
   if (!fused_ok(C, ncopy) || (rscale && !rshift) || rows < 1) return -1;
-  hipLaunchKernelGGL(bn_fwd_fused_kernel, dim3(fused_grid(rows, C)), dim3(NT), 0, st, y, res, z, sum, sumsq, ncopy,
-                     gamma, beta, save_mean, save_invstd, scale, shift, run_mean, run_var, rscale, rshift, rows, C,
-                     eps, momentum, relu);
+#define MLC_BNF(U) hipLaunchKernelGGL(bn_fwd_fused_kernel<U>, dim3(fused_grid(rows, C)), dim3(NT), 0, st, y, res, z, \
+                                      sum, sumsq, ncopy, gamma, beta, save_mean, save_invstd, scale, shift, run_mean, \
+                                      run_var, rscale, rshift, rows, C, eps, momentum, relu)
+  if (g_unroll >= 4) MLC_BNF(4); else if (g_unroll == 2) MLC_BNF(2); else MLC_BNF(1);
+#undef MLC_BNF
   return hipGetLastError();
 }
 
@@ -582,8 +610,10 @@ MLC_EXPORT int mlc_bn_bwd_fused(const bf16* dz, const bf16* z, const bf16* y, co
                                 int ncopy, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
                                 bf16* dy, bf16* dres, long rows, int C, hipStream_t st) {
   if (!fused_ok(C, ncopy) || rows < 1) return -1;
-  hipLaunchKernelGGL(bn_bwd_fused_kernel, dim3(fused_grid(rows, C)), dim3(NT), 0, st, dz, z, y, mean, sums, ncopy,
-                     invstd, gamma, dgamma, dbeta, dy, dres, rows, C);
+#define MLC_BNB(U) hipLaunchKernelGGL(bn_bwd_fused_kernel<U>, dim3(fused_grid(rows, C)), dim3(NT), 0, st, dz, z, y, \
+                                      mean, sums, ncopy, invstd, gamma, dgamma, dbeta, dy, dres, rows, C)
+  if (g_unroll >= 4) MLC_BNB(4); else if (g_unroll == 2) MLC_BNB(2); else MLC_BNB(1);
+#undef MLC_BNB
   return hipGetLastError();
 }
 

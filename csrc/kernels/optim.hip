@@ -249,6 +249,38 @@ MLC_EXPORT int mlc_adam(float* p, const float* g, float* m, float* v, bf16* pbf,
   return hipGetLastError();
 }
 
+// zero up to four fp32 buffers in one launch (a training step's scratch workspace and its
+// gradient arenas: one dispatch instead of one memset each)
+struct Zero4 {
+  float* p[4];
+  long n[4];
+};
+
+__global__ void __launch_bounds__(256) zero4_kernel(Zero4 z) {
+  const long stride = (long)gridDim.x * 256;
+  for (int b = 0; b < 4; ++b) {
+    float* p = z.p[b];
+    if (!p) continue;
+    const long n = z.n[b];
+    const long n4 = ((uintptr_t)p % 16 == 0) ? n / 4 : 0;    // 16-byte stores where aligned
+    float4* q = reinterpret_cast<float4*>(p);
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) q[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (long i = n4 * 4 + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) p[i] = 0.f;
+  }
+}
+
+MLC_EXPORT int mlc_zero4(float* p0, long n0, float* p1, long n1, float* p2, long n2, float* p3, long n3,
+                         hipStream_t st) {
+  Zero4 z{{p0, p1, p2, p3}, {p0 ? n0 : 0, p1 ? n1 : 0, p2 ? n2 : 0, p3 ? n3 : 0}};
+  long most = 0;
+  for (int b = 0; b < 4; ++b) most = z.n[b] > most ? z.n[b] : most;
+  long blocks = (most / 4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(zero4_kernel, dim3((unsigned)blocks), dim3(256), 0, st, z);
+  return hipGetLastError();
+}
+
 MLC_EXPORT int mlc_sqnorm(const float* x, long n, float* out, float scale, hipStream_t st) {
   long b = (n + NT * 8 - 1) / (NT * 8);
   if (b > 2048) b = 2048;

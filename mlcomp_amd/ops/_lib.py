@@ -118,6 +118,7 @@ _SIGS = {
     'mlc_dwconv_dgrad': [vp] * 3 + [i32] * 11 + [vp],
     'mlc_dwconv_wgrad': [vp] * 4 + [i32] * 12 + [vp],
     'mlc_bn_stats': [vp, vp, vp, i64, i32, vp],
+    'mlc_zero4': [vp, i64, vp, i64, vp, i64, vp, i64, vp],
     'mlc_bn_stats_ld': [vp, vp, vp, i64, i32, i32, vp],
     'mlc_bnact_apply': [vp] * 7 + [i64, i32, i32, f32, vp, i64, vp],
     'mlc_bnact_bwd_reduce': [vp] * 10 + [i64, i32, i32, f32, vp, i64, vp],

@@ -1268,6 +1268,24 @@ def conv2d_wgrad_bias(dy, x, w_shape, dbias, stride=1, pad=0, dil=1, out=None, a
     return conv2d_wgrad(dy, x, w_shape, stride, pad, dil, out=out, accumulate=accumulate)
 
 
+def zero_many(tensors):
+    """Zero contiguous fp32 tensors, up to four per launch (a step's workspace and gradient
+    arenas in one dispatch instead of one memset each)."""
+    ts = [t for t in tensors if t is not None and t.numel()]
+    if not ts:
+        return
+    if not _cuda(ts[0]) or any(t.dtype != torch.float32 or not t.is_contiguous() for t in ts):
+        for t in ts:
+            t.zero_()
+        return
+    for i in range(0, len(ts), 4):
+        chunk = ts[i:i + 4] + [None] * (4 - len(ts[i:i + 4]))
+        args = []
+        for t in chunk:
+            args += [_lib.ptr(t), t.numel() if t is not None else 0]
+        _lib.call('mlc_zero4', *args, _lib.stream())
+
+
 def bn_stats(x, s1, s2, ld=None):
     """Per-channel sum / sum of squares of NHWC x into (s1, s2) ([NSTAT*C] fp32 each, added);
     ``ld``: the copies' row stride (>= C; s1 / s2 then point at a channel offset of wider

@@ -791,7 +791,9 @@ class _HeadFn(torch.autograd.Function):
         ctx.h = h
         ctx.xshape = tuple(x.shape)
         ctx.save_for_backward(pooled, dl)
-        return ws[h.k_loss].clone()
+        # the workspace slot itself (no copy kernel): it is read before the next step's
+        # workspace zeroing, and the backward never reads it
+        return ws[h.k_loss].view(1)
 
     @staticmethod
     def backward(ctx, dloss):

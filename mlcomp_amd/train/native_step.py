@@ -90,11 +90,13 @@ class NativeClassifierStep(GraphedStep):
 
     # ------------------------------------------------------------------ step
     def _body(self):
-        self.net.ctx.ws.zero()
-        self.net.arena.zero_grad()   # one memset; wgrad kernels then accumulate
+        # the workspace and both gradient arenas in one launch; wgrad kernels then accumulate
+        Fn.zero_many([self.net.ctx.ws.buf] + [a.grad for a in self.net.arena.arenas()])
         self.bucketer.begin()
         loss = self.net.loss(self.x, self.y)
-        loss.backward()
+        if getattr(self, '_one', None) is None or self._one.device != loss.device:
+            self._one = torch.ones_like(loss)        # the backward seed, made once (not per step)
+        loss.backward(self._one)
         self.bucketer.finish()
         if not self.opt_in_bwd:
             self.opt.step()
