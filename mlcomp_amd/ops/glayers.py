@@ -184,7 +184,7 @@ def _nthwc(g: torch.Tensor, N: int, C: int, T: int, H: int, W: int) -> torch.Ten
     return g.to(torch.bfloat16).contiguous()
 
 
-def _link_grad(link: 'Frames', dx: Optional[torch.Tensor], x_shape) -> Optional[torch.Tensor]:
+def _link_grad(link: 'Frames', dx: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     """Receiver / sender side of a Frames gradient hand-off around the input gradient ``dx``
     of the site's 5D input (None when the caller already summed the pending addend)."""
     if link.send_to is not None:
@@ -217,7 +217,7 @@ class _TemporalUnfold(torch.autograd.Function):
         link = ctx.link
         dx = temporal_fold(g, N, C, T, H, W, kt, st, pt, dt, To, addend=_take_pending(link)).to(dtype)
         if link is not None:
-            dx = _link_grad(link, dx, (N, C, T, H, W))
+            dx = _link_grad(link, dx)
         return dx, None, None, None, None, None, None
 
 
@@ -239,7 +239,7 @@ class _GradLink(torch.autograd.Function):
             N, C, T, H, W = g.shape
             a = add.reshape(N, T, H, W, C).permute(0, 4, 1, 2, 3) if add.dim() == 4 else add
             g = g + a.to(g.dtype)
-        return _link_grad(link, g, tuple(g.shape)), None
+        return _link_grad(link, g), None
 
 
 class TemporalAs2d:
