@@ -29,6 +29,7 @@ NCCL watchdog, which the reference relies on through ``init_process_group('nccl'
 from __future__ import annotations
 
 import collections
+import contextlib
 import ctypes as C
 import os
 import threading
@@ -161,6 +162,21 @@ class Watchdog:
         self.lock = threading.Lock()
         self._thread = None
         self._stop = threading.Event()
+        # graph capture in progress (GraphedStep._capture): no probes - an event query from
+        # this thread while another thread captures invalidates the capture (global mode)
+        self._busy = threading.Lock()
+        self._paused = 0
+
+    @contextlib.contextmanager
+    def paused(self):
+        """No probe runs while the block runs (a pass in progress finishes first)."""
+        with self._busy:
+            self._paused += 1
+        try:
+            yield
+        finally:
+            with self._busy:
+                self._paused -= 1
 
     def register(self, comm: Watched):
         with self.lock:
@@ -238,10 +254,13 @@ class Watchdog:
 
     def _loop(self):
         while not self._stop.wait(self.poll):
-            try:
-                self.check_once()
-            except Exception:   # never let the watchdog thread die on a probe
-                pass
+            with self._busy:
+                if self._paused:
+                    continue
+                try:
+                    self.check_once()
+                except Exception:   # never let the watchdog thread die on a probe
+                    pass
 
 
 WATCHDOG = Watchdog(poll=float(os.environ.get('MLC_COMM_WATCHDOG_POLL', '1.0')))

@@ -20,6 +20,7 @@ step protocol from :class:`GraphedStep`:
 from __future__ import annotations
 
 import contextlib
+import gc
 import os
 import warnings
 
@@ -103,11 +104,23 @@ class GraphedStep:
         # the graph's split-K slabs and zero-on-entry scratch belong to this step (and
         # die with it): eager work elsewhere never writes what a replay reads
         self._capture_ws = {}
+        # no garbage collection while the stream captures: a collected object from earlier
+        # work (an event, a graph, a stream) whose destructor calls the HIP runtime during
+        # capture aborts the process (seen once in the full GPU suite: "Fatal Python error:
+        # Aborted" with "Garbage-collecting" at the top of the capturing thread's stack)
+        gc.collect()
+        was = gc.isenabled()
+        gc.disable()
+        from ..parallel.comm import WATCHDOG
         try:
-            with torch.cuda.graph(graph), Fn.capture_scope(self._capture_ws):
+            # the RCCL watchdog's event probes wait while this thread captures
+            with WATCHDOG.paused(), torch.cuda.graph(graph), Fn.capture_scope(self._capture_ws):
                 self._body()
         except Exception as e:   # capture refused (a collective or op the runtime cannot
             err = e              # capture): decided collectively below
+        finally:
+            if was:
+                gc.enable()
         torch.cuda.synchronize(self.device)
         if self._agree(err is None):
             return graph

@@ -113,6 +113,25 @@ def test_watchdog_thread_fails_a_stuck_step():
         c.check()
 
 
+def test_watchdog_probes_nothing_while_paused():
+    """GraphedStep captures inside ``WATCHDOG.paused()``: no event query / async-error probe
+    may run on the watchdog thread then (it would invalidate a global-mode capture); probing
+    resumes afterwards."""
+    import time
+    wd, c = Watchdog(poll=0.005), FakeComm(timeout=100.0)
+    probes = []
+    c._async_error = lambda: probes.append(time.monotonic()) or 0
+    wd.register(c)
+    with wd.paused():
+        t0 = time.monotonic()
+        time.sleep(0.1)
+        t1 = time.monotonic()
+    assert not [t for t in probes if t0 < t < t1]
+    time.sleep(0.1)
+    wd.stop()
+    assert [t for t in probes if t > t1], 'probing did not resume'
+
+
 def test_torch_comm_has_no_watchdog_hooks():
     """The gloo path keeps torch.distributed's own timeouts (GraphedStep only watches
     communicators with ``watch_stream``)."""
