@@ -1794,14 +1794,17 @@ MLC_EXPORT int mlc_gemm_get_set(int key, int value) {
 // in_sc/in_sh (optional, [C] fp32): x is the PRE-BatchNorm tensor of a ReLU BN and the
 // conv reads relu(x * in_sc + in_sh) (BnIn transform in the A loader; zero padding stays
 // zero), so the BN output never has to be written.
-MLC_EXPORT int mlc_conv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, float* sumsq,
-                            int N, int H, int W, int C, int Co, int KH, int KW, int stride,
-                            int pad, int dil, int Ho, int Wo, const float* in_sc, const float* in_sh,
-                            hipStream_t st) {
-  if (C % 8 || Co % 8 || KH > 15 || KW > 16 || ((in_sc == nullptr) != (in_sh == nullptr))) return -1;
+// y rows of stride ldy >= Co (ldy > Co: y is a channel slice of wider rows - a DenseNet layer's
+// new features written straight into its block's concat buffer)
+static int conv_fwd_impl(const bf16* x, const bf16* w, bf16* y, int ldy, float* sum, float* sumsq,
+                         int N, int H, int W, int C, int Co, int KH, int KW, int stride,
+                         int pad, int dil, int Ho, int Wo, const float* in_sc, const float* in_sh,
+                         hipStream_t st) {
+  if (C % 8 || Co % 8 || ldy < Co || ldy % 8 || KH > 15 || KW > 16 || ((in_sc == nullptr) != (in_sh == nullptr)))
+    return -1;
   const int M = N * Ho * Wo, K = KH * KW * C;
   const int tile = pick_tile(M, Co);
-  EpiBF16<> epi{y, Co, sum, sumsq, IdentityRows{}};
+  EpiBF16<> epi{y, ldy, sum, sumsq, IdentityRows{}};
   epi.ncopy = g_mlc_ncopy;
   if (sum && g_mlc_det && (M + 63) / 64 > g_mlc_ncopy) return -2;   // one copy per 64-row group
   const BnIn bn{in_sc, in_sh};
@@ -1826,6 +1829,19 @@ MLC_EXPORT int mlc_conv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, f
   MLC_TILE_DISPATCH(tile, M, Co, K, 1, st, epi, MKA, MKB);
 #undef MKA
 #undef MKB
+}
+
+MLC_EXPORT int mlc_conv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum, float* sumsq,
+                            int N, int H, int W, int C, int Co, int KH, int KW, int stride,
+                            int pad, int dil, int Ho, int Wo, const float* in_sc, const float* in_sh,
+                            hipStream_t st) {
+  return conv_fwd_impl(x, w, y, Co, sum, sumsq, N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo, in_sc, in_sh, st);
+}
+
+MLC_EXPORT int mlc_conv_fwd_ld(const bf16* x, const bf16* w, bf16* y, int ldy, int N, int H, int W, int C, int Co,
+                               int KH, int KW, int stride, int pad, int dil, int Ho, int Wo, hipStream_t st) {
+  return conv_fwd_impl(x, w, y, ldy, nullptr, nullptr, N, H, W, C, Co, KH, KW, stride, pad, dil, Ho, Wo, nullptr,
+                       nullptr, st);
 }
 
 // dx[N,H,W,C] = conv_transpose(dy[N,Ho,Wo,Co], w) (+ addend, same layout as dx; may

@@ -80,9 +80,19 @@ __device__ __forceinline__ void load_ch(Ch& c, const float* scale, const float* 
   }
 }
 
+// element offset of 8-channel chunk i (row i / G, group i % G) in rows of stride ld elements
+// (ld == 8G: dense rows; otherwise a channel slice of wider rows - a DenseNet concat buffer's
+// channels - and rows * G < 2^32, checked on the host)
+__device__ __forceinline__ long chunk_off(long i, int G, long ld) {
+  if (ld == 8L * G) return i * 8;
+  const unsigned q = (unsigned)i / (unsigned)G;
+  return (long)q * ld + (long)((unsigned)i - q * (unsigned)G) * 8;
+}
+
+// x rows of stride x_ld (chunk_off); copies of row stride ld
 __global__ void __launch_bounds__(NT)
 stats_kernel(const bf16* __restrict__ x, float* __restrict__ sum, float* __restrict__ sumsq, long rows, int C,
-             int ncopy, int ld) {
+             int ncopy, int ld, long x_ld) {
   __shared__ float rb[NT][17];
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
@@ -94,7 +104,7 @@ stats_kernel(const bf16* __restrict__ x, float* __restrict__ sum, float* __restr
   long i = gtid;
   for (; i + stride < total; i += 2 * stride) {
     float f[8], g[8];
-    const uint4 a = ldg16(x + i * 8), b = ldg16(x + (i + stride) * 8);
+    const uint4 a = ldg16(x + chunk_off(i, G, x_ld)), b = ldg16(x + chunk_off(i + stride, G, x_ld));
     unpack8(a, f);
     unpack8(b, g);
 #pragma unroll
@@ -102,7 +112,7 @@ stats_kernel(const bf16* __restrict__ x, float* __restrict__ sum, float* __restr
   }
   if (i < total) {
     float f[8];
-    unpack8(ldg16(x + i * 8), f);
+    unpack8(ldg16(x + chunk_off(i, G, x_ld)), f);
 #pragma unroll
     for (int e = 0; e < 8; ++e) { s1[e] += f[e]; s2[e] += f[e] * f[e]; }
   }
@@ -132,10 +142,10 @@ stats_kernel(const bf16* __restrict__ x, float* __restrict__ sum, float* __restr
 // z chunk i = act(y*scale + shift [* row scale] [+ res*rscale + rshift]); y and res loads
 // issued together (one round trip per chunk)
 template <int ACT>
-__device__ __forceinline__ void apply_chunk(const bf16* __restrict__ y, const bf16* __restrict__ res,
+__device__ __forceinline__ void apply_chunk(const bf16* __restrict__ y, long yo, const bf16* __restrict__ res,
                                             bf16* __restrict__ z, long i, int G, const Ch& c, int act, float alpha,
                                             const RowScale& rsc) {
-  const uint4 yv = ldg16(y + i * 8);
+  const uint4 yv = ldg16(y + yo);
   const uint4 rv = res ? ldg16(res + i * 8) : make_uint4(0u, 0u, 0u, 0u);
   float f[8];
   unpack8(yv, f);
@@ -175,7 +185,7 @@ apply_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf16* __r
   load_ch(c, scale, shift, rscale, rshift, c0);
   const long total = rows * G;
   for (long i = gtid; i < total; i += stride)
-    apply_chunk<ACT>(y, res, z, i, G, c, act, alpha, rsc);
+    apply_chunk<ACT>(y, i * 8, res, z, i, G, c, act, alpha, rsc);
 }
 
 // the fused finalize of batchnorm.hip (bn_fwd_fused_kernel) for the generic engine: each block
@@ -193,7 +203,7 @@ apply_fused_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf1
                    float* __restrict__ run_mean, float* __restrict__ run_var, const float* __restrict__ rscale,
                    const float* __restrict__ rshift, long rows, int C, float eps, float momentum, int act_,
                    float alpha, RowScale rsc, const float* __restrict__ prev_tot, int prev_c,
-                   float* __restrict__ tot_out) {
+                   float* __restrict__ tot_out, long y_ld) {
   const int act = ACT >= 0 ? ACT : act_;
   __shared__ float red[2][NT], lsc[FG * 8], lsh[FG * 8];
   const int G = C >> 3;
@@ -250,7 +260,7 @@ apply_fused_kernel(const bf16* __restrict__ y, const bf16* __restrict__ res, bf1
     c.rh[j] = rscale ? rshift[cg * 8 + j] : 0.f;
   }
   for (long r = (long)part * rpi + t / gb; r < rows; r += (long)nparts * rpi)
-    apply_chunk<ACT>(y, res, z, r * G + cg, G, c, act, alpha, rsc);
+    apply_chunk<ACT>(y, r * y_ld + cg * 8, res, z, r * G + cg, G, c, act, alpha, rsc);
 }
 
 // dU of one chunk: dz * act'(a), a recomputed from y (and res) with the forward's affine
@@ -280,7 +290,7 @@ bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const
                   const bf16* __restrict__ res, const float* __restrict__ mean, const float* __restrict__ scale,
                   const float* __restrict__ shift, const float* __restrict__ rscale, const float* __restrict__ rshift,
                   float* __restrict__ sums, long rows, int C, int act, float alpha, int direct, RowScale rsc,
-                  int ncopy) {
+                  int ncopy, long y_ld) {
   __shared__ float rb[NT][17];
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
@@ -298,7 +308,7 @@ bwd_reduce_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const
     const long i1 = two ? i0 + stride : i0;
     uint4 dv[2], yv[2], zv[2], rv[2];
     dv[0] = ldg16(dz + i0 * 8); dv[1] = ldg16(dz + i1 * 8);
-    yv[0] = ldg16(y + i0 * 8); yv[1] = ldg16(y + i1 * 8);
+    yv[0] = ldg16(y + chunk_off(i0, G, y_ld)); yv[1] = ldg16(y + chunk_off(i1, G, y_ld));
     zv[0] = z ? ldg16(z + i0 * 8) : z4; zv[1] = z ? ldg16(z + i1 * 8) : z4;
     rv[0] = res ? ldg16(res + i0 * 8) : z4; rv[1] = res ? ldg16(res + i1 * 8) : z4;
 #pragma unroll
@@ -356,7 +366,8 @@ bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const 
                  const bf16* __restrict__ res, const float* __restrict__ mean, const float* __restrict__ coef,
                  const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ rscale,
                  const float* __restrict__ rshift, bf16* __restrict__ dy, bf16* __restrict__ dres, long rows, int C,
-                 int act, float alpha, RowScale rsc, const bf16* __restrict__ add, long add_ld) {
+                 int act, float alpha, RowScale rsc, const bf16* __restrict__ add, long add_ld, long y_ld,
+                 bf16* __restrict__ dy2, int gsplit) {
   const int G = C >> 3;
   const long gtid = (long)blockIdx.x * NT + threadIdx.x;
   const long stride = (long)gridDim.x * NT;
@@ -374,10 +385,10 @@ bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const 
   const long total = rows * G;
   const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
   for (long i = gtid; i < total; i += stride) {
-    const uint4 dv = ldg16(dz + i * 8), yv = ldg16(y + i * 8);
+    const uint4 dv = ldg16(dz + i * 8), yv = ldg16(y + chunk_off(i, G, y_ld));
     const uint4 zv = z ? ldg16(z + i * 8) : z4, rv = res ? ldg16(res + i * 8) : z4;
     // another consumer's gradient of y, rows of stride add_ld (a DenseNet concat's slice)
-    const uint4 av = add ? ldg16(add + (i / G) * add_ld + (i % G) * 8) : z4;
+    const uint4 av = add ? ldg16(add + chunk_off(i, G, add_ld)) : z4;
     float d[8], yy[8], o[8];
     unpack8(dv, d);
     unpack8(yv, yy);
@@ -396,7 +407,12 @@ bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ z, const 
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] += q[j];
     }
-    *reinterpret_cast<uint4*>(dy + i * 8) = pack8(o);
+    bf16* dst = dy + i * 8;
+    if (dy2) {      // channel groups [0, gsplit) to dy (rows of 8*gsplit), the rest to dy2
+      const unsigned q = (unsigned)i / (unsigned)G, g = (unsigned)i - q * (unsigned)G;
+      dst = (int)g < gsplit ? dy + ((long)q * gsplit + g) * 8 : dy2 + ((long)q * (G - gsplit) + (g - gsplit)) * 8;
+    }
+    *reinterpret_cast<uint4*>(dst) = pack8(o);
   }
 }
 
@@ -616,6 +632,13 @@ inline int apply_cap() {
   return v;
 }
 
+// y's row stride (0: dense); -1 when it cannot be addressed (chunk_off's 32-bit row index)
+inline long y_stride(long y_ld, long rows, int C) {
+  if (y_ld == 0) return C;
+  if (y_ld < C || y_ld % 8 || (y_ld != C && rows * (C / 8) >= (1L << 32))) return -1;
+  return y_ld;
+}
+
 inline int blocks_for(long work) {
   long b = (work + NT - 1) / NT;
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
@@ -636,17 +659,22 @@ MLC_EXPORT int mlc_bn_stats(const bf16* x, float* sum, float* sumsq, long rows, 
   if (C % 8) return -1;
   const int blocks = grid_for(rows, C, reduce_cap());
   if (!det_blocks_ok(blocks)) return -2;
-  hipLaunchKernelGGL(stats_kernel, dim3(blocks), dim3(NT), 0, st, x, sum, sumsq, rows, C, atomic_copies(), C);
+  hipLaunchKernelGGL(stats_kernel, dim3(blocks), dim3(NT), 0, st, x, sum, sumsq, rows, C, atomic_copies(), C,
+                     (long)C);
   return hipGetLastError();
 }
 
 // the same into copies of row stride ld >= C (a channel slice of a wider BatchNorm's statistics:
-// a DenseNet concat's new segment, its older channels' sums copied from the previous BN)
-MLC_EXPORT int mlc_bn_stats_ld(const bf16* x, float* sum, float* sumsq, long rows, int C, int ld, hipStream_t st) {
-  if (C % 8 || ld < C) return -1;
+// a DenseNet concat's new segment, its older channels' sums copied from the previous BN), x
+// read as rows of stride x_ld (0: dense; > C: the new segment in place in the block's concat
+// buffer)
+MLC_EXPORT int mlc_bn_stats_ld(const bf16* x, float* sum, float* sumsq, long rows, int C, int ld, long x_ld,
+                               hipStream_t st) {
+  x_ld = y_stride(x_ld, rows, C);
+  if (C % 8 || ld < C || x_ld < 0) return -1;
   const int blocks = grid_for(rows, C, reduce_cap());
   if (!det_blocks_ok(blocks)) return -2;
-  hipLaunchKernelGGL(stats_kernel, dim3(blocks), dim3(NT), 0, st, x, sum, sumsq, rows, C, atomic_copies(), ld);
+  hipLaunchKernelGGL(stats_kernel, dim3(blocks), dim3(NT), 0, st, x, sum, sumsq, rows, C, atomic_copies(), ld, x_ld);
   return hipGetLastError();
 }
 
@@ -667,10 +695,11 @@ MLC_EXPORT int mlc_bnact_fused(const bf16* y, const bf16* res, bf16* z, const fl
                                float* scale, float* shift, float* run_mean, float* run_var, const float* rscale,
                                const float* rshift, long rows, int C, float eps, float momentum, int act, float alpha,
                                const float* row_scale, long hw, const float* prev_tot, int prev_c, float* tot_out,
-                               hipStream_t st) {
+                               long y_ld, hipStream_t st) {
   const int G = C >> 3;
+  y_ld = y_stride(y_ld, rows, C);
   if (C % 8 || (rscale && !rshift) || (row_scale && (act != 0 || hw < 1)) || rows < 1 || ncopy < 1 || ncopy > 64 ||
-      G < 1 || prev_c < 0 || prev_c > C)
+      G < 1 || prev_c < 0 || prev_c > C || y_ld < 0)
     return -1;
   const int gb = slice_groups(G, FG), nslices = G / gb, rpi = NT / gb;
   long parts = (rows + (long)rpi * 4 - 1) / ((long)rpi * 4);
@@ -681,7 +710,7 @@ MLC_EXPORT int mlc_bnact_fused(const bf16* y, const bf16* res, bf16* z, const fl
   const RowScale rsc{row_scale, hw};
   NA_LAUNCH(apply_fused_kernel, parts * nslices, st, act, y, res, z, sum, sumsq, ncopy, gamma, beta, mean, invstd,
             scale, shift, run_mean, run_var, rscale, rshift, rows, C, eps, momentum, act, alpha, rsc, prev_tot, prev_c,
-            tot_out);
+            tot_out, y_ld);
   return hipGetLastError();
 }
 
@@ -689,13 +718,14 @@ MLC_EXPORT int mlc_bnact_fused(const bf16* y, const bf16* res, bf16* z, const fl
 MLC_EXPORT int mlc_bnact_bwd_reduce(const bf16* dz, const bf16* z, const bf16* y, const bf16* res, const float* mean,
                                     const float* scale, const float* shift, const float* rscale, const float* rshift,
                                     float* sums, long rows, int C, int act, float alpha, const float* row_scale, long hw,
-                                    hipStream_t st) {
-  if (C % 8 || (row_scale && (act != 0 || hw < 1))) return -1;
+                                    long y_ld, hipStream_t st) {
+  y_ld = y_stride(y_ld, rows, C);
+  if (C % 8 || (row_scale && (act != 0 || hw < 1)) || y_ld < 0) return -1;
   const RowScale rsc{row_scale, hw};
   const int blocks = grid_for(rows, C, reduce_cap());
   if (!det_blocks_ok(blocks)) return -2;
   NA_LAUNCH(bwd_reduce_kernel, blocks, st, act, dz, z, y, res, mean, scale, shift, rscale,
-            rshift, sums, rows, C, act, alpha, 0, rsc, atomic_copies());
+            rshift, sums, rows, C, act, alpha, 0, rsc, atomic_copies(), y_ld);
   return hipGetLastError();
 }
 
@@ -704,15 +734,20 @@ MLC_EXPORT int mlc_bnact_bwd_reduce(const bf16* dz, const bf16* z, const bf16* y
 // instead of float atomics onto 32 copies: reduce -> finalize over the rows -> apply.
 // rscale / rshift (optional): the residual is another BatchNorm's input, applied in the
 // forward as res*rscale + rshift (a folded shortcut BN); the activation derivative is taken
-// at that pre-activation.
+// at that pre-activation.  dy2 (optional): dy split by channel - channels [0, c_split) to dy
+// (rows of c_split), the rest to dy2 (rows of C - c_split): the two operands' gradients of a
+// DenseNet concatenation, each dense.
 MLC_EXPORT int mlc_bnact_bwd(const bf16* dz, const bf16* z, const bf16* y, const bf16* res, const float* mean,
                              const float* scale, const float* shift, const float* rscale, const float* rshift,
                              const float* invstd, const float* gamma,
                              float* part, long part_floats, float* coef, float* dgamma, float* dbeta, bf16* dy,
                              bf16* dres, long rows, int C, int act, float alpha, const float* row_scale, long hw,
-                             const bf16* add, long add_ld, hipStream_t st) {
+                             const bf16* add, long add_ld, long y_ld, bf16* dy2, int c_split, hipStream_t st) {
   if (row_scale && (act != 0 || hw < 1)) return -1;
-  if (add && (add_ld < C || add_ld % 8)) return -1;
+  if (dy2 && (c_split <= 0 || c_split >= C || c_split % 8 || rows * (C / 8) >= (1L << 32))) return -1;
+  if (add && (add_ld < C || add_ld % 8 || (add_ld != C && rows * (C / 8) >= (1L << 32)))) return -1;
+  y_ld = y_stride(y_ld, rows, C);
+  if (y_ld < 0) return -1;
   const RowScale rsc{row_scale, hw};
   const int G = C >> 3;
   if (C % 8 || G > NT || part_floats < 2L * C || (rscale && !rshift)) return -1;
@@ -722,22 +757,27 @@ MLC_EXPORT int mlc_bnact_bwd(const bf16* dz, const bf16* z, const bf16* y, const
   while (blocks > cap && blocks > 1) blocks = grid_for(rows, C, blocks / 2);   // rounding to C/8 multiples
   if ((long)blocks * 2 * C > part_floats) return -1;
   NA_LAUNCH(bwd_reduce_kernel, blocks, st, act, dz, z, y, res, mean, scale, shift, rscale, rshift, part, rows, C, act,
-            alpha, 1, rsc, 1);
+            alpha, 1, rsc, 1, y_ld);
   hipLaunchKernelGGL(bwd_finalize_rows_kernel, dim3((C + NT / 64 - 1) / (NT / 64)), dim3(NT), 0, st, part, blocks,
                      invstd, gamma, coef, dgamma, dbeta, rows, C);
   NA_LAUNCH(bwd_apply_kernel, grid_for(rows, C, apply_cap()), st, act, dz, z, y, res, mean, coef, scale, shift, rscale, rshift,
-            dy, dres, rows, C, act, alpha, rsc, add, add_ld);
+            dy, dres, rows, C, act, alpha, rsc, add, add_ld, y_ld, dy2, c_split / 8);
   return hipGetLastError();
 }
 
 MLC_EXPORT int mlc_bnact_bwd_apply(const bf16* dz, const bf16* z, const bf16* y, const bf16* res, const float* mean,
                                    const float* coef, const float* scale, const float* shift, const float* rscale,
                                    const float* rshift, bf16* dy, bf16* dres, long rows, int C, int act, float alpha,
-                                   const float* row_scale, long hw, const bf16* add, long add_ld, hipStream_t st) {
-  if (C % 8 || (row_scale && (act != 0 || hw < 1)) || (add && (add_ld < C || add_ld % 8))) return -1;
+                                   const float* row_scale, long hw, const bf16* add, long add_ld, long y_ld,
+                                   bf16* dy2, int c_split, hipStream_t st) {
+  if (dy2 && (c_split <= 0 || c_split >= C || c_split % 8 || rows * (C / 8) >= (1L << 32))) return -1;
+  y_ld = y_stride(y_ld, rows, C);
+  if (C % 8 || (row_scale && (act != 0 || hw < 1)) || y_ld < 0 ||
+      (add && (add_ld < C || add_ld % 8 || (add_ld != C && rows * (C / 8) >= (1L << 32)))))
+    return -1;
   const RowScale rsc{row_scale, hw};
   NA_LAUNCH(bwd_apply_kernel, grid_for(rows, C, apply_cap()), st, act, dz, z, y, res, mean, coef, scale, shift, rscale, rshift,
-            dy, dres, rows, C, act, alpha, rsc, add, add_ld);
+            dy, dres, rows, C, act, alpha, rsc, add, add_ld, y_ld, dy2, c_split / 8);
   return hipGetLastError();
 }
 

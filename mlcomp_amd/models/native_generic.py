@@ -45,7 +45,7 @@ import torch.nn.functional as F
 
 from mlcomp_amd.ops import functional as Fn
 from mlcomp_amd.ops.glayers import (AdaptiveAvgPool, AvgPool, BilinearUp, BNAct, BNParams, ChannelGate, Conv3dAs2d,
-                                    ConvBNAct, ConvParams, DenseCat, Frames, GlobalAvgPool, GradAcc, LinearAct, LinearParams,
+                                    ConvBNAct, ConvParams, DenseCat, DenseChain, Frames, GlobalAvgPool, GradAcc, LinearAct, LinearParams,
                                     MaxPool, TemporalAs2d, UpCat, VolumePool)
 from mlcomp_amd.ops import gtransformer as GT
 from mlcomp_amd.ops.layers import NativeContext
@@ -923,6 +923,86 @@ class _Lowering:
             self._replace([cat], new)
             object.__setattr__(sa, 'slice_expected', True)
 
+    def _chain_dense_cats(self):
+        """Runs of :class:`DenseCat` sites each over the previous one's output (a DenseNet block)
+        share one concat buffer (glayers.DenseChain).  An inner concatenation's only users are
+        the next DenseCat and its layer's first BN site (``_lower_dense_cats`` checked that),
+        and both read the buffer's leading channels in place.  ``MLC_DENSE_CHAIN=0``: off (A/B)."""
+        if os.environ.get('MLC_DENSE_CHAIN', '1') != '1':
+            return
+        mods = dict(self.gm.named_modules())
+
+        def dense_cat(n):
+            return isinstance(n, fx.Node) and n.op == 'call_module' and isinstance(mods.get(n.target), DenseCat)
+
+        runs = []
+        for n in self.gm.graph.nodes:
+            if not dense_cat(n):
+                continue
+            site = mods[n.target]
+            a, b = n.args[0], n.args[1]
+            ca, cb = site.a_site.bn.C, self._channels(b)
+            if cb is None or cb % 8 or ca % 8:
+                continue
+            prev = mods[a.target] if dense_cat(a) else None
+            run = next((r for r in runs if prev is not None and r[-1][0] is prev), None)
+            if run is not None and run[-1][1] == ca and len(a.users) == 2:     # n and its layer's BN
+                run.append((site, ca + cb))
+            else:
+                runs.append([(site, ca + cb)])
+        node_of = {mods[n.target]: n for n in self.gm.graph.nodes if dense_cat(n)}
+        for run in runs:
+            if len(run) < 2:
+                continue
+            chain = DenseChain(run[-1][1])
+            for site, _ in run:
+                object.__setattr__(site, 'chain', chain)
+                self._cat_out(node_of[site], site)
+            object.__setattr__(run[0][0], 'chain_first', True)
+            object.__setattr__(run[-1][0], 'chain_last', True)
+
+    def _split_cat_grads(self):
+        """A DenseCat whose output's gradient comes from one BN site X alone (its other users
+        are DenseCats, whose backward hands their first operand's gradient on instead of
+        returning it): X's apply pass stores that gradient as the two operands' gradients, each
+        dense (BNAct.split_to) - no strided slice of it is copied for the growth conv's
+        backward.  ``MLC_DENSE_CHAIN=0``: off (A/B)."""
+        if os.environ.get('MLC_DENSE_CHAIN', '1') != '1':
+            return
+        mods = dict(self.gm.named_modules())
+        for n in self.gm.graph.nodes:
+            d = mods.get(n.target) if n.op == 'call_module' else None
+            if not isinstance(d, DenseCat):
+                continue
+            xs = [u for u in n.users if u.op == 'call_module' and isinstance(mods.get(u.target), BNAct)
+                  and u.args and u.args[0] is n]
+            cats = [u for u in n.users if u.op == 'call_module' and isinstance(mods.get(u.target), DenseCat)
+                    and u.args[0] is n and u.args[1] is not n]
+            if len(xs) != 1 or len(xs) + len(cats) != len(n.users) or xs[0].args[1:].count(n):
+                continue
+            x = mods[xs[0].target]
+            if (x.residual or x.acc is not None or x.bn.C != x.bn.Cp or d.off % 8 or not 0 < d.off < x.bn.C
+                    or x.split_to is not None):
+                continue
+            object.__setattr__(x, 'split_to', d)
+            object.__setattr__(d, 'split_expected', True)
+
+    def _cat_out(self, n: fx.Node, site):
+        """The new segment b of chained DenseCat ``n``: a plain dense conv (no BN / bias /
+        activation / residual) whose other users only take b's statistics in place (the next
+        BN's concat tail) writes its output straight into the block's concat buffer."""
+        b = n.args[1]
+        conv = getattr(self.gm, b.target, None) if isinstance(b, fx.Node) and b.op == 'call_module' else None
+        if (not isinstance(conv, ConvBNAct) or conv.bn is not None or conv.conv.kind != 'dense' or conv.conv.b is not None
+                or conv.act or conv.residual or conv.epi_act or conv.conv.Co != conv.conv.Cop or len(b.args) != 1):
+            return
+        for u in b.users:
+            m = getattr(self.gm, u.target, None) if u.op == 'call_module' else None
+            if u is not n and not (isinstance(m, BNAct) and m.cat_prev is not None and len(u.args) == 2
+                                   and u.args[1] is b and u.args[0] is not b):
+                return
+        object.__setattr__(conv, 'cat_out', site)
+
     def _link_bn_backward(self):
         """A conv+BN site A (ReLU or no activation, batch statistics) whose output is used
         only as the input of a dense conv site B (and, at a residual block boundary, as the
@@ -1081,6 +1161,8 @@ class _Lowering:
         self._link_fanout()
         self._link_cat_stats()
         self._lower_dense_cats()
+        self._chain_dense_cats()
+        self._split_cat_grads()
         self._link_bn_backward()
         g.lint()
         self.gm.delete_all_unused_submodules()

@@ -30,6 +30,7 @@ vp, i32, i64, f32, u32 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_uint
 
 _SIGS = {
     'mlc_conv_fwd': [vp, vp, vp, vp, vp] + [i32] * 12 + [vp, vp, vp],
+    'mlc_conv_fwd_ld': [vp, vp, vp] + [i32] * 13 + [vp],
     'mlc_conv_dgrad': [vp] * 4 + [i32] * 12 + [vp] * 11 + [vp],
     'mlc_conv_dgrad_t': [vp] * 4 + [i32] * 12 + [vp] * 11 + [vp],
     'mlc_bilinear_up_fwd': [vp, vp] + [i32] * 6 + [vp],
@@ -85,7 +86,7 @@ _SIGS = {
     'mlc_bn_bwd_finalize': [vp] * 6 + [i64, i32, vp],
     'mlc_bn_fwd_fused': [vp] * 5 + [i32] + [vp] * 10 + [i64, i32, f32, f32, i32, vp],
     'mlc_bn_bwd_fused': [vp] * 5 + [i32] + [vp] * 6 + [i64, i32, vp],
-    'mlc_bnact_fused': [vp] * 5 + [i32] + [vp] * 10 + [i64, i32, f32, f32, i32, f32, vp, i64, vp, i32, vp, vp],
+    'mlc_bnact_fused': [vp] * 5 + [i32] + [vp] * 10 + [i64, i32, f32, f32, i32, f32, vp, i64, vp, i32, vp, i64, vp],
     'mlc_bn_bwd_apply': [vp] * 7 + [i64, i32, vp],
     'mlc_maxpool_fwd': [vp, vp, vp] + [i32] * 9 + [vp],
     'mlc_maxpool_bwd': [vp, vp, vp] + [i32] * 9 + [vp],
@@ -119,11 +120,11 @@ _SIGS = {
     'mlc_dwconv_wgrad': [vp] * 4 + [i32] * 12 + [vp],
     'mlc_bn_stats': [vp, vp, vp, i64, i32, vp],
     'mlc_zero4': [vp, i64, vp, i64, vp, i64, vp, i64, vp],
-    'mlc_bn_stats_ld': [vp, vp, vp, i64, i32, i32, vp],
+    'mlc_bn_stats_ld': [vp, vp, vp, i64, i32, i32, i64, vp],
     'mlc_bnact_apply': [vp] * 7 + [i64, i32, i32, f32, vp, i64, vp],
-    'mlc_bnact_bwd_reduce': [vp] * 10 + [i64, i32, i32, f32, vp, i64, vp],
-    'mlc_bnact_bwd': [vp] * 12 + [i64] + [vp] * 5 + [i64, i32, i32, f32, vp, i64, vp, i64, vp],
-    'mlc_bnact_bwd_apply': [vp] * 12 + [i64, i32, i32, f32, vp, i64, vp, i64, vp],
+    'mlc_bnact_bwd_reduce': [vp] * 10 + [i64, i32, i32, f32, vp, i64, i64, vp],
+    'mlc_bnact_bwd': [vp] * 12 + [i64] + [vp] * 5 + [i64, i32, i32, f32, vp, i64, vp, i64, i64, vp, i32, vp],
+    'mlc_bnact_bwd_apply': [vp] * 12 + [i64, i32, i32, f32, vp, i64, vp, i64, i64, vp, i32, vp],
     'mlc_act_fwd': [vp, vp, i64, i32, f32, vp],
     'mlc_act_bwd': [vp] * 4 + [i64, i32, f32, vp],
     'mlc_chscale_fwd': [vp] * 4 + [i32, i64, i32, i32, vp],

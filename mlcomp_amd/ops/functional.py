@@ -66,6 +66,12 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, stride=1, pad=0, dil=1,
     Ho, Wo = conv_out_hw(H, W, KH, KW, stride, pad, dil)
     if _cuda(x):
         y = out if out is not None else torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.bfloat16)
+        ldy = rows_ld(y)
+        if ldy != Co:       # out: the channel slice of wider rows (a DenseNet block's concat buffer)
+            assert ldy is not None and stats is None and in_affine is None, (y.shape, y.stride())
+            _lib.call('mlc_conv_fwd_ld', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), ldy, N, H, W, C, Co, KH, KW, stride,
+                      pack_pad(pad), dil, Ho, Wo, _lib.stream())
+            return y
         s1, s2 = (stats if stats is not None else (None, None))
         sc, sh = in_affine if in_affine is not None else (None, None)
         _lib.call('mlc_conv_fwd', _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(s1), _lib.ptr(s2),
@@ -1286,17 +1292,42 @@ def zero_many(tensors):
         _lib.call('mlc_zero4', *args, _lib.stream())
 
 
+def rows_ld(t):
+    """Row stride of an ``[..., C]`` tensor stored as rows of C contiguous elements at one fixed
+    stride: C when dense, > C for the leading channels of wider rows (a DenseNet concat buffer's
+    view); None for any other layout."""
+    C = t.shape[-1]
+    if t.dim() < 2 or t.stride(-1) != 1:
+        return C if t.dim() == 1 and t.stride(-1) == 1 else None
+    ld = t.stride(-2)
+    want = ld
+    for d in range(t.dim() - 2, -1, -1):
+        if t.shape[d] != 1 and t.stride(d) != want:
+            return None
+        want *= t.shape[d]
+    return ld if ld >= C else None
+
+
+def dense_rows(t):
+    """``t`` itself when its rows are dense, else a contiguous copy (for passes that read dense rows)."""
+    return t if rows_ld(t) == t.shape[-1] else t.contiguous()
+
+
 def bn_stats(x, s1, s2, ld=None):
     """Per-channel sum / sum of squares of NHWC x into (s1, s2) ([NSTAT*C] fp32 each, added);
     ``ld``: the copies' row stride (>= C; s1 / s2 then point at a channel offset of wider
-    statistics buffers)."""
+    statistics buffers).  x may be the channel slice of wider rows (:func:`rows_ld`)."""
     C = x.shape[-1]
     rows = x.numel() // C
     if _cuda(x):
-        if ld is None:
+        x_ld = rows_ld(x)
+        if x_ld is None:
+            x, x_ld = x.contiguous(), C
+        if ld is None and x_ld == C:
             _lib.call('mlc_bn_stats', _lib.ptr(x), _lib.ptr(s1), _lib.ptr(s2), rows, C, _lib.stream())
         else:
-            _lib.call('mlc_bn_stats_ld', _lib.ptr(x), _lib.ptr(s1), _lib.ptr(s2), rows, C, ld, _lib.stream())
+            _lib.call('mlc_bn_stats_ld', _lib.ptr(x), _lib.ptr(s1), _lib.ptr(s2), rows, C, ld or C, x_ld,
+                      _lib.stream())
         return
     xf = x.float().reshape(rows, C)
     t1, t2 = (s1[0], s2[0]) if s1.dim() == 2 else (s1, s2)     # copy 0 of a strided slice
@@ -1334,6 +1365,7 @@ def bnact_apply(y, res, scale, shift, act=0, alpha=0.0, res_affine=None, row_sca
     rows = y.numel() // C
     hw = rows // y.shape[0]
     if _cuda(y):
+        y = dense_rows(y)
         z = torch.empty_like(y)
         rs, rh = res_affine if res_affine is not None else (None, None)
         _lib.call('mlc_bnact_apply', _lib.ptr(y), _lib.ptr(res), _lib.ptr(z), _lib.ptr(scale), _lib.ptr(shift),
@@ -1357,30 +1389,38 @@ def bnact_fused(y, res, s1, s2, gamma, beta, mean, invstd, scale, shift, run_mea
     ``s1`` / ``s2`` and returns z; None when the shape does not fit (use the two calls).
     ``prev_tot`` ([2, prev_c] fp32): per-channel totals of the first ``prev_c`` channels, added
     to the copies' sums there (a DenseNet concat's older segment); ``tot_out`` ([2, C]): this
-    BN's per-channel totals, published for the next BN of such a chain."""
+    BN's per-channel totals, published for the next BN of such a chain.  ``y`` may be the
+    leading channels of wider rows (:func:`rows_ld`); z is dense."""
     C = y.shape[-1]
     ncopy = s1.numel() // C
     if not (_cuda(y) and _bn_fused_ok(C, ncopy)):
         return None
     rows = y.numel() // C
-    z = torch.empty_like(y)
+    y_ld = rows_ld(y)
+    if y_ld is None:
+        y, y_ld = y.contiguous(), C
+    z = torch.empty(y.shape, device=y.device, dtype=y.dtype)
     rs, rh = res_affine if res_affine is not None else (None, None)
     _lib.call('mlc_bnact_fused', _lib.ptr(y), _lib.ptr(res), _lib.ptr(z), _lib.ptr(s1), _lib.ptr(s2), ncopy,
               _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(mean), _lib.ptr(invstd), _lib.ptr(scale), _lib.ptr(shift),
               _lib.ptr(run_mean), _lib.ptr(run_var), _lib.ptr(rs), _lib.ptr(rh), rows, C, float(eps), float(momentum),
               int(act), float(alpha), _lib.ptr(row_scale), rows // y.shape[0], _lib.ptr(prev_tot), int(prev_c),
-              _lib.ptr(tot_out), _lib.stream())
+              _lib.ptr(tot_out), y_ld, _lib.stream())
     return z
 
 
 def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0, dgamma=None, dbeta=None,
-              sums=None, coef=None, want_dres=False, res_affine=None, row_scale=None, addend=None):
+              sums=None, coef=None, want_dres=False, res_affine=None, row_scale=None, addend=None, split=None):
     """Backward of z = act(BN(y) [* row_scale[n]] [+ res (*rscale + rshift)]) with the forward's
     (scale, shift): returns (dy, dres or None) and writes dgamma / dbeta; dres is the gradient
     of the residual term (before ``res_affine``, i.e. of a folded shortcut BN's output).
     ``sums`` (NSTAT*2*C fp32) must be zero on entry.  ``addend``: another consumer's gradient of
     y added to dy in the apply pass - an NHWC tensor whose last dim may be a channel slice of
-    wider rows (a DenseNet concat's gradient, row stride ``addend.stride(-2)``)."""
+    wider rows (a DenseNet concat's gradient, row stride ``addend.stride(-2)``).  ``y`` may be
+    such a slice as well (a DenseNet concat buffer's leading channels); dy / dres are dense.
+    ``split`` (a multiple of 8 in (0, C)): dy comes back as two dense tensors, channels [0, split)
+    and [split, C) - the gradients of a DenseNet concatenation's two operands, stored apart by
+    the apply pass."""
     C = y.shape[-1]
     rows = y.numel() // C
     hw = rows // y.shape[0]
@@ -1388,40 +1428,40 @@ def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0
     add_ld = 0
     if addend is not None:
         # rows of C channels at a row stride >= C (the channel slice of a contiguous NHWC tensor)
-        add_ld = addend.stride(-2)
-        want = [1, add_ld]
-        for d in range(addend.dim() - 2, 0, -1):
-            want.append(want[-1] * addend.shape[d])
-        assert addend.shape == y.shape and list(addend.stride()) == want[::-1], (addend.shape, addend.stride())
+        add_ld = rows_ld(addend)
+        assert addend.shape == y.shape and add_ld is not None, (addend.shape, addend.stride())
     if _cuda(dz):
+        y_ld = rows_ld(y)
+        if y_ld is None:
+            y, y_ld = y.contiguous(), C
         if coef is None:
             coef = torch.empty(3 * C, device=dz.device, dtype=torch.float32)
         zz = z if act in (4, 5) else None        # sigmoid / tanh read their derivative off z
         if C <= 2048:          # (fixed summation order: deterministic as well)
             # one call: reduce to per-block partial rows (no float atomics), finalize, apply
             part = slab_workspace(dz.device, 2048 * 2 * C)    # the kernel caps the blocks (MLC_NORMACT_CAP)
-            dy = torch.empty_like(y)
-            dres = torch.empty_like(y) if want_dres else None
+            dy, dy2 = _bwd_out(y, split)
+            dres = torch.empty(y.shape, device=y.device, dtype=y.dtype) if want_dres else None
             _lib.call('mlc_bnact_bwd', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
                       _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(rs), _lib.ptr(rh), _lib.ptr(invstd), _lib.ptr(gamma),
                       _lib.ptr(part), part.numel(), _lib.ptr(coef), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(dy),
                       _lib.ptr(dres), rows, C, int(act), float(alpha), _lib.ptr(row_scale), hw, _lib.ptr(addend),
-                      add_ld, _lib.stream())
-            return dy, dres
+                      add_ld, y_ld, _lib.ptr(dy2), int(split or 0), _lib.stream())
+            return (dy, dy2) if split else dy, dres
         if sums is None:
             sums = torch.zeros(NSTAT * 2 * C, device=dz.device, dtype=torch.float32)
         _lib.call('mlc_bnact_bwd_reduce', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
                   _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(rs), _lib.ptr(rh), _lib.ptr(sums), rows, C, int(act),
-                  float(alpha), _lib.ptr(row_scale), hw, _lib.stream())
+                  float(alpha), _lib.ptr(row_scale), hw, y_ld, _lib.stream())
         _lib.call('mlc_bn_bwd_finalize', _lib.ptr(sums), _lib.ptr(invstd), _lib.ptr(gamma), _lib.ptr(coef),
                   _lib.ptr(dgamma), _lib.ptr(dbeta), rows, C, _lib.stream())
-        dy = torch.empty_like(y)
-        dres = torch.empty_like(y) if want_dres else None
+        dy, dy2 = _bwd_out(y, split)
+        dres = torch.empty(y.shape, device=y.device, dtype=y.dtype) if want_dres else None
         _lib.call('mlc_bnact_bwd_apply', _lib.ptr(dz), _lib.ptr(zz), _lib.ptr(y), _lib.ptr(res), _lib.ptr(mean),
                   _lib.ptr(coef), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(rs), _lib.ptr(rh), _lib.ptr(dy),
                   _lib.ptr(dres), rows, C, int(act), float(alpha), _lib.ptr(row_scale), hw, _lib.ptr(addend), add_ld,
-                  _lib.stream())
-        return dy, dres
+                  y_ld, _lib.ptr(dy2), int(split or 0), _lib.stream())
+        return (dy, dy2) if split else dy, dres
     rsc = row_scale.repeat_interleave(hw)[:, None] if row_scale is not None else None
     a = y.float().reshape(rows, C) * scale + shift
     if rsc is not None:
@@ -1448,7 +1488,21 @@ def bnact_bwd(dz, z, y, res, mean, scale, shift, invstd, gamma, act=0, alpha=0.0
     dyf = k1 * d - k1 * S1 / rows - k1 * invstd * invstd * S2 / rows * yc
     if addend is not None:
         dyf = dyf + addend.float().reshape(rows, C)
-    return dyf.reshape(y.shape).to(torch.bfloat16), dres
+    dy = dyf.reshape(y.shape).to(torch.bfloat16)
+    if split:
+        return (dy[..., :split].contiguous(), dy[..., split:].contiguous()), dres
+    return dy, dres
+
+
+def _bwd_out(y, split):
+    """dy of :func:`bnact_bwd`: one dense tensor, or two split at channel ``split``."""
+    if not split:
+        return torch.empty(y.shape, device=y.device, dtype=y.dtype), None
+    C = y.shape[-1]
+    assert 0 < split < C and split % 8 == 0, (split, C)
+    lead = tuple(y.shape[:-1])
+    return (torch.empty(*lead, split, device=y.device, dtype=y.dtype),
+            torch.empty(*lead, C - split, device=y.device, dtype=y.dtype))
 
 
 def act_fwd(x, act, alpha=0.0):

@@ -453,9 +453,10 @@ class ConvParams:
         return Fn.conv_out_hw(H, W, self.k[0], self.k[1], self.stride, self.pad, self.dil)
 
     # ---- the three GEMMs by kind
-    def fwd(self, x, stats=None, act=0):
+    def fwd(self, x, stats=None, act=0, out=None):
         """x: NHWC bf16 with Cip channels -> y [N, Ho, Wo, Cop] (bias and a ReLU act fused for
-        dense convs without BN: ``act`` 3)."""
+        dense convs without BN: ``act`` 3).  ``out``: where a plain dense conv writes y (the
+        channel slice of a DenseNet block's concat buffer)."""
         wb = self.w.bf16
         if self.kind == 's2d':       # x: the s2d image (s2d_input)
             if self.b is not None or act:
@@ -467,7 +468,8 @@ class ConvParams:
                 assert stats is None
                 return Fn.conv2d_fwd_ex(x, wb, self.b.master if self.b is not None else None, act, self.stride,
                                         self.pad, self.dil)
-            return Fn.conv2d_fwd(x, wb, self.stride, self.pad, self.dil, stats=stats)
+            return Fn.conv2d_fwd(x, wb, self.stride, self.pad, self.dil, stats=stats, out=out)
+        assert out is None
         if self.kind == 'dw':
             return Fn.dwconv_fwd(x, wb, self.stride, self.pad, self.dil, stats=stats)
         if self.kind == 'tr':     # the dgrad parity-class GEMMs (BN statistics in the epilogue)
@@ -813,6 +815,23 @@ class ConvBNAct(Site):
         # per-sample drop-path factor mask / drop_keep before the residual add (EfficientNet's
         # MBConv in training), in the same apply pass; the third input is the [N,1,1,1] mask
         object.__setattr__(self, 'drop_keep', None)
+        # concat-buffer output (set by the lowering, _chain_dense_cats): this BN-less dense conv's
+        # output is the new segment of a chained DenseCat, so it is written straight into the
+        # block's concat buffer (channels [off, off + Co), rows of the buffer's width)
+        object.__setattr__(self, 'cat_out', None)
+
+    def _cat_slot(self, xn):
+        dc = self.cat_out
+        c = self.conv
+        if dc is None or dc.chain is None or not xn.is_cuda:
+            return None
+        _, KH, KW, _ = c.w.bf16.shape
+        Ho, Wo = Fn.conv_out_hw(xn.shape[1], xn.shape[2], KH, KW, c.stride, c.pad, c.dil)
+        ch, N = dc.chain, xn.shape[0]
+        buf = ch.buf
+        if dc.chain_first or buf is None or tuple(buf.shape[:3]) != (N, Ho, Wo) or buf.device != xn.device:
+            buf = ch.fresh(N, Ho, Wo, xn.device)
+        return buf[..., dc.off:dc.off + c.Co]
 
     def forward(self, x, res=None, mask=None):
         if mask is not None:
@@ -860,7 +879,8 @@ class ConvBNAct(Site):
                     object.__setattr__(self.res_bn, '_fold', None)
                 z = Fn.bnact_apply(y, rn, scale, shift, self.act, self.alpha, res_affine=rsh, row_scale=rsc)
             return self._bn_out(xn, y, z, rn, scale, shift, mean, inv, rsh, rsc, stats)
-        y = c.fwd(xn, None, self.epi_act)        # dense: bias (+ ReLU) in the GEMM epilogue
+        out = self._cat_slot(xn) if (rn is None and not self.epi_act and not self.act) else None
+        y = c.fwd(xn, None, self.epi_act, out=out)      # dense: bias (+ ReLU) in the GEMM epilogue
         if c.b is not None and c.kind != 'dense':
             y = (y.float() + c.b.master).to(torch.bfloat16)
         a = y if rn is None else (y.float() + rn.float()).to(torch.bfloat16)
@@ -1034,6 +1054,12 @@ class BNAct(Site):
         # gradient slice here; the apply pass adds it (no copy, no autograd add)
         object.__setattr__(self, 'slice_expected', False)
         object.__setattr__(self, '_slice_pending', None)
+        # split input gradient (set by the lowering, _split_cat_grads): this site's input is a
+        # DenseCat's output whose gradient only this site produces; the apply pass stores it
+        # as the concat's two operand gradients, each dense, handed to that DenseCat (no slice
+        # copies); autograd gets a zero-stride placeholder
+        object.__setattr__(self, 'split_to', None)
+        object.__setattr__(self, '_ph', None)
 
     def forward(self, x, res=None):
         return _run(self, x, res) if res is not None else _run(self, x)
@@ -1047,7 +1073,9 @@ class BNAct(Site):
             Fn.bn_stats(yn, s1, s2)
             return None, 0
         Cp, Ca = self.bn.Cp, A.bn.Cp
-        tn = to_nhwc(tail, tail.shape[1])
+        tn = tail.permute(0, 2, 3, 1)
+        if Fn.rows_ld(tn) is None or tn.dtype != torch.bfloat16:    # (in place in a concat buffer: no copy)
+            tn = to_nhwc(tail, tail.shape[1])
         s1v, s2v = s1.view(-1, Cp), s2.view(-1, Cp)
         Fn.bn_stats(tn, s1v[:, Ca:], s2v[:, Ca:], ld=Cp)
         if use_tot and A._tot_ok:
@@ -1056,7 +1084,20 @@ class BNAct(Site):
         s2v[:, :Ca].copy_(prev[1].view(-1, Ca))
         return None, 0
 
-    def _to(self, x):
+    def _placeholder(self, like):
+        """A zero-stride zero tensor of ``like``'s shape: the input gradient autograd carries to
+        the DenseCat that takes the real one from ``_split_pending``."""
+        ph = self._ph
+        if ph is None or ph.device != like.device or ph.dtype != like.dtype:
+            ph = torch.zeros((), device=like.device, dtype=like.dtype)
+            object.__setattr__(self, '_ph', ph)
+        return ph.expand(like.shape)
+
+    def _to(self, x, keep_rows=False):
+        if keep_rows and x.dim() == 4 and x.dtype == torch.bfloat16 and x.shape[1] == self.bn.Cp:
+            y = x.permute(0, 2, 3, 1)
+            if Fn.rows_ld(y) is not None:    # the leading channels of a DenseNet concat buffer: no copy
+                return y
         if x.dim() == 2:              # BatchNorm1d over [N, C] / [N, C, L]
             x = x[:, :, None, None]
         elif x.dim() == 3:
@@ -1078,7 +1119,7 @@ class BNAct(Site):
         tail = None
         if self.cat_prev is not None:         # the second input is the concat's new segment
             tail, res = res, None
-        yn = self._to(x)
+        yn = self._to(x, keep_rows=True)
         rn = self._to(res) if res is not None else None
         rows = yn.numel() // yn.shape[-1]
         stats = None
@@ -1114,15 +1155,21 @@ class BNAct(Site):
         if self.slice_expected and needs[0] and addend is None:
             raise RuntimeError(f'{bn.name}: the concat gradient hand-off did not arrive (backward order differs '
                                'from the one the lowering assumed)')
+        D = self.split_to
+        split = D.off if (D is not None and needs[0] and dout.dim() == 4) else None
         dy, dres = Fn.bnact_bwd(dz, z, yn, rn if has_res else None, mean, scale, shift, inv, bn.gamma.master,
                                 self.act, self.alpha, dgamma=_acc_view(bn.gamma, d), dbeta=_acc_view(bn.beta, d),
-                                sums=self.ctx.ws[self.k_bw], want_dres=has_res, addend=addend)
+                                sums=self.ctx.ws[self.k_bw], want_dres=has_res, addend=addend, split=split)
         _acc_commit(bn.gamma, d)
         _acc_commit(bn.beta, d)
         if bn.uses.bwd_done():
             bn.mark_ready()
         like = dout
-        out = [self._from(dy, like) if needs[0] else None]
+        if split:
+            object.__setattr__(D, '_split_pending', dy)
+            out = [self._placeholder(dout)]
+        else:
+            out = [self._from(dy, like) if needs[0] else None]
         if has_res:
             out.append(self._from(dres, like) if needs[1] else None)
         return out + [None] * (len(needs) - len(out))      # the concat tail: statistics only
@@ -1206,24 +1253,86 @@ class LinearAct(Site):
         return out
 
 
+class DenseChain:
+    """The concat buffer of a run of :class:`DenseCat` sites (one DenseNet block: x_{i+1} =
+    cat(x_i, b_i) for i = 0 .. L-1): one NHWC tensor of the block's final width; x_i is the view
+    of its leading C_i channels (rows of stride C_L), so each layer copies only its own b_i into
+    the buffer instead of the whole concatenation - the block's forward copies its channels
+    once, not quadratically many times.  ``width``: C_L, set by the lowering."""
+
+    def __init__(self, width: int):
+        self.width, self.buf = width, None
+
+    def fresh(self, N, H, W, device):
+        self.buf = torch.empty(N, H, W, self.width, device=device, dtype=torch.bfloat16)
+        return self.buf
+
+    def placed(self, t, off) -> bool:
+        """t (NHWC) is channels [off, off + C) of the current buffer, in place."""
+        buf = self.buf
+        return (buf is not None and t.shape[:3] == buf.shape[:3] and t.device == buf.device
+                and t.data_ptr() == buf.data_ptr() + off * buf.element_size() and Fn.rows_ld(t) == self.width)
+
+
 class DenseCat(Site):
     """``torch.cat([a, b], 1)`` of a DenseNet layer (x_{i+1} = cat(x_i, layer_i(x_i))) whose first
     operand's other consumer is a BN site (``a_site``, the layer's first BN, whose backward runs
     after this one): the backward leaves a's gradient - a channel slice of the output gradient,
-    no copy - with that site, whose apply pass adds it; autograd adds nothing."""
+    no copy - with that site, whose apply pass adds it; autograd adds nothing.  With a
+    ``chain`` (the lowering, ``_chain_dense_cats``) the forward writes b into the block's
+    concat buffer and returns a view of it (:class:`DenseChain`)."""
 
     def __init__(self, ctx, a_site: 'BNAct'):
         super().__init__(ctx)
         object.__setattr__(self, 'a_site', a_site)
+        object.__setattr__(self, 'chain', None)
+        object.__setattr__(self, 'chain_first', False)
+        object.__setattr__(self, 'chain_last', False)
+        object.__setattr__(self, 'off', a_site.bn.C)   # a's channel count (b's offset in the buffer)
+        # the output's gradient arrives split in two from the consumer BN site's apply pass
+        # (BNAct.split_to); the autograd gradient is then a placeholder
+        object.__setattr__(self, 'split_expected', False)
+        object.__setattr__(self, '_split_pending', None)
 
     def forward(self, a, b):
         return _run(self, a, b)
 
     def fwd(self, a, b):
-        return torch.cat([a, b], 1), [], (a.shape[1], b.shape[1])
+        Ca, Cb = a.shape[1], b.shape[1]
+        ch = self.chain
+        if ch is None or a.dim() != 4 or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or Ca + Cb > ch.width:
+            return torch.cat([a, b], 1), [], (Ca, Cb)
+        an, bn = a.permute(0, 2, 3, 1), b.permute(0, 2, 3, 1)
+        # b is normally in place already (its conv site wrote it into the buffer, ConvBNAct
+        # .cat_out), and a is the buffer's leading Ca channels except at the block's first
+        # concat; whatever is not in place is copied in (a fresh buffer when it does not fit)
+        b_in = ch.placed(bn, Ca)
+        a_in = ch.placed(an, 0)
+        if not (b_in or a_in):
+            ch.fresh(*an.shape[:3], a.device)
+        buf = ch.buf
+        # the copies extend the buffer past every view handed out so far; the views' saved
+        # copies (earlier BN sites' inputs) are unchanged, so their version stays valid
+        with torch.autograd._unsafe_preserve_version_counter(buf):
+            if not a_in:
+                buf[..., :Ca].copy_(an)
+            if not b_in:
+                buf[..., Ca:Ca + Cb].copy_(bn)
+        ch.buf = None if self.chain_last else buf
+        return buf[..., :Ca + Cb].permute(0, 3, 1, 2), [], (Ca, Cb)
 
     def bwd(self, dout, saved, keep, needs):
         Ca, Cb = keep
+        sp = self._split_pending
+        object.__setattr__(self, '_split_pending', None)
+        if sp is not None:
+            da, db = sp
+            if needs[0]:
+                object.__setattr__(self.a_site, '_slice_pending', da)
+            return [None, from_nhwc(db, Cb) if needs[1] else None]
+        if self.split_expected and dout.stride() == (0,) * dout.dim():
+            raise RuntimeError('DenseCat: the split gradient hand-off did not arrive (backward order differs from '
+                               'the one the lowering assumed)')
         g = to_nhwc(dout, Ca + Cb)                 # the channels_last view, no copy
         if needs[0]:
             object.__setattr__(self.a_site, '_slice_pending', g[..., :Ca])

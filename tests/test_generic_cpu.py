@@ -975,7 +975,8 @@ def test_dense_block_bn_statistics_reuse_the_previous_layers(monkeypatch):
     """DenseNet's BN over cat([x_i, f_i]): the site copies x_i's per-channel sums from the
     previous layer's BN and reduces only the new channels (BNAct.cat_prev), and the concat's
     backward hands x_i's gradient slice to that BN's apply pass (DenseCat); output, running
-    statistics and weight gradients equal the plain lowering's."""
+    statistics and weight gradients equal the plain lowering's.  The block's concatenations
+    share one buffer (DenseChain): each BN reads its input as the buffer's leading channels."""
     from mlcomp_amd.contrib.segmentation.encoders import _DenseLayer
     from mlcomp_amd.models.native_generic import _Lowering
     from mlcomp_amd.ops.glayers import BNAct, DenseCat
@@ -1003,6 +1004,9 @@ def test_dense_block_bn_statistics_reuse_the_previous_layers(monkeypatch):
         monkeypatch.undo()
         k = sum(isinstance(m, BNAct) and m.cat_prev is not None for m in net.train_gm.modules())
         k += 10 * sum(isinstance(m, DenseCat) for m in net.train_gm.modules())
+        k += 100 * sum(isinstance(m, DenseCat) and m.chain is not None for m in net.train_gm.modules())
+        k += 1000 * sum(getattr(m, 'cat_out', None) is not None for m in net.train_gm.modules())
+        k += 10000 * sum(isinstance(m, BNAct) and m.split_to is not None for m in net.train_gm.modules())
         out = net(x)
         F.cross_entropy(out.float(), y).backward()
         rv = [m.bn.run_var.clone() for m in net.train_gm.modules() if isinstance(m, BNAct)]
@@ -1010,7 +1014,10 @@ def test_dense_block_bn_statistics_reuse_the_previous_layers(monkeypatch):
 
     k1, o1, r1, g1 = run(True)
     k0, o0, r0, g0 = run(False)
-    assert (k1, k0) == (33, 0)         # 3 concat-statistics BNs (layers 2, 3, final), 3 DenseCats
+    # 3 concat-statistics BNs (layers 2, 3, final), 3 DenseCats sharing one concat buffer, into
+    # which the 3 growth convs write their outputs (on the GPU); the BN after each concat stores
+    # its input gradient split into the concat's two operand gradients
+    assert (k1, k0) == (33333, 0)
     assert _rel(o1, o0) < 1e-2
     for a, b in zip(r1, r0):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-6)

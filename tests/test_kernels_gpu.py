@@ -6,6 +6,7 @@ which is plain fp32 PyTorch math), and compares.
 """
 import pytest
 import torch
+import torch.nn.functional as F
 
 from mlcomp_amd.ops import functional as Fn
 
@@ -855,3 +856,78 @@ def test_bnact_bwd_adds_a_strided_channel_slice(act):
     torch.cuda.synchronize()
     for a, b in zip(out, ref):
         assert rel_err(a, b) < 1e-2
+
+
+@pytest.mark.parametrize('C,W', [(24, 40), (64, 256), (2064, 2080)])
+@pytest.mark.parametrize('act', [1, 3])
+def test_bnact_reads_the_leading_channels_of_wider_rows(C, W, act):
+    """The normact forward (folded finalize + apply) and backward (reduce, finalize, apply;
+    C > 2048 takes the atomic-copies reduce) reading y as the leading C channels of W-wide rows
+    (a DenseNet concat buffer, glayers.DenseChain) give what they give on a dense copy of y,
+    and the backward matches the fp32 CPU path."""
+    N, H, Wd = 2, 3, 4
+    wide = (_bf(N, H, Wd, W, scale=2.0, seed=81) + 0.3).to(DEV)
+    y = wide[..., :C]
+    assert Fn.rows_ld(y) == W
+    dz = _bf(N, H, Wd, C, seed=82).to(DEV)
+    g = torch.Generator().manual_seed(83)
+    gamma, beta = (torch.rand(C, generator=g) + 0.5).to(DEV), (torch.randn(C, generator=g) * 0.1).to(DEV)
+    yf = y.float().reshape(-1, C)
+    s1, s2 = Fn.stat_buffers(C, DEV)
+    s1[:C], s2[:C] = yf.sum(0), (yf * yf).sum(0)
+
+    def run(yy):
+        st = torch.zeros(4, C, device=DEV)
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        z = Fn.bnact_fused(yy, None, s1, s2, gamma, beta, st[2], st[3], st[0], st[1], rm, rv, 1e-5, 0.1, act, 0.0)
+        assert z is not None and z.is_contiguous()
+        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        dy, _ = Fn.bnact_bwd(dz, z, yy, None, st[2], st[0], st[1], st[3], gamma, act, dgamma=dg, dbeta=db)
+        torch.cuda.synchronize()
+        return [z, st, rm, rv, dy, dg, db]
+
+    strided, dense = run(y), run(y.contiguous())
+    for a, b in zip(strided, dense):
+        assert rel_err(a, b) < 1e-6, rel_err(a, b)
+    # the input gradient stored split in two dense tensors (a DenseNet concat's operands)
+    z, st = strided[0], strided[1]
+    sp = C - 8
+    (da, db), _ = Fn.bnact_bwd(dz, z, y, None, st[2], st[0], st[1], st[3], gamma, act,
+                               dgamma=torch.zeros(C, device=DEV), dbeta=torch.zeros(C, device=DEV), split=sp)
+    torch.cuda.synchronize()
+    assert da.is_contiguous() and db.is_contiguous() and da.shape[-1] == sp and db.shape[-1] == C - sp
+    assert torch.equal(da, strided[4][..., :sp]) and torch.equal(db, strided[4][..., sp:])
+    z, st = strided[0], strided[1]
+    dg, db = torch.zeros(C), torch.zeros(C)
+    cpu = Fn.bnact_bwd(dz.cpu(), z.cpu(), y.cpu(), None, st[2].cpu(), st[0].cpu(), st[1].cpu(), st[3].cpu(),
+                       gamma.cpu(), act, dgamma=dg, dbeta=db)[0]
+    assert rel_err(strided[4], cpu) < 1e-2
+    assert rel_err(strided[5], dg) < 1e-2 and rel_err(strided[6], db) < 1e-2
+
+
+@pytest.mark.parametrize('k,Ci,Co,off,W', [(3, 64, 32, 96, 160), (1, 128, 32, 64, 96), (3, 32, 48, 0, 48 + 80)])
+def test_conv_fwd_into_a_channel_slice(k, Ci, Co, off, W):
+    """mlc_conv_fwd_ld: a conv writes its output as channels [off, off + Co) of W-wide rows (a
+    DenseNet layer's growth channels straight into its block's concat buffer), leaving the other
+    channels untouched; equal to the dense conv, which matches fp32 F.conv2d; and the BN
+    statistics of that slice read in place equal those of a dense copy."""
+    N, H, Wd = 2, 9, 7
+    x = _bf(N, H, Wd, Ci, seed=91).to(DEV)
+    w = (_bf(Co, k, k, Ci, seed=92) * 0.2).to(DEV)
+    buf = torch.full((N, H, Wd, W), 7.0, device=DEV, dtype=torch.bfloat16)
+    out = buf[..., off:off + Co]
+    y = Fn.conv2d_fwd(x, w, 1, k // 2, 1, out=out)
+    dense = Fn.conv2d_fwd(x, w, 1, k // 2, 1)
+    torch.cuda.synchronize()
+    assert y.data_ptr() == out.data_ptr()
+    assert torch.equal(buf[..., off:off + Co], dense)
+    assert bool((buf[..., :off] == 7.0).all()) and bool((buf[..., off + Co:] == 7.0).all())
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2).cpu(), w.float().permute(0, 3, 1, 2).cpu(), None, 1, k // 2)
+    assert rel_err(dense, ref.permute(0, 2, 3, 1)) < 1e-2
+    s1, s2 = Fn.stat_buffers(Co, DEV)
+    Fn.bn_stats(out, s1, s2)
+    r1, r2 = Fn.stat_buffers(Co, DEV)
+    Fn.bn_stats(dense, r1, r2)
+    torch.cuda.synchronize()
+    assert rel_err(s1.view(-1, Co).sum(0), r1.view(-1, Co).sum(0)) < 1e-5
+    assert rel_err(s2.view(-1, Co).sum(0), r2.view(-1, Co).sum(0)) < 1e-5
