@@ -20,6 +20,7 @@
 // bandwidth.  Threads own a fixed 8-channel group (16 B accesses, grid = multiple of C/8
 // threads, as the BatchNorm passes) and walk pixels; the weight gradient reduces per
 // thread, then per block (LDS), then over 32 partial copies.
+#include <numeric>
 #include "common.h"
 #include <stdlib.h>
 
@@ -778,6 +779,31 @@ dw_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* 
 // zeroed), so a thread has ~20 16-byte loads in flight instead of one.
 constexpr int DW_SW = 8;
 
+// n / d for 0 <= n < 2^31 as a multiply-high, an add and a shift, with the divisor's magic
+// number computed on the host: the strip kernels split their item index into (image, row,
+// strip, channel group) once per item, and three 64-bit divisions there cost more
+// instructions than the item's FMAs
+struct FastDiv {
+  unsigned d, m, s;
+  FastDiv() = default;
+  explicit FastDiv(unsigned dv) : d(dv), m(0), s(0) {
+    while ((1u << s) < d) ++s;   // ceil(log2 d)
+    m = (unsigned)((((unsigned long long)1 << 32) * (((unsigned long long)1 << s) - d)) / d + 1);
+  }
+  __device__ __forceinline__ unsigned div(unsigned n) const { return (__umulhi(n, m) + n) >> s; }
+};
+// item i = ((n * R + row) * Q + q) * G + cg
+struct Idx3 {
+  FastDiv g, q, r;
+};
+struct Item {
+  int n, row, q, cg;
+};
+__device__ __forceinline__ Item split_item(long i, const Idx3& ix) {
+  const unsigned u = (unsigned)i, t0 = ix.g.div(u), t1 = ix.q.div(t0), t2 = ix.r.div(t1);
+  return Item{(int)t2, (int)(t1 - t2 * ix.r.d), (int)(t0 - t1 * ix.q.d), (int)(u - t0 * ix.g.d)};
+}
+
 __device__ __forceinline__ uint4 ld_or_zero(const bf16* base, long off, bool ok) {
   const uint4 v = ldg16(base + (ok ? off : 0));
   return ok ? v : make_uint4(0u, 0u, 0u, 0u);
@@ -788,7 +814,7 @@ template <int KW, int S>
 __global__ void __launch_bounds__(NT)
 dw_fwd_strip_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, bf16* __restrict__ y,
                     float* __restrict__ sum, float* __restrict__ sumsq, int N, int H, int W, int C, int Ho, int Wo,
-                    int KH, int P) {
+                    int KH, int P, Idx3 ix) {
   constexpr int XS = (DW_SW - 1) * S + KW;
   const int G = C >> 3;
   const int Wq = (Wo + DW_SW - 1) / DW_SW;
@@ -799,10 +825,8 @@ dw_fwd_strip_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, bf16
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
   for (long i = gtid; i < total; i += (long)gridDim.x * NT) {
-    long t = i / G;
-    const int wq = (int)(t % Wq); t /= Wq;
-    const int ho = (int)(t % Ho);
-    const int n = (int)(t / Ho);
+    const Item it = split_item(i, ix);
+    const int wq = it.q, ho = it.row, n = it.n;
     const int wo0 = wq * DW_SW;
     const int wi0 = wo0 * S - P;
     float acc[DW_SW][8];
@@ -849,30 +873,39 @@ dw_fwd_strip_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, bf16
   if (sum) red_stats(s1, s2, sum, sumsq, C, G);
 }
 
-// weight gradient of filter row r = blockIdx.y: acc[q] = sum over pixels dy[p] * x[p@(r,q)],
-// reduced per block (LDS) and added into copy (block % NCOPY) of ws[NCOPY][KH*KW][C]
+// weight gradient of filter row r: acc[q] = sum over pixels dy[p] * x[p@(r,q)], reduced per
+// block (LDS) and added into copy (spatial block % NCOPY) of ws[NCOPY][KH*KW][C].
+// The KH filter rows re-read the same dy rows and overlapping x rows. With xcd != 0 the grid
+// is 1-D and the KH row-blocks of one spatial block sit on one XCD (dispatch round-robins
+// blocks over the 8 XCDs) in consecutive dispatch slots, so they run together and share those
+// reads through that XCD's L2. Otherwise blockIdx.y is the filter row, and the KH slices of the
+// grid sweep the whole tensor one after another.
 template <int KW, int S>
 __global__ void __launch_bounds__(NT)
 dw_wgrad_strip_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* __restrict__ ws, int N,
-                      int H, int W, int C, int Ho, int Wo, int KH, int P) {
+                      int H, int W, int C, int Ho, int Wo, int KH, int P, int xcd, Idx3 ix) {
   constexpr int XS = (DW_SW - 1) * S + KW;
   __shared__ float rb[NT][KW * 8 + 1];
   const int G = C >> 3;
-  const int r = blockIdx.y;
+  int r = blockIdx.y, sb = blockIdx.x, nb = gridDim.x;
+  if (xcd) {
+    const int k = blockIdx.x >> 3;
+    r = k % KH;
+    sb = (k / KH) * 8 + (blockIdx.x & 7);
+    nb = gridDim.x / KH;
+  }
   const int Wq = (Wo + DW_SW - 1) / DW_SW;
   const long total = (long)N * Ho * Wq * G;
-  const long gtid = (long)blockIdx.x * NT + threadIdx.x;
+  const long gtid = (long)sb * NT + threadIdx.x;
   const int cg = (int)(gtid % G);
   float acc[KW][8];
 #pragma unroll
   for (int q = 0; q < KW; ++q)
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[q][e] = 0.f;
-  for (long i = gtid; i < total; i += (long)gridDim.x * NT) {
-    long t = i / G;
-    const int wq = (int)(t % Wq); t /= Wq;
-    const int ho = (int)(t % Ho);
-    const int n = (int)(t / Ho);
+  for (long i = gtid; i < total; i += (long)nb * NT) {
+    const Item it = split_item(i, ix);
+    const int wq = it.q, ho = it.row, n = it.n;
     const int hi = ho * S - P + r;
     if ((unsigned)hi >= (unsigned)H) continue;
     const int wo0 = wq * DW_SW;
@@ -907,8 +940,8 @@ dw_wgrad_strip_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, f
     for (int e = 0; e < 8; ++e) rb[tid][q * 8 + e] = acc[q][e];
   __syncthreads();
   const int lanes = NT < G ? NT : G;
-  const int base_cg = (int)(((long)blockIdx.x * NT) % G);
-  float* dst = ws + (long)(blockIdx.x % NCOPY) * KH * KW * C;
+  const int base_cg = (int)(((long)sb * NT) % G);
+  float* dst = ws + (long)(sb % NCOPY) * KH * KW * C;
   for (int qq = tid; qq < lanes * KW * 8; qq += NT) {
     const int l = qq % lanes, ke = qq / lanes;
     const int q = ke >> 3, e = ke & 7;
@@ -927,18 +960,15 @@ constexpr int fdiv2(int a) { return a >= 0 ? a / 2 : -((-a + 1) / 2); }
 template <int KW, int S, int PP>
 __global__ void __launch_bounds__(NT)
 dw_dgrad_strip_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ w, bf16* __restrict__ dx, int N, int H,
-                      int W, int C, int Ho, int Wo, int KH, int P) {
+                      int W, int C, int Ho, int Wo, int KH, int P, Idx3 ix) {
   constexpr int FB = S == 1 ? -(KW - 1) : fdiv2(PP - (KW - 1));
   constexpr int NW = S == 1 ? DW_SW + KW - 1 : (DW_SW - 1 + PP) / 2 - FB + 1;
   const int G = C >> 3;
   const int Wq = (W + DW_SW - 1) / DW_SW;
   const long total = (long)N * H * Wq * G;
   for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-    const int cg = (int)(i % G);
-    long t = i / G;
-    const int wq = (int)(t % Wq); t /= Wq;
-    const int hi = (int)(t % H);
-    const int n = (int)(t / H);
+    const Item it = split_item(i, ix);
+    const int cg = it.cg, wq = it.q, hi = it.row, n = it.n;
     const int wi0 = wq * DW_SW;
     const int col0 = S == 1 ? wi0 + P + FB : wi0 / 2 + (P - PP) / 2 + FB;
     float acc[DW_SW][8];
@@ -1000,8 +1030,8 @@ inline long group_mult(int G) {
   while (b) { const int r = a % b; a = b; b = r; }
   return G / a;
 }
-inline int grid_groups(long work, int G, int cap) {
-  long blocks = (work + NT * 4 - 1) / (NT * 4);
+inline int grid_groups(long work, int G, int cap, int per_thread = 4) {
+  long blocks = (work + (long)NT * per_thread - 1) / ((long)NT * per_thread);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   const long m = group_mult(G);
@@ -1019,6 +1049,29 @@ inline int blocks_for(long work) {
   long b = (work + NT - 1) / NT;
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
 }
+
+inline int dw_wg_items() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MLC_DW_WG_ITEMS");
+    v = e ? atoi(e) : 32;
+    if (v < 1) v = 1;
+  }
+  return v;
+}
+
+// MLC_DW_XCD=0: the depthwise weight gradient's filter rows as grid.y slices (A/B)
+inline bool dw_xcd() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MLC_DW_XCD");
+    v = e ? atoi(e) : 1;
+  }
+  return v != 0;
+}
+
+inline Idx3 idx3(int G, int Q, int R) { return Idx3{FastDiv((unsigned)G), FastDiv((unsigned)Q), FastDiv((unsigned)R)}; }
+inline bool items_fit(int N, int R, int Q, int G) { return (long)N * R * Q * G < (1L << 31); }
 
 // MLC_DW_STRIPS=0 selects the per-pixel depthwise kernels (A/B)
 inline bool dw_strips() {
@@ -1169,11 +1222,13 @@ MLC_EXPORT int mlc_dwconv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum,
     return rc ? rc : mlc_bn_stats(y, sum, sumsq, (long)N * Ho * Wo, C, st);
   }
   const int G = C / 8;
-  if (D == 1 && (S == 1 || S == 2) && (KW == 3 || KW == 5 || KW == 7) && dw_strips()) {
-    const long work = (long)N * Ho * ((Wo + DW_SW - 1) / DW_SW) * G;
+  const int Wqo = (Wo + DW_SW - 1) / DW_SW;
+  if (D == 1 && (S == 1 || S == 2) && (KW == 3 || KW == 5 || KW == 7) && dw_strips() && items_fit(N, Ho, Wqo, G)) {
+    const long work = (long)N * Ho * Wqo * G;
     const dim3 grid(grid_groups(work, G, 2048));
+    const Idx3 ix = idx3(G, Wqo, Ho);
 #define DWF(K, SS) hipLaunchKernelGGL((dw_fwd_strip_kernel<K, SS>), grid, dim3(NT), 0, st, x, w, y, sum, sumsq, N, H, \
-                                      W, C, Ho, Wo, KH, P)
+                                      W, C, Ho, Wo, KH, P, ix)
     if (S == 1) { if (KW == 3) DWF(3, 1); else if (KW == 5) DWF(5, 1); else DWF(7, 1); }
     else { if (KW == 3) DWF(3, 2); else if (KW == 5) DWF(5, 2); else DWF(7, 2); }
 #undef DWF
@@ -1188,11 +1243,13 @@ MLC_EXPORT int mlc_dwconv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum,
 MLC_EXPORT int mlc_dwconv_dgrad(const bf16* dy, const bf16* w, bf16* dx, int N, int H, int W, int C, int KH, int KW,
                                 int S, int P, int D, int Ho, int Wo, hipStream_t st) {
   if (C % 8) return -1;
-  if (D == 1 && (S == 1 || S == 2) && (KW == 3 || KW == 5 || KW == 7) && dw_strips()) {
-    const long work = (long)N * H * ((W + DW_SW - 1) / DW_SW) * (C / 8);
+  const int Wqi = (W + DW_SW - 1) / DW_SW;
+  if (D == 1 && (S == 1 || S == 2) && (KW == 3 || KW == 5 || KW == 7) && dw_strips() && items_fit(N, H, Wqi, C / 8)) {
+    const long work = (long)N * H * Wqi * (C / 8);
     const dim3 grid(blocks_for(work));
+    const Idx3 ix = idx3(C / 8, Wqi, H);
 #define DWD(K, SS, PP) hipLaunchKernelGGL((dw_dgrad_strip_kernel<K, SS, PP>), grid, dim3(NT), 0, st, dy, w, dx, N, H, \
-                                          W, C, Ho, Wo, KH, P)
+                                          W, C, Ho, Wo, KH, P, ix)
     if (S == 1) { if (KW == 3) DWD(3, 1, 0); else if (KW == 5) DWD(5, 1, 0); else DWD(7, 1, 0); }
     else if (P & 1) { if (KW == 3) DWD(3, 2, 1); else if (KW == 5) DWD(5, 2, 1); else DWD(7, 2, 1); }
     else { if (KW == 3) DWD(3, 2, 0); else if (KW == 5) DWD(5, 2, 0); else DWD(7, 2, 0); }
@@ -1214,11 +1271,22 @@ MLC_EXPORT int mlc_dwconv_wgrad(const bf16* dy, const bf16* x, float* dw, float*
   // (copies_reduce_kernel sums the copies in a fixed order)
   const int cap_strip = g_mlc_det ? det_group_cap(G) : 512, cap_tap = g_mlc_det ? det_group_cap(G) : 1024;
   if (cap_strip == 0) return -2;
-  if (D == 1 && (S == 1 || S == 2) && (KW == 3 || KW == 5 || KW == 7) && dw_strips()) {
-    const long work = (long)N * Ho * ((Wo + DW_SW - 1) / DW_SW) * G;
-    const dim3 grid(grid_groups(work, G, cap_strip), KH);
+  const int Wqo = (Wo + DW_SW - 1) / DW_SW;
+  if (D == 1 && (S == 1 || S == 2) && (KW == 3 || KW == 5 || KW == 7) && dw_strips() && items_fit(N, Ho, Wqo, G)) {
+    const long work = (long)N * Ho * Wqo * G;
+    const Idx3 ix = idx3(G, Wqo, Ho);
+    // items per thread: every block ends in KW*C float atomics (device-scope, past the XCD's
+    // L2), so small-spatial layers (7x7, 14x14) want few, long-running blocks (MLC_DW_WG_ITEMS)
+    int nb = grid_groups(work, G, cap_strip, dw_wg_items());
+    // XCD-grouped row-blocks (not in deterministic mode, whose grid is capped at NCOPY blocks):
+    // the spatial block count rounded up to a multiple of 8 that keeps the channel-group
+    // alignment of group_mult
+    const long m = group_mult(G), l8 = m * 8 / std::gcd(m, 8L);
+    const int xcd = !g_mlc_det && dw_xcd();
+    if (xcd) nb = (int)(((nb + l8 - 1) / l8) * l8);
+    const dim3 grid = xcd ? dim3(nb * KH) : dim3(nb, KH);
 #define DWW(K, SS) hipLaunchKernelGGL((dw_wgrad_strip_kernel<K, SS>), grid, dim3(NT), 0, st, dy, x, ws, N, H, W, C, \
-                                      Ho, Wo, KH, P)
+                                      Ho, Wo, KH, P, xcd, ix)
     if (S == 1) { if (KW == 3) DWW(3, 1); else if (KW == 5) DWW(5, 1); else DWW(7, 1); }
     else { if (KW == 3) DWW(3, 2); else if (KW == 5) DWW(5, 2); else DWW(7, 2); }
 #undef DWW

@@ -71,7 +71,8 @@ def test_grouped_conv_kernels_vs_fp32(N, H, W, C, Cg, k, s, p, d, Co):
                                              (2, 9, 9, 40, 3, 2, 1, 1), (2, 12, 12, 32, 3, 1, 2, 2),
                                              (1, 7, 7, 1152, 5, 1, 2, 1), (3, 14, 21, 24, 7, 1, 3, 1),
                                              (2, 19, 23, 16, 7, 2, 3, 1), (2, 11, 13, 8, 3, 1, 0, 1),
-                                             (2, 8, 8, 48, 4, 1, 1, 1)])
+                                             (2, 8, 8, 48, 4, 1, 1, 1), (8, 28, 28, 240, 5, 1, 2, 1),
+                                             (4, 56, 56, 96, 3, 2, 1, 1)])
 def test_depthwise_conv_kernels_vs_fp32(N, H, W, C, k, s, p, d):
     """Strip kernels (k 3/5/7, stride 1/2, no dilation, tails of the 8-column strips) and
     the per-pixel kernels (dilation 2, k 4)."""
