@@ -621,6 +621,22 @@ inline int reduce_cap() {
   return v;
 }
 
+// block cap of the one-call backward's reduction (mlc_bnact_bwd): its blocks store partial rows
+// (no atomics), so the row finalize grows with blocks x C while a wider grid keeps more loads in
+// flight.  Default (0): 1024 blocks for tensors of >= 2^26 elements (EfficientNet's early
+// expanded activations), else 512 - on the generic zoo 1024 everywhere is +2.6 % on
+// EfficientNet-b0 and -1.7 % on SE-ResNeXt-50, and 1024 up to 256 channels still loses on
+// SE-ResNeXt (profiles/round6/normact_bwd_cap_ab*.jsonl); A/B knob MLC_NORMACT_BWD_CAP
+inline int bwd_cap(long rows, int C) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MLC_NORMACT_BWD_CAP");
+    v = e ? atoi(e) : 0;
+  }
+  if (v <= 0) return rows * C >= (1L << 26) ? 1024 : 512;
+  return v < 32 ? 32 : v;
+}
+
 // block cap of the streaming (apply) passes (A/B knob MLC_NORMACT_APPLY_CAP)
 inline int apply_cap() {
   static int v = -1;
@@ -752,7 +768,7 @@ MLC_EXPORT int mlc_bnact_bwd(const bf16* dz, const bf16* z, const bf16* y, const
   const int G = C >> 3;
   if (C % 8 || G > NT || part_floats < 2L * C || (rscale && !rshift)) return -1;
   long cap = part_floats / (2L * C);
-  if (cap > reduce_cap()) cap = reduce_cap();
+  if (cap > bwd_cap(rows, C)) cap = bwd_cap(rows, C);
   int blocks = grid_for(rows, C, (int)cap);
   while (blocks > cap && blocks > 1) blocks = grid_for(rows, C, blocks / 2);   // rounding to C/8 multiples
   if ((long)blocks * 2 * C > part_floats) return -1;
