@@ -1060,6 +1060,16 @@ inline int dw_wg_items() {
   return v;
 }
 
+inline int dw_fwd_items() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MLC_DW_FWD_ITEMS");
+    v = e ? atoi(e) : 4;
+    if (v < 1) v = 1;
+  }
+  return v;
+}
+
 // MLC_DW_XCD=0: the depthwise weight gradient's filter rows as grid.y slices (A/B)
 inline bool dw_xcd() {
   static int v = -1;
@@ -1225,7 +1235,8 @@ MLC_EXPORT int mlc_dwconv_fwd(const bf16* x, const bf16* w, bf16* y, float* sum,
   const int Wqo = (Wo + DW_SW - 1) / DW_SW;
   if (D == 1 && (S == 1 || S == 2) && (KW == 3 || KW == 5 || KW == 7) && dw_strips() && items_fit(N, Ho, Wqo, G)) {
     const long work = (long)N * Ho * Wqo * G;
-    const dim3 grid(grid_groups(work, G, 2048));
+    // the BN statistics end every block in 2*C float atomics: fewer, longer blocks (MLC_DW_FWD_ITEMS)
+    const dim3 grid(grid_groups(work, G, 2048, sum ? dw_fwd_items() : 4));
     const Idx3 ix = idx3(G, Wqo, Ho);
 #define DWF(K, SS) hipLaunchKernelGGL((dw_fwd_strip_kernel<K, SS>), grid, dim3(NT), 0, st, x, w, y, sum, sumsq, N, H, \
                                       W, C, Ho, Wo, KH, P, ix)
