@@ -1070,6 +1070,17 @@ inline int dw_fwd_items() {
   return v;
 }
 
+// block cap of the depthwise input-gradient strips (A/B knob MLC_DW_DGRAD_CAP)
+inline int dw_dgrad_cap() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MLC_DW_DGRAD_CAP");
+    v = e ? atoi(e) : 8192;
+    if (v < 64) v = 64;
+  }
+  return v;
+}
+
 // MLC_DW_XCD=0: the depthwise weight gradient's filter rows as grid.y slices (A/B)
 inline bool dw_xcd() {
   static int v = -1;
@@ -1257,7 +1268,8 @@ MLC_EXPORT int mlc_dwconv_dgrad(const bf16* dy, const bf16* w, bf16* dx, int N, 
   const int Wqi = (W + DW_SW - 1) / DW_SW;
   if (D == 1 && (S == 1 || S == 2) && (KW == 3 || KW == 5 || KW == 7) && dw_strips() && items_fit(N, H, Wqi, C / 8)) {
     const long work = (long)N * H * Wqi * (C / 8);
-    const dim3 grid(blocks_for(work));
+    const int nb = blocks_for(work);
+    const dim3 grid(nb < dw_dgrad_cap() ? nb : dw_dgrad_cap());
     const Idx3 ix = idx3(C / 8, Wqi, H);
 #define DWD(K, SS, PP) hipLaunchKernelGGL((dw_dgrad_strip_kernel<K, SS, PP>), grid, dim3(NT), 0, st, dy, w, dx, N, H, \
                                           W, C, Ho, Wo, KH, P, ix)
